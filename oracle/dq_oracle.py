@@ -1,0 +1,1193 @@
+"""CPU restatement of Deequ's fused scan semantics -- TEST INFRASTRUCTURE ONLY.
+
+This module is the *checker* for the MI355X path.  Only ``tests/``,
+``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import
+it; the product (``deequ_amd``) never does, and must fail loudly when its HIP
+library is missing instead of falling back to anything in here.
+
+What it restates (reference = malcolmgreaves/deequ, paths relative to
+``src/main/scala/com/amazon/deequ/``):
+
+* analyzer aggregation semantics: ``analyzers/{Size,Completeness,Compliance,Sum,
+  Mean,StandardDeviation,Minimum,Maximum,Correlation,ApproxCountDistinct}.scala``
+  and ``analyzers/Analyzer.scala:220-234, 337-443`` (conditionalSelection /
+  conditionalCount / ifNoNullsIn / merge / metricFromEmpty);
+* state algebra (``State.sum``) of every hot-path state type;
+* HLL++ register update / pack / merge / estimate
+  (``analyzers/catalyst/StatefulHyperloglogPlus.scala:89-297``, constants
+  ``analyzers/catalyst/HLLConstants.scala:27-37,51,84``);
+* ``HdfsStateProvider`` byte formats and file identifiers
+  (``analyzers/StateProvider.scala:81-83, 176-294``).
+
+Spark 2.2.2 itself is not vendored in the reference (pom.xml:79-83), so the
+following are restated from Spark's published source and pinned by the
+reference's own known-answer tests (see tests/golden/reference_kats.json) and,
+for the hash, by the independent ``xxhash`` 3.8.1 Python package:
+
+* ``CentralMomentAgg`` update/merge (StandardDeviation; call site
+  ``analyzers/catalyst/StatefulStdDevPop.scala:24``),
+* ``Corr`` update/merge (Correlation; ``analyzers/catalyst/StatefulCorrelation.scala:24``),
+* ``XxHash64Function`` / ``XXH64.hashLong|hashInt|hashUnsafeBytes`` with seed 42
+  (``analyzers/catalyst/StatefulHyperloglogPlus.scala:93``),
+* SQL ``sum``/``count``/``min``/``max`` null semantics and three-valued logic.
+
+Spark's partial/final aggregation is simulated exactly: rows are split into
+``n_partitions`` contiguous partitions, each partition is folded sequentially
+with the update expressions, and the final aggregate folds the partition
+buffers in order into the zero buffer with the merge expressions.
+"""
+from __future__ import annotations
+
+import math
+import struct
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+MASK64 = (1 << 64) - 1
+
+# --------------------------------------------------------------------------------------
+# Java numeric helpers
+# --------------------------------------------------------------------------------------
+
+
+def to_i64(x: int) -> int:
+    x &= MASK64
+    return x - (1 << 64) if x >> 63 else x
+
+
+def to_i32(x: int) -> int:
+    x &= 0xFFFFFFFF
+    return x - (1 << 32) if x >> 31 else x
+
+
+def java_math_round(a: float) -> int:
+    """java.lang.Math.round(double) (JDK 8 bit algorithm; = floor(a + 1/2) exactly)."""
+    if math.isnan(a):
+        return 0
+    bits = struct.unpack("<q", struct.pack("<d", a))[0]
+    biased_exp = (bits & 0x7FF0000000000000) >> 52
+    shift = (52 - 1 + 1023) - biased_exp
+    if (shift & -64) == 0:
+        r = (bits & 0x000FFFFFFFFFFFFF) | 0x0010000000000000
+        if bits < 0:
+            r = -r
+        return ((r >> shift) + 1) >> 1
+    # |a| >= 2^52 or tiny: (long) a  (saturating cast)
+    if a >= 9.223372036854776e18:
+        return (1 << 63) - 1
+    if a <= -9.223372036854776e18:
+        return -(1 << 63)
+    return int(a)
+
+
+def java_min(a: float, b: float) -> float:
+    """java.lang.Math.min(double,double): NaN propagates, -0.0 < 0.0."""
+    if a != a:
+        return a
+    if b != b:
+        return b
+    if a == 0.0 and b == 0.0:
+        return a if math.copysign(1.0, a) < 0 else b
+    return a if a <= b else b
+
+
+def java_max(a: float, b: float) -> float:
+    if a != a:
+        return a
+    if b != b:
+        return b
+    if a == 0.0 and b == 0.0:
+        return a if math.copysign(1.0, a) > 0 else b
+    return a if a >= b else b
+
+
+def jdiv(a: float, b: float) -> float:
+    """IEEE-754 double division as on the JVM (x/0 -> +-Infinity, 0/0 -> NaN)."""
+    try:
+        return a / b
+    except ZeroDivisionError:
+        if a != a or a == 0.0:
+            return float("nan")
+        return math.copysign(float("inf"), a) * math.copysign(1.0, b)
+
+
+def double_to_long_bits(d: float) -> int:
+    """java.lang.Double.doubleToLongBits (canonical NaN)."""
+    if d != d:
+        return 0x7FF8000000000000
+    return struct.unpack("<q", struct.pack("<d", d))[0]
+
+
+# --------------------------------------------------------------------------------------
+# XXH64 as used by Spark's XxHash64Function (seed 42)
+# --------------------------------------------------------------------------------------
+
+P1 = 0x9E3779B185EBCA87
+P2 = 0xC2B2AE3D27D4EB4F
+P3 = 0x165667B19E3779F9
+P4 = 0x85EBCA77C2B2AE63
+P5 = 0x27D4EB2F165667C5
+HLL_SEED = 42
+
+
+def _rotl(x: int, r: int) -> int:
+    x &= MASK64
+    return ((x << r) | (x >> (64 - r))) & MASK64
+
+
+def _fmix(h: int) -> int:
+    h ^= h >> 33
+    h = (h * P2) & MASK64
+    h ^= h >> 29
+    h = (h * P3) & MASK64
+    h ^= h >> 32
+    return h
+
+
+def xxh64_long(v: int, seed: int = HLL_SEED) -> int:
+    """XXH64.hashLong -> signed Java long."""
+    h = (seed + P5 + 8) & MASK64
+    h ^= (_rotl((v & MASK64) * P2, 31) * P1) & MASK64
+    h = (_rotl(h, 27) * P1 + P4) & MASK64
+    return to_i64(_fmix(h))
+
+
+def xxh64_int(v: int, seed: int = HLL_SEED) -> int:
+    """XXH64.hashInt -> signed Java long."""
+    h = (seed + P5 + 4) & MASK64
+    h ^= ((v & 0xFFFFFFFF) * P1) & MASK64
+    h = (_rotl(h, 23) * P2 + P3) & MASK64
+    return to_i64(_fmix(h))
+
+
+def xxh64_bytes(b: bytes, seed: int = HLL_SEED) -> int:
+    """XXH64.hashUnsafeBytes (little-endian words) -> signed Java long."""
+    n = len(b)
+    off = 0
+    if n >= 32:
+        v1 = (seed + P1 + P2) & MASK64
+        v2 = (seed + P2) & MASK64
+        v3 = seed & MASK64
+        v4 = (seed - P1) & MASK64
+        while off <= n - 32:
+            w = struct.unpack_from("<4Q", b, off)
+            v1 = (_rotl(v1 + w[0] * P2, 31) * P1) & MASK64
+            v2 = (_rotl(v2 + w[1] * P2, 31) * P1) & MASK64
+            v3 = (_rotl(v3 + w[2] * P2, 31) * P1) & MASK64
+            v4 = (_rotl(v4 + w[3] * P2, 31) * P1) & MASK64
+            off += 32
+        h = (_rotl(v1, 1) + _rotl(v2, 7) + _rotl(v3, 12) + _rotl(v4, 18)) & MASK64
+        for v in (v1, v2, v3, v4):
+            v = (_rotl(v * P2, 31) * P1) & MASK64
+            h ^= v
+            h = (h * P1 + P4) & MASK64
+    else:
+        h = (seed + P5) & MASK64
+    h = (h + n) & MASK64
+    while off <= n - 8:
+        k1 = struct.unpack_from("<Q", b, off)[0]
+        h ^= (_rotl(k1 * P2, 31) * P1) & MASK64
+        h = (_rotl(h, 27) * P1 + P4) & MASK64
+        off += 8
+    if off + 4 <= n:
+        k = struct.unpack_from("<I", b, off)[0]
+        h ^= (k * P1) & MASK64
+        h = (_rotl(h, 23) * P2 + P3) & MASK64
+        off += 4
+    while off < n:
+        h ^= (b[off] * P5) & MASK64
+        h = (_rotl(h, 11) * P1) & MASK64
+        off += 1
+    return to_i64(_fmix(h))
+
+
+# vectorised numpy forms (uint64 arithmetic wraps modulo 2^64)
+_U = np.uint64
+
+
+def _np_rotl(x, r):
+    return (x << _U(r)) | (x >> _U(64 - r))
+
+
+def _np_fmix(h):
+    h = h ^ (h >> _U(33))
+    h = h * _U(P2)
+    h = h ^ (h >> _U(29))
+    h = h * _U(P3)
+    h = h ^ (h >> _U(32))
+    return h
+
+
+def np_xxh64_long(v: np.ndarray, seed: int = HLL_SEED) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        x = np.asarray(v).astype(np.int64).view(np.uint64)
+        h = np.full(x.shape, (seed + P5 + 8) & MASK64, dtype=np.uint64)
+        h ^= _np_rotl(x * _U(P2), 31) * _U(P1)
+        h = _np_rotl(h, 27) * _U(P1) + _U(P4)
+        return _np_fmix(h)
+
+
+def np_xxh64_int(v: np.ndarray, seed: int = HLL_SEED) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        x = np.asarray(v).astype(np.int32).view(np.uint32).astype(np.uint64)
+        h = np.full(x.shape, (seed + P5 + 4) & MASK64, dtype=np.uint64)
+        h ^= x * _U(P1)
+        h = _np_rotl(h, 23) * _U(P2) + _U(P3)
+        return _np_fmix(h)
+
+
+def np_double_to_long_bits(d: np.ndarray) -> np.ndarray:
+    d = np.asarray(d, dtype=np.float64)
+    bits = d.view(np.int64).copy()
+    bits[np.isnan(d)] = 0x7FF8000000000000
+    return bits
+
+
+# --------------------------------------------------------------------------------------
+# HLL++ (StatefulHyperloglogPlus.scala / HLLConstants.scala)
+# --------------------------------------------------------------------------------------
+
+RELATIVE_SD = 0.05
+HLL_P = int(math.ceil(2.0 * math.log(1.106 / RELATIVE_SD) / math.log(2.0)))  # :157 -> 9
+HLL_M = 1 << HLL_P  # :161 -> 512
+IDX_SHIFT = 64 - HLL_P  # :159
+W_PADDING = 1 << (HLL_P - 1)  # :160
+REGISTER_SIZE = 6  # HLLConstants.scala:29
+REGISTER_WORD_MASK = (1 << REGISTER_SIZE) - 1  # :31
+REGISTERS_PER_WORD = 64 // REGISTER_SIZE  # :33 -> 10
+NUM_WORDS = 52  # StatefulHyperloglogPlus.scala:154
+HLL_K = 6  # HLLConstants.scala:35
+THRESHOLDS = [10, 20, 40, 80, 220, 400, 900, 1800, 3100, 6500, 15500, 20000, 50000, 120000, 350000]
+ALPHA_M2 = (0.7213 / (1.0 + 1.079 / HLL_M)) * HLL_M * HLL_M  # :163-168 (P >= 7 branch)
+
+
+def _load_bias_tables():
+    import json
+    import os
+
+    path = os.path.join(os.path.dirname(__file__), "..", "tests", "golden", "hll_p9_tables.json")
+    with open(path) as f:
+        t = json.load(f)
+    return t["raw_estimate_p9"], t["bias_p9"]
+
+
+RAW_ESTIMATE_P9, BIAS_P9 = _load_bias_tables()
+
+
+def hll_index_and_pw(x_signed: int) -> Tuple[int, int]:
+    """idx = x >>> IDX_SHIFT; pw = nlz((x << P) | W_PADDING) + 1 (:96-99)."""
+    x = x_signed & MASK64
+    idx = x >> IDX_SHIFT
+    w = ((x << HLL_P) | W_PADDING) & MASK64
+    pw = 64 - w.bit_length() + 1
+    return idx, pw
+
+
+def np_hll_registers(hashes_u64: np.ndarray, regs: Optional[np.ndarray] = None) -> np.ndarray:
+    """Fold 64-bit hashes into 512 byte-registers (max of pw per index)."""
+    if regs is None:
+        regs = np.zeros(HLL_M, dtype=np.uint8)
+    h = np.asarray(hashes_u64, dtype=np.uint64)
+    if h.size == 0:
+        return regs
+    idx = (h >> _U(IDX_SHIFT)).astype(np.int64)
+    w = (h << _U(HLL_P)) | _U(W_PADDING)
+    # nlz via float exponent is unsafe for 64-bit; do it with bit_length on 32-bit halves
+    hi = (w >> _U(32)).astype(np.uint64)
+    lo = (w & _U(0xFFFFFFFF)).astype(np.uint64)
+    nlz_hi = 32 - _bitlen32(hi)
+    nlz_lo = 32 - _bitlen32(lo)
+    nlz = np.where(hi != 0, nlz_hi, 32 + nlz_lo)
+    pw = (nlz + 1).astype(np.uint8)
+    np.maximum.at(regs, idx, pw)
+    return regs
+
+
+def _bitlen32(x: np.ndarray) -> np.ndarray:
+    x = x.astype(np.uint64)
+    n = np.zeros(x.shape, dtype=np.int64)
+    for s in (16, 8, 4, 2, 1):
+        m = x >= _U(1 << s)
+        n += np.where(m, s, 0)
+        x = np.where(m, x >> _U(s), x)
+    n += (x > 0).astype(np.int64)
+    return n
+
+
+def registers_to_words(regs: Sequence[int]) -> List[int]:
+    """512 registers -> 52 signed longs (10 x 6-bit registers per word, :102-112)."""
+    words = [0] * NUM_WORDS
+    for i, r in enumerate(regs):
+        wo = i // REGISTERS_PER_WORD
+        shift = REGISTER_SIZE * (i - wo * REGISTERS_PER_WORD)
+        words[wo] |= (int(r) & REGISTER_WORD_MASK) << shift
+    return [to_i64(w) for w in words]
+
+
+def words_to_registers(words: Sequence[int]) -> List[int]:
+    regs = []
+    for i in range(HLL_M):
+        wo = i // REGISTERS_PER_WORD
+        shift = REGISTER_SIZE * (i - wo * REGISTERS_PER_WORD)
+        regs.append(((words[wo] & MASK64) >> shift) & REGISTER_WORD_MASK)
+    return regs
+
+
+def hll_update_words(words: List[int], x_signed: int) -> None:
+    """Exact StatefulHyperloglogPlus.update (:89-115) on a 52-word buffer."""
+    idx, pw = hll_index_and_pw(x_signed)
+    wo = idx // REGISTERS_PER_WORD
+    word = words[wo] & MASK64
+    shift = REGISTER_SIZE * (idx - wo * REGISTERS_PER_WORD)
+    mask = REGISTER_WORD_MASK << shift
+    m = (word & mask) >> shift
+    if pw > m:
+        words[wo] = to_i64((word & ~mask & MASK64) | (pw << shift))
+
+
+def hll_merge_words(w1: Sequence[int], w2: Sequence[int]) -> List[int]:
+    """DeequHyperLogLogPlusPlusUtils.merge (:188-208): per-register max."""
+    dest = []
+    idx = 0
+    for wo in range(NUM_WORDS):
+        a, b = w1[wo] & MASK64, w2[wo] & MASK64
+        word = 0
+        mask = REGISTER_WORD_MASK
+        i = 0
+        while idx < HLL_M and i < REGISTERS_PER_WORD:
+            word |= max(a & mask, b & mask)
+            mask <<= REGISTER_SIZE
+            i += 1
+            idx += 1
+        dest.append(to_i64(word))
+    return dest
+
+
+def _estimate_bias(e: float) -> float:
+    """DeequHyperLogLogPlusPlusUtils.estimateBias (:259-297) incl. Arrays.binarySearch."""
+    est = RAW_ESTIMATE_P9
+    n = len(est)
+    lo, hi = 0, n - 1
+    found = None
+    while lo <= hi:  # java.util.Arrays.binarySearch(double[], ...)
+        mid = (lo + hi) >> 1
+        v = est[mid]
+        if v < e:
+            lo = mid + 1
+        elif v > e:
+            hi = mid - 1
+        else:
+            found = mid
+            break
+    nearest = found if found is not None else lo
+
+    def distance(i):
+        d = e - est[i]
+        return d * d
+
+    low = max(nearest - HLL_K + 1, 0)
+    high = min(low + HLL_K, n)
+    while high < n and distance(high) < distance(low):
+        low += 1
+        high += 1
+    s = 0.0
+    for i in range(low, high):
+        s += BIAS_P9[i]
+    return s / (high - low)
+
+
+def hll_count(words: Sequence[int]) -> float:
+    """DeequHyperLogLogPlusPlusUtils.count (:210-257) incl. the JVM `1 << Midx` Int quirk."""
+    z_inverse = 0.0
+    V = 0.0
+    idx = 0
+    for wo in range(len(words)):
+        word = words[wo] & MASK64
+        i = 0
+        shift = 0
+        while idx < HLL_M and i < REGISTERS_PER_WORD:
+            m = (word >> shift) & REGISTER_WORD_MASK
+            denom = to_i32(1 << (m & 31))  # Int << Long: shift count masked to 5 bits
+            z_inverse += 1.0 / denom
+            if m == 0:
+                V += 1.0
+            shift += REGISTER_SIZE
+            i += 1
+            idx += 1
+
+    def e_bias_corrected():
+        e = ALPHA_M2 / z_inverse
+        if HLL_P < 19 and e < 5.0 * HLL_M:
+            return e - _estimate_bias(e)
+        return e
+
+    if V > 0:
+        H = HLL_M * math.log(HLL_M / V)
+        estimate = H if H <= THRESHOLDS[HLL_P - 4] else e_bias_corrected()
+    else:
+        estimate = e_bias_corrected()
+    return float(java_math_round(estimate))
+
+
+def words_to_bytes(words: Sequence[int]) -> bytes:
+    """wordsToBytes (:170-178): ByteBuffer default = big-endian."""
+    return struct.pack(">52q", *[to_i64(w) for w in words])
+
+
+def words_from_bytes(b: bytes) -> List[int]:
+    assert len(b) == NUM_WORDS * 8
+    return list(struct.unpack(">52q", b))
+
+
+# --------------------------------------------------------------------------------------
+# States (A12) -- exact State.sum semantics
+# --------------------------------------------------------------------------------------
+
+
+@dataclass(frozen=True)
+class NumMatches:  # Size.scala:23-33
+    numMatches: int
+
+    def sum(self, o):
+        return NumMatches(to_i64(self.numMatches + o.numMatches))
+
+    def metricValue(self):
+        return float(self.numMatches)
+
+
+@dataclass(frozen=True)
+class NumMatchesAndCount:  # Analyzer.scala:220-234
+    numMatches: int
+    count: int
+
+    def sum(self, o):
+        return NumMatchesAndCount(to_i64(self.numMatches + o.numMatches), to_i64(self.count + o.count))
+
+    def metricValue(self):
+        return float("nan") if self.count == 0 else float(self.numMatches) / self.count
+
+
+@dataclass(frozen=True)
+class SumState:  # Sum.scala:25-34
+    sum_: float
+
+    def sum(self, o):
+        return SumState(self.sum_ + o.sum_)
+
+    def metricValue(self):
+        return self.sum_
+
+
+@dataclass(frozen=True)
+class MeanState:  # Mean.scala:25-34
+    sum_: float
+    count: int
+
+    def sum(self, o):
+        return MeanState(self.sum_ + o.sum_, to_i64(self.count + o.count))
+
+    def metricValue(self):
+        return float("nan") if self.count == 0 else jdiv(self.sum_, float(self.count))
+
+
+@dataclass(frozen=True)
+class StandardDeviationState:  # StandardDeviation.scala:25-45
+    n: float
+    avg: float
+    m2: float
+
+    def __post_init__(self):
+        if not self.n > 0.0:
+            raise ValueError("Standard deviation is undefined for n = 0.")
+
+    def sum(self, o):
+        newN = self.n + o.n
+        delta = o.avg - self.avg
+        deltaN = 0.0 if newN == 0.0 else delta / newN
+        return StandardDeviationState(newN, self.avg + deltaN * o.n,
+                                      self.m2 + o.m2 + delta * deltaN * self.n * o.n)
+
+    def metricValue(self):
+        q = jdiv(self.m2, self.n)
+        return math.sqrt(q) if q >= 0 else float("nan")
+
+
+@dataclass(frozen=True)
+class MinState:  # Minimum.scala:25-34
+    minValue: float
+
+    def sum(self, o):
+        return MinState(java_min(self.minValue, o.minValue))
+
+    def metricValue(self):
+        return self.minValue
+
+
+@dataclass(frozen=True)
+class MaxState:  # Maximum.scala:25-34
+    maxValue: float
+
+    def sum(self, o):
+        return MaxState(java_max(self.maxValue, o.maxValue))
+
+    def metricValue(self):
+        return self.maxValue
+
+
+@dataclass(frozen=True)
+class CorrelationState:  # Correlation.scala:26-57
+    n: float
+    xAvg: float
+    yAvg: float
+    ck: float
+    xMk: float
+    yMk: float
+
+    def __post_init__(self):
+        if not self.n > 0.0:
+            raise ValueError("Correlation undefined for n = 0.")
+
+    def sum(self, o):
+        n1, n2 = self.n, o.n
+        newN = n1 + n2
+        dx = o.xAvg - self.xAvg
+        dxN = 0.0 if newN == 0.0 else dx / newN
+        dy = o.yAvg - self.yAvg
+        dyN = 0.0 if newN == 0.0 else dy / newN
+        return CorrelationState(newN, self.xAvg + dxN * n2, self.yAvg + dyN * n2,
+                                self.ck + o.ck + dx * dyN * n1 * n2,
+                                self.xMk + o.xMk + dx * dxN * n1 * n2,
+                                self.yMk + o.yMk + dy * dyN * n1 * n2)
+
+    def metricValue(self):
+        prod = self.xMk * self.yMk
+        return jdiv(self.ck, math.sqrt(prod)) if prod >= 0 else float("nan")
+
+
+@dataclass(frozen=True)
+class ApproxCountDistinctState:  # ApproxCountDistinct.scala:26-40
+    words: Tuple[int, ...]
+
+    def sum(self, o):
+        return ApproxCountDistinctState(tuple(hll_merge_words(self.words, o.words)))
+
+    def metricValue(self):
+        return hll_count(self.words)
+
+
+def merge_states(*states):
+    """Analyzers.merge (Analyzer.scala:343-362)."""
+    acc = None
+    for s in states:
+        if acc is None:
+            acc = s
+        elif s is not None:
+            acc = acc.sum(s)
+    return acc
+
+
+# --------------------------------------------------------------------------------------
+# Columns and the three-valued predicate evaluator (SQL semantics, Check.scala grammar)
+# --------------------------------------------------------------------------------------
+
+
+@dataclass
+class OColumn:
+    """A column for the oracle: dtype in {f64,i64,i32,utf8}; values + boolean validity."""
+
+    dtype: str
+    values: object  # np.ndarray for numerics, list[bytes|None] for utf8
+    valid: np.ndarray  # bool
+
+    def __len__(self):
+        return len(self.valid)
+
+
+class _Tok:
+    def __init__(self, s: str):
+        self.toks = []
+        i = 0
+        while i < len(s):
+            c = s[i]
+            if c.isspace():
+                i += 1
+            elif c == "`":
+                j = s.index("`", i + 1)
+                self.toks.append(("id", s[i + 1:j]))
+                i = j + 1
+            elif c == "'":
+                j = s.index("'", i + 1)
+                self.toks.append(("str", s[i + 1:j]))
+                i = j + 1
+            elif c.isdigit() or (c == "." and i + 1 < len(s) and s[i + 1].isdigit()):
+                j = i
+                while j < len(s) and (s[j].isdigit() or s[j] in ".eE" or
+                                      (s[j] in "+-" and s[j - 1] in "eE")):
+                    j += 1
+                self.toks.append(("num", s[i:j]))
+                i = j
+            elif c.isalpha() or c == "_":
+                j = i
+                while j < len(s) and (s[j].isalnum() or s[j] == "_"):
+                    j += 1
+                w = s[i:j]
+                if w.upper() in ("AND", "OR", "NOT", "IS", "NULL", "COALESCE", "IN", "TRUE", "FALSE"):
+                    self.toks.append(("kw", w.upper()))
+                else:
+                    self.toks.append(("id", w))
+                i = j
+            elif s.startswith(("<=", ">=", "!=", "<>", "=="), i):
+                self.toks.append(("op", s[i:i + 2]))
+                i += 2
+            elif c in "<>=(),-":
+                self.toks.append(("op", c))
+                i += 1
+            else:
+                raise ValueError(f"unexpected character {c!r} in {s!r}")
+        self.pos = 0
+
+    def peek(self):
+        return self.toks[self.pos] if self.pos < len(self.toks) else (None, None)
+
+    def take(self):
+        t = self.peek()
+        self.pos += 1
+        return t
+
+
+class OracleExpr:
+    """Evaluates a Spark-SQL predicate string with three-valued logic over OColumns.
+
+    Value model: (values, type, notnull) with type in {'int','dec','dbl','str','bool'}.
+    Literal typing follows Spark 2.2: `3` int, `3.0` decimal, `3e0` double.
+    Comparisons: int/dec vs int/dec exact (python ints / fractions); anything vs double
+    in double; strings compared as UTF-8 bytes.
+    """
+
+    def __init__(self, text: str):
+        self.text = text
+        self.t = _Tok(text)
+        self.ast = self._or()
+        if self.t.peek()[0] is not None:
+            raise ValueError(f"trailing tokens in {text!r}")
+
+    def _or(self):
+        a = self._and()
+        while self.t.peek() == ("kw", "OR"):
+            self.t.take()
+            a = ("or", a, self._and())
+        return a
+
+    def _and(self):
+        a = self._not()
+        while self.t.peek() == ("kw", "AND"):
+            self.t.take()
+            a = ("and", a, self._not())
+        return a
+
+    def _not(self):
+        if self.t.peek() == ("kw", "NOT"):
+            self.t.take()
+            return ("not", self._not())
+        return self._cmp()
+
+    def _cmp(self):
+        a = self._atom()
+        k, v = self.t.peek()
+        if k == "op" and v in ("<", "<=", ">", ">=", "=", "==", "!=", "<>"):
+            self.t.take()
+            b = self._atom()
+            v = {"==": "=", "<>": "!="}.get(v, v)
+            return ("cmp", v, a, b)
+        if (k, v) == ("kw", "IS"):
+            self.t.take()
+            neg = False
+            if self.t.peek() == ("kw", "NOT"):
+                self.t.take()
+                neg = True
+            assert self.t.take() == ("kw", "NULL")
+            return ("isnotnull" if neg else "isnull", a)
+        if (k, v) == ("kw", "IN") or (k, v) == ("kw", "NOT"):
+            neg = False
+            if v == "NOT":
+                self.t.take()
+                neg = True
+            assert self.t.take() == ("kw", "IN")
+            assert self.t.take() == ("op", "(")
+            items = [self._atom()]
+            while self.t.peek() == ("op", ","):
+                self.t.take()
+                items.append(self._atom())
+            assert self.t.take() == ("op", ")")
+            e = ("in", a, items)
+            return ("not", e) if neg else e
+        return a
+
+    def _atom(self):
+        k, v = self.t.take()
+        if k == "op" and v == "(":
+            e = self._or()
+            assert self.t.take() == ("op", ")")
+            return e
+        if k == "op" and v == "-":
+            k2, v2 = self.t.take()
+            assert k2 == "num"
+            return self._num("-" + v2)
+        if k == "num":
+            return self._num(v)
+        if k == "str":
+            return ("lit", "str", v.encode("utf-8"))
+        if k == "kw" and v == "NULL":
+            return ("lit", "null", None)
+        if k == "kw" and v in ("TRUE", "FALSE"):
+            return ("lit", "bool", v == "TRUE")
+        if k == "kw" and v == "COALESCE":
+            assert self.t.take() == ("op", "(")
+            args = [self._or()]
+            while self.t.peek() == ("op", ","):
+                self.t.take()
+                args.append(self._or())
+            assert self.t.take() == ("op", ")")
+            return ("coalesce", args)
+        if k == "id":
+            return ("col", v)
+        raise ValueError(f"unexpected token {(k, v)} in {self.text!r}")
+
+    @staticmethod
+    def _num(s: str):
+        from fractions import Fraction
+
+        if "e" in s or "E" in s:
+            return ("lit", "dbl", float(s))
+        if "." in s:
+            return ("lit", "dec", Fraction(s))
+        return ("lit", "int", int(s))
+
+    # ---- evaluation: returns (vals: list, typ, notnull: np.bool_ array) ----
+    def eval(self, cols: dict, n: int):
+        return self._ev(self.ast, cols, n)
+
+    def eval_bool(self, cols: dict, n: int):
+        vals, typ, nn = self._ev(self.ast, cols, n)
+        assert typ == "bool", f"predicate {self.text!r} is not boolean"
+        return np.array([bool(x) for x in vals], dtype=bool) & nn, nn
+
+    def _ev(self, e, cols, n):
+        from fractions import Fraction
+
+        kind = e[0]
+        if kind == "lit":
+            typ, v = e[1], e[2]
+            if typ == "null":
+                return [None] * n, "null", np.zeros(n, dtype=bool)
+            return [v] * n, typ, np.ones(n, dtype=bool)
+        if kind == "col":
+            c = cols[e[1]]
+            if c.dtype == "f64":
+                return [float(x) for x in c.values], "dbl", c.valid.copy()
+            if c.dtype in ("i64", "i32"):
+                return [int(x) for x in c.values], "int", c.valid.copy()
+            if c.dtype == "utf8":
+                return list(c.values), "str", c.valid.copy()
+            raise ValueError(c.dtype)
+        if kind == "coalesce":
+            parts = [self._ev(a, cols, n) for a in e[1]]
+            typ = _widen([p[1] for p in parts if p[1] != "null"])
+            vals = [None] * n
+            nn = np.zeros(n, dtype=bool)
+            for pv, pt, pn in parts:
+                for i in range(n):
+                    if not nn[i] and pn[i]:
+                        vals[i] = _coerce(pv[i], pt, typ)
+                        nn[i] = True
+            return vals, typ, nn
+        if kind == "cmp":
+            op = e[1]
+            av, at, an = self._ev(e[2], cols, n)
+            bv, bt, bn = self._ev(e[3], cols, n)
+            if at == "str" or bt == "str":
+                if at != bt:
+                    raise NotImplementedError("string/number comparison")
+                typ = "str"
+            else:
+                typ = _widen([at, bt])
+            nn = an & bn
+            out = []
+            for i in range(n):
+                if not nn[i]:
+                    out.append(False)
+                    continue
+                x, y = _coerce(av[i], at, typ), _coerce(bv[i], bt, typ)
+                out.append(_cmp(op, x, y))
+            return out, "bool", nn
+        if kind == "in":
+            av, at, an = self._ev(e[1], cols, n)
+            items = [self._ev(it, cols, n) for it in e[2]]
+            # x IN (a,b) == x = a OR x = b (three-valued)
+            t = np.zeros(n, dtype=bool)
+            anynull = ~an
+            for iv, it, inn in items:
+                for i in range(n):
+                    if an[i] and inn[i] and iv[i] == av[i]:
+                        t[i] = True
+                anynull = anynull | ~inn
+            nn = t | ~anynull
+            return list(t), "bool", nn
+        if kind in ("and", "or"):
+            av, _, an = self._ev(e[1], cols, n)
+            bv, _, bn = self._ev(e[2], cols, n)
+            a_t = np.array(av, dtype=bool) & an
+            b_t = np.array(bv, dtype=bool) & bn
+            a_f = ~np.array(av, dtype=bool) & an
+            b_f = ~np.array(bv, dtype=bool) & bn
+            if kind == "and":
+                t = a_t & b_t
+                f = a_f | b_f
+            else:
+                t = a_t | b_t
+                f = a_f & b_f
+            return list(t), "bool", t | f
+        if kind == "not":
+            av, _, an = self._ev(e[1], cols, n)
+            return [not x for x in av], "bool", an
+        if kind == "isnull":
+            _, _, an = self._ev(e[1], cols, n)
+            return list(~an), "bool", np.ones(n, dtype=bool)
+        if kind == "isnotnull":
+            _, _, an = self._ev(e[1], cols, n)
+            return list(an), "bool", np.ones(n, dtype=bool)
+        raise ValueError(kind)
+
+
+def _widen(types):
+    types = [t for t in types if t != "null"]
+    if not types:
+        return "null"
+    if "dbl" in types:
+        return "dbl"
+    if "dec" in types:
+        return "dec"
+    if "bool" in types:
+        return "bool"
+    if "str" in types:
+        return "str"
+    return "int"
+
+
+def _coerce(v, frm, to):
+    from fractions import Fraction
+
+    if v is None:
+        return None
+    if to == "dbl":
+        return float(v)
+    if to == "dec":
+        return Fraction(v)
+    return v
+
+
+def _cmp(op, x, y):
+    if isinstance(x, float) or isinstance(y, float):
+        # Spark compares doubles with NaN as the largest value (nanSafe ordering for =, <, >)
+        xn, yn = x != x, y != y
+        if xn or yn:
+            c = 0 if (xn and yn) else (1 if xn else -1)
+        else:
+            c = (x > y) - (x < y)
+    else:
+        c = (x > y) - (x < y)
+    return {"<": c < 0, "<=": c <= 0, ">": c > 0, ">=": c >= 0, "=": c == 0, "!=": c != 0}[op]
+
+
+# --------------------------------------------------------------------------------------
+# Spark aggregation semantics (partial per partition + ordered final merge)
+# --------------------------------------------------------------------------------------
+
+
+def _partitions(n: int, n_partitions: int):
+    n_partitions = max(1, n_partitions)
+    bounds = [(n * p) // n_partitions for p in range(n_partitions + 1)]
+    return [(bounds[p], bounds[p + 1]) for p in range(n_partitions)]
+
+
+def _as_double_list(c: OColumn):
+    if c.dtype == "f64":
+        return [float(x) for x in c.values]
+    return [float(int(x)) for x in c.values]
+
+
+def spark_stddev_buffer(x: List[float], sel: np.ndarray, n_partitions: int = 1):
+    """CentralMomentAgg (momentOrder 2) partial updates + final merges; returns (n, avg, m2)."""
+    partials = []
+    for lo, hi in _partitions(len(sel), n_partitions):
+        n = avg = m2 = 0.0
+        for i in range(lo, hi):
+            if sel[i]:
+                newN = n + 1.0
+                delta = x[i] - avg
+                deltaN = delta / newN
+                avg = avg + deltaN
+                m2 = m2 + delta * (delta - deltaN)
+                n = newN
+        partials.append((n, avg, m2))
+    n = avg = m2 = 0.0  # final aggregate starts from the initial (zero) buffer
+    for n2, avg2, m22 in partials:
+        newN = n + n2
+        delta = avg2 - avg
+        deltaN = 0.0 if newN == 0.0 else delta / newN
+        avg = avg + deltaN * n2
+        m2 = m2 + m22 + delta * deltaN * n * n2
+        n = newN
+    return n, avg, m2
+
+
+def spark_corr_buffer(x: List[float], y: List[float], sel: np.ndarray, n_partitions: int = 1):
+    """Corr partial updates + final merges; returns (n, xAvg, yAvg, ck, xMk, yMk)."""
+    partials = []
+    for lo, hi in _partitions(len(sel), n_partitions):
+        n = xAvg = yAvg = ck = xMk = yMk = 0.0
+        for i in range(lo, hi):
+            if sel[i]:
+                newN = n + 1.0
+                dx = x[i] - xAvg
+                dxN = dx / newN
+                dy = y[i] - yAvg
+                dyN = dy / newN
+                newXAvg = xAvg + dxN
+                newYAvg = yAvg + dyN
+                ck = ck + dx * (y[i] - newYAvg)
+                xMk = xMk + dx * (x[i] - newXAvg)
+                yMk = yMk + dy * (y[i] - newYAvg)
+                xAvg, yAvg, n = newXAvg, newYAvg, newN
+        partials.append((n, xAvg, yAvg, ck, xMk, yMk))
+    n = xAvg = yAvg = ck = xMk = yMk = 0.0
+    for n2, xA2, yA2, ck2, xM2, yM2 in partials:
+        n1 = n
+        newN = n1 + n2
+        dx = xA2 - xAvg
+        dxN = 0.0 if newN == 0.0 else dx / newN
+        dy = yA2 - yAvg
+        dyN = 0.0 if newN == 0.0 else dy / newN
+        xAvg = xAvg + dxN * n2
+        yAvg = yAvg + dyN * n2
+        ck = ck + ck2 + dx * dyN * n1 * n2
+        xMk = xMk + xM2 + dx * dxN * n1 * n2
+        yMk = yMk + yM2 + dy * dyN * n1 * n2
+        n = newN
+    return n, xAvg, yAvg, ck, xMk, yMk
+
+
+def spark_sum(c: OColumn, sel: np.ndarray, n_partitions: int = 1):
+    """sum(col): integral -> wrapping long sum; double -> sequential double sum; None if empty."""
+    if not sel.any():
+        return None
+    parts = []
+    for lo, hi in _partitions(len(sel), n_partitions):
+        if not sel[lo:hi].any():
+            continue
+        if c.dtype in ("i64", "i32"):
+            s = 0
+            for i in range(lo, hi):
+                if sel[i]:
+                    s = to_i64(s + int(c.values[i]))
+        else:
+            s = 0.0
+            for i in range(lo, hi):
+                if sel[i]:
+                    s += float(c.values[i])
+        parts.append(s)
+    tot = parts[0]
+    for p in parts[1:]:
+        tot = to_i64(tot + p) if c.dtype in ("i64", "i32") else tot + p
+    return float(tot)
+
+
+def _nan_safe_lt(a, b):
+    an, bn = a != a, b != b
+    if an or bn:
+        return (not an) and bn
+    return a < b
+
+
+def spark_min(c: OColumn, sel: np.ndarray, is_max: bool = False):
+    """min/max(col) with Spark's NaN-as-largest ordering; integral compared as integers."""
+    if not sel.any():
+        return None
+    best = None
+    for i in np.nonzero(sel)[0]:
+        v = int(c.values[i]) if c.dtype in ("i64", "i32") else float(c.values[i])
+        if best is None:
+            best = v
+        elif is_max:
+            if _nan_safe_lt(best, v):
+                best = v
+        else:
+            if _nan_safe_lt(v, best):
+                best = v
+    return float(best)
+
+
+def hll_words_for(c: OColumn, sel: np.ndarray) -> Tuple[int, ...]:
+    """stateful_approx_count_distinct registers for a column (XxHash64 seed 42)."""
+    idx = np.nonzero(sel)[0]
+    if c.dtype == "i64":
+        h = np_xxh64_long(np.asarray(c.values)[idx])
+    elif c.dtype == "f64":
+        h = np_xxh64_long(np_double_to_long_bits(np.asarray(c.values)[idx]))
+    elif c.dtype == "i32":
+        h = np_xxh64_int(np.asarray(c.values)[idx])
+    elif c.dtype == "utf8":
+        h = np.array([xxh64_bytes(c.values[i]) & MASK64 for i in idx], dtype=np.uint64)
+    else:
+        raise ValueError(c.dtype)
+    regs = np_hll_registers(h)
+    return tuple(registers_to_words(regs.tolist()))
+
+
+# --------------------------------------------------------------------------------------
+# Analyzers -> Option[State]   (the oracle's runScanningAnalyzers)
+# --------------------------------------------------------------------------------------
+
+
+def _where(cols, n, where: Optional[str]):
+    """(where_true, where_notnull) masks; no where -> all true."""
+    if where is None:
+        return np.ones(n, dtype=bool), np.ones(n, dtype=bool)
+    return OracleExpr(where).eval_bool(cols, n)
+
+
+def _conditional_count(cols, n, where):
+    """conditionalCount (Analyzer.scala:404-408): count(*) or sum(cast(where as long))."""
+    if where is None:
+        return n
+    t, nn = _where(cols, n, where)
+    if not nn.any():
+        return None
+    return int(t.sum())
+
+
+def compute_state(spec: tuple, cols: dict, n: int, n_partitions: int = 1):
+    """spec = (op, args...) mirroring the Scala case classes; returns Option[State]."""
+    op = spec[0]
+    if op == "Size":
+        c = _conditional_count(cols, n, spec[1])
+        return None if c is None else NumMatches(c)
+    if op == "Completeness":
+        col, where = spec[1], spec[2]
+        wt, _ = _where(cols, n, where)
+        count = _conditional_count(cols, n, where)
+        matches = int((cols[col].valid & wt).sum())
+        if count is None or (n == 0):
+            return None
+        return NumMatchesAndCount(matches, count)
+    if op == "Compliance":
+        _, pred, where = spec[1], spec[2], spec[3]
+        wt, _ = _where(cols, n, where)
+        pt, pn = OracleExpr(pred).eval_bool(cols, n)
+        # sum(cast(CASE WHEN where THEN pred END AS INT)): NULL if no non-null term
+        nonnull_terms = pn & wt
+        count = _conditional_count(cols, n, where)
+        if not nonnull_terms.any() or count is None:
+            return None
+        return NumMatchesAndCount(int((pt & wt).sum()), count)
+    if op in ("Sum", "Mean", "StandardDeviation", "Minimum", "Maximum", "ApproxCountDistinct"):
+        col, where = spec[1], spec[2]
+        c = cols[col]
+        wt, _ = _where(cols, n, where)
+        sel = c.valid & wt
+        if op == "Sum":
+            s = spark_sum(c, sel, n_partitions)
+            return None if s is None else SumState(s)
+        if op == "Mean":
+            s = spark_sum(c, sel, n_partitions)
+            return None if s is None else MeanState(s, int(sel.sum()))
+        if op == "StandardDeviation":
+            nn, avg, m2 = spark_stddev_buffer(_as_double_list(c), sel, n_partitions)
+            return None if nn == 0.0 else StandardDeviationState(nn, avg, m2)
+        if op in ("Minimum", "Maximum"):
+            v = spark_min(c, sel, is_max=(op == "Maximum"))
+            if v is None:
+                return None
+            return MinState(v) if op == "Minimum" else MaxState(v)
+        return ApproxCountDistinctState(hll_words_for(c, sel))
+    if op == "Correlation":
+        a, b, where = spec[1], spec[2], spec[3]
+        wt, _ = _where(cols, n, where)
+        sel = cols[a].valid & cols[b].valid & wt
+        r = spark_corr_buffer(_as_double_list(cols[a]), _as_double_list(cols[b]), sel, n_partitions)
+        return None if not r[0] > 0.0 else CorrelationState(*r)
+    raise ValueError(op)
+
+
+def metric_value(state) -> Optional[float]:
+    return None if state is None else state.metricValue()
+
+
+# --------------------------------------------------------------------------------------
+# HdfsStateProvider formats (StateProvider.scala:81-83, 176-294) and identifiers
+# --------------------------------------------------------------------------------------
+
+
+def _mix_last(h: int, k: int) -> int:
+    k = (k * 0xCC9E2D51) & 0xFFFFFFFF
+    k = ((k << 15) | (k >> 17)) & 0xFFFFFFFF
+    k = (k * 0x1B873593) & 0xFFFFFFFF
+    return h ^ k
+
+
+def _mix(h: int, k: int) -> int:
+    h = _mix_last(h, k)
+    h = ((h << 13) | (h >> 19)) & 0xFFFFFFFF
+    return (h * 5 + 0xE6546B64) & 0xFFFFFFFF
+
+
+def murmur3_string_hash(s: str, seed: int = 42) -> int:
+    """scala.util.hashing.MurmurHash3.stringHash (UTF-16 code units, pairs per mix)."""
+    units = []
+    for ch in s:
+        cp = ord(ch)
+        if cp >= 0x10000:
+            cp -= 0x10000
+            units += [0xD800 + (cp >> 10), 0xDC00 + (cp & 0x3FF)]
+        else:
+            units.append(cp)
+    h = seed & 0xFFFFFFFF
+    i = 0
+    while i + 1 < len(units):
+        h = _mix(h, ((units[i] << 16) + units[i + 1]) & 0xFFFFFFFF)
+        i += 2
+    if i < len(units):
+        h = _mix_last(h, units[i])
+    h ^= len(units)
+    h ^= h >> 16
+    h = (h * 0x85EBCA6B) & 0xFFFFFFFF
+    h ^= h >> 13
+    h = (h * 0xC2B2AE35) & 0xFFFFFFFF
+    h ^= h >> 16
+    return to_i32(h)
+
+
+def state_to_bytes(state) -> bytes:
+    """Java DataOutputStream (big-endian) images written by HdfsStateProvider.persist."""
+    if isinstance(state, NumMatches):
+        return struct.pack(">q", state.numMatches)
+    if isinstance(state, NumMatchesAndCount):
+        return struct.pack(">qq", state.numMatches, state.count)
+    if isinstance(state, SumState):
+        return struct.pack(">d", state.sum_)
+    if isinstance(state, MeanState):
+        return struct.pack(">dq", state.sum_, state.count)
+    if isinstance(state, MinState):
+        return struct.pack(">d", state.minValue)
+    if isinstance(state, MaxState):
+        return struct.pack(">d", state.maxValue)
+    if isinstance(state, StandardDeviationState):
+        return struct.pack(">ddd", state.n, state.avg, state.m2)
+    if isinstance(state, CorrelationState):
+        return struct.pack(">dddddd", state.n, state.xAvg, state.yAvg, state.ck, state.xMk, state.yMk)
+    if isinstance(state, ApproxCountDistinctState):
+        b = words_to_bytes(state.words)
+        return struct.pack(">i", len(b)) + b
+    raise TypeError(type(state))

@@ -1,0 +1,162 @@
+"""Write reference_kats.json: the reference's own hot-path fixtures and known answers.
+
+Every dataset is transcribed from the reference's test fixtures and every expected value
+from an assertion in the reference's test suite (paths relative to
+src/test/scala/com/amazon/deequ/).  This is data only: tables + expected metrics.
+`expected` is a float, "NaN", or "EmptyState" (metric fails with EmptyStateException,
+Analyzer.scala:420-431).  `needs` lists GPU-path capabilities a case depends on beyond
+numeric columns (e.g. a string predicate), so tests can route/skip with a reason.
+"""
+import json
+import os
+
+N = None
+
+datasets = {
+    "dfMissing": {  # utils/FixtureSupport.scala:45-62
+        "columns": {
+            "item": ["utf8", [str(i) for i in range(1, 13)]],
+            "att1": ["utf8", ["a", "b", N, "a", "a", N, N, "b", "a", N, N, N]],
+            "att2": ["utf8", ["f", "d", "f", N, "f", "d", "d", N, "f", N, "f", "d"]],
+        }
+    },
+    "dfFull": {  # utils/FixtureSupport.scala:64-73
+        "columns": {
+            "item": ["utf8", ["1", "2", "3", "4"]],
+            "att1": ["utf8", ["a", "a", "a", "b"]],
+            "att2": ["utf8", ["c", "c", "c", "d"]],
+        }
+    },
+    "dfWithNumericValues": {  # utils/FixtureSupport.scala:137-148 (att1, att2: Int)
+        "columns": {
+            "item": ["utf8", ["1", "2", "3", "4", "5", "6"]],
+            "att1": ["i32", [1, 2, 3, 4, 5, 6]],
+            "att2": ["i32", [0, 0, 0, 5, 6, 7]],
+        }
+    },
+    "dfWithNumericFractionalValues": {  # utils/FixtureSupport.scala:150-160
+        "columns": {
+            "item": ["utf8", ["1", "2", "3", "4", "5", "6"]],
+            "att1": ["f64", [1.0, 2.0, 3.0, 4.0, 5.0, 6.0]],
+            "att2": ["f64", [0.0, 0.0, 0.0, 5.0, 6.0, 7.0]],
+        }
+    },
+    "dfWithUniqueColumns": {  # utils/FixtureSupport.scala:162-175
+        "columns": {
+            "unique": ["utf8", ["1", "2", "3", "4", "5", "6"]],
+            "nonUnique": ["utf8", ["0", "0", "0", "5", "6", "7"]],
+            "nonUniqueWithNulls": ["utf8", ["3", "3", "3", N, N, N]],
+            "uniqueWithNulls": ["utf8", ["1", "2", N, "3", "4", "5"]],
+            "onlyUniqueWithOtherNonUnique": ["utf8", ["5", "6", "7", "0", "0", "0"]],
+            "halfUniqueCombinedWithNonUnique": ["utf8", ["0", "0", "0", "4", "5", "6"]],
+        }
+    },
+    "dfWithConditionallyUninformativeColumns": {  # utils/FixtureSupport.scala:190-197
+        "columns": {"att1": ["i32", [1, 2, 3]], "att2": ["i32", [0, 0, 0]]}
+    },
+    "dfWithConditionallyInformativeColumns": {  # utils/FixtureSupport.scala:199-206
+        "columns": {"att1": ["i32", [1, 2, 3]], "att2": ["i32", [4, 5, 6]]}
+    },
+    "dataWithNullColumns": {  # analyzers/NullHandlingTests.scala:32-50 (numSlices = 2)
+        "partitions": 2,
+        "columns": {
+            "stringCol": ["utf8", [N] * 8],
+            "numericCol": ["f64", [N] * 8],
+            "numericCol2": ["f64", [N] * 8],
+            "numericCol3": ["f64", [1.0, 2.0, 3.0, 4.0, 5.0, 6.0, 7.0, 8.0]],
+        },
+    },
+    "incrementalInitial": {  # analyzers/IncrementalAnalyzerTest.scala (initialData)
+        "columns": {
+            "item": ["utf8", ["1", "2", "3"]],
+            "att1": ["utf8", ["a", "b", N]],
+        }
+    },
+    "stateAggregation": {  # analyzers/StateAggregationIntegrationTest.scala:34-50
+        "partitions": 2,
+        "columns": {
+            "item": ["utf8", ["item1", "item1", "item1", "item2", "item2", "item3", "item4", "item5"]],
+            "origin": ["utf8", ["US", "US", "US", "DE", "DE", N, N, N]],
+            "sales": ["i32", [100, 1000, 20, 20, 333, 12, 45, 123]],
+            "marketplace": ["utf8", ["EU", "NA", "IN", "EU", "NA", "NA", "NA", "NA"]],
+        },
+    },
+}
+
+S = "analyzers/AnalyzerTests.scala"
+cases = [
+    # Size / Completeness
+    ("dfMissing", ["Size", N], 12.0, S + ":39-42", []),
+    ("dfFull", ["Size", N], 4.0, S + ":39-42", []),
+    ("dfMissing", ["Completeness", "att1", N], 0.5, S + ":52-53", []),
+    ("dfMissing", ["Completeness", "att2", N], 0.75, S + ":54-55", []),
+    ("dfMissing", ["Completeness", "att1", "item IN ('1', '2')"], 1.0, S + ":73-74", ["string_predicate"]),
+    # Compliance
+    ("dfWithNumericValues", ["Compliance", "rule1", "att1 > 3", N], 3.0 / 6, S + ":175-176", []),
+    ("dfWithNumericValues", ["Compliance", "rule2", "att1 > 2", N], 4.0 / 6, S + ":177-178", []),
+    ("dfWithNumericValues", ["Compliance", "rule1", "att2 = 0", "att1 < 4"], 1.0, S + ":184-185", []),
+    # basic statistics
+    ("dfWithNumericValues", ["Mean", "att1", N], 3.5, S + ":427-428", []),
+    ("dfWithNumericValues", ["Mean", "att1", "item != '6'"], 3.0, S + ":437-438", ["string_predicate"]),
+    ("dfWithNumericValues", ["StandardDeviation", "att1", N], 1.707825127659933, S + ":443-444", []),
+    ("dfWithNumericValues", ["Minimum", "att1", N], 1.0, S + ":453-454", []),
+    ("dfWithNumericValues", ["Maximum", "att1", N], 6.0, S + ":463-464", []),
+    ("dfWithNumericValues", ["Maximum", "att1", "item != '6'"], 5.0, S + ":470-471", ["string_predicate"]),
+    ("dfWithNumericValues", ["Sum", "att1", N], 21.0, S + ":481", []),
+    # HLL
+    ("dfWithUniqueColumns", ["ApproxCountDistinct", "uniqueWithNulls", N], 5.0, S + ":509-513", []),
+    # Correlation
+    ("dfWithConditionallyUninformativeColumns", ["Correlation", "att1", "att2", N], "NaN", S + ":604-608", []),
+    ("dfWithConditionallyInformativeColumns", ["Correlation", "att1", "att2", N], 1.0, S + ":610-617", []),
+    ("dfWithConditionallyInformativeColumns", ["Correlation", "att2", "att1", N], 1.0, S + ":619-623", []),
+    # fused runner (analyzers/AnalysisTest.scala:86-92)
+    ("dfWithNumericValues", ["ApproxCountDistinct", "att1", N], 6.0, "analyzers/AnalysisTest.scala:91-92", []),
+    # null handling (analyzers/NullHandlingTests.scala:87-118)
+    ("dataWithNullColumns", ["Size", N], 8.0, "analyzers/NullHandlingTests.scala:91", []),
+    ("dataWithNullColumns", ["Completeness", "stringCol", N], 0.0, "analyzers/NullHandlingTests.scala:92", []),
+    ("dataWithNullColumns", ["Mean", "numericCol", N], "EmptyState", "analyzers/NullHandlingTests.scala:94", []),
+    ("dataWithNullColumns", ["StandardDeviation", "numericCol", N], "EmptyState", "analyzers/NullHandlingTests.scala:96", []),
+    ("dataWithNullColumns", ["Minimum", "numericCol", N], "EmptyState", "analyzers/NullHandlingTests.scala:97", []),
+    ("dataWithNullColumns", ["Maximum", "numericCol", N], "EmptyState", "analyzers/NullHandlingTests.scala:98", []),
+    ("dataWithNullColumns", ["Sum", "numericCol", N], "EmptyState", "analyzers/NullHandlingTests.scala:103", []),
+    ("dataWithNullColumns", ["ApproxCountDistinct", "stringCol", N], 0.0, "analyzers/NullHandlingTests.scala:107", []),
+    ("dataWithNullColumns", ["Correlation", "numericCol", "numericCol2", N], "EmptyState", "analyzers/NullHandlingTests.scala:114", []),
+    ("dataWithNullColumns", ["Correlation", "numericCol", "numericCol3", N], "EmptyState", "analyzers/NullHandlingTests.scala:115", []),
+    # checks -> Compliance (checks/CheckTest.scala:156-273), metric values implied by the statuses
+    ("dfWithNumericValues", ["Compliance", "rule1", "att1 > 0", N], 1.0, "checks/CheckTest.scala:158-170", []),
+    ("dfWithNumericValues", ["Compliance", "rule1", "att1 < att2", "att1 > 3"], 1.0, "checks/CheckTest.scala:176-192", []),
+    ("dfWithNumericValues", ["Compliance", "rule2", "att2 > 0", "att1 > 0"], 0.5, "checks/CheckTest.scala:179-192", []),
+    ("dfWithNumericValues", ["Compliance", "att1 is less than att2", "att1 < att2", N], 0.5, "checks/CheckTest.scala:200-213", []),
+    ("dfWithNumericValues", ["Compliance", "nr1", "`att2` IS NULL OR (`att2` >= 0.0 AND `att2` <= 7.0)", N], 1.0, "checks/CheckTest.scala:235-267; Check.scala:867-868", []),
+    ("dfWithNumericValues", ["Compliance", "nr2", "`att2` IS NULL OR (`att2` >= 1.0 AND `att2` <= 7.0)", N], 0.5, "checks/CheckTest.scala:238-268", []),
+    ("dfWithNumericValues", ["Compliance", "nr3", "`att2` IS NULL OR (`att2` >= 0.0 AND `att2` <= 6.0)", N], 5.0 / 6, "checks/CheckTest.scala:241-269", []),
+    ("dfWithNumericValues", ["Compliance", "nr4", "`att2` IS NULL OR (`att2` > 0.0 AND `att2` < 7.0)", N], 2.0 / 6, "checks/CheckTest.scala:244-270", []),
+    ("dfWithNumericValues", ["Compliance", "nr5", "`att2` IS NULL OR (`att2` > -1.0 AND `att2` < 8.0)", N], 1.0, "checks/CheckTest.scala:247-271", []),
+    ("dfWithNumericValues", ["Compliance", "nr6", "`att2` IS NULL OR (`att2` >= 0.0 AND `att2` < 7.0)", N], 5.0 / 6, "checks/CheckTest.scala:250-272", []),
+    ("dfWithNumericValues", ["Compliance", "nr7", "`att2` IS NULL OR (`att2` >= 0.0 AND `att2` < 8.0)", N], 1.0, "checks/CheckTest.scala:253-273", []),
+    ("dfWithNumericValues", ["Compliance", "nr8", "`att2` IS NULL OR (`att2` > 0.0 AND `att2` <= 7.0)", N], 3.0 / 6, "checks/CheckTest.scala:256-274", []),
+    ("dfWithNumericValues", ["Compliance", "nr9", "`att2` IS NULL OR (`att2` > -1.0 AND `att2` <= 7.0)", N], 1.0, "checks/CheckTest.scala:259-275", []),
+    ("dfWithNumericValues", ["Compliance", "att1 is non-negative", "COALESCE(att1, 0.0) >= 0", N], 1.0, "predicate form Check.scala:676 (isNonNegative); expected value computed by hand", []),
+    ("dfWithNumericValues", ["Compliance", "att2 is positive", "COALESCE(att2, 1.0) > 0", N], 0.5, "predicate form Check.scala:687 (isPositive); expected value computed by hand", []),
+    # incremental (analyzers/IncrementalAnalyzerTest.scala:49-99)
+    ("incrementalInitial", ["Size", N], 3.0, "analyzers/IncrementalAnalyzerTest.scala:58", []),
+    ("incrementalInitial", ["Completeness", "att1", N], 0.6666666666666666, "analyzers/IncrementalAnalyzerTest.scala:96", []),
+    ("incrementalInitial", ["Compliance", "att1", "att1 = 'b'", N], 0.3333333333333333, "analyzers/IncrementalAnalyzerTest.scala:77", ["string_predicate"]),
+    # partition merge (analyzers/StateAggregationIntegrationTest.scala:56-104)
+    ("stateAggregation", ["Completeness", "origin", N], 0.625, "analyzers/StateAggregationIntegrationTest.scala:77", []),
+]
+
+out = {
+    "doc": __doc__,
+    "datasets": datasets,
+    "cases": [
+        {"dataset": d, "analyzer": a, "expected": e, "source": s, "needs": nd}
+        for (d, a, e, s, nd) in cases
+    ],
+}
+
+if __name__ == "__main__":
+    dst = os.path.join(os.path.dirname(os.path.abspath(__file__)), "reference_kats.json")
+    with open(dst, "w") as f:
+        json.dump(out, f, indent=1)
+    print(dst, len(cases))
