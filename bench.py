@@ -1,0 +1,165 @@
+"""Benchmark: fused 16-column profile scan (BASELINE.json metric).
+
+Per GPU: ROWS rows (default 1e9) x 16 columns (8 fp64 + 4 int64 + 4 UTF8, 10 % nulls, synthetic,
+generated on the device), held in HBM as CHUNK-row chunks (UTF8 int32 offsets < 2 GiB per chunk).
+One step = one fused scan of every chunk with the ColumnProfiler pass-1/2 analyzer set
+(Size, Completeness x16, ApproxCountDistinct x16, Min/Max/Mean/StdDev/Sum x12), dq_finish, and for
+N > 1 the RCCL allgather of the per-rank state blobs + fixed-order merge.  Rows shard across ranks
+(weak scaling).  Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md (HBM3E peak 8.0 TB/s)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--rows", type=int, default=1_000_000_000, help="rows per GPU")
+    p.add_argument("--chunk", type=int, default=62_500_000, help="rows per chunk")
+    p.add_argument("--cpu-sample", type=int, default=16_000_000, help="rows timed on the CPU baseline (0 = skip)")
+    p.add_argument("--cpu-threads", type=int, default=16)
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import deequ_amd as dq
+    from deequ_amd import distributed, synth
+    from deequ_amd.runner import ScanPlan
+
+    n_total = args.rows
+    chunk = min(args.chunk, n_total)
+    row0 = rank * n_total
+    chunks = []
+    r = 0
+    while r < n_total:
+        m = min(chunk, n_total - r)
+        chunks.append(synth.c5_table(m, row0=row0 + r, seed=42))
+        r += m
+    torch.cuda.synchronize()
+    analyzers = synth.profile_analyzers(chunks[0])
+    plan = ScanPlan(analyzers, chunks[0].schema)
+    str_bytes = sum(c.data_bytes for t in chunks for c in t.columns.values() if c.dtype in ("utf8", "large_utf8"))
+    algo_bytes_per_step = plan.bytes_per_row() * n_total + str_bytes  # each needed buffer once
+
+    def step():
+        plan.reset()
+        for t in chunks:
+            plan.scan(t)
+        states = plan.finish()
+        if world > 1:
+            states = distributed.allgather_combine(states)
+        return states
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    plan.enable_timing(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        states = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    col_ms, col_launches = plan.kernel_time(1)
+    fin_ms, _ = plan.kernel_time(3)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    rows_all = n_total * world * args.steps
+    value = rows_all / elapsed
+    # roofline of the dominant kernel (dq_column_scan): algorithmic bytes per launch / avg duration
+    per_launch_bytes = algo_bytes_per_step / len(chunks)
+    avg_launch_s = (col_ms / 1e3) / max(1, col_launches)
+    achieved = per_launch_bytes / avg_launch_s / 1e9
+    out = {
+        "metric": "rows/sec (whole node) for fused 16-col profile scan; % of HBM peak BW",
+        "value": value,
+        "unit": "rows/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64+int64+utf8",
+        "data": "synthetic (device-generated, seeded; SURVEY 8d C5 distributions)",
+        "config": {"workload": "C5 fused 16-col profile scan (8 f64 + 4 i64 + 4 utf8, 10% nulls)",
+                   "rows_per_gpu": n_total, "chunk_rows": chunk, "analyzers": len(analyzers),
+                   "parallelism": f"row-shard x{world}"},
+        "hbm_frac_of_step": (algo_bytes_per_step / (elapsed / args.steps)) / 1e9 / HBM_PEAK_GBS,
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "dq_column_scan", "bytes_per_launch": per_launch_bytes,
+                     "avg_launch_ms": avg_launch_s * 1e3, "launches": col_launches,
+                     "finalize_ms_per_step": fin_ms / args.steps},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        out["cpu_baseline"] = cpu_baseline(chunks[0], min(args.cpu_sample, chunks[0].num_rows), args.cpu_threads)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    plan.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(table, n, threads):
+    """The C restatement (oracle/, "port") of the same profile scan on the host cores."""
+    import numpy as np
+
+    from oracle import dq_oracle_c as C
+
+    cols = []
+    for c in table.columns.values():
+        bm = c.validity[: (n + 7) // 8 + 16].cpu().numpy() if c.validity is not None else None
+        if c.dtype in ("utf8", "large_utf8"):
+            w = 4 if c.dtype == "utf8" else 8
+            offs = c.offsets[: (n + 1) * w].cpu().numpy().view(np.int32 if w == 4 else np.int64)
+            data = c.values[: int(offs[-1]) + 16].cpu().numpy()
+            cols.append((c.dtype, data, offs, bm))
+        else:
+            w = 4 if c.dtype == "i32" else 8
+            cols.append((c.dtype, c.values[: n * w].cpu().numpy().view({"f64": np.float64, "i64": np.int64,
+                                                                       "i32": np.int32}[c.dtype]), None, bm))
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    t0 = time.perf_counter()
+    C.profile_scan(cols, n, nparts=threads * 4, nthreads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "rows/s", "cores": threads, "kind": "port",
+            "sample": f"{n} rows x 16 cols of the same C5 data, profile scan in oracle/c (Spark-order "
+                      f"Welford + XXH64 HLL), {threads} OpenMP threads, {dt:.2f} s"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,15 @@
+"""deequ_amd -- MI355X-native replacement of Deequ's fused single-pass metric scan.
+
+The hot path (AnalysisRunner.runScanningAnalyzers / ScanShareableAnalyzer aggregation) runs in
+libdqscan.so: hand-written gfx950 HIP kernels behind the C ABI in include/dqscan.h.  This package
+is the host-side mirror of the reference's analyzer / state / runner API over that ABI.
+"""
+from ._lib import DQError, lib  # noqa: F401  (fails loudly if libdqscan.so is missing)
+from .analyzers import (ApproxCountDistinct, Completeness, Compliance, Correlation, Maximum, Mean,  # noqa: F401
+                        Minimum, Size, StandardDeviation, Sum)
+from .metrics import DoubleMetric, Entity  # noqa: F401
+from .runner import AnalysisRunner, AnalyzerContext  # noqa: F401
+from .state_provider import HdfsStateProvider, InMemoryStateProvider  # noqa: F401
+from .states import (ApproxCountDistinctState, CorrelationState, MaxState, MeanState, MinState,  # noqa: F401
+                     NumMatches, NumMatchesAndCount, StandardDeviationState, SumState)
+from .table import Column, Table  # noqa: F401

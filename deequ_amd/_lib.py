@@ -1,0 +1,190 @@
+"""ctypes binding of libdqscan.so (include/dqscan.h).
+
+The HIP library is the product: there is no fallback.  If the shared library is missing this
+module raises at import time, and every scan goes through dq_plan_create / dq_scan / dq_finish.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libdqscan.so")
+
+DQ_OK = 0
+DQ_E_INVALID = -1
+DQ_E_TYPE = -2
+DQ_E_UNSUPPORTED = -3
+DQ_E_HIP = -4
+DQ_E_OOM = -5
+DQ_E_STATE = -6
+
+TYPE_F64, TYPE_I64, TYPE_I32, TYPE_UTF8, TYPE_LARGE_UTF8 = 1, 2, 3, 4, 5
+
+OP_SIZE = 1
+OP_COMPLETENESS = 2
+OP_COMPLIANCE = 3
+OP_SUM = 4
+OP_MEAN = 5
+OP_STDDEV = 6
+OP_MIN = 7
+OP_MAX = 8
+OP_CORRELATION = 9
+OP_APPROX_COUNT_DISTINCT = 10
+
+PRED_COLUMN = 1
+PRED_LIT_INT = 2
+PRED_LIT_DECIMAL = 3
+PRED_LIT_DOUBLE = 4
+PRED_LIT_NULL = 5
+PRED_LIT_BOOL = 6
+PRED_CMP = 7
+PRED_AND = 8
+PRED_OR = 9
+PRED_NOT = 10
+PRED_IS_NULL = 11
+PRED_IS_NOT_NULL = 12
+PRED_COALESCE = 13
+
+CMP_LT, CMP_LE, CMP_GT, CMP_GE, CMP_EQ, CMP_NE = 1, 2, 3, 4, 5, 6
+
+
+class ColumnDesc(ctypes.Structure):
+    _fields_ = [("type", ctypes.c_int32), ("nullable", ctypes.c_int32)]
+
+
+class AnalyzerSpec(ctypes.Structure):
+    _fields_ = [("op", ctypes.c_int32), ("col_a", ctypes.c_int32), ("col_b", ctypes.c_int32),
+                ("pred_root", ctypes.c_int32), ("where_root", ctypes.c_int32)]
+
+
+class PredNode(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("a", ctypes.c_int32), ("b", ctypes.c_int32),
+                ("cmp", ctypes.c_int32), ("i64", ctypes.c_int64), ("f64", ctypes.c_double)]
+
+
+class ColumnView(ctypes.Structure):
+    _fields_ = [("values", ctypes.c_void_p), ("validity", ctypes.c_void_p), ("offsets", ctypes.c_void_p),
+                ("reserved", ctypes.c_int64)]
+
+
+class _Size(ctypes.Structure):
+    _fields_ = [("num_matches", ctypes.c_int64)]
+
+
+class _Ratio(ctypes.Structure):
+    _fields_ = [("num_matches", ctypes.c_int64), ("count", ctypes.c_int64)]
+
+
+class _Sum(ctypes.Structure):
+    _fields_ = [("sum", ctypes.c_double)]
+
+
+class _Mean(ctypes.Structure):
+    _fields_ = [("sum", ctypes.c_double), ("count", ctypes.c_int64)]
+
+
+class _StdDev(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_double), ("avg", ctypes.c_double), ("m2", ctypes.c_double)]
+
+
+class _MinMax(ctypes.Structure):
+    _fields_ = [("value", ctypes.c_double)]
+
+
+class _Corr(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_double), ("x_avg", ctypes.c_double), ("y_avg", ctypes.c_double),
+                ("ck", ctypes.c_double), ("x_mk", ctypes.c_double), ("y_mk", ctypes.c_double)]
+
+
+class _Hll(ctypes.Structure):
+    _fields_ = [("words", ctypes.c_int64 * 52)]
+
+
+class _StateUnion(ctypes.Union):
+    _fields_ = [("size", _Size), ("ratio", _Ratio), ("sum", _Sum), ("mean", _Mean), ("stddev", _StdDev),
+                ("minmax", _MinMax), ("corr", _Corr), ("hll", _Hll)]
+
+
+class State(ctypes.Structure):
+    _fields_ = [("op", ctypes.c_int32), ("has_value", ctypes.c_uint8 * 2), ("reserved", ctypes.c_uint8 * 2),
+                ("u", _StateUnion)]
+
+
+STATE_SIZE = ctypes.sizeof(State)
+
+
+class DQError(RuntimeError):
+    def __init__(self, status: int, message: str):
+        super().__init__(f"dqscan error {status}: {message}")
+        self.status = status
+        self.message = message
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `make -C deequ_amd` or __graft_entry__.build(); "
+            "the MI355X scan has no CPU fallback")
+    L = ctypes.CDLL(LIB_PATH)
+    c = ctypes
+    P = c.POINTER
+    L.dq_abi_version.restype = c.c_int32
+    L.dq_last_error.restype = c.c_char_p
+    L.dq_plan_create.restype = c.c_int32
+    L.dq_plan_create.argtypes = [P(AnalyzerSpec), c.c_int32, P(ColumnDesc), c.c_int32, P(PredNode), c.c_int32,
+                                 c.c_int32, P(c.c_void_p)]
+    L.dq_plan_set_stream.restype = c.c_int32
+    L.dq_plan_set_stream.argtypes = [c.c_void_p, c.c_void_p]
+    L.dq_scan.restype = c.c_int32
+    L.dq_scan.argtypes = [c.c_void_p, P(ColumnView), c.c_int64, c.c_int64]
+    L.dq_finish.restype = c.c_int32
+    L.dq_finish.argtypes = [c.c_void_p, P(State)]
+    L.dq_plan_reset.restype = c.c_int32
+    L.dq_plan_reset.argtypes = [c.c_void_p]
+    L.dq_plan_destroy.restype = None
+    L.dq_plan_destroy.argtypes = [c.c_void_p]
+    L.dq_plan_bytes_per_row_x1000.restype = c.c_int64
+    L.dq_plan_bytes_per_row_x1000.argtypes = [c.c_void_p]
+    L.dq_plan_num_launches.restype = c.c_int32
+    L.dq_plan_num_launches.argtypes = [c.c_void_p]
+    L.dq_plan_enable_timing.restype = c.c_int32
+    L.dq_plan_enable_timing.argtypes = [c.c_void_p, c.c_int32]
+    L.dq_plan_kernel_time.restype = c.c_int32
+    L.dq_plan_kernel_time.argtypes = [c.c_void_p, c.c_int32, P(c.c_double), P(c.c_int64)]
+    L.dq_state_merge.restype = c.c_int32
+    L.dq_state_merge.argtypes = [P(State), P(State), P(State)]
+    L.dq_state_combine.restype = c.c_int32
+    L.dq_state_combine.argtypes = [P(State), P(State), P(State)]
+    L.dq_state_is_defined.restype = c.c_int32
+    L.dq_state_is_defined.argtypes = [P(State)]
+    L.dq_state_metric.restype = c.c_int32
+    L.dq_state_metric.argtypes = [P(State), P(c.c_double)]
+    L.dq_hll_estimate.restype = c.c_int32
+    L.dq_hll_estimate.argtypes = [P(c.c_int64), P(c.c_double)]
+    L.dq_state_to_bytes.restype = c.c_int64
+    L.dq_state_to_bytes.argtypes = [P(State), c.c_void_p, c.c_int64]
+    L.dq_state_from_bytes.restype = c.c_int32
+    L.dq_state_from_bytes.argtypes = [c.c_int32, c.c_char_p, c.c_int64, P(State)]
+    L.dq_state_identifier.restype = c.c_int32
+    L.dq_state_identifier.argtypes = [c.c_char_p]
+    if L.dq_abi_version() != 1:
+        raise ImportError(f"libdqscan ABI {L.dq_abi_version()} != 1")
+    return L
+
+
+lib = _load()
+
+# every symbol include/dqscan.h declares (checked by tests/test_boundary.py)
+EXPORTED = [
+    "dq_abi_version", "dq_last_error", "dq_plan_create", "dq_plan_set_stream", "dq_scan", "dq_finish",
+    "dq_plan_reset", "dq_plan_destroy", "dq_plan_bytes_per_row_x1000", "dq_plan_num_launches",
+    "dq_plan_enable_timing", "dq_plan_kernel_time",
+    "dq_state_merge", "dq_state_combine", "dq_state_is_defined", "dq_state_metric", "dq_hll_estimate",
+    "dq_state_to_bytes", "dq_state_from_bytes", "dq_state_identifier",
+]
+
+
+def check(status: int) -> None:
+    if status != DQ_OK:
+        raise DQError(status, lib.dq_last_error().decode("utf-8", "replace"))

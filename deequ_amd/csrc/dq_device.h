@@ -1,0 +1,133 @@
+// dq_device.h -- POD structures shared by the planner (host) and the gfx950 kernels.
+//
+// HBM layout of one plan (all device-resident, allocated once at dq_plan_create):
+//   ColTask[ncol_tasks], PairTask[npair_tasks], PredProgram        (static task tables)
+//   ColPartial[ncol_tasks][kMaxWG]     per-workgroup partial states of the current scan
+//   uint8 hll[nhll][kMaxWG][512]       per-workgroup HLL registers (one byte per register)
+//   CorrPartial[npair][kMaxWG], PredPartial[kMaxWG]
+//   ColPartial / hll[512] / CorrPartial / PredPartial accumulators (merged over chunks, in order)
+//   where bitmaps: uint64[n_rows/64] TRUE bits per `where` root used by column / pair tasks
+#pragma once
+
+#include <cstdint>
+
+namespace dq {
+
+constexpr int kBlock = 256;                 // threads per workgroup (4 waves of 64)
+constexpr int kWaves = kBlock / 64;
+constexpr int kRowsPerLane = 8;
+constexpr int kRowsPerIter = kBlock * kRowsPerLane;  // 2048 rows per workgroup iteration
+constexpr int kMaxWG = 2048;                // max row ranges (workgroups) per task per scan
+constexpr int kMaxCols = 64;
+constexpr int kMaxWhere = 8;
+constexpr int kMaxRoots = 32;
+constexpr int kMaxCounters = 16;
+constexpr int kMaxInstr = 96;
+constexpr int kPredRowsPerIter = kBlock;    // predicate pass: one row per lane per iteration
+
+// column kinds seen by the kernels
+enum ColKind : int32_t { CK_F64 = 1, CK_I64 = 2, CK_I32 = 3, CK_UTF8 = 4, CK_LUTF8 = 5 };
+
+// column-pass variants (kind x what is accumulated); VALIDITY = count of selected rows only
+enum ColVariant : int32_t {
+  CV_VALIDITY = 0,
+  CV_F64_S = 1, CV_F64_SH = 2, CV_F64_H = 3,
+  CV_I64_S = 4, CV_I64_SH = 5, CV_I64_H = 6,
+  CV_I32_S = 7, CV_I32_SH = 8, CV_I32_H = 9,
+  CV_UTF8_H = 10, CV_LUTF8_H = 11,
+};
+
+struct ColTask {
+  int32_t variant;   // ColVariant
+  int32_t col;       // column index
+  int32_t where;     // where-bitmap index or -1
+  int32_t hll_slot;  // index into HLL partial / accumulator arrays, -1 if none
+};
+
+struct PairTask {
+  int32_t col_x, col_y;
+  int32_t kind_x, kind_y;
+  int32_t where;
+  int32_t pad[3];
+};
+
+// Per-workgroup partial of one column task.  Moments are Chan-mergeable (n, mean, m2).
+struct alignas(16) ColPartial {
+  double n, mean, m2;   // over selected rows, values converted to double
+  double sum;           // fp64 sum of selected values (F64 columns)
+  int64_t isum;         // wrapping int64 sum (I64 / I32 columns)
+  int64_t count;        // selected rows (non-null AND where-true)
+  int64_t nan_count;    // selected NaN values (F64)
+  double fmin, fmax;    // min / max over selected non-NaN values (F64)
+  int64_t imin, imax;   // min / max (I64 / I32)
+  int64_t pad;
+};
+static_assert(sizeof(ColPartial) == 96, "ColPartial layout");
+
+struct alignas(16) CorrPartial {
+  double n, xa, ya, ck, xm, ym, pad0, pad1;
+};
+static_assert(sizeof(CorrPartial) == 64, "CorrPartial layout");
+
+struct alignas(16) PredPartial {
+  int64_t t[kMaxCounters];   // sum over rows of (pred TRUE  AND where TRUE)
+  int64_t nn[kMaxCounters];  // sum over rows of (pred NOT NULL AND where TRUE)
+};
+
+// Predicate program: postfix over three-valued atoms.
+enum PredOp : int32_t {
+  PO_ATOM_CMP = 1,     // col_a CMP (col_b | literal)
+  PO_ATOM_ISNULL = 2,  // col_a IS NULL
+  PO_ATOM_NOTNULL = 3, // col_a IS NOT NULL
+  PO_CONST = 4,        // push constant (null_res: 0 FALSE, 1 TRUE, 2 NULL)
+  PO_AND = 5,
+  PO_OR = 6,
+  PO_NOT = 7,
+  PO_STORE = 8,        // pop into root slot `slot`
+};
+enum CmpOp : int32_t { C_LT = 1, C_LE = 2, C_GT = 3, C_GE = 4, C_EQ = 5, C_NE = 6, C_FALSE = 7, C_TRUE = 8 };
+enum CmpType : int32_t { CT_INT = 1, CT_DBL = 2 };
+enum NullRes : int32_t { NR_FALSE = 0, NR_TRUE = 1, NR_NULL = 2 };
+
+struct PredInstr {
+  int32_t op;
+  int32_t cmp;
+  int32_t ctype;
+  int32_t null_res;   // ATOM_CMP: result when col_a is NULL (COALESCE fallback), else NR_NULL
+  int32_t col_a;
+  int32_t col_b;      // -1: compare against the literal
+  int32_t kind_a;
+  int32_t kind_b;
+  int64_t lit_i;
+  double lit_d;
+  int32_t slot;
+  int32_t pad;
+};
+
+struct PredCounter {
+  int32_t pred;   // root slot
+  int32_t where;  // root slot or -1
+};
+
+struct PredProgram {
+  int32_t n_instr;
+  int32_t n_counters;
+  int32_t n_bitmaps;
+  int32_t pad;
+  int32_t bitmap_root[kMaxWhere];  // root slot whose TRUE bits fill where-bitmap i
+  PredCounter counters[kMaxCounters];
+  PredInstr instr[kMaxInstr];
+};
+
+// Per-scan column pointers, passed by value as a kernel argument (copied at launch).
+struct ScanCols {
+  const void* values[kMaxCols];
+  const uint32_t* validity[kMaxCols];
+  const void* offsets[kMaxCols];
+};
+
+struct ScanBitmaps {
+  uint64_t* where_bits[kMaxWhere];
+};
+
+}  // namespace dq

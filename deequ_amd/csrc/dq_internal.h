@@ -1,0 +1,35 @@
+// dq_internal.h -- host-side internals shared by the C ABI translation units.
+#pragma once
+
+#include <cstdarg>
+#include <cstdint>
+
+#include "../../include/dqscan.h"
+
+namespace dq {
+
+// HLL++ geometry (StatefulHyperloglogPlus.scala:154-161, HLLConstants.scala:27-35)
+constexpr int kHllP = 9;
+constexpr int kHllM = 1 << kHllP;       // 512 registers
+constexpr int kHllRegisterBits = 6;
+constexpr int kHllRegsPerWord = 10;     // 64 / 6
+constexpr int kHllWords = 52;
+constexpr int kHllK = 6;
+
+// Thread-local last error; returns `code` for `return set_error(...)` chaining.
+dq_status set_error(dq_status code, const char* fmt, ...);
+
+double java_min(double a, double b);
+double java_max(double a, double b);
+int64_t java_math_round(double a);
+void hll_registers_to_words(const uint8_t* regs512, int64_t* words52);
+double hll_count(const int64_t* words52);
+int32_t state_is_defined(const dq_state& s);
+dq_status state_merge(const dq_state& a, const dq_state& b, dq_state& o);
+dq_status state_combine(const dq_state& a, const dq_state& b, dq_state& o);
+dq_status state_metric(const dq_state& s, double& out);
+int64_t state_to_bytes(const dq_state& s, uint8_t* buf, int64_t cap);
+dq_status state_from_bytes(int32_t op, const uint8_t* buf, int64_t len, dq_state& o);
+int32_t murmur3_string_hash_utf8(const char* s, uint32_t seed);
+
+}  // namespace dq

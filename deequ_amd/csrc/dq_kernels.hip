@@ -1,0 +1,804 @@
+// dq_kernels.hip -- gfx950 (MI355X, CDNA4) kernels of the fused Deequ metric scan.
+//
+// The reference computes these aggregates with one Spark job (AnalysisRunner.scala:303): a
+// per-partition partial aggregate followed by a final merge.  Here one scan of a row chunk is:
+//   1. dq_pred_scan   (only if predicates exist): three-valued predicate program per row ->
+//                     Compliance / conditional-count counters, and `where` TRUE bitmaps.
+//   2. dq_column_scan: ONE launch for every single-column task (Completeness, Sum, Mean,
+//                     StandardDeviation, Minimum, Maximum, ApproxCountDistinct).  Workgroups are
+//                     interleaved task-fastest (blockIdx % ntasks) so HBM-bound and VALU-bound
+//                     (XXH64) column tasks run side by side on all 256 CUs.
+//   3. dq_pair_scan   (only if Correlations exist): co-moments per column pair.
+//   4. dq_finalize:   fixed-order merge of the per-workgroup partials, then in-order merge into
+//                     the plan's accumulators (chunk order) -> results are deterministic.
+// Streaming loads are 16 B per lane (global_load_dwordx4) for 8-/4-byte columns; there are no
+// global atomics; HLL registers are privatised per workgroup in LDS (ds_max_u32).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <type_traits>
+
+#include "dq_device.h"
+
+namespace dq {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// ------------------------------------------------------------------------------------------
+// XXH64 (Spark XxHash64Function, seed 42) -- StatefulHyperloglogPlus.scala:93
+// ------------------------------------------------------------------------------------------
+constexpr uint64_t XP1 = 0x9E3779B185EBCA87ull;
+constexpr uint64_t XP2 = 0xC2B2AE3D27D4EB4Full;
+constexpr uint64_t XP3 = 0x165667B19E3779F9ull;
+constexpr uint64_t XP4 = 0x85EBCA77C2B2AE63ull;
+constexpr uint64_t XP5 = 0x27D4EB2F165667C5ull;
+constexpr uint64_t kSeed = 42;
+
+__device__ __forceinline__ uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+__device__ __forceinline__ uint64_t fmix64(uint64_t h) {
+  h ^= h >> 33; h *= XP2; h ^= h >> 29; h *= XP3; h ^= h >> 32; return h;
+}
+__device__ __forceinline__ uint64_t xxh64_long(uint64_t v) {
+  uint64_t h = kSeed + XP5 + 8;
+  h ^= rotl64(v * XP2, 31) * XP1;
+  h = rotl64(h, 27) * XP1 + XP4;
+  return fmix64(h);
+}
+__device__ __forceinline__ uint64_t xxh64_int(uint32_t v) {
+  uint64_t h = kSeed + XP5 + 4;
+  h ^= (uint64_t)v * XP1;
+  h = rotl64(h, 23) * XP2 + XP3;
+  return fmix64(h);
+}
+
+// Byte reads from a 4-byte aligned buffer at an arbitrary byte position, via aligned dwords.
+__device__ __forceinline__ uint32_t ld32(const uint8_t* base, int64_t a) {
+  return *reinterpret_cast<const uint32_t*>(base + a);
+}
+__device__ __forceinline__ uint32_t read4(const uint8_t* base, int64_t pos) {
+  int64_t a = pos & ~int64_t(3);
+  uint32_t sh = (uint32_t)(pos & 3) * 8u;
+  uint32_t w0 = ld32(base, a);
+  if (sh == 0) return w0;
+  uint32_t w1 = ld32(base, a + 4);
+  return __builtin_amdgcn_alignbit(w1, w0, sh);
+}
+__device__ __forceinline__ uint64_t read8(const uint8_t* base, int64_t pos) {
+  int64_t a = pos & ~int64_t(3);
+  uint32_t sh = (uint32_t)(pos & 3) * 8u;
+  uint32_t w0 = ld32(base, a), w1 = ld32(base, a + 4);
+  if (sh == 0) return ((uint64_t)w1 << 32) | w0;
+  uint32_t w2 = ld32(base, a + 8);
+  uint32_t lo = __builtin_amdgcn_alignbit(w1, w0, sh);
+  uint32_t hi = __builtin_amdgcn_alignbit(w2, w1, sh);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// XXH64.hashUnsafeBytes over data[pos, pos + n)
+__device__ uint64_t xxh64_bytes(const uint8_t* data, int64_t pos, int64_t n) {
+  int64_t off = pos, end = pos + n;
+  uint64_t h;
+  if (n >= 32) {
+    uint64_t v1 = kSeed + XP1 + XP2, v2 = kSeed + XP2, v3 = kSeed, v4 = kSeed - XP1;
+    for (; off <= end - 32; off += 32) {
+      v1 = rotl64(v1 + read8(data, off) * XP2, 31) * XP1;
+      v2 = rotl64(v2 + read8(data, off + 8) * XP2, 31) * XP1;
+      v3 = rotl64(v3 + read8(data, off + 16) * XP2, 31) * XP1;
+      v4 = rotl64(v4 + read8(data, off + 24) * XP2, 31) * XP1;
+    }
+    h = rotl64(v1, 1) + rotl64(v2, 7) + rotl64(v3, 12) + rotl64(v4, 18);
+    h ^= rotl64(v1 * XP2, 31) * XP1; h = h * XP1 + XP4;
+    h ^= rotl64(v2 * XP2, 31) * XP1; h = h * XP1 + XP4;
+    h ^= rotl64(v3 * XP2, 31) * XP1; h = h * XP1 + XP4;
+    h ^= rotl64(v4 * XP2, 31) * XP1; h = h * XP1 + XP4;
+  } else {
+    h = kSeed + XP5;
+  }
+  h += (uint64_t)n;
+  for (; off <= end - 8; off += 8) {
+    h ^= rotl64(read8(data, off) * XP2, 31) * XP1;
+    h = rotl64(h, 27) * XP1 + XP4;
+  }
+  if (off + 4 <= end) {
+    h ^= (uint64_t)read4(data, off) * XP1;
+    h = rotl64(h, 23) * XP2 + XP3;
+    off += 4;
+  }
+  for (; off < end; ++off) {
+    h ^= (uint64_t)(read4(data, off) & 0xFFu) * XP5;
+    h = rotl64(h, 11) * XP1;
+  }
+  return fmix64(h);
+}
+
+// HLL++ update (StatefulHyperloglogPlus.scala:96-113) on LDS registers (one u32 per register).
+__device__ __forceinline__ void hll_update(uint32_t* regs, uint64_t x) {
+  uint32_t idx = (uint32_t)(x >> 55);
+  uint64_t w = (x << 9) | 256ull;
+  uint32_t pw = (uint32_t)__clzll((long long)w) + 1u;
+  atomicMax(&regs[idx], pw);
+}
+
+__device__ __forceinline__ uint64_t f64_hash_bits(double d) {
+  // doubleToLongBits: canonical NaN
+  return d != d ? 0x7FF8000000000000ull : (uint64_t)__double_as_longlong(d);
+}
+
+// ------------------------------------------------------------------------------------------
+// Chan-mergeable column statistics
+// ------------------------------------------------------------------------------------------
+struct ColStats {
+  double n, mean, m2, sum;
+  int64_t isum, count, nan_count;
+  double fmin, fmax;
+  int64_t imin, imax;
+};
+
+__device__ __forceinline__ void stats_init(ColStats& s) {
+  s.n = 0.0; s.mean = 0.0; s.m2 = 0.0; s.sum = 0.0;
+  s.isum = 0; s.count = 0; s.nan_count = 0;
+  s.fmin = __longlong_as_double(0x7FF0000000000000ll);   // +inf
+  s.fmax = __longlong_as_double((long long)0xFFF0000000000000ull);  // -inf
+  s.imin = INT64_MAX; s.imax = INT64_MIN;
+}
+
+// a <- a (+) b ; exact Chan/Welford combination (same algebra as StandardDeviationState.sum)
+__device__ __forceinline__ void stats_merge(ColStats& a, const ColStats& b) {
+  double n = a.n + b.n;
+  if (b.n != 0.0) {
+    if (a.n == 0.0) {
+      a.mean = b.mean; a.m2 = b.m2;
+    } else {
+      double delta = b.mean - a.mean;
+      double r = b.n / n;
+      a.mean = a.mean + delta * r;
+      a.m2 = a.m2 + b.m2 + delta * delta * a.n * r;
+    }
+  }
+  a.n = n;
+  a.sum += b.sum;
+  a.isum = (int64_t)((uint64_t)a.isum + (uint64_t)b.isum);
+  a.count += b.count;
+  a.nan_count += b.nan_count;
+  a.fmin = fmin(a.fmin, b.fmin);
+  a.fmax = fmax(a.fmax, b.fmax);
+  a.imin = b.imin < a.imin ? b.imin : a.imin;
+  a.imax = b.imax > a.imax ? b.imax : a.imax;
+}
+
+__device__ __forceinline__ ColStats stats_shfl_xor(const ColStats& s, int m) {
+  ColStats o;
+  o.n = __shfl_xor(s.n, m); o.mean = __shfl_xor(s.mean, m); o.m2 = __shfl_xor(s.m2, m);
+  o.sum = __shfl_xor(s.sum, m);
+  o.isum = __shfl_xor(s.isum, m); o.count = __shfl_xor(s.count, m); o.nan_count = __shfl_xor(s.nan_count, m);
+  o.fmin = __shfl_xor(s.fmin, m); o.fmax = __shfl_xor(s.fmax, m);
+  o.imin = __shfl_xor(s.imin, m); o.imax = __shfl_xor(s.imax, m);
+  return o;
+}
+
+__device__ __forceinline__ void stats_store(ColPartial* p, const ColStats& s) {
+  p->n = s.n; p->mean = s.mean; p->m2 = s.m2; p->sum = s.sum; p->isum = s.isum; p->count = s.count;
+  p->nan_count = s.nan_count; p->fmin = s.fmin; p->fmax = s.fmax; p->imin = s.imin; p->imax = s.imax;
+  p->pad = 0;
+}
+__device__ __forceinline__ ColStats stats_load(const ColPartial* p) {
+  ColStats s;
+  s.n = p->n; s.mean = p->mean; s.m2 = p->m2; s.sum = p->sum; s.isum = p->isum; s.count = p->count;
+  s.nan_count = p->nan_count; s.fmin = p->fmin; s.fmax = p->fmax; s.imin = p->imin; s.imax = p->imax;
+  return s;
+}
+
+// Fold up to 8 values (bit j of `bits` = row j selected) into the running statistics:
+// per-chunk shifted sums around the running mean, one division per chunk.
+template <int KIND>
+__device__ __forceinline__ void stats_chunk(ColStats& s, const double (&x)[8], const int64_t (&xi)[8], uint32_t bits) {
+  int k = __popc(bits);
+  if (k == 0) return;
+  double shift = s.mean;
+  if (s.n == 0.0) {
+#pragma unroll
+    for (int j = 7; j >= 0; --j) shift = ((bits >> j) & 1u) ? x[j] : shift;
+  }
+  double sd = 0.0, sdd = 0.0, sm = 0.0;
+  double lo = s.fmin, hi = s.fmax;
+  int64_t is = 0, imn = s.imin, imx = s.imax;
+  int nn = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    bool b = (bits >> j) & 1u;
+    double d = b ? x[j] - shift : 0.0;
+    sd += d;
+    sdd = __builtin_fma(d, d, sdd);
+    if (KIND == CK_F64) {
+      sm += b ? x[j] : 0.0;
+      bool isn = b && (x[j] != x[j]);
+      nn += isn ? 1 : 0;
+      lo = (b && !isn) ? fmin(lo, x[j]) : lo;
+      hi = (b && !isn) ? fmax(hi, x[j]) : hi;
+    } else {
+      is += b ? xi[j] : 0;
+      imn = (b && xi[j] < imn) ? xi[j] : imn;
+      imx = (b && xi[j] > imx) ? xi[j] : imx;
+    }
+  }
+  double n2 = s.n + (double)k;
+  double q = sd / n2;
+  s.mean = shift + q;
+  s.m2 = s.m2 + (sdd - sd * q);
+  s.n = n2;
+  s.count += k;
+  if (KIND == CK_F64) {
+    s.sum += sm; s.nan_count += nn; s.fmin = lo; s.fmax = hi;
+  } else {
+    s.isum = (int64_t)((uint64_t)s.isum + (uint64_t)is); s.imin = imn; s.imax = imx;
+  }
+}
+
+template <int KIND>
+__device__ __forceinline__ void hash_chunk(uint32_t* regs, const double (&x)[8], const int64_t (&xi)[8], uint32_t bits) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    uint64_t h;
+    if (KIND == CK_F64) h = xxh64_long(f64_hash_bits(x[j]));
+    else if (KIND == CK_I64) h = xxh64_long((uint64_t)xi[j]);
+    else h = xxh64_int((uint32_t)xi[j]);
+    if ((bits >> j) & 1u) hll_update(regs, h);
+  }
+}
+
+// Reduce the 256 threads' statistics -> one ColPartial (fixed order: lanes by butterfly, waves 0..3).
+__device__ void block_reduce_store(ColStats s, ColPartial* out, ColStats* lds) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    ColStats o = stats_shfl_xor(s, m);
+    stats_merge(s, o);
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) lds[wave] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    ColStats a = lds[0];
+#pragma unroll
+    for (int w = 1; w < kWaves; ++w) stats_merge(a, lds[w]);
+    stats_store(out, a);
+  }
+}
+
+__device__ __forceinline__ uint32_t word_or_ones(const uint32_t* p, int64_t i) { return p ? p[i] : 0xFFFFFFFFu; }
+
+// 8-/4-byte numeric column: 16-byte loads, lane l of wave w holds rows
+//   base + k*64*R + l*R + [0, R)  (R = 16 / sizeof(T) rows per load, 8 / R loads)
+template <int KIND, bool STATS, bool HLL>
+__device__ void numeric_range(const void* values, const uint32_t* validity, const uint32_t* mask,
+                              int64_t row0, int64_t row1, ColStats& s, uint32_t* regs) {
+  using T = typename std::conditional<KIND == CK_I32, int32_t, typename std::conditional<KIND == CK_I64, int64_t, double>::type>::type;
+  constexpr int R = 16 / sizeof(T);
+  constexpr int L = 8 / R;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const T* v = reinterpret_cast<const T*>(values);
+  for (int64_t blk = row0; blk < row1; blk += kRowsPerIter) {
+    const int64_t base = blk + (int64_t)wave * 512;
+    double x[8];
+    int64_t xi[8];
+    uint32_t bits = 0;
+    if (blk + kRowsPerIter <= row1) {
+      // fast path: whole 2048-row block in range
+      u32x4 raw[L];
+#pragma unroll
+      for (int k = 0; k < L; ++k)
+        raw[k] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(v + base + (int64_t)k * 64 * R) + lane);
+#pragma unroll
+      for (int k = 0; k < L; ++k) {
+        const int64_t widx = (base + (int64_t)k * 64 * R) / 32 + (lane * R) / 32;
+        uint32_t w = word_or_ones(validity, widx);
+        if (mask) w &= mask[widx];
+        uint32_t b = (w >> ((lane * R) & 31)) & ((1u << R) - 1u);
+        bits |= b << (k * R);
+        const T* e = reinterpret_cast<const T*>(&raw[k]);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          if (KIND == CK_F64) { x[k * R + r] = (double)e[r]; xi[k * R + r] = 0; }
+          else { xi[k * R + r] = (int64_t)e[r]; x[k * R + r] = (double)xi[k * R + r]; }
+        }
+      }
+    } else {
+      // tail: same row mapping, guarded scalar loads
+#pragma unroll
+      for (int k = 0; k < L; ++k) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int64_t row = base + (int64_t)k * 64 * R + (int64_t)lane * R + r;
+          const int j = k * R + r;
+          if (row < row1) {
+            uint32_t w = word_or_ones(validity, row >> 5);
+            if (mask) w &= mask[row >> 5];
+            bits |= ((w >> (row & 31)) & 1u) << j;
+            T e = v[row];
+            if (KIND == CK_F64) { x[j] = (double)e; xi[j] = 0; }
+            else { xi[j] = (int64_t)e; x[j] = (double)xi[j]; }
+          } else {
+            x[j] = 0.0; xi[j] = 0;
+          }
+        }
+      }
+    }
+    if (STATS) stats_chunk<KIND>(s, x, xi, bits);
+    else s.count += __popc(bits);
+    if (HLL) hash_chunk<KIND>(regs, x, xi, bits);
+  }
+}
+
+// UTF8 column: one row per lane per step (rows base + 64*j + lane), offsets int32 or int64.
+template <typename OffT>
+__device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint32_t* validity,
+                           const uint32_t* mask, int64_t row0, int64_t row1, ColStats& s, uint32_t* regs) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int64_t blk = row0; blk < row1; blk += kRowsPerIter) {
+    const int64_t base = blk + (int64_t)wave * 512;
+#pragma unroll 2
+    for (int j = 0; j < 8; ++j) {
+      const int64_t row = base + j * 64 + lane;
+      bool b = false;
+      if (row < row1) {
+        uint32_t w = word_or_ones(validity, row >> 5);
+        if (mask) w &= mask[row >> 5];
+        b = (w >> (row & 31)) & 1u;
+      }
+      s.count += b ? 1 : 0;
+      if (b) {
+        const int64_t o0 = (int64_t)offsets[row], o1 = (int64_t)offsets[row + 1];
+        hll_update(regs, xxh64_bytes(data, o0, o1 - o0));
+      }
+    }
+  }
+}
+
+// Only the count of selected rows (Completeness): popcount of validity (& where) words.
+__device__ void validity_range(const uint32_t* validity, const uint32_t* mask, int64_t row0, int64_t row1, ColStats& s) {
+  // row0 is a multiple of 2048 -> word aligned; each thread handles whole 32-row words
+  const int64_t w0 = row0 >> 5, w1 = (row1 + 31) >> 5;
+  int64_t c = 0;
+  for (int64_t w = w0 + threadIdx.x; w < w1; w += kBlock) {
+    uint32_t bits = word_or_ones(validity, w);
+    if (mask) bits &= mask[w];
+    const int64_t r = w << 5;
+    if (r + 32 > row1) bits &= (1u << (row1 - r)) - 1u;
+    c += __popc(bits);
+  }
+  s.count += c;
+}
+
+template <int KIND, bool STATS, bool HLL>
+__device__ void run_numeric(const ColTask& t, const ScanCols& cols, const ScanBitmaps& bm, int64_t row0, int64_t row1,
+                            ColStats& s, uint32_t* regs) {
+  const uint32_t* mask = t.where >= 0 ? reinterpret_cast<const uint32_t*>(bm.where_bits[t.where]) : nullptr;
+  numeric_range<KIND, STATS, HLL>(cols.values[t.col], cols.validity[t.col], mask, row0, row1, s, regs);
+}
+
+// ------------------------------------------------------------------------------------------
+// Kernel 2: all single-column tasks of one chunk in one launch.
+// grid = ntasks * nranges; workgroup b -> task b % ntasks, row range b / ntasks.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void dq_column_scan(const ColTask* __restrict__ tasks, int32_t ntasks,
+                                                         ScanCols cols, ScanBitmaps bm, int64_t n_rows,
+                                                         int64_t rows_per_range, ColPartial* __restrict__ partials,
+                                                         uint8_t* __restrict__ hll_partials) {
+  __shared__ uint32_t regs[512];
+  __shared__ ColStats red[kWaves];
+  const int32_t ti = blockIdx.x % ntasks;
+  const int32_t range = blockIdx.x / ntasks;
+  const ColTask t = tasks[ti];
+  const int64_t row0 = (int64_t)range * rows_per_range;
+  int64_t row1 = row0 + rows_per_range;
+  if (row1 > n_rows) row1 = n_rows;
+  const bool hll = t.hll_slot >= 0;
+  if (hll) {
+    for (int i = threadIdx.x; i < 512; i += kBlock) regs[i] = 0;
+    __syncthreads();
+  }
+  ColStats s;
+  stats_init(s);
+  const uint32_t* mask = t.where >= 0 ? reinterpret_cast<const uint32_t*>(bm.where_bits[t.where]) : nullptr;
+  switch (t.variant) {
+    case CV_VALIDITY: validity_range(cols.validity[t.col], mask, row0, row1, s); break;
+    case CV_F64_S: run_numeric<CK_F64, true, false>(t, cols, bm, row0, row1, s, regs); break;
+    case CV_F64_SH: run_numeric<CK_F64, true, true>(t, cols, bm, row0, row1, s, regs); break;
+    case CV_F64_H: run_numeric<CK_F64, false, true>(t, cols, bm, row0, row1, s, regs); break;
+    case CV_I64_S: run_numeric<CK_I64, true, false>(t, cols, bm, row0, row1, s, regs); break;
+    case CV_I64_SH: run_numeric<CK_I64, true, true>(t, cols, bm, row0, row1, s, regs); break;
+    case CV_I64_H: run_numeric<CK_I64, false, true>(t, cols, bm, row0, row1, s, regs); break;
+    case CV_I32_S: run_numeric<CK_I32, true, false>(t, cols, bm, row0, row1, s, regs); break;
+    case CV_I32_SH: run_numeric<CK_I32, true, true>(t, cols, bm, row0, row1, s, regs); break;
+    case CV_I32_H: run_numeric<CK_I32, false, true>(t, cols, bm, row0, row1, s, regs); break;
+    case CV_UTF8_H:
+      utf8_range<int32_t>(reinterpret_cast<const uint8_t*>(cols.values[t.col]),
+                          reinterpret_cast<const int32_t*>(cols.offsets[t.col]), cols.validity[t.col], mask, row0,
+                          row1, s, regs);
+      break;
+    case CV_LUTF8_H:
+      utf8_range<int64_t>(reinterpret_cast<const uint8_t*>(cols.values[t.col]),
+                          reinterpret_cast<const int64_t*>(cols.offsets[t.col]), cols.validity[t.col], mask, row0,
+                          row1, s, regs);
+      break;
+    default: break;
+  }
+  block_reduce_store(s, partials + (size_t)ti * kMaxWG + range, red);
+  if (hll) {
+    __syncthreads();
+    uint8_t* dst = hll_partials + ((size_t)t.hll_slot * kMaxWG + range) * 512;
+    for (int i = threadIdx.x; i < 512; i += kBlock) dst[i] = (uint8_t)regs[i];
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Kernel 3: Correlation co-moments, one task per column pair (Corr update/merge algebra).
+// ------------------------------------------------------------------------------------------
+struct CorrStats { double n, xa, ya, ck, xm, ym; };
+
+__device__ __forceinline__ void corr_merge(CorrStats& a, const CorrStats& b) {
+  double n = a.n + b.n;
+  if (b.n != 0.0) {
+    if (a.n == 0.0) { a.xa = b.xa; a.ya = b.ya; a.ck = b.ck; a.xm = b.xm; a.ym = b.ym; }
+    else {
+      double dx = b.xa - a.xa, dy = b.ya - a.ya;
+      double r = b.n / n;
+      double dxr = dx * r, dyr = dy * r;
+      a.ck = a.ck + b.ck + dx * dyr * a.n;
+      a.xm = a.xm + b.xm + dx * dxr * a.n;
+      a.ym = a.ym + b.ym + dy * dyr * a.n;
+      a.xa = a.xa + dxr;
+      a.ya = a.ya + dyr;
+    }
+  }
+  a.n = n;
+}
+
+__device__ __forceinline__ double load_as_double(const void* p, int kind, int64_t row) {
+  if (kind == CK_F64) return reinterpret_cast<const double*>(p)[row];
+  if (kind == CK_I64) return (double)reinterpret_cast<const int64_t*>(p)[row];
+  return (double)reinterpret_cast<const int32_t*>(p)[row];
+}
+
+__global__ __launch_bounds__(kBlock) void dq_pair_scan(const PairTask* __restrict__ tasks, int32_t ntasks, ScanCols cols,
+                                                       ScanBitmaps bm, int64_t n_rows, int64_t rows_per_range,
+                                                       CorrPartial* __restrict__ partials) {
+  __shared__ CorrStats red[kWaves];
+  const int32_t ti = blockIdx.x % ntasks;
+  const int32_t range = blockIdx.x / ntasks;
+  const PairTask t = tasks[ti];
+  const int64_t row0 = (int64_t)range * rows_per_range;
+  int64_t row1 = row0 + rows_per_range;
+  if (row1 > n_rows) row1 = n_rows;
+  const void* xv = cols.values[t.col_x];
+  const void* yv = cols.values[t.col_y];
+  const uint32_t* vx = cols.validity[t.col_x];
+  const uint32_t* vy = cols.validity[t.col_y];
+  const uint32_t* mask = t.where >= 0 ? reinterpret_cast<const uint32_t*>(bm.where_bits[t.where]) : nullptr;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  CorrStats s = {0, 0, 0, 0, 0, 0};
+  for (int64_t blk = row0; blk < row1; blk += kRowsPerIter) {
+    const int64_t base = blk + (int64_t)wave * 512;
+    double x[8], y[8];
+    uint32_t bits = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int64_t row = base + j * 64 + lane;
+      bool b = false;
+      x[j] = 0.0; y[j] = 0.0;
+      if (row < row1) {
+        uint32_t w = word_or_ones(vx, row >> 5) & word_or_ones(vy, row >> 5);
+        if (mask) w &= mask[row >> 5];
+        b = (w >> (row & 31)) & 1u;
+        x[j] = load_as_double(xv, t.kind_x, row);
+        y[j] = load_as_double(yv, t.kind_y, row);
+      }
+      bits |= (uint32_t)b << j;
+    }
+    int k = __popc(bits);
+    if (k == 0) continue;
+    double sx = s.xa, sy = s.ya;
+    if (s.n == 0.0) {
+#pragma unroll
+      for (int j = 7; j >= 0; --j) {
+        bool b = (bits >> j) & 1u;
+        sx = b ? x[j] : sx;
+        sy = b ? y[j] : sy;
+      }
+    }
+    double Sx = 0, Sy = 0, Sxy = 0, Sxx = 0, Syy = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      bool b = (bits >> j) & 1u;
+      double dx = b ? x[j] - sx : 0.0, dy = b ? y[j] - sy : 0.0;
+      Sx += dx; Sy += dy;
+      Sxy = __builtin_fma(dx, dy, Sxy);
+      Sxx = __builtin_fma(dx, dx, Sxx);
+      Syy = __builtin_fma(dy, dy, Syy);
+    }
+    double n2 = s.n + (double)k;
+    double qx = Sx / n2, qy = Sy / n2;
+    s.xa = sx + qx; s.ya = sy + qy;
+    s.ck = s.ck + (Sxy - Sx * qy);
+    s.xm = s.xm + (Sxx - Sx * qx);
+    s.ym = s.ym + (Syy - Sy * qy);
+    s.n = n2;
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    CorrStats o;
+    o.n = __shfl_xor(s.n, m); o.xa = __shfl_xor(s.xa, m); o.ya = __shfl_xor(s.ya, m);
+    o.ck = __shfl_xor(s.ck, m); o.xm = __shfl_xor(s.xm, m); o.ym = __shfl_xor(s.ym, m);
+    corr_merge(s, o);
+  }
+  if (lane == 0) red[wave] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    CorrStats a = red[0];
+    for (int w = 1; w < kWaves; ++w) corr_merge(a, red[w]);
+    CorrPartial* p = partials + (size_t)ti * kMaxWG + range;
+    p->n = a.n; p->xa = a.xa; p->ya = a.ya; p->ck = a.ck; p->xm = a.xm; p->ym = a.ym; p->pad0 = 0; p->pad1 = 0;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Kernel 1: predicate program (three-valued logic), one row per lane.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ bool valid_bit(const uint32_t* v, int64_t row) {
+  return v ? ((v[row >> 5] >> (row & 31)) & 1u) : true;
+}
+__device__ __forceinline__ int64_t load_as_int(const void* p, int kind, int64_t row) {
+  if (kind == CK_I64) return reinterpret_cast<const int64_t*>(p)[row];
+  return (int64_t)reinterpret_cast<const int32_t*>(p)[row];
+}
+// Spark comparison of doubles (nanSafeCompare / genEqual): NaN == NaN, NaN > everything.
+__device__ __forceinline__ int cmp_dbl(double a, double b) {
+  bool an = a != a, bn = b != b;
+  if (an || bn) return (an && bn) ? 0 : (an ? 1 : -1);
+  return (a > b) - (a < b);
+}
+__device__ __forceinline__ bool apply_cmp(int op, int c) {
+  switch (op) {
+    case C_LT: return c < 0;
+    case C_LE: return c <= 0;
+    case C_GT: return c > 0;
+    case C_GE: return c >= 0;
+    case C_EQ: return c == 0;
+    case C_NE: return c != 0;
+    case C_TRUE: return true;
+    default: return false;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void dq_pred_scan(const PredProgram* __restrict__ prog_g, ScanCols cols,
+                                                       ScanBitmaps bm, int64_t n_rows, int64_t rows_per_range,
+                                                       PredPartial* __restrict__ partials) {
+  __shared__ int64_t red_t[kWaves][kMaxCounters];
+  __shared__ int64_t red_n[kWaves][kMaxCounters];
+  const PredProgram& prog = *prog_g;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t row0 = (int64_t)blockIdx.x * rows_per_range;
+  int64_t row1 = row0 + rows_per_range;
+  if (row1 > n_rows) row1 = n_rows;
+  const int n_instr = prog.n_instr, n_counters = prog.n_counters, n_bitmaps = prog.n_bitmaps;
+  if (lane < kMaxCounters) { red_t[wave][lane] = 0; red_n[wave][lane] = 0; }
+
+  for (int64_t blk = row0; blk < row1; blk += kPredRowsPerIter) {
+    const int64_t row = blk + wave * 64 + lane;
+    const bool in_range = row < row1;
+    uint32_t root_t = 0, root_n = 0;
+    if (in_range) {
+      uint32_t st_t = 0, st_n = 0;
+      for (int i = 0; i < n_instr; ++i) {
+        const PredInstr& ins = prog.instr[i];
+        uint32_t t = 0, nl = 0;
+        switch (ins.op) {
+          case PO_ATOM_CMP: {
+            const bool va = valid_bit(cols.validity[ins.col_a], row);
+            const bool vb = ins.col_b < 0 ? true : valid_bit(cols.validity[ins.col_b], row);
+            if (!vb) { nl = 1; }
+            else if (!va) { t = ins.null_res == NR_TRUE; nl = ins.null_res == NR_NULL; }
+            else {
+              int c;
+              if (ins.ctype == CT_INT) {
+                int64_t a = load_as_int(cols.values[ins.col_a], ins.kind_a, row);
+                int64_t b = ins.col_b < 0 ? ins.lit_i : load_as_int(cols.values[ins.col_b], ins.kind_b, row);
+                c = (a > b) - (a < b);
+              } else {
+                double a = load_as_double(cols.values[ins.col_a], ins.kind_a, row);
+                double b = ins.col_b < 0 ? ins.lit_d : load_as_double(cols.values[ins.col_b], ins.kind_b, row);
+                c = cmp_dbl(a, b);
+              }
+              t = apply_cmp(ins.cmp, c);
+            }
+            st_t = (st_t << 1) | t; st_n = (st_n << 1) | nl;
+            break;
+          }
+          case PO_ATOM_ISNULL:
+          case PO_ATOM_NOTNULL: {
+            const bool va = valid_bit(cols.validity[ins.col_a], row);
+            t = (ins.op == PO_ATOM_ISNULL) ? !va : va;
+            st_t = (st_t << 1) | t; st_n = (st_n << 1);
+            break;
+          }
+          case PO_CONST:
+            st_t = (st_t << 1) | (ins.null_res == NR_TRUE); st_n = (st_n << 1) | (ins.null_res == NR_NULL);
+            break;
+          case PO_AND:
+          case PO_OR: {
+            const uint32_t bt = st_t & 1u, bn = st_n & 1u, at = (st_t >> 1) & 1u, an = (st_n >> 1) & 1u;
+            st_t >>= 2; st_n >>= 2;
+            const uint32_t af = !at & !an, bf = !bt & !bn;
+            uint32_t rt, rf;
+            if (ins.op == PO_AND) { rt = at & bt; rf = af | bf; }
+            else { rt = at | bt; rf = af & bf; }
+            st_t = (st_t << 1) | rt; st_n = (st_n << 1) | (!rt & !rf);
+            break;
+          }
+          case PO_NOT: {
+            const uint32_t at = st_t & 1u, an = st_n & 1u;
+            st_t = (st_t & ~1u) | (!at & !an);
+            (void)an;
+            break;
+          }
+          case PO_STORE: {
+            root_t |= (st_t & 1u) << ins.slot; root_n |= (st_n & 1u) << ins.slot;
+            st_t >>= 1; st_n >>= 1;
+            break;
+          }
+          default: break;
+        }
+      }
+    }
+    // outputs: where bitmaps (64 rows per word) and counters
+    for (int b = 0; b < n_bitmaps; ++b) {
+      const unsigned long long word = __ballot(in_range && ((root_t >> prog.bitmap_root[b]) & 1u));
+      if (lane == 0) bm.where_bits[b][(blk + wave * 64) >> 6] = word;
+    }
+    for (int c = 0; c < n_counters; ++c) {
+      const PredCounter pc = prog.counters[c];
+      const bool tw = pc.where < 0 ? true : ((root_t >> pc.where) & 1u);
+      const bool tp = (root_t >> pc.pred) & 1u;
+      const bool np = !((root_n >> pc.pred) & 1u);
+      const int64_t a = __popcll(__ballot(in_range && tp && tw));
+      const int64_t b = __popcll(__ballot(in_range && np && tw));
+      if (lane == 0) { red_t[wave][c] += a; red_n[wave][c] += b; }  // each wave owns its row
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < kMaxCounters) {
+    int64_t a = 0, b = 0;
+    for (int w = 0; w < kWaves; ++w) { a += red_t[w][threadIdx.x]; b += red_n[w][threadIdx.x]; }
+    partials[blockIdx.x].t[threadIdx.x] = a;
+    partials[blockIdx.x].nn[threadIdx.x] = b;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Kernel 4: fixed-order merge of per-workgroup partials into the plan accumulators.
+// blockIdx.x: [0, ncol) column tasks, [ncol, ncol + npair) pairs, then one block for counters.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void dq_finalize(const ColTask* __restrict__ col_tasks, int32_t ncol, int32_t nranges_col,
+                                                      const ColPartial* __restrict__ col_part,
+                                                      const uint8_t* __restrict__ hll_part, ColPartial* __restrict__ col_acc,
+                                                      uint8_t* __restrict__ hll_acc, int32_t npair, int32_t nranges_pair,
+                                                      const CorrPartial* __restrict__ pair_part,
+                                                      CorrPartial* __restrict__ pair_acc, int32_t has_pred,
+                                                      int32_t nranges_pred, const PredPartial* __restrict__ pred_part,
+                                                      PredPartial* __restrict__ pred_acc) {
+  __shared__ ColStats cs[kBlock];
+  __shared__ CorrStats ps[kBlock];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  if (b < ncol) {
+    ColStats s;
+    stats_init(s);
+    for (int r = tid; r < nranges_col; r += kBlock) stats_merge(s, stats_load(col_part + (size_t)b * kMaxWG + r));
+    cs[tid] = s;
+    __syncthreads();
+    for (int stride = kBlock / 2; stride >= 1; stride >>= 1) {
+      if (tid < stride) { ColStats a = cs[tid]; stats_merge(a, cs[tid + stride]); cs[tid] = a; }
+      __syncthreads();
+    }
+    if (tid == 0) {
+      ColStats acc = stats_load(col_acc + b);
+      stats_merge(acc, cs[0]);
+      stats_store(col_acc + b, acc);
+    }
+    const int hs = col_tasks[b].hll_slot;
+    if (hs >= 0) {
+      for (int i = tid; i < 512; i += kBlock) {
+        uint32_t m = hll_acc[(size_t)hs * 512 + i];
+        for (int r = 0; r < nranges_col; ++r) {
+          uint32_t v = hll_part[((size_t)hs * kMaxWG + r) * 512 + i];
+          m = v > m ? v : m;
+        }
+        hll_acc[(size_t)hs * 512 + i] = (uint8_t)m;
+      }
+    }
+  } else if (b < ncol + npair) {
+    const int p = b - ncol;
+    CorrStats s = {0, 0, 0, 0, 0, 0};
+    for (int r = tid; r < nranges_pair; r += kBlock) {
+      const CorrPartial& q = pair_part[(size_t)p * kMaxWG + r];
+      CorrStats o = {q.n, q.xa, q.ya, q.ck, q.xm, q.ym};
+      corr_merge(s, o);
+    }
+    ps[tid] = s;
+    __syncthreads();
+    for (int stride = kBlock / 2; stride >= 1; stride >>= 1) {
+      if (tid < stride) { CorrStats a = ps[tid]; corr_merge(a, ps[tid + stride]); ps[tid] = a; }
+      __syncthreads();
+    }
+    if (tid == 0) {
+      CorrPartial& q = pair_acc[p];
+      CorrStats acc = {q.n, q.xa, q.ya, q.ck, q.xm, q.ym};
+      corr_merge(acc, ps[0]);
+      q.n = acc.n; q.xa = acc.xa; q.ya = acc.ya; q.ck = acc.ck; q.xm = acc.xm; q.ym = acc.ym;
+    }
+  } else if (has_pred) {
+    if (tid < kMaxCounters) {
+      int64_t t = pred_acc->t[tid], nn = pred_acc->nn[tid];
+      for (int r = 0; r < nranges_pred; ++r) { t += pred_part[r].t[tid]; nn += pred_part[r].nn[tid]; }
+      pred_acc->t[tid] = t;
+      pred_acc->nn[tid] = nn;
+    }
+  }
+}
+
+__global__ void dq_init_acc(ColPartial* col_acc, int32_t ncol, CorrPartial* pair_acc, int32_t npair) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < ncol) {
+    ColStats s;
+    stats_init(s);
+    stats_store(col_acc + i, s);
+  }
+  if (i < npair) {
+    CorrPartial& q = pair_acc[i];
+    q.n = q.xa = q.ya = q.ck = q.xm = q.ym = q.pad0 = q.pad1 = 0.0;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// host-side launchers (called from dq_plan.cpp)
+// ------------------------------------------------------------------------------------------
+hipError_t launch_pred_scan(const PredProgram* prog, const ScanCols& cols, const ScanBitmaps& bm, int64_t n_rows,
+                            int64_t rows_per_range, int32_t nranges, PredPartial* partials, hipStream_t st) {
+  hipLaunchKernelGGL(dq_pred_scan, dim3(nranges), dim3(kBlock), 0, st, prog, cols, bm, n_rows, rows_per_range, partials);
+  return hipGetLastError();
+}
+
+hipError_t launch_column_scan(const ColTask* tasks, int32_t ntasks, const ScanCols& cols, const ScanBitmaps& bm,
+                              int64_t n_rows, int64_t rows_per_range, int32_t nranges, ColPartial* partials,
+                              uint8_t* hll_partials, hipStream_t st) {
+  hipLaunchKernelGGL(dq_column_scan, dim3((uint32_t)ntasks * (uint32_t)nranges), dim3(kBlock), 0, st, tasks, ntasks,
+                     cols, bm, n_rows, rows_per_range, partials, hll_partials);
+  return hipGetLastError();
+}
+
+hipError_t launch_pair_scan(const PairTask* tasks, int32_t ntasks, const ScanCols& cols, const ScanBitmaps& bm,
+                            int64_t n_rows, int64_t rows_per_range, int32_t nranges, CorrPartial* partials,
+                            hipStream_t st) {
+  hipLaunchKernelGGL(dq_pair_scan, dim3((uint32_t)ntasks * (uint32_t)nranges), dim3(kBlock), 0, st, tasks, ntasks, cols,
+                     bm, n_rows, rows_per_range, partials);
+  return hipGetLastError();
+}
+
+hipError_t launch_finalize(const ColTask* col_tasks, int32_t ncol, int32_t nranges_col, const ColPartial* col_part,
+                           const uint8_t* hll_part, ColPartial* col_acc, uint8_t* hll_acc, int32_t npair,
+                           int32_t nranges_pair, const CorrPartial* pair_part, CorrPartial* pair_acc, int32_t has_pred,
+                           int32_t nranges_pred, const PredPartial* pred_part, PredPartial* pred_acc, hipStream_t st) {
+  const uint32_t nb = (uint32_t)(ncol + npair + (has_pred ? 1 : 0));
+  if (nb == 0) return hipSuccess;
+  hipLaunchKernelGGL(dq_finalize, dim3(nb), dim3(kBlock), 0, st, col_tasks, ncol, nranges_col, col_part, hll_part,
+                     col_acc, hll_acc, npair, nranges_pair, pair_part, pair_acc, has_pred, nranges_pred, pred_part,
+                     pred_acc);
+  return hipGetLastError();
+}
+
+hipError_t launch_init_acc(ColPartial* col_acc, int32_t ncol, CorrPartial* pair_acc, int32_t npair, hipStream_t st) {
+  const int n = ncol > npair ? ncol : npair;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(dq_init_acc, dim3((n + 255) / 256), dim3(256), 0, st, col_acc, ncol, pair_acc, npair);
+  return hipGetLastError();
+}
+
+}  // namespace dq

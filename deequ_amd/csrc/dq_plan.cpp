@@ -1,0 +1,993 @@
+// dq_plan.cpp -- planner + scan driver behind the C ABI (include/dqscan.h).
+//
+// Replaces the body of AnalysisRunner.runScanningAnalyzers for the GPU-eligible analyzers
+// (analyzers/runners/AnalysisRunner.scala:279-326): instead of building
+// `aggregations = shareableAnalyzers.flatMap(_.aggregationFunctions())` and running
+// `data.agg(...)`, the planner lowers the analyzers into column tasks, pair tasks and one
+// predicate program, and dq_scan runs them over HBM-resident column chunks.  Identical analyzers
+// are deduplicated (case-class equality, analyzers/AnalysisTest.scala:57-68) and shared
+// sub-aggregates (count(*), the same column's moments, the same `where`) are computed once.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <limits>
+#include <map>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "dq_device.h"
+#include "dq_internal.h"
+
+namespace dq {
+
+hipError_t launch_pred_scan(const PredProgram* prog, const ScanCols& cols, const ScanBitmaps& bm, int64_t n_rows,
+                            int64_t rows_per_range, int32_t nranges, PredPartial* partials, hipStream_t st);
+hipError_t launch_column_scan(const ColTask* tasks, int32_t ntasks, const ScanCols& cols, const ScanBitmaps& bm,
+                              int64_t n_rows, int64_t rows_per_range, int32_t nranges, ColPartial* partials,
+                              uint8_t* hll_partials, hipStream_t st);
+hipError_t launch_pair_scan(const PairTask* tasks, int32_t ntasks, const ScanCols& cols, const ScanBitmaps& bm,
+                            int64_t n_rows, int64_t rows_per_range, int32_t nranges, CorrPartial* partials,
+                            hipStream_t st);
+hipError_t launch_finalize(const ColTask* col_tasks, int32_t ncol, int32_t nranges_col, const ColPartial* col_part,
+                           const uint8_t* hll_part, ColPartial* col_acc, uint8_t* hll_acc, int32_t npair,
+                           int32_t nranges_pair, const CorrPartial* pair_part, CorrPartial* pair_acc, int32_t has_pred,
+                           int32_t nranges_pred, const PredPartial* pred_part, PredPartial* pred_acc, hipStream_t st);
+hipError_t launch_init_acc(ColPartial* col_acc, int32_t ncol, CorrPartial* pair_acc, int32_t npair, hipStream_t st);
+
+static thread_local char g_err[1024] = "";
+
+dq_status set_error(dq_status code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  std::vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                              \
+  do {                                                                                             \
+    hipError_t e_ = (expr);                                                                        \
+    if (e_ != hipSuccess)                                                                          \
+      return set_error(e_ == hipErrorOutOfMemory ? DQ_E_OOM : DQ_E_HIP, "%s failed: %s (%s:%d)", \
+                       #expr, hipGetErrorString(e_), __FILE__, __LINE__);                          \
+  } while (0)
+
+static bool is_numeric(int32_t t) { return t == DQ_TYPE_F64 || t == DQ_TYPE_I64 || t == DQ_TYPE_I32; }
+static bool is_integral(int32_t t) { return t == DQ_TYPE_I64 || t == DQ_TYPE_I32; }
+static int32_t kind_of(int32_t t) {
+  switch (t) {
+    case DQ_TYPE_F64: return CK_F64;
+    case DQ_TYPE_I64: return CK_I64;
+    case DQ_TYPE_I32: return CK_I32;
+    case DQ_TYPE_UTF8: return CK_UTF8;
+    default: return CK_LUTF8;
+  }
+}
+
+// Where one analyzer's aggregation-result slots come from.
+struct SpecOut {
+  int32_t op = 0;
+  int32_t col_task = -1;   // column task index
+  int32_t pair_task = -1;  // pair task index
+  int32_t ctr_a = -1;      // counter: (pred, where)  -- matches
+  int32_t ctr_b = -1;      // counter: (where, none)  -- conditionalCount(where)
+  int32_t col_type = 0;
+  bool has_where = false;
+};
+
+// ------------------------------------------------------------------------------------------
+// Predicate lowering: IR tree -> postfix program over three-valued atoms
+// ------------------------------------------------------------------------------------------
+struct Lit {  // exact literal: int / decimal (unscaled, scale) / double / null / bool
+  enum K { INT, DEC, DBL, NUL, BOOL } k;
+  int64_t i = 0;
+  int32_t scale = 0;
+  double d = 0.0;
+};
+
+static double lit_to_double(const Lit& l) {
+  if (l.k == Lit::DBL) return l.d;
+  if (l.k == Lit::INT || l.k == Lit::BOOL) return (double)l.i;
+  // decimal -> correctly rounded double via its decimal text (Decimal.toDouble)
+  char buf[64];
+  long long u = (long long)l.i;
+  bool neg = u < 0;
+  unsigned long long a = neg ? (unsigned long long)(-(u + 1)) + 1ull : (unsigned long long)u;
+  std::string digits = std::to_string(a);
+  while ((int)digits.size() <= l.scale) digits = "0" + digits;
+  std::string txt = (neg ? "-" : "") + digits.substr(0, digits.size() - l.scale) +
+                    (l.scale ? "." + digits.substr(digits.size() - l.scale) : "");
+  std::snprintf(buf, sizeof(buf), "%s", txt.c_str());
+  return std::strtod(buf, nullptr);
+}
+
+static bool pow10_i64(int s, int64_t& out) {
+  if (s < 0 || s > 18) return false;
+  int64_t p = 1;
+  for (int i = 0; i < s; ++i) p *= 10;
+  out = p;
+  return true;
+}
+
+// exact compare of two non-double literals: returns -1/0/1
+static int exact_cmp(const Lit& a, const Lit& b) {
+  int64_t pa = 1, pb = 1;
+  pow10_i64(a.k == Lit::DEC ? a.scale : 0, pa);
+  pow10_i64(b.k == Lit::DEC ? b.scale : 0, pb);
+  __int128 x = (__int128)a.i * pb, y = (__int128)b.i * pa;
+  return (x > y) - (x < y);
+}
+
+static int flip_cmp(int c) {
+  switch (c) {
+    case DQ_CMP_LT: return DQ_CMP_GT;
+    case DQ_CMP_LE: return DQ_CMP_GE;
+    case DQ_CMP_GT: return DQ_CMP_LT;
+    case DQ_CMP_GE: return DQ_CMP_LE;
+    default: return c;
+  }
+}
+
+static bool cmp_holds(int c, int r) {
+  switch (c) {
+    case DQ_CMP_LT: return r < 0;
+    case DQ_CMP_LE: return r <= 0;
+    case DQ_CMP_GT: return r > 0;
+    case DQ_CMP_GE: return r >= 0;
+    case DQ_CMP_EQ: return r == 0;
+    default: return r != 0;
+  }
+}
+
+static int dbl_cmp(double a, double b) {  // Spark nanSafeCompare
+  bool an = a != a, bn = b != b;
+  if (an || bn) return (an && bn) ? 0 : (an ? 1 : -1);
+  return (a > b) - (a < b);
+}
+
+// literal-vs-literal comparison under Spark coercion: any double -> double, else exact decimal
+static int lit_cmp_result(int cmp, const Lit& a, const Lit& b) {  // returns NR_*
+  if (a.k == Lit::NUL || b.k == Lit::NUL) return NR_NULL;
+  int r = (a.k == Lit::DBL || b.k == Lit::DBL) ? dbl_cmp(lit_to_double(a), lit_to_double(b)) : exact_cmp(a, b);
+  return cmp_holds(cmp, r) ? NR_TRUE : NR_FALSE;
+}
+
+static int to_cmpop(int c) {
+  switch (c) {
+    case DQ_CMP_LT: return C_LT;
+    case DQ_CMP_LE: return C_LE;
+    case DQ_CMP_GT: return C_GT;
+    case DQ_CMP_GE: return C_GE;
+    case DQ_CMP_EQ: return C_EQ;
+    default: return C_NE;
+  }
+}
+
+struct Lowering {
+  const dq_pred_node* pool;
+  int32_t n_pred;
+  const std::vector<dq_column_desc>* schema;
+  std::vector<PredInstr> out;
+
+  dq_status lit_of(int32_t idx, Lit& l) {
+    const dq_pred_node& n = pool[idx];
+    switch (n.kind) {
+      case DQ_PRED_LIT_INT: l.k = Lit::INT; l.i = n.i64; return DQ_OK;
+      case DQ_PRED_LIT_DECIMAL:
+        if (n.cmp < 0 || n.cmp > 18) return set_error(DQ_E_UNSUPPORTED, "decimal literal scale %d unsupported", n.cmp);
+        l.k = Lit::DEC; l.i = n.i64; l.scale = n.cmp; return DQ_OK;
+      case DQ_PRED_LIT_DOUBLE: l.k = Lit::DBL; l.d = n.f64; return DQ_OK;
+      case DQ_PRED_LIT_NULL: l.k = Lit::NUL; return DQ_OK;
+      case DQ_PRED_LIT_BOOL: l.k = Lit::BOOL; l.i = n.i64 ? 1 : 0; return DQ_OK;
+      default: return set_error(DQ_E_UNSUPPORTED, "node %d is not a literal", idx);
+    }
+  }
+  bool is_lit(int32_t idx) const {
+    int k = pool[idx].kind;
+    return k >= DQ_PRED_LIT_INT && k <= DQ_PRED_LIT_BOOL;
+  }
+  dq_status check_idx(int32_t idx) {
+    if (idx < 0 || idx >= n_pred) return set_error(DQ_E_INVALID, "predicate node index %d out of range", idx);
+    return DQ_OK;
+  }
+  dq_status check_col(int32_t c) {
+    if (c < 0 || c >= (int32_t)schema->size()) return set_error(DQ_E_INVALID, "predicate column %d out of range", c);
+    return DQ_OK;
+  }
+  void push_const(int nr) {
+    PredInstr p{};
+    p.op = PO_CONST; p.null_res = nr; p.col_a = -1; p.col_b = -1;
+    out.push_back(p);
+  }
+
+  // operand = column, or COALESCE(column, literal)
+  struct Operand { int32_t col = -1; bool has_fallback = false; Lit fallback{}; };
+
+  dq_status operand_of(int32_t idx, Operand& o) {
+    const dq_pred_node& n = pool[idx];
+    if (n.kind == DQ_PRED_COLUMN) {
+      if (dq_status s = check_col(n.a)) return s;
+      o.col = n.a;
+      return DQ_OK;
+    }
+    if (n.kind == DQ_PRED_COALESCE) {
+      if (dq_status s = check_idx(n.a)) return s;
+      if (dq_status s = check_idx(n.b)) return s;
+      if (pool[n.a].kind != DQ_PRED_COLUMN || !is_lit(n.b))
+        return set_error(DQ_E_UNSUPPORTED, "COALESCE supported only as COALESCE(column, literal)");
+      if (dq_status s = check_col(pool[n.a].a)) return s;
+      o.col = pool[n.a].a;
+      o.has_fallback = true;
+      return lit_of(n.b, o.fallback);
+    }
+    return set_error(DQ_E_UNSUPPORTED, "unsupported comparison operand (node kind %d)", n.kind);
+  }
+
+  // column CMP literal, with Spark 2.2 coercions (integral vs decimal exact, anything vs double in double)
+  dq_status emit_col_lit(const Operand& o, int cmp, const Lit& lit) {
+    const dq_column_desc& cd = (*schema)[o.col];
+    if (!is_numeric(cd.type)) return set_error(DQ_E_UNSUPPORTED, "comparison on a non-numeric column (%d)", o.col);
+    PredInstr p{};
+    p.op = PO_ATOM_CMP; p.col_a = o.col; p.col_b = -1; p.kind_a = kind_of(cd.type); p.kind_b = 0;
+    p.null_res = o.has_fallback ? lit_cmp_result(cmp, o.fallback, lit) : NR_NULL;
+    if (lit.k == Lit::NUL) { push_const(NR_NULL); return DQ_OK; }
+    if (lit.k == Lit::BOOL) return set_error(DQ_E_UNSUPPORTED, "boolean literal compared with a number");
+    if (cd.type == DQ_TYPE_F64 || lit.k == Lit::DBL) {
+      p.ctype = CT_DBL; p.cmp = to_cmpop(cmp); p.lit_d = lit_to_double(lit);
+    } else if (lit.k == Lit::INT || (lit.k == Lit::DEC && lit.scale == 0)) {
+      p.ctype = CT_INT; p.cmp = to_cmpop(cmp); p.lit_i = lit.i;
+    } else {
+      // integral column vs decimal literal v = u / 10^s: exact rewrite to integer bounds
+      int64_t p10;
+      pow10_i64(lit.scale, p10);
+      int64_t u = lit.i;
+      int64_t fl = u >= 0 ? u / p10 : -((-u + p10 - 1) / p10);  // floor
+      bool integral = (u % p10) == 0;
+      int64_t ce = integral ? fl : fl + 1;                      // ceil
+      p.ctype = CT_INT;
+      switch (cmp) {
+        case DQ_CMP_LT: p.cmp = C_LT; p.lit_i = ce; break;      // x < v  <=> x < ceil(v)
+        case DQ_CMP_LE: p.cmp = C_LE; p.lit_i = fl; break;      // x <= v <=> x <= floor(v)
+        case DQ_CMP_GT: p.cmp = C_GT; p.lit_i = fl; break;      // x > v  <=> x > floor(v)
+        case DQ_CMP_GE: p.cmp = C_GE; p.lit_i = ce; break;      // x >= v <=> x >= ceil(v)
+        case DQ_CMP_EQ: p.cmp = integral ? C_EQ : C_FALSE; p.lit_i = fl; break;
+        default: p.cmp = integral ? C_NE : C_TRUE; p.lit_i = fl; break;
+      }
+    }
+    out.push_back(p);
+    return DQ_OK;
+  }
+
+  dq_status lower(int32_t idx, int depth) {
+    if (dq_status s = check_idx(idx)) return s;
+    if (depth > 30) return set_error(DQ_E_UNSUPPORTED, "predicate nesting too deep");
+    const dq_pred_node& n = pool[idx];
+    switch (n.kind) {
+      case DQ_PRED_AND:
+      case DQ_PRED_OR: {
+        if (dq_status s = lower(n.a, depth + 1)) return s;
+        if (dq_status s = lower(n.b, depth + 1)) return s;
+        PredInstr p{};
+        p.op = n.kind == DQ_PRED_AND ? PO_AND : PO_OR; p.col_a = p.col_b = -1;
+        out.push_back(p);
+        return DQ_OK;
+      }
+      case DQ_PRED_NOT: {
+        if (dq_status s = lower(n.a, depth + 1)) return s;
+        PredInstr p{};
+        p.op = PO_NOT; p.col_a = p.col_b = -1;
+        out.push_back(p);
+        return DQ_OK;
+      }
+      case DQ_PRED_IS_NULL:
+      case DQ_PRED_IS_NOT_NULL: {
+        if (dq_status s = check_idx(n.a)) return s;
+        const dq_pred_node& c = pool[n.a];
+        bool isnull = n.kind == DQ_PRED_IS_NULL;
+        if (c.kind == DQ_PRED_COLUMN) {
+          if (dq_status s = check_col(c.a)) return s;
+          PredInstr p{};
+          p.op = isnull ? PO_ATOM_ISNULL : PO_ATOM_NOTNULL; p.col_a = c.a; p.col_b = -1;
+          out.push_back(p);
+          return DQ_OK;
+        }
+        if (is_lit(n.a)) {
+          bool lit_null = c.kind == DQ_PRED_LIT_NULL;
+          push_const((lit_null == isnull) ? NR_TRUE : NR_FALSE);
+          return DQ_OK;
+        }
+        if (c.kind == DQ_PRED_COALESCE && is_lit(c.b) && pool[c.b].kind != DQ_PRED_LIT_NULL) {
+          push_const(isnull ? NR_FALSE : NR_TRUE);  // COALESCE(col, non-null literal) is never NULL
+          return DQ_OK;
+        }
+        return set_error(DQ_E_UNSUPPORTED, "IS NULL over an unsupported expression");
+      }
+      case DQ_PRED_LIT_BOOL: push_const(n.i64 ? NR_TRUE : NR_FALSE); return DQ_OK;
+      case DQ_PRED_LIT_NULL: push_const(NR_NULL); return DQ_OK;
+      case DQ_PRED_CMP: {
+        if (dq_status s = check_idx(n.a)) return s;
+        if (dq_status s = check_idx(n.b)) return s;
+        int cmp = n.cmp;
+        if (cmp < DQ_CMP_LT || cmp > DQ_CMP_NE) return set_error(DQ_E_INVALID, "bad comparison op %d", cmp);
+        bool la = is_lit(n.a), lb = is_lit(n.b);
+        if (la && lb) {
+          Lit a, b;
+          if (dq_status s = lit_of(n.a, a)) return s;
+          if (dq_status s = lit_of(n.b, b)) return s;
+          push_const(lit_cmp_result(cmp, a, b));
+          return DQ_OK;
+        }
+        if (la || lb) {
+          int32_t oi = la ? n.b : n.a, li = la ? n.a : n.b;
+          if (la) cmp = flip_cmp(cmp);
+          Operand o;
+          Lit l;
+          if (dq_status s = operand_of(oi, o)) return s;
+          if (dq_status s = lit_of(li, l)) return s;
+          return emit_col_lit(o, cmp, l);
+        }
+        // column vs column
+        if (pool[n.a].kind != DQ_PRED_COLUMN || pool[n.b].kind != DQ_PRED_COLUMN)
+          return set_error(DQ_E_UNSUPPORTED, "comparison of two non-column expressions");
+        int32_t ca = pool[n.a].a, cb = pool[n.b].a;
+        if (dq_status s = check_col(ca)) return s;
+        if (dq_status s = check_col(cb)) return s;
+        int32_t ta = (*schema)[ca].type, tb = (*schema)[cb].type;
+        if (!is_numeric(ta) || !is_numeric(tb)) return set_error(DQ_E_UNSUPPORTED, "comparison of non-numeric columns");
+        PredInstr p{};
+        p.op = PO_ATOM_CMP; p.col_a = ca; p.col_b = cb; p.kind_a = kind_of(ta); p.kind_b = kind_of(tb);
+        p.null_res = NR_NULL; p.cmp = to_cmpop(cmp);
+        p.ctype = (is_integral(ta) && is_integral(tb)) ? CT_INT : CT_DBL;
+        out.push_back(p);
+        return DQ_OK;
+      }
+      default:
+        return set_error(DQ_E_UNSUPPORTED, "predicate node kind %d is not a boolean expression", n.kind);
+    }
+  }
+};
+
+// canonical text of a predicate subtree (dedup of roots)
+static std::string canon(const dq_pred_node* pool, int32_t n_pred, int32_t idx, int depth = 0) {
+  if (idx < 0 || idx >= n_pred || depth > 64) return "?";
+  const dq_pred_node& n = pool[idx];
+  char buf[128];
+  std::snprintf(buf, sizeof(buf), "(%d:%d:%lld:%a", n.kind, n.cmp, (long long)n.i64, n.f64);
+  std::string s = buf;
+  if (n.kind == DQ_PRED_COLUMN) s += ":c" + std::to_string(n.a);
+  else {
+    if (n.kind == DQ_PRED_CMP || n.kind == DQ_PRED_AND || n.kind == DQ_PRED_OR || n.kind == DQ_PRED_NOT ||
+        n.kind == DQ_PRED_IS_NULL || n.kind == DQ_PRED_IS_NOT_NULL || n.kind == DQ_PRED_COALESCE)
+      s += canon(pool, n_pred, n.a, depth + 1);
+    if (n.kind == DQ_PRED_CMP || n.kind == DQ_PRED_AND || n.kind == DQ_PRED_OR || n.kind == DQ_PRED_COALESCE)
+      s += canon(pool, n_pred, n.b, depth + 1);
+  }
+  return s + ")";
+}
+
+}  // namespace dq
+
+using namespace dq;
+
+struct dq_plan {
+  int32_t device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  std::vector<dq_column_desc> schema;
+  std::vector<dq_analyzer_spec> specs;
+  std::vector<SpecOut> outs;
+
+  std::vector<ColTask> col_tasks;
+  std::vector<PairTask> pair_tasks;
+  PredProgram prog{};
+  int32_t n_hll = 0;
+  bool has_pred = false;
+
+  // device memory
+  ColTask* d_col_tasks = nullptr;
+  PairTask* d_pair_tasks = nullptr;
+  PredProgram* d_prog = nullptr;
+  ColPartial* d_col_part = nullptr;
+  uint8_t* d_hll_part = nullptr;
+  CorrPartial* d_pair_part = nullptr;
+  PredPartial* d_pred_part = nullptr;
+  ColPartial* d_col_acc = nullptr;
+  uint8_t* d_hll_acc = nullptr;
+  CorrPartial* d_pair_acc = nullptr;
+  PredPartial* d_pred_acc = nullptr;
+  uint64_t* d_where_bits[kMaxWhere] = {nullptr};
+  int64_t where_cap_words = 0;
+
+  int64_t total_rows = 0;
+  int64_t next_chunk = 0;
+
+  // optional per-kernel timing with hipEvents on the plan's stream (bench / profiling)
+  bool timing = false;
+  std::vector<hipEvent_t> ev_pool;
+  struct Pending { int kernel; hipEvent_t a, b; };
+  std::vector<Pending> pending;
+  double kernel_ms[4] = {0, 0, 0, 0};
+  int64_t kernel_launches[4] = {0, 0, 0, 0};
+  int64_t bytes_per_row_x1000 = 0;
+  int32_t launches_per_scan = 0;
+};
+
+static dq_status take_event(dq_plan* p, hipEvent_t* e) {
+  if (!p->ev_pool.empty()) { *e = p->ev_pool.back(); p->ev_pool.pop_back(); return DQ_OK; }
+  HIP_TRY(hipEventCreate(e));
+  return DQ_OK;
+}
+
+static dq_status resolve_timing(dq_plan* p) {
+  if (p->pending.empty()) return DQ_OK;
+  HIP_TRY(hipStreamSynchronize(p->stream));
+  for (auto& q : p->pending) {
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, q.a, q.b));
+    p->kernel_ms[q.kernel] += ms;
+    p->kernel_launches[q.kernel] += 1;
+    p->ev_pool.push_back(q.a);
+    p->ev_pool.push_back(q.b);
+  }
+  p->pending.clear();
+  return DQ_OK;
+}
+
+// launch `fn` bracketed by timing events when enabled
+template <typename F>
+static dq_status timed(dq_plan* p, int kernel, F fn) {
+  hipEvent_t a = nullptr, b = nullptr;
+  if (p->timing) {
+    if (dq_status s = take_event(p, &a)) return s;
+    if (dq_status s = take_event(p, &b)) return s;
+    HIP_TRY(hipEventRecord(a, p->stream));
+  }
+  HIP_TRY(fn());
+  if (p->timing) {
+    HIP_TRY(hipEventRecord(b, p->stream));
+    p->pending.push_back({kernel, a, b});
+  }
+  return DQ_OK;
+}
+
+static dq_status free_plan_mem(dq_plan* p) {
+  for (auto& q : p->pending) { p->ev_pool.push_back(q.a); p->ev_pool.push_back(q.b); }
+  p->pending.clear();
+  for (hipEvent_t e : p->ev_pool) (void)hipEventDestroy(e);
+  p->ev_pool.clear();
+  void* ptrs[] = {p->d_col_tasks, p->d_pair_tasks, p->d_prog, p->d_col_part, p->d_hll_part, p->d_pair_part,
+                  p->d_pred_part, p->d_col_acc, p->d_hll_acc, p->d_pair_acc, p->d_pred_acc};
+  for (void* q : ptrs)
+    if (q) (void)hipFree(q);
+  for (int i = 0; i < kMaxWhere; ++i)
+    if (p->d_where_bits[i]) (void)hipFree(p->d_where_bits[i]);
+  return DQ_OK;
+}
+
+static dq_status reset_acc(dq_plan* p) {
+  HIP_TRY(launch_init_acc(p->d_col_acc, (int32_t)p->col_tasks.size(), p->d_pair_acc, (int32_t)p->pair_tasks.size(),
+                          p->stream));
+  if (p->n_hll) HIP_TRY(hipMemsetAsync(p->d_hll_acc, 0, (size_t)p->n_hll * 512, p->stream));
+  if (p->has_pred) HIP_TRY(hipMemsetAsync(p->d_pred_acc, 0, sizeof(PredPartial), p->stream));
+  p->total_rows = 0;
+  p->next_chunk = 0;
+  return DQ_OK;
+}
+
+template <typename T>
+static dq_status dmalloc(T** ptr, size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  HIP_TRY(hipMalloc((void**)ptr, bytes));
+  return DQ_OK;
+}
+
+static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred) {
+  const int32_t ncols = (int32_t)p->schema.size();
+  std::map<std::string, int32_t> root_slot;          // canonical predicate text -> root slot
+  std::vector<std::vector<PredInstr>> root_code;
+  std::map<std::pair<int32_t, int32_t>, int32_t> col_task_of;      // (col, where bitmap) -> task
+  std::map<std::tuple<int32_t, int32_t, int32_t>, int32_t> pair_of; // (x, y, where bitmap) -> task
+  std::map<std::pair<int32_t, int32_t>, int32_t> counter_of;      // (pred slot, where slot) -> counter
+  std::map<int32_t, int32_t> bitmap_of;                             // where slot -> bitmap index
+  std::vector<std::pair<bool, bool>> col_task_needs;                // (stats, hll)
+  Lowering low{pool, n_pred, &p->schema, {}};
+
+  auto root = [&](int32_t node, int32_t& slot) -> dq_status {
+    if (node < 0 || node >= n_pred) return set_error(DQ_E_INVALID, "predicate root %d out of range", node);
+    std::string key = canon(pool, n_pred, node);
+    auto it = root_slot.find(key);
+    if (it != root_slot.end()) { slot = it->second; return DQ_OK; }
+    if ((int32_t)root_slot.size() >= kMaxRoots) return set_error(DQ_E_UNSUPPORTED, "more than %d distinct predicates", kMaxRoots);
+    low.out.clear();
+    if (dq_status s = low.lower(node, 0)) return s;
+    slot = (int32_t)root_slot.size();
+    root_slot[key] = slot;
+    root_code.push_back(low.out);
+    return DQ_OK;
+  };
+  auto notnull_root = [&](int32_t col, int32_t& slot) -> dq_status {
+    std::string key = "notnull:" + std::to_string(col);
+    auto it = root_slot.find(key);
+    if (it != root_slot.end()) { slot = it->second; return DQ_OK; }
+    if ((int32_t)root_slot.size() >= kMaxRoots) return set_error(DQ_E_UNSUPPORTED, "more than %d distinct predicates", kMaxRoots);
+    PredInstr ins{};
+    ins.op = PO_ATOM_NOTNULL; ins.col_a = col; ins.col_b = -1;
+    slot = (int32_t)root_slot.size();
+    root_slot[key] = slot;
+    root_code.push_back({ins});
+    return DQ_OK;
+  };
+  auto counter = [&](int32_t pred, int32_t where, int32_t& c) -> dq_status {
+    auto key = std::make_pair(pred, where);
+    auto it = counter_of.find(key);
+    if (it != counter_of.end()) { c = it->second; return DQ_OK; }
+    if ((int32_t)counter_of.size() >= kMaxCounters) return set_error(DQ_E_UNSUPPORTED, "more than %d predicate counters", kMaxCounters);
+    c = (int32_t)counter_of.size();
+    counter_of[key] = c;
+    return DQ_OK;
+  };
+  auto bitmap = [&](int32_t where_slot, int32_t& b) -> dq_status {
+    if (where_slot < 0) { b = -1; return DQ_OK; }
+    auto it = bitmap_of.find(where_slot);
+    if (it != bitmap_of.end()) { b = it->second; return DQ_OK; }
+    if ((int32_t)bitmap_of.size() >= kMaxWhere) return set_error(DQ_E_UNSUPPORTED, "more than %d distinct where filters on value analyzers", kMaxWhere);
+    b = (int32_t)bitmap_of.size();
+    bitmap_of[where_slot] = b;
+    return DQ_OK;
+  };
+  auto col_task = [&](int32_t col, int32_t bm, bool stats, bool hll, int32_t& t) -> dq_status {
+    auto key = std::make_pair(col, bm);
+    auto it = col_task_of.find(key);
+    if (it == col_task_of.end()) {
+      if ((int32_t)p->col_tasks.size() >= 256) return set_error(DQ_E_UNSUPPORTED, "too many column tasks");
+      t = (int32_t)p->col_tasks.size();
+      col_task_of[key] = t;
+      ColTask ct{};
+      ct.col = col; ct.where = bm; ct.hll_slot = -1; ct.variant = CV_VALIDITY;
+      p->col_tasks.push_back(ct);
+      col_task_needs.push_back({false, false});
+    } else {
+      t = it->second;
+    }
+    col_task_needs[t].first |= stats;
+    col_task_needs[t].second |= hll;
+    return DQ_OK;
+  };
+
+  p->outs.resize(p->specs.size());
+  for (size_t i = 0; i < p->specs.size(); ++i) {
+    const dq_analyzer_spec& s = p->specs[i];
+    SpecOut& o = p->outs[i];
+    o.op = s.op;
+    auto need_col = [&](int32_t c) -> dq_status {
+      if (c < 0 || c >= ncols) return set_error(DQ_E_INVALID, "spec %zu: column %d out of range", i, c);
+      return DQ_OK;
+    };
+    int32_t where_slot = -1;
+    if (s.where_root >= 0) {
+      if (dq_status st = root(s.where_root, where_slot)) return st;
+      o.has_where = true;
+    }
+    switch (s.op) {
+      case DQ_OP_SIZE:
+        if (where_slot >= 0) {
+          if (dq_status st = counter(where_slot, -1, o.ctr_b)) return st;
+        }
+        break;
+      case DQ_OP_COMPLETENESS: {
+        if (dq_status st = need_col(s.col_a)) return st;
+        o.col_type = p->schema[s.col_a].type;
+        if (where_slot >= 0) {
+          int32_t nn;
+          if (dq_status st = notnull_root(s.col_a, nn)) return st;
+          if (dq_status st = counter(nn, where_slot, o.ctr_a)) return st;
+          if (dq_status st = counter(where_slot, -1, o.ctr_b)) return st;
+        } else if (p->schema[s.col_a].nullable) {
+          if (dq_status st = col_task(s.col_a, -1, false, false, o.col_task)) return st;
+        }
+        break;
+      }
+      case DQ_OP_COMPLIANCE: {
+        int32_t ps;
+        if (s.pred_root < 0) return set_error(DQ_E_INVALID, "spec %zu: Compliance without predicate", i);
+        if (dq_status st = root(s.pred_root, ps)) return st;
+        if (dq_status st = counter(ps, where_slot, o.ctr_a)) return st;
+        if (where_slot >= 0)
+          if (dq_status st = counter(where_slot, -1, o.ctr_b)) return st;
+        break;
+      }
+      case DQ_OP_SUM:
+      case DQ_OP_MEAN:
+      case DQ_OP_STDDEV:
+      case DQ_OP_MIN:
+      case DQ_OP_MAX:
+      case DQ_OP_APPROX_COUNT_DISTINCT: {
+        if (dq_status st = need_col(s.col_a)) return st;
+        o.col_type = p->schema[s.col_a].type;
+        bool hll = s.op == DQ_OP_APPROX_COUNT_DISTINCT;
+        if (!hll && !is_numeric(o.col_type))  // Preconditions.isNumeric (Analyzer.scala:322-334)
+          return set_error(DQ_E_TYPE, "spec %zu: column %d is not numeric", i, s.col_a);
+        int32_t bm;
+        if (dq_status st = bitmap(where_slot, bm)) return st;
+        if (dq_status st = col_task(s.col_a, bm, !hll, hll, o.col_task)) return st;
+        break;
+      }
+      case DQ_OP_CORRELATION: {
+        if (dq_status st = need_col(s.col_a)) return st;
+        if (dq_status st = need_col(s.col_b)) return st;
+        if (!is_numeric(p->schema[s.col_a].type) || !is_numeric(p->schema[s.col_b].type))
+          return set_error(DQ_E_TYPE, "spec %zu: Correlation needs numeric columns", i);
+        int32_t bm;
+        if (dq_status st = bitmap(where_slot, bm)) return st;
+        auto key = std::make_tuple(s.col_a, s.col_b, bm);
+        auto it = pair_of.find(key);
+        if (it == pair_of.end()) {
+          o.pair_task = (int32_t)p->pair_tasks.size();
+          pair_of[key] = o.pair_task;
+          PairTask pt{};
+          pt.col_x = s.col_a; pt.col_y = s.col_b;
+          pt.kind_x = kind_of(p->schema[s.col_a].type); pt.kind_y = kind_of(p->schema[s.col_b].type);
+          pt.where = bm;
+          p->pair_tasks.push_back(pt);
+        } else {
+          o.pair_task = it->second;
+        }
+        break;
+      }
+      default:
+        return set_error(DQ_E_INVALID, "spec %zu: unknown op %d", i, s.op);
+    }
+  }
+
+  // column task variants
+  for (size_t t = 0; t < p->col_tasks.size(); ++t) {
+    ColTask& ct = p->col_tasks[t];
+    bool stats = col_task_needs[t].first, hll = col_task_needs[t].second;
+    int32_t type = p->schema[ct.col].type;
+    if (hll) ct.hll_slot = p->n_hll++;
+    if (!stats && !hll) ct.variant = CV_VALIDITY;
+    else if (type == DQ_TYPE_UTF8) ct.variant = CV_UTF8_H;
+    else if (type == DQ_TYPE_LARGE_UTF8) ct.variant = CV_LUTF8_H;
+    else {
+      int base = type == DQ_TYPE_F64 ? CV_F64_S : (type == DQ_TYPE_I64 ? CV_I64_S : CV_I32_S);
+      ct.variant = base + (stats && hll ? 1 : (stats ? 0 : 2));
+    }
+  }
+
+  // predicate program: roots in slot order, each followed by STORE
+  p->has_pred = !root_code.empty() && (!counter_of.empty() || !bitmap_of.empty());
+  PredProgram& prog = p->prog;
+  std::memset(&prog, 0, sizeof(prog));
+  if (p->has_pred) {
+    std::vector<PredInstr> code;
+    for (size_t r = 0; r < root_code.size(); ++r) {
+      for (const PredInstr& ins : root_code[r]) code.push_back(ins);
+      PredInstr st{};
+      st.op = PO_STORE; st.slot = (int32_t)r; st.col_a = st.col_b = -1;
+      code.push_back(st);
+    }
+    if ((int32_t)code.size() > kMaxInstr) return set_error(DQ_E_UNSUPPORTED, "predicate program too long (%zu)", code.size());
+    prog.n_instr = (int32_t)code.size();
+    std::copy(code.begin(), code.end(), prog.instr);
+    prog.n_counters = (int32_t)counter_of.size();
+    for (auto& kv : counter_of) prog.counters[kv.second] = PredCounter{kv.first.first, kv.first.second};
+    prog.n_bitmaps = (int32_t)bitmap_of.size();
+    for (auto& kv : bitmap_of) prog.bitmap_root[kv.second] = kv.first;
+  }
+
+  // algorithmic bytes per row: each (column, buffer) read once
+  std::vector<int> need_values(ncols, 0), need_validity(ncols, 0);
+  for (const ColTask& ct : p->col_tasks) {
+    need_validity[ct.col] = 1;
+    if (ct.variant != CV_VALIDITY) need_values[ct.col] = 1;
+  }
+  for (const PairTask& pt : p->pair_tasks) {
+    need_values[pt.col_x] = need_values[pt.col_y] = 1;
+    need_validity[pt.col_x] = need_validity[pt.col_y] = 1;
+  }
+  for (int i = 0; i < prog.n_instr; ++i) {
+    const PredInstr& ins = prog.instr[i];
+    if (ins.col_a >= 0) {
+      need_validity[ins.col_a] = 1;
+      if (ins.op == PO_ATOM_CMP) need_values[ins.col_a] = 1;
+    }
+    if (ins.col_b >= 0) { need_validity[ins.col_b] = 1; need_values[ins.col_b] = 1; }
+  }
+  int64_t b1000 = 0;
+  for (int c = 0; c < ncols; ++c) {
+    int32_t t = p->schema[c].type;
+    if (need_values[c]) b1000 += (t == DQ_TYPE_I32 || t == DQ_TYPE_UTF8) ? 4000 : 8000;  // value or offset bytes
+    if (need_validity[c] && p->schema[c].nullable) b1000 += 125;
+  }
+  p->bytes_per_row_x1000 = b1000;
+  p->launches_per_scan = (p->has_pred ? 1 : 0) + (p->col_tasks.empty() ? 0 : 1) + (p->pair_tasks.empty() ? 0 : 1) +
+                         ((p->col_tasks.size() + p->pair_tasks.size() + (p->has_pred ? 1 : 0)) ? 1 : 0);
+
+  // device allocations
+  const size_t nct = p->col_tasks.size(), npt = p->pair_tasks.size();
+  if (dq_status s = dmalloc(&p->d_col_tasks, nct * sizeof(ColTask))) return s;
+  if (dq_status s = dmalloc(&p->d_pair_tasks, npt * sizeof(PairTask))) return s;
+  if (dq_status s = dmalloc(&p->d_prog, sizeof(PredProgram))) return s;
+  if (dq_status s = dmalloc(&p->d_col_part, nct * kMaxWG * sizeof(ColPartial))) return s;
+  if (dq_status s = dmalloc(&p->d_hll_part, (size_t)p->n_hll * kMaxWG * 512)) return s;
+  if (dq_status s = dmalloc(&p->d_pair_part, npt * kMaxWG * sizeof(CorrPartial))) return s;
+  if (dq_status s = dmalloc(&p->d_pred_part, (p->has_pred ? kMaxWG : 1) * sizeof(PredPartial))) return s;
+  if (dq_status s = dmalloc(&p->d_col_acc, nct * sizeof(ColPartial))) return s;
+  if (dq_status s = dmalloc(&p->d_hll_acc, (size_t)p->n_hll * 512)) return s;
+  if (dq_status s = dmalloc(&p->d_pair_acc, npt * sizeof(CorrPartial))) return s;
+  if (dq_status s = dmalloc(&p->d_pred_acc, sizeof(PredPartial))) return s;
+  if (nct) HIP_TRY(hipMemcpyAsync(p->d_col_tasks, p->col_tasks.data(), nct * sizeof(ColTask), hipMemcpyHostToDevice, p->stream));
+  if (npt) HIP_TRY(hipMemcpyAsync(p->d_pair_tasks, p->pair_tasks.data(), npt * sizeof(PairTask), hipMemcpyHostToDevice, p->stream));
+  HIP_TRY(hipMemcpyAsync(p->d_prog, &p->prog, sizeof(PredProgram), hipMemcpyHostToDevice, p->stream));
+  if (dq_status s = reset_acc(p)) return s;
+  HIP_TRY(hipStreamSynchronize(p->stream));
+  return DQ_OK;
+}
+
+static int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+extern "C" {
+
+int32_t dq_abi_version(void) { return DQ_ABI_VERSION; }
+const char* dq_last_error(void) { return g_err; }
+
+dq_status dq_plan_create(const dq_analyzer_spec* specs, int32_t n_specs, const dq_column_desc* schema, int32_t n_cols,
+                         const dq_pred_node* pred_pool, int32_t n_pred, int32_t device, dq_plan** out) {
+  if (!out) return set_error(DQ_E_INVALID, "dq_plan_create: out is NULL");
+  *out = nullptr;
+  if (n_specs < 0 || (n_specs > 0 && !specs)) return set_error(DQ_E_INVALID, "dq_plan_create: bad specs");
+  if (n_cols < 0 || n_cols > kMaxCols || (n_cols > 0 && !schema))
+    return set_error(DQ_E_INVALID, "dq_plan_create: bad schema (at most %d columns)", kMaxCols);
+  if (n_pred < 0 || (n_pred > 0 && !pred_pool)) return set_error(DQ_E_INVALID, "dq_plan_create: bad predicate pool");
+  for (int32_t c = 0; c < n_cols; ++c)
+    if (schema[c].type < DQ_TYPE_F64 || schema[c].type > DQ_TYPE_LARGE_UTF8)
+      return set_error(DQ_E_TYPE, "dq_plan_create: column %d has unknown type %d", c, schema[c].type);
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return set_error(DQ_E_INVALID, "dq_plan_create: device %d of %d", device, ndev);
+  HIP_TRY(hipSetDevice(device));
+  dq_plan* p = new dq_plan();
+  p->device = device;
+  p->schema.assign(schema, schema + n_cols);
+  p->specs.assign(specs, specs + n_specs);
+  hipError_t e = hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete p;
+    return set_error(DQ_E_HIP, "hipStreamCreate: %s", hipGetErrorString(e));
+  }
+  p->own_stream = true;
+  dq_status st = build_plan(p, pred_pool, n_pred);
+  if (st != DQ_OK) {
+    std::string msg = g_err;
+    dq_plan_destroy(p);
+    return set_error(st, "%s", msg.c_str());
+  }
+  *out = p;
+  return DQ_OK;
+}
+
+dq_status dq_plan_set_stream(dq_plan* p, void* hip_stream) {
+  if (!p) return set_error(DQ_E_INVALID, "dq_plan_set_stream: plan is NULL");
+  HIP_TRY(hipSetDevice(p->device));
+  HIP_TRY(hipStreamSynchronize(p->stream));
+  if (hip_stream) {
+    if (p->own_stream) (void)hipStreamDestroy(p->stream);
+    p->stream = (hipStream_t)hip_stream;
+    p->own_stream = false;
+  } else if (!p->own_stream) {
+    HIP_TRY(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
+    p->own_stream = true;
+  }
+  return DQ_OK;
+}
+
+dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_t chunk_index) {
+  if (!p) return set_error(DQ_E_INVALID, "dq_scan: plan is NULL");
+  if (n_rows < 0) return set_error(DQ_E_INVALID, "dq_scan: n_rows < 0");
+  if (chunk_index != p->next_chunk)
+    return set_error(DQ_E_INVALID, "dq_scan: chunk_index %lld out of order (expected %lld)", (long long)chunk_index,
+                     (long long)p->next_chunk);
+  const int32_t ncols = (int32_t)p->schema.size();
+  if (ncols > 0 && !cols) return set_error(DQ_E_INVALID, "dq_scan: cols is NULL");
+  HIP_TRY(hipSetDevice(p->device));
+  ScanCols sc{};
+  for (int32_t c = 0; c < ncols; ++c) {
+    const dq_column_view& v = cols[c];
+    int32_t t = p->schema[c].type;
+    if (v.reserved != 0) return set_error(DQ_E_INVALID, "dq_scan: column %d reserved field must be 0", c);
+    if (n_rows > 0 && !v.values) return set_error(DQ_E_INVALID, "dq_scan: column %d has no values buffer", c);
+    if (((uintptr_t)v.values & 15) != 0)
+      return set_error(DQ_E_INVALID, "dq_scan: column %d values buffer must be 16-byte aligned", c);
+    if (((uintptr_t)v.validity & 3) != 0)
+      return set_error(DQ_E_INVALID, "dq_scan: column %d validity bitmap must be 4-byte aligned", c);
+    if ((t == DQ_TYPE_UTF8 || t == DQ_TYPE_LARGE_UTF8) && n_rows > 0 && !v.offsets)
+      return set_error(DQ_E_INVALID, "dq_scan: UTF8 column %d has no offsets", c);
+    sc.values[c] = v.values;
+    sc.validity[c] = p->schema[c].nullable ? reinterpret_cast<const uint32_t*>(v.validity) : nullptr;
+    sc.offsets[c] = v.offsets;
+  }
+  p->next_chunk++;
+  if (n_rows == 0) return DQ_OK;
+
+  // where bitmaps (64 rows per word), grown on demand
+  const int64_t words = ceil_div(n_rows, 64);
+  if (p->prog.n_bitmaps > 0 && words > p->where_cap_words) {
+    HIP_TRY(hipStreamSynchronize(p->stream));
+    for (int b = 0; b < p->prog.n_bitmaps; ++b) {
+      if (p->d_where_bits[b]) (void)hipFree(p->d_where_bits[b]);
+      p->d_where_bits[b] = nullptr;
+      if (dq_status s = dmalloc(&p->d_where_bits[b], (size_t)words * 8 + 64)) return s;
+    }
+    p->where_cap_words = words;
+  }
+  ScanBitmaps bm{};
+  for (int b = 0; b < kMaxWhere; ++b) bm.where_bits[b] = p->d_where_bits[b];
+
+  // row ranges: column / pair passes in multiples of 2048 rows, predicate pass in multiples of 256
+  int32_t nr_col = (int32_t)std::min<int64_t>(kMaxWG, ceil_div(n_rows, kRowsPerIter));
+  int64_t rpr_col = ceil_div(ceil_div(n_rows, nr_col), kRowsPerIter) * kRowsPerIter;
+  nr_col = (int32_t)ceil_div(n_rows, rpr_col);
+  int32_t nr_pred = (int32_t)std::min<int64_t>(kMaxWG, ceil_div(n_rows, kPredRowsPerIter));
+  int64_t rpr_pred = ceil_div(ceil_div(n_rows, nr_pred), kPredRowsPerIter) * kPredRowsPerIter;
+  nr_pred = (int32_t)ceil_div(n_rows, rpr_pred);
+
+  if (p->has_pred)
+    if (dq_status s = timed(p, 0, [&] {
+          return launch_pred_scan(p->d_prog, sc, bm, n_rows, rpr_pred, nr_pred, p->d_pred_part, p->stream);
+        }))
+      return s;
+  if (!p->col_tasks.empty())
+    if (dq_status s = timed(p, 1, [&] {
+          return launch_column_scan(p->d_col_tasks, (int32_t)p->col_tasks.size(), sc, bm, n_rows, rpr_col, nr_col,
+                                    p->d_col_part, p->d_hll_part, p->stream);
+        }))
+      return s;
+  if (!p->pair_tasks.empty())
+    if (dq_status s = timed(p, 2, [&] {
+          return launch_pair_scan(p->d_pair_tasks, (int32_t)p->pair_tasks.size(), sc, bm, n_rows, rpr_col, nr_col,
+                                  p->d_pair_part, p->stream);
+        }))
+      return s;
+  if (dq_status s = timed(p, 3, [&] {
+        return launch_finalize(p->d_col_tasks, (int32_t)p->col_tasks.size(), nr_col, p->d_col_part, p->d_hll_part,
+                               p->d_col_acc, p->d_hll_acc, (int32_t)p->pair_tasks.size(), nr_col, p->d_pair_part,
+                               p->d_pair_acc, p->has_pred ? 1 : 0, nr_pred, p->d_pred_part, p->d_pred_acc, p->stream);
+      }))
+    return s;
+  p->total_rows += n_rows;
+  return DQ_OK;
+}
+
+dq_status dq_finish(dq_plan* p, dq_state* out) {
+  if (!p) return set_error(DQ_E_INVALID, "dq_finish: plan is NULL");
+  if (!out && !p->specs.empty()) return set_error(DQ_E_INVALID, "dq_finish: out is NULL");
+  HIP_TRY(hipSetDevice(p->device));
+  std::vector<ColPartial> col(p->col_tasks.size());
+  std::vector<uint8_t> hll((size_t)p->n_hll * 512);
+  std::vector<CorrPartial> pair(p->pair_tasks.size());
+  PredPartial pred{};
+  if (!col.empty()) HIP_TRY(hipMemcpyAsync(col.data(), p->d_col_acc, col.size() * sizeof(ColPartial), hipMemcpyDeviceToHost, p->stream));
+  if (!hll.empty()) HIP_TRY(hipMemcpyAsync(hll.data(), p->d_hll_acc, hll.size(), hipMemcpyDeviceToHost, p->stream));
+  if (!pair.empty()) HIP_TRY(hipMemcpyAsync(pair.data(), p->d_pair_acc, pair.size() * sizeof(CorrPartial), hipMemcpyDeviceToHost, p->stream));
+  if (p->has_pred) HIP_TRY(hipMemcpyAsync(&pred, p->d_pred_acc, sizeof(PredPartial), hipMemcpyDeviceToHost, p->stream));
+  HIP_TRY(hipStreamSynchronize(p->stream));
+
+  const int64_t rows = p->total_rows;
+  const double nan = std::numeric_limits<double>::quiet_NaN();
+  for (size_t i = 0; i < p->specs.size(); ++i) {
+    const SpecOut& o = p->outs[i];
+    dq_state& s = out[i];
+    std::memset(&s, 0, sizeof(s));
+    s.op = o.op;
+    auto set1 = [&](bool v) { s.has_value[0] = s.has_value[1] = v ? 1 : 0; };
+    const ColPartial* c = o.col_task >= 0 ? &col[o.col_task] : nullptr;
+    switch (o.op) {
+      case DQ_OP_SIZE:  // count(*) is never NULL; sum(cast(where as long)) is NULL if all where are NULL
+        if (o.ctr_b >= 0) { s.u.size.num_matches = pred.t[o.ctr_b]; set1(pred.nn[o.ctr_b] > 0); }
+        else { s.u.size.num_matches = rows; set1(true); }
+        break;
+      case DQ_OP_COMPLETENESS:
+        if (o.has_where) {
+          s.u.ratio.num_matches = pred.t[o.ctr_a];
+          s.u.ratio.count = pred.t[o.ctr_b];
+          s.has_value[0] = rows > 0;
+          s.has_value[1] = pred.nn[o.ctr_b] > 0;
+        } else {
+          s.u.ratio.num_matches = c ? c->count : rows;
+          s.u.ratio.count = rows;
+          s.has_value[0] = rows > 0;  // sum over zero rows is NULL
+          s.has_value[1] = 1;
+        }
+        break;
+      case DQ_OP_COMPLIANCE:
+        s.u.ratio.num_matches = pred.t[o.ctr_a];
+        s.has_value[0] = pred.nn[o.ctr_a] > 0;
+        if (o.has_where) { s.u.ratio.count = pred.t[o.ctr_b]; s.has_value[1] = pred.nn[o.ctr_b] > 0; }
+        else { s.u.ratio.count = rows; s.has_value[1] = 1; }
+        break;
+      case DQ_OP_SUM:
+        s.u.sum.sum = o.col_type == DQ_TYPE_F64 ? c->sum : (double)c->isum;
+        set1(c->count > 0);
+        break;
+      case DQ_OP_MEAN:
+        s.u.mean.sum = o.col_type == DQ_TYPE_F64 ? c->sum : (double)c->isum;
+        s.u.mean.count = c->count;
+        s.has_value[0] = c->count > 0;
+        s.has_value[1] = 1;  // count(...) is never NULL
+        break;
+      case DQ_OP_STDDEV:
+        s.u.stddev.n = c->n; s.u.stddev.avg = c->mean; s.u.stddev.m2 = c->m2;
+        set1(true);  // the struct is never NULL; n == 0 -> None (StandardDeviation.scala:46-47)
+        break;
+      case DQ_OP_MIN:
+      case DQ_OP_MAX: {
+        set1(c->count > 0);
+        if (o.col_type == DQ_TYPE_F64) {
+          const bool all_nan = c->nan_count == c->count;
+          if (o.op == DQ_OP_MIN) s.u.minmax.value = all_nan ? nan : c->fmin;
+          else s.u.minmax.value = c->nan_count > 0 ? nan : c->fmax;  // NaN is the largest value
+        } else {
+          s.u.minmax.value = (double)(o.op == DQ_OP_MIN ? c->imin : c->imax);
+        }
+        break;
+      }
+      case DQ_OP_CORRELATION: {
+        const CorrPartial& q = pair[o.pair_task];
+        s.u.corr.n = q.n; s.u.corr.x_avg = q.xa; s.u.corr.y_avg = q.ya;
+        s.u.corr.ck = q.ck; s.u.corr.x_mk = q.xm; s.u.corr.y_mk = q.ym;
+        set1(true);
+        break;
+      }
+      case DQ_OP_APPROX_COUNT_DISTINCT:
+        hll_registers_to_words(hll.data() + (size_t)p->col_tasks[o.col_task].hll_slot * 512, s.u.hll.words);
+        set1(true);  // nullable = false (StatefulHyperloglogPlus.scala:59)
+        break;
+    }
+  }
+  return DQ_OK;
+}
+
+dq_status dq_plan_reset(dq_plan* p) {
+  if (!p) return set_error(DQ_E_INVALID, "dq_plan_reset: plan is NULL");
+  HIP_TRY(hipSetDevice(p->device));
+  return reset_acc(p);
+}
+
+void dq_plan_destroy(dq_plan* p) {
+  if (!p) return;
+  (void)hipSetDevice(p->device);
+  if (p->stream) (void)hipStreamSynchronize(p->stream);
+  free_plan_mem(p);
+  if (p->own_stream && p->stream) (void)hipStreamDestroy(p->stream);
+  delete p;
+}
+
+int64_t dq_plan_bytes_per_row_x1000(const dq_plan* p) { return p ? p->bytes_per_row_x1000 : 0; }
+
+dq_status dq_plan_enable_timing(dq_plan* p, int32_t on) {
+  if (!p) return set_error(DQ_E_INVALID, "dq_plan_enable_timing: plan is NULL");
+  HIP_TRY(hipSetDevice(p->device));
+  if (dq_status s = resolve_timing(p)) return s;
+  p->timing = on != 0;
+  for (int k = 0; k < 4; ++k) { p->kernel_ms[k] = 0; p->kernel_launches[k] = 0; }
+  return DQ_OK;
+}
+
+dq_status dq_plan_kernel_time(dq_plan* p, int32_t kernel, double* total_ms, int64_t* launches) {
+  if (!p || kernel < 0 || kernel > 3 || !total_ms || !launches)
+    return set_error(DQ_E_INVALID, "dq_plan_kernel_time: bad argument");
+  HIP_TRY(hipSetDevice(p->device));
+  if (dq_status s = resolve_timing(p)) return s;
+  *total_ms = p->kernel_ms[kernel];
+  *launches = p->kernel_launches[kernel];
+  return DQ_OK;
+}
+int32_t dq_plan_num_launches(const dq_plan* p) { return p ? p->launches_per_scan : 0; }
+
+}  // extern "C"

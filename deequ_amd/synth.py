@@ -1,0 +1,163 @@
+"""Seeded synthetic device tables for tests and bench.py (test/bench infrastructure, not the product).
+
+Values are generated on the device by libdqsynth.so (counter-based RNG, so every chunk / shard is a
+pure function of (seed, global row index)); see csrc/dq_synth.hip for the distributions.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import List, Sequence
+
+from .table import Column, Table
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        path = os.path.join(_HERE, "libdqsynth.so")
+        if not os.path.exists(path):
+            raise ImportError(f"{path} missing: run `make -C deequ_amd`")
+        L = ctypes.CDLL(path)
+        i64, u64, vp, d, i32 = ctypes.c_int64, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_double, ctypes.c_int32
+        L.dqs_f64.argtypes = [vp, i64, i64, u64, d, d, vp]
+        L.dqs_corr.argtypes = [vp, i64, i64, u64, u64, d, d, d, vp]
+        L.dqs_i64.argtypes = [vp, i64, i64, u64, u64, i64, vp]
+        L.dqs_validity.argtypes = [vp, i64, i64, u64, d, vp]
+        L.dqs_utf8_lengths.argtypes = [vp, i64, i64, u64, u64, i32, i32, vp]
+        L.dqs_utf8_bytes.argtypes = [vp, vp, i64, i64, u64, u64, vp]
+        L.dqs_i64_to_i32.argtypes = [vp, vp, i64, vp]
+        _lib = L
+    return _lib
+
+
+def _stream():
+    import torch
+
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _check(rc):
+    if rc != 0:
+        raise RuntimeError(f"synth kernel launch failed: hipError {rc}")
+
+
+def _alloc(nbytes: int):
+    import torch
+
+    n = ((nbytes + 15) // 16) * 16 + 16
+    return torch.empty(n, dtype=torch.uint8, device="cuda")
+
+
+def validity(n: int, seed: int, null_frac: float, row0: int = 0):
+    if null_frac <= 0.0:
+        return None
+    assert row0 % 32 == 0
+    buf = _alloc(((n + 63) // 64) * 8 + 8)
+    _check(lib().dqs_validity(buf.data_ptr(), row0, n, seed, null_frac, _stream()))
+    return buf
+
+
+def f64_column(name, n, seed, mean=0.0, sd=1.0, null_frac=0.0, row0=0) -> Column:
+    v = _alloc(n * 8)
+    _check(lib().dqs_f64(v.data_ptr(), row0, n, seed, mean, sd, _stream()))
+    bm = validity(n, seed ^ 0xABCDEF, null_frac, row0)
+    return Column(name, "f64", n, v, bm, None, nullable=bm is not None)
+
+
+def corr_column(name, n, seed, col_seed, a, b, offset, null_frac=0.0, row0=0) -> Column:
+    v = _alloc(n * 8)
+    _check(lib().dqs_corr(v.data_ptr(), row0, n, seed, col_seed, a, b, offset, _stream()))
+    bm = validity(n, col_seed ^ 0x1234567, null_frac, row0)
+    return Column(name, "f64", n, v, bm, None, nullable=bm is not None)
+
+
+def i64_column(name, n, seed, distinct, base=0, null_frac=0.0, row0=0) -> Column:
+    v = _alloc(n * 8)
+    _check(lib().dqs_i64(v.data_ptr(), row0, n, seed, distinct, base, _stream()))
+    bm = validity(n, seed ^ 0xABCDEF, null_frac, row0)
+    return Column(name, "i64", n, v, bm, None, nullable=bm is not None)
+
+
+def i32_column(name, n, seed, distinct, base=0, null_frac=0.0, row0=0) -> Column:
+    import torch
+
+    tmp = _alloc(n * 8)
+    _check(lib().dqs_i64(tmp.data_ptr(), row0, n, seed, distinct, base, _stream()))
+    v = _alloc(n * 4)
+    _check(lib().dqs_i64_to_i32(v.data_ptr(), tmp.data_ptr(), n, _stream()))
+    del tmp
+    bm = validity(n, seed ^ 0xABCDEF, null_frac, row0)
+    return Column(name, "i32", n, v, bm, None, nullable=bm is not None)
+
+
+def utf8_column(name, n, seed, distinct, lmin=8, lmax=24, null_frac=0.0, row0=0, large=False) -> Column:
+    import torch
+
+    lens = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    lens[0] = 0
+    _check(lib().dqs_utf8_lengths(lens[1:].data_ptr(), row0, n, seed, distinct, lmin, lmax, _stream()))
+    offs = torch.cumsum(lens, 0)
+    del lens
+    total = int(offs[-1].item())
+    if not large and total >= 2 ** 31:
+        raise ValueError("utf8 chunk > 2 GiB: use large=True or smaller chunks")
+    data = _alloc(total)
+    _check(lib().dqs_utf8_bytes(data.data_ptr(), offs.data_ptr(), row0, n, seed, distinct, _stream()))
+    if large:
+        o = _alloc((n + 1) * 8)
+        o[: (n + 1) * 8].copy_(offs.view(torch.uint8))
+    else:
+        o = _alloc((n + 1) * 4)
+        _check(lib().dqs_i64_to_i32(o.data_ptr(), offs.data_ptr(), n + 1, _stream()))
+    del offs
+    bm = validity(n, seed ^ 0xABCDEF, null_frac, row0)
+    return Column(name, "large_utf8" if large else "utf8", n, data, bm, o, nullable=bm is not None, data_bytes=total)
+
+
+# ---------------------------------------------------------------------------------------------
+# benchmark configurations
+# ---------------------------------------------------------------------------------------------
+INT_DISTINCT = [1000, 1_000_000, 100_000_000, 1 << 62]
+STR_DISTINCT = [1000, 1_000_000, 100_000_000, 0]  # 0 = unique (a fresh id per row)
+
+
+def c2_table(n, row0=0, seed=42, null_frac=0.10) -> Table:
+    """8 fp64 columns, column c ~ N(1000 c, (1 + c)^2), 10% nulls."""
+    return Table([f64_column(f"c{c}", n, seed + c, 1000.0 * c, 1.0 + c, null_frac, row0) for c in range(8)])
+
+
+def c3_table(n, row0=0, seed=42, null_frac=0.10) -> Table:
+    cols = [i64_column(f"i{c}", n, seed + 100 + c, INT_DISTINCT[c], 0, null_frac, row0) for c in range(4)]
+    cols += [utf8_column(f"s{c}", n, seed + 200 + c, STR_DISTINCT[c], 8, 24, null_frac, row0) for c in range(4)]
+    return Table(cols)
+
+
+def c4_table(n, row0=0, seed=42, null_frac=0.10) -> Table:
+    cols = []
+    for c in range(8):
+        a, b = 0.3 + 0.1 * c, 1.0 - 0.05 * c
+        cols.append(corr_column(f"x{c}", n, seed, seed + 300 + c, a, b, 1000.0 * c, null_frac, row0))
+    return Table(cols)
+
+
+def c5_table(n, row0=0, seed=42, null_frac=0.10) -> Table:
+    """16 mixed columns: C2's 8 fp64 + C3's 4 int64 + 4 UTF8."""
+    return Table(list(c2_table(n, row0, seed, null_frac).columns.values()) +
+                 list(c3_table(n, row0, seed, null_frac).columns.values()))
+
+
+def profile_analyzers(table: Table):
+    """ColumnProfiler passes 1-2 minus DataType / ApproxQuantiles (profiles/ColumnProfiler.scala:200-235)."""
+    from .analyzers import (ApproxCountDistinct, Completeness, Maximum, Mean, Minimum, Size, StandardDeviation,
+                            Sum)
+
+    out = [Size()]
+    for name, dtype, _ in table.schema:
+        out += [Completeness(name), ApproxCountDistinct(name)]
+        if dtype in ("f64", "i64", "i32"):
+            out += [Minimum(name), Maximum(name), Mean(name), StandardDeviation(name), Sum(name)]
+    return out

@@ -1,0 +1,201 @@
+/*
+ * dqscan.h -- C ABI of libdqscan.so, the MI355X (gfx950) replacement for Deequ's fused
+ * single-pass metric scan.
+ *
+ * Reference interface this replaces (paths relative to src/main/scala/com/amazon/deequ/):
+ *   AnalysisRunner.runScanningAnalyzers            analyzers/runners/AnalysisRunner.scala:279-326
+ *     -> data.agg(aggregations...).collect().head   analyzers/runners/AnalysisRunner.scala:303
+ *   ScanShareableAnalyzer.aggregationFunctions /
+ *     fromAggregationResult(row, offset)           analyzers/Analyzer.scala:159-187
+ *   State.sum / Analyzers.merge                    analyzers/Analyzer.scala:34-48, 343-362
+ *   DeequHyperLogLogPlusPlusUtils.count            analyzers/catalyst/StatefulHyperloglogPlus.scala:210-257
+ *   HdfsStateProvider persist / load byte images   analyzers/StateProvider.scala:176-294
+ *
+ * Call pattern of a drop-in shim (Scala/JNI, C++, or the Python host in deequ_amd/):
+ *   dq_plan_create(specs, schema, predicate IR)    <- the GPU-eligible ScanShareableAnalyzers
+ *   dq_scan(plan, columns, n_rows, chunk) ...      <- one or more row chunks, HBM-resident buffers
+ *   dq_finish(plan, states)                        <- one aggregation "Row" slot set per spec
+ *   dq_state_* / dq_hll_estimate                   <- state algebra for StateLoader/Persister merges
+ *
+ * All functions return DQ_OK (0) or a negative dq_status; dq_last_error() (thread-local) holds the
+ * message.  A shim maps ANY failure of plan/scan/finish to a failure metric on every GPU-routed
+ * analyzer, as runScanningAnalyzers does for an aggregation exception (AnalysisRunner.scala:310-313).
+ * Plans are not thread-safe: one plan per calling thread.  State functions are pure and reentrant.
+ */
+#ifndef DQSCAN_H
+#define DQSCAN_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DQ_ABI_VERSION 1
+
+typedef int32_t dq_status;
+#define DQ_OK 0
+#define DQ_E_INVALID (-1)     /* bad argument / malformed spec */
+#define DQ_E_TYPE (-2)        /* column type not valid for the analyzer (preconditions) */
+#define DQ_E_UNSUPPORTED (-3) /* predicate outside the GPU grammar: route to the fallback */
+#define DQ_E_HIP (-4)         /* HIP runtime / kernel failure */
+#define DQ_E_OOM (-5)         /* device allocation failed */
+#define DQ_E_STATE (-6)       /* state algebra misuse (op mismatch, bad byte image) */
+
+/* Column physical types (Arrow layouts). */
+enum dq_type {
+  DQ_TYPE_F64 = 1,        /* DoubleType: 8-byte values */
+  DQ_TYPE_I64 = 2,        /* LongType: 8-byte values */
+  DQ_TYPE_I32 = 3,        /* IntegerType: 4-byte values */
+  DQ_TYPE_UTF8 = 4,       /* StringType: int32 offsets[n+1] + data bytes */
+  DQ_TYPE_LARGE_UTF8 = 5  /* StringType with int64 offsets[n+1] (chunks > 2 GiB) */
+};
+
+/* Analyzer ops: the GPU-eligible ScanShareableAnalyzers. */
+enum dq_op {
+  DQ_OP_SIZE = 1,                 /* analyzers/Size.scala:36-48 */
+  DQ_OP_COMPLETENESS = 2,         /* analyzers/Completeness.scala:26-46 */
+  DQ_OP_COMPLIANCE = 3,           /* analyzers/Compliance.scala:37-53 */
+  DQ_OP_SUM = 4,                  /* analyzers/Sum.scala:36-52 */
+  DQ_OP_MEAN = 5,                 /* analyzers/Mean.scala:36-54 */
+  DQ_OP_STDDEV = 6,               /* analyzers/StandardDeviation.scala:47-73 */
+  DQ_OP_MIN = 7,                  /* analyzers/Minimum.scala:36-53 */
+  DQ_OP_MAX = 8,                  /* analyzers/Maximum.scala:36-53 */
+  DQ_OP_CORRELATION = 9,          /* analyzers/Correlation.scala:65-105 */
+  DQ_OP_APPROX_COUNT_DISTINCT = 10 /* analyzers/ApproxCountDistinct.scala:47-64 */
+};
+
+typedef struct dq_column_desc {
+  int32_t type;     /* enum dq_type */
+  int32_t nullable; /* 0: validity bitmaps are ignored (may be NULL) */
+} dq_column_desc;
+
+/* One analyzer instance (a Scala case class).  Unused fields = -1. */
+typedef struct dq_analyzer_spec {
+  int32_t op;         /* enum dq_op */
+  int32_t col_a;      /* column index (COMPLETENESS..MAX, ACD, CORRELATION first column) */
+  int32_t col_b;      /* CORRELATION second column */
+  int32_t pred_root;  /* COMPLIANCE predicate: root index into the predicate node pool */
+  int32_t where_root; /* optional `where` filter root, -1 = none */
+} dq_analyzer_spec;
+
+/* Predicate IR: a pool of nodes, referenced by index.  This is the lowered form of the Spark SQL
+ * expressions deequ builds with expr(...) (Check.scala:538-548, 670-871): comparisons with SQL
+ * three-valued logic, AND / OR / NOT, IS [NOT] NULL, COALESCE(column, literal).  Literal typing
+ * follows Spark 2.2: `3` -> LIT_INT, `3.0` -> LIT_DECIMAL (exact), `3e0` -> LIT_DOUBLE. */
+enum dq_pred_kind {
+  DQ_PRED_COLUMN = 1,      /* a = column index */
+  DQ_PRED_LIT_INT = 2,     /* i64 */
+  DQ_PRED_LIT_DECIMAL = 3, /* i64 = unscaled value, cmp = scale (value = i64 / 10^scale) */
+  DQ_PRED_LIT_DOUBLE = 4,  /* f64 */
+  DQ_PRED_LIT_NULL = 5,
+  DQ_PRED_LIT_BOOL = 6,    /* i64 = 0 / 1 */
+  DQ_PRED_CMP = 7,         /* a CMP b, cmp = enum dq_cmp */
+  DQ_PRED_AND = 8,         /* a AND b */
+  DQ_PRED_OR = 9,          /* a OR b */
+  DQ_PRED_NOT = 10,        /* NOT a */
+  DQ_PRED_IS_NULL = 11,    /* a IS NULL */
+  DQ_PRED_IS_NOT_NULL = 12,/* a IS NOT NULL */
+  DQ_PRED_COALESCE = 13    /* COALESCE(a, b): a = COLUMN node, b = literal node */
+};
+enum dq_cmp { DQ_CMP_LT = 1, DQ_CMP_LE = 2, DQ_CMP_GT = 3, DQ_CMP_GE = 4, DQ_CMP_EQ = 5, DQ_CMP_NE = 6 };
+
+typedef struct dq_pred_node {
+  int32_t kind;
+  int32_t a;
+  int32_t b;
+  int32_t cmp;
+  int64_t i64;
+  double f64;
+} dq_pred_node;
+
+/* One column of one row chunk.  All pointers are DEVICE pointers (HBM-resident, e.g. uploaded
+ * Spark/Arrow batches).  values: 16-byte aligned; validity: Arrow LSB-first bitmap, 4-byte
+ * aligned, bit 0 = row 0 of the chunk, NULL when the column has no nulls.  UTF8 columns pass the
+ * data bytes in `values` and the offsets (n_rows + 1 entries) in `offsets`. */
+typedef struct dq_column_view {
+  const void* values;
+  const uint8_t* validity;
+  const void* offsets;
+  int64_t reserved; /* must be 0 */
+} dq_column_view;
+
+/* The aggregation-result slots of one analyzer (the reference's Row slice at its offset,
+ * SURVEY §8b).  has_value[i] = SQL non-null flag of slot i; single-slot analyzers mirror slot 0
+ * into has_value[1].  fromAggregationResult yields Some(state) iff both flags are 1 (and, for
+ * StandardDeviation / Correlation, n > 0). */
+typedef struct dq_state {
+  int32_t op;           /* enum dq_op */
+  uint8_t has_value[2];
+  uint8_t reserved[2];
+  union {
+    struct { int64_t num_matches; } size;                     /* NumMatches */
+    struct { int64_t num_matches; int64_t count; } ratio;     /* NumMatchesAndCount */
+    struct { double sum; } sum;                               /* SumState */
+    struct { double sum; int64_t count; } mean;               /* MeanState */
+    struct { double n, avg, m2; } stddev;                     /* StandardDeviationState */
+    struct { double value; } minmax;                          /* MinState / MaxState */
+    struct { double n, x_avg, y_avg, ck, x_mk, y_mk; } corr;  /* CorrelationState */
+    struct { int64_t words[52]; } hll;                        /* ApproxCountDistinctState */
+  } u;
+} dq_state;
+
+typedef struct dq_plan dq_plan;
+
+/* Library identity. */
+int32_t dq_abi_version(void);
+const char* dq_last_error(void);
+
+/* Plan: validate + dedup the analyzers, lower predicates, allocate device partial states. */
+dq_status dq_plan_create(const dq_analyzer_spec* specs, int32_t n_specs, const dq_column_desc* schema,
+                         int32_t n_cols, const dq_pred_node* pred_pool, int32_t n_pred, int32_t device,
+                         dq_plan** out);
+/* Launch on this hipStream_t (NULL = the plan's own stream). */
+dq_status dq_plan_set_stream(dq_plan* plan, void* hip_stream);
+/* Scan one chunk of rows (asynchronous on the plan's stream).  chunk_index must increase by one
+ * per call starting at 0: chunk results are merged in that order, so results are deterministic. */
+dq_status dq_scan(dq_plan* plan, const dq_column_view* cols, int64_t n_rows, int64_t chunk_index);
+/* Synchronise and write one dq_state per spec (caller-allocated, n_specs entries). */
+dq_status dq_finish(dq_plan* plan, dq_state* out_states);
+/* Forget all scanned chunks (keeps allocations). */
+dq_status dq_plan_reset(dq_plan* plan);
+void dq_plan_destroy(dq_plan* plan);
+/* Algorithmic HBM bytes one scan of n_rows reads (each needed buffer counted once; UTF8 data
+ * bytes are data-dependent and reported by the caller). */
+int64_t dq_plan_bytes_per_row_x1000(const dq_plan* plan);
+/* Number of kernel launches one dq_scan issues. */
+int32_t dq_plan_num_launches(const dq_plan* plan);
+/* Optional per-kernel timing (hipEvents recorded on the plan's stream around every launch).
+ * kernel: 0 = predicate pass, 1 = column pass, 2 = pair (correlation) pass, 3 = finalize.
+ * dq_plan_kernel_time synchronises, then returns the summed duration and launch count since
+ * timing was (re-)enabled. */
+dq_status dq_plan_enable_timing(dq_plan* plan, int32_t on);
+dq_status dq_plan_kernel_time(dq_plan* plan, int32_t kernel, double* total_ms, int64_t* launches);
+
+/* State algebra.
+ * dq_state_merge:   Analyzers.merge / State.sum on Option[State] (Analyzer.scala:343-362):
+ *                   None + x = x; Min/Max merge with java.lang.Math.min/max.
+ * dq_state_combine: Spark partial-aggregate merge of two aggregation-result slot sets (row
+ *                   shards of one scan: GPUs, chunks): SQL null-skipping per slot, NaN-as-largest
+ *                   min/max ordering.  Used for the multi-GPU allgather merge. */
+dq_status dq_state_merge(const dq_state* a, const dq_state* b, dq_state* out);
+dq_status dq_state_combine(const dq_state* a, const dq_state* b, dq_state* out);
+/* 1 if fromAggregationResult would produce Some(state). */
+int32_t dq_state_is_defined(const dq_state* s);
+/* metricValue() of a defined state. */
+dq_status dq_state_metric(const dq_state* s, double* out);
+/* HLL++ estimate of 52 packed words, bit-exact with DeequHyperLogLogPlusPlusUtils.count. */
+dq_status dq_hll_estimate(const int64_t* words52, double* out);
+
+/* HdfsStateProvider byte images (Java DataOutputStream, big-endian).  Returns the image length,
+ * or a negative dq_status; writes nothing when buf is NULL / cap too small (returns length). */
+int64_t dq_state_to_bytes(const dq_state* s, uint8_t* buf, int64_t cap);
+dq_status dq_state_from_bytes(int32_t op, const uint8_t* buf, int64_t len, dq_state* out);
+/* HdfsStateProvider.toIdentifier: MurmurHash3.stringHash(analyzer.toString, 42) of UTF-8 text. */
+int32_t dq_state_identifier(const char* analyzer_to_string_utf8);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DQSCAN_H */

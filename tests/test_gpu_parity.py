@@ -1,0 +1,412 @@
+"""Parity of the MI355X path (libdqscan.so through the C ABI) with the CPU oracle.
+
+Tolerances (BASELINE.json north_star): counts, min/max, compliance matches and HLL registers /
+estimates bit-exact; fp64 sum / mean / stddev / correlation within 1e-12 relative (sums: relative
+to sum(|x|), the condition number of a floating-point sum, since both sides round differently).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import pytest
+
+from oracle import dq_oracle as O
+from oracle import dq_oracle_c as C
+from tests.helpers import close, host_column, oracle_columns
+
+pytestmark = pytest.mark.gpu
+
+REL = 1e-12
+
+
+@pytest.fixture(scope="module")
+def dq():
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    import deequ_amd
+
+    return deequ_amd
+
+
+def _device_table(dq, ds):
+    data = {name: (t, vals) for name, (t, vals) in ds["columns"].items()}
+    return dq.Table.from_pydict(data)
+
+
+def _analyzer(dq, spec):
+    op = spec[0]
+    cls = getattr(dq, op)
+    args = [a for a in spec[1:]]
+    return cls(*args)
+
+
+def assert_state_close(prod, ref, scale=None):
+    """prod: deequ_amd state (or None); ref: oracle state (or None)."""
+    if ref is None or prod is None:
+        assert prod is None and ref is None, (prod, ref)
+        return
+    name = type(ref).__name__
+    assert type(prod).__name__ == name
+    if name in ("NumMatches", "NumMatchesAndCount", "MinState", "MaxState"):
+        a, b = prod.__dict__, ref.__dict__
+        for k in a:
+            x, y = a[k], b[k]
+            assert x == y or (isinstance(x, float) and math.isnan(x) and math.isnan(y)), (name, k, x, y)
+    elif name == "ApproxCountDistinctState":
+        assert tuple(prod.words) == tuple(ref.words)
+    elif name == "SumState":
+        assert close(prod.sum_, ref.sum_, REL, REL * (scale or 0.0)), (prod, ref)
+    elif name == "MeanState":
+        assert prod.count == ref.count
+        assert close(prod.sum_, ref.sum_, REL, REL * (scale or 0.0)), (prod, ref)
+    elif name == "StandardDeviationState":
+        assert prod.n == ref.n
+        sd = math.sqrt(ref.m2 / ref.n) if ref.m2 >= 0 else 0.0
+        assert close(prod.avg, ref.avg, REL, REL * (abs(ref.avg) + sd)), (prod, ref)
+        assert close(prod.m2, ref.m2, REL, REL * ref.n * (sd * sd + 1e-300)), (prod, ref)
+        assert close(prod.metricValue(), ref.metricValue(), REL), (prod.metricValue(), ref.metricValue())
+    elif name == "CorrelationState":
+        assert prod.n == ref.n
+        for k in ("xAvg", "yAvg"):
+            assert close(getattr(prod, k), getattr(ref, k), REL, REL * (abs(getattr(ref, k)) + math.sqrt(abs(ref.xMk) / ref.n + abs(ref.yMk) / ref.n))), k
+        for k in ("xMk", "yMk"):
+            assert close(getattr(prod, k), getattr(ref, k), REL, REL * abs(getattr(ref, k))), k
+        assert close(prod.ck, ref.ck, REL, REL * math.sqrt(abs(ref.xMk * ref.yMk))), (prod.ck, ref.ck)
+        a, b = prod.metricValue(), ref.metricValue()
+        assert close(a, b, 0.0, 1e-12), (a, b)
+    else:
+        raise AssertionError(name)
+
+
+# ---------------------------------------------------------------------------------------------
+# 1. the reference's own known-answer tests, through AnalysisRunner (fused) and Analyzer.calculate
+# ---------------------------------------------------------------------------------------------
+def test_reference_kats_fused_and_single(dq, kats):
+    from deequ_amd.metrics import EmptyStateException, UnsupportedOnGpuPathException
+
+    by_ds = {}
+    for case in kats["cases"]:
+        by_ds.setdefault(case["dataset"], []).append(case)
+    for ds_name, cases in by_ds.items():
+        ds = kats["datasets"][ds_name]
+        table = _device_table(dq, ds)
+        analyzers = [_analyzer(dq, c["analyzer"]) for c in cases]
+        ctx = dq.AnalysisRunner.onData(table).addAnalyzers(analyzers).run()
+        for c, a in zip(cases, analyzers):
+            for metric in (ctx.metric(a), a.calculate(table)):
+                exp = c["expected"]
+                if "string_predicate" in c["needs"]:
+                    assert metric.value.isFailure
+                    assert isinstance(metric.value.failed, UnsupportedOnGpuPathException), metric
+                    continue
+                if exp == "EmptyState":
+                    assert metric.value.isFailure and isinstance(metric.value.failed, EmptyStateException), (c, metric)
+                elif exp == "NaN":
+                    assert math.isnan(metric.value.get()), (c, metric)
+                else:
+                    assert metric.value.get() == exp, (c["source"], a, metric, exp)
+
+
+def test_empty_state_message(dq, kats):
+    # NullHandlingTests.scala:122-133
+    table = _device_table(dq, kats["datasets"]["dataWithNullColumns"])
+    m = dq.Mean("numericCol").calculate(table)
+    assert str(m.value.failed) == "Empty state for analyzer Mean(numericCol,None), all input values were NULL."
+
+
+def test_kat_states_match_oracle(dq, kats):
+    """Every KAT analyzer's full state (not only the metric) equals the oracle's state."""
+    for case in kats["cases"]:
+        if case["needs"]:
+            continue
+        ds = kats["datasets"][case["dataset"]]
+        cols, n = oracle_columns(ds)
+        ref = O.compute_state(tuple(case["analyzer"]), cols, n, ds.get("partitions", 1))
+        table = _device_table(dq, ds)
+        prod = _analyzer(dq, case["analyzer"]).computeStateFrom(table)
+        assert_state_close(prod, ref, scale=1.0)
+
+
+# ---------------------------------------------------------------------------------------------
+# 2. randomised single-column parity vs the C oracle, edge sizes around the 2048-row block
+# ---------------------------------------------------------------------------------------------
+SIZES = [0, 1, 7, 63, 64, 65, 2047, 2048, 2049, 4097, 100_003]
+
+
+def _rand_table(dq, n, seed, null_frac):
+    rng = np.random.default_rng(seed)
+    valid = rng.random(n) >= null_frac
+    f = rng.normal(1000.0, 7.5, n)
+    i64 = rng.integers(-(1 << 40), 1 << 40, n)
+    i32 = rng.integers(-50000, 50000, n).astype(np.int32)
+    strs = [None if not valid[i] else (b"v%d-" % int(rng.integers(0, 5000))) * int(1 + i % 5) for i in range(n)]
+    from deequ_amd.table import column_from_numpy, utf8_column
+
+    t = dq.Table([column_from_numpy("f", "f64", f, valid), column_from_numpy("l", "i64", i64, valid),
+                  column_from_numpy("i", "i32", i32, ~valid if null_frac < 1 else valid),
+                  utf8_column("s", strs)])
+    return t
+
+
+def _profile(dq, t):
+    from deequ_amd.synth import profile_analyzers
+
+    return profile_analyzers(t)
+
+
+@pytest.mark.parametrize("n", SIZES)
+@pytest.mark.parametrize("null_frac", [0.0, 0.1, 1.0])
+def test_profile_vs_oracle(dq, n, null_frac):
+    t = _rand_table(dq, n, seed=n + int(null_frac * 10), null_frac=null_frac)
+    analyzers = _profile(dq, t)
+    from deequ_amd.runner import scan_states
+
+    states = scan_states(t, analyzers)
+    host = {name: host_column(c, n) for name, c in t.columns.items()}
+    for a in analyzers:
+        prod = states[a]
+        if type(a).__name__ == "Size":
+            assert prod.numMatches == n
+            continue
+        vals, valid, bm = host[a.column]
+        dtype = t.columns[a.column].dtype
+        ocol = O.OColumn(dtype, vals, valid)
+        if type(a).__name__ in ("ApproxCountDistinct", "Completeness"):
+            ref = O.compute_state((type(a).__name__, a.column, None), {a.column: ocol}, n)
+            assert_state_close(prod, ref)
+            continue
+        s = C.column_stats(dtype, vals, bm, None, 1)
+        name = type(a).__name__
+        if s.count == 0:
+            ref = None
+        elif name == "Sum":
+            ref = O.SumState(s.sum_f64)
+        elif name == "Mean":
+            ref = O.MeanState(s.sum_f64, s.count)
+        elif name == "StandardDeviation":
+            ref = O.StandardDeviationState(s.n, s.avg, s.m2)
+        elif name == "Minimum":
+            ref = O.MinState(s.min)
+        else:
+            ref = O.MaxState(s.max)
+        scale = float(np.abs(np.asarray(vals, dtype=np.float64)[valid]).sum()) if len(vals) else 0.0
+        assert_state_close(prod, ref, scale=scale)
+
+
+def test_chunked_equals_single_scan(dq):
+    """dq_scan over row chunks (chunk_index order) == one scan (PartitionedTableIntegrationTest analogue)."""
+    from deequ_amd import synth
+    from deequ_amd.runner import scan_states
+
+    n = 3 * 65536 + 123
+    whole = synth.c5_table(n, seed=3)
+    parts = [synth.c5_table(65536, row0=r, seed=3) for r in (0, 65536, 131072)] + [synth.c5_table(n - 196608, row0=196608, seed=3)]
+    analyzers = synth.profile_analyzers(whole)
+    a = scan_states(whole, analyzers)
+    b = scan_states(parts, analyzers)
+    for an in analyzers:
+        ref = a[an]
+        got = b[an]
+        if ref is None:
+            assert got is None
+            continue
+        if hasattr(ref, "words"):
+            assert got.words == ref.words
+        elif type(ref).__name__ in ("NumMatches", "NumMatchesAndCount", "MinState", "MaxState"):
+            assert got == ref
+        else:
+            assert close(got.metricValue(), ref.metricValue(), REL), (an, got, ref)
+
+
+def test_nan_min_max_and_hash(dq):
+    """Spark orders NaN above every double: max = NaN if any NaN; min ignores NaN unless all NaN."""
+    from deequ_amd.runner import scan_states
+
+    t = dq.Table.from_pydict({"x": ("f64", [1.0, float("nan"), -3.5, None, 2.0])})
+    s = scan_states(t, [dq.Minimum("x"), dq.Maximum("x"), dq.ApproxCountDistinct("x")])
+    assert s[dq.Minimum("x")].minValue == -3.5
+    assert math.isnan(s[dq.Maximum("x")].maxValue)
+    cols = {"x": O.OColumn("f64", np.array([1.0, float("nan"), -3.5, 0.0, 2.0]), np.array([1, 1, 1, 0, 1], bool))}
+    assert s[dq.ApproxCountDistinct("x")].words == O.compute_state(("ApproxCountDistinct", "x", None), cols, 5).words
+    t2 = dq.Table.from_pydict({"y": ("f64", [float("nan"), None, float("nan")])})
+    s2 = scan_states(t2, [dq.Minimum("y"), dq.Maximum("y")])
+    assert math.isnan(s2[dq.Minimum("y")].minValue) and math.isnan(s2[dq.Maximum("y")].maxValue)
+
+
+# ---------------------------------------------------------------------------------------------
+# 3. predicates (Compliance / where) vs the oracle's independent SQL evaluator
+# ---------------------------------------------------------------------------------------------
+PREDICATES = [
+    "a > 3", "a >= 3.0", "a > 2.5", "a < -1.5", "a = 4", "a = 4.5", "a != 4.5", "a <> 7",
+    "b <= 0.25", "b > 1e1", "a < b", "b >= a", "a = c", "c > a",
+    "COALESCE(a, 0.0) >= 0", "COALESCE(b, 1.0) > 0", "COALESCE(a, 5) < 3",
+    "`a` IS NULL OR (`a` >= 0.0 AND `a` <= 7.0)", "`b` IS NULL OR (`b` > -1.0 AND `b` < 8.0)",
+    "a IS NOT NULL", "NOT (a > 2 AND b < 0.5)", "a > 2 OR b IS NULL", "NOT a > 2",
+    "(a > 1 AND b > 0.1) OR (c < 0 AND a IS NULL)", "TRUE", "NULL", "a > NULL", "1 < 2", "1.5 > 2",
+]
+
+
+@pytest.fixture(scope="module")
+def pred_data():
+    rng = np.random.default_rng(11)
+    n = 5000
+    a = rng.integers(-8, 12, n).astype(np.int64)
+    b = np.round(rng.normal(0.5, 2.0, n), 2)
+    c = rng.integers(-5, 10, n).astype(np.int32)
+    va, vb, vc = rng.random(n) > 0.15, rng.random(n) > 0.2, rng.random(n) > 0.1
+    return n, {"a": ("i64", a, va), "b": ("f64", b, vb), "c": ("i32", c, vc)}
+
+
+def _tables(dq, pred_data):
+    from deequ_amd.table import column_from_numpy
+
+    n, d = pred_data
+    dev = dq.Table([column_from_numpy(k, t, v, m) for k, (t, v, m) in d.items()])
+    ocols = {k: O.OColumn(t, v, m) for k, (t, v, m) in d.items()}
+    return n, dev, ocols
+
+
+def test_compliance_predicates_vs_oracle(dq, pred_data):
+    n, dev, ocols = _tables(dq, pred_data)
+    analyzers = [dq.Compliance(f"r{i}", p) for i, p in enumerate(PREDICATES)]
+    from deequ_amd.runner import scan_states
+
+    got = scan_states(dev, analyzers)
+    for a in analyzers:
+        ref = O.compute_state(("Compliance", a.instance, a.predicate, None), ocols, n)
+        assert got[a] == (None if ref is None else dq.NumMatchesAndCount(ref.numMatches, ref.count)), (a.predicate, got[a], ref)
+
+
+WHERES = ["a > 2", "b < 0.5", "c IS NULL", "COALESCE(a, 0.0) >= 0", "a > 100"]
+
+
+def test_where_filters_vs_oracle(dq, pred_data):
+    n, dev, ocols = _tables(dq, pred_data)
+    analyzers = []
+    for w in WHERES:
+        analyzers += [dq.Size(w), dq.Completeness("b", w), dq.Compliance("w", "a < b", w), dq.Sum("a", w),
+                      dq.Mean("b", w), dq.StandardDeviation("b", w), dq.Minimum("c", w), dq.Maximum("b", w),
+                      dq.ApproxCountDistinct("a", w), dq.Correlation("a", "b", w)]
+    from deequ_amd.runner import scan_states
+
+    got = scan_states(dev, analyzers)
+    for a in analyzers:
+        name = type(a).__name__
+        if name == "Size":
+            spec = ("Size", a.where)
+        elif name == "Compliance":
+            spec = ("Compliance", a.instance, a.predicate, a.where)
+        elif name == "Correlation":
+            spec = ("Correlation", a.firstColumn, a.secondColumn, a.where)
+        else:
+            spec = (name, a.column, a.where)
+        ref = O.compute_state(spec, ocols, n)
+        prod = got[a]
+        if ref is None:
+            assert prod is None, (a, prod)
+            continue
+        conv = {"NumMatches": lambda r: dq.NumMatches(r.numMatches),
+                "NumMatchesAndCount": lambda r: dq.NumMatchesAndCount(r.numMatches, r.count)}
+        if type(ref).__name__ in conv:
+            assert prod == conv[type(ref).__name__](ref), (a, prod, ref)
+        else:
+            assert_state_close(prod, ref, scale=float(np.abs(ocols["b"].values).sum() + np.abs(ocols["a"].values).sum()))
+
+
+def test_unsupported_predicate_routes_to_fallback(dq, pred_data):
+    from deequ_amd.metrics import UnsupportedOnGpuPathException
+
+    n, dev, _ = _tables(dq, pred_data)
+    good, bad = dq.Compliance("ok", "a > 1"), dq.Compliance("bad", "a IN (1, 2)")
+    ctx = dq.AnalysisRunner.onData(dev).addAnalyzers([good, bad]).run()
+    assert ctx.metric(good).value.isSuccess
+    assert isinstance(ctx.metric(bad).value.failed, UnsupportedOnGpuPathException)
+
+
+def test_missing_column_in_predicate_fails_whole_pass(dq, pred_data):
+    """A predicate that cannot be analysed fails every shareable analyzer (AnalysisRunner.scala:310-313)."""
+    n, dev, _ = _tables(dq, pred_data)
+    ctx = dq.AnalysisRunner.onData(dev).addAnalyzers([dq.Size(), dq.Compliance("x", "nosuch > 3")]).run()
+    assert all(m.value.isFailure for m in ctx.allMetrics)
+
+
+# ---------------------------------------------------------------------------------------------
+# 4. the benchmark configurations at reduced row counts vs the C oracle (Spark partition simulation)
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("cfg", ["c2", "c3", "c4", "c5"])
+def test_configs_vs_oracle(dq, cfg):
+    from deequ_amd import synth
+    from deequ_amd.runner import scan_states
+
+    n = 1_000_003
+    t = getattr(synth, f"{cfg}_table")(n, seed=5)
+    if cfg == "c4":
+        names = list(t.columns)
+        analyzers = [dq.Correlation(names[i], names[j]) for i in range(8) for j in range(i + 1, 8)]
+        analyzers += [dq.Mean(c) for c in names] + [dq.StandardDeviation(c) for c in names]
+    elif cfg == "c3":
+        analyzers = [dq.Size()] + [dq.ApproxCountDistinct(c) for c in t.columns]
+        analyzers += [dq.Compliance("p0", "i0 >= 0"), dq.Compliance("p1", "`i1` IS NULL OR (`i1` >= 10.0 AND `i1` <= 1000.0)"),
+                      dq.Compliance("p2", "i2 < i3"), dq.Compliance("p3", "COALESCE(i3, 0.0) >= 0")]
+    else:
+        analyzers = synth.profile_analyzers(t)
+    got = scan_states(t, analyzers)
+    host = {name: host_column(c, n) for name, c in t.columns.items()}
+    nparts = 8
+    for a in analyzers:
+        name = type(a).__name__
+        prod = got[a]
+        if name == "Size":
+            assert prod.numMatches == n
+        elif name == "Completeness":
+            assert prod.numMatches == int(host[a.column][1].sum()) and prod.count == n
+        elif name == "ApproxCountDistinct":
+            vals, valid, bm = host[a.column]
+            col = t.columns[a.column]
+            if col.dtype == "utf8":
+                offs = col.offsets.cpu().numpy()[: (n + 1) * 4].view(np.int32)
+                data = np.frombuffer(col.values.cpu().numpy().tobytes(), dtype=np.uint8)
+                regs = C.hll_registers("utf8", data, offs, bm, None, n)
+            else:
+                regs = C.hll_registers(col.dtype, vals, None, bm, None, n)
+            assert prod.words == tuple(O.registers_to_words(regs.tolist())), a
+        elif name == "Compliance":
+            cols = {k: O.OColumn(t.columns[k].dtype, host[k][0], host[k][1]) for k in ("i0", "i1", "i2", "i3")}
+            sub = 200_000  # python oracle evaluator on a prefix; the full count via numpy below
+            ref = O.compute_state(("Compliance", a.instance, a.predicate, None),
+                                  {k: O.OColumn(v.dtype, v.values[:sub], v.valid[:sub]) for k, v in cols.items()}, sub)
+            pre = dq.Compliance(a.instance, a.predicate)
+            from deequ_amd.table import column_from_numpy
+            dev_sub = dq.Table([column_from_numpy(k, "i64", cols[k].values[:sub], cols[k].valid[:sub]) for k in cols])
+            assert pre.computeStateFrom(dev_sub) == dq.NumMatchesAndCount(ref.numMatches, ref.count), a
+        elif name == "Correlation":
+            x, vx, bx = host[a.firstColumn]
+            y, vy, by = host[a.secondColumn]
+            r = C.corr("f64", x, bx, "f64", y, by, None, nparts)
+            assert_state_close(prod, O.CorrelationState(*r))
+        else:
+            vals, valid, bm = host[a.column]
+            dtype = t.columns[a.column].dtype
+            s = C.column_stats(dtype, vals, bm, None, nparts)
+            ref = {"Sum": lambda: O.SumState(s.sum_f64), "Mean": lambda: O.MeanState(s.sum_f64, s.count),
+                   "StandardDeviation": lambda: O.StandardDeviationState(s.n, s.avg, s.m2),
+                   "Minimum": lambda: O.MinState(s.min), "Maximum": lambda: O.MaxState(s.max)}[name]()
+            assert_state_close(prod, ref, scale=float(np.abs(vals.astype(np.float64)[valid]).sum()))
+
+
+def test_incremental_state_provider_roundtrip(dq, tmp_path):
+    """persist -> load -> merge (IncrementalAnalysisTest / StateProviderTest analogue)."""
+    from deequ_amd import synth
+
+    t1 = synth.c5_table(50_000, seed=9)
+    t2 = synth.c5_table(30_000, row0=50_016, seed=9)
+    analyzers = synth.profile_analyzers(t1) + [dq.Correlation("c0", "c1")]
+    for provider in (dq.InMemoryStateProvider(), dq.HdfsStateProvider(str(tmp_path / "state"), allowOverwrite=True)):
+        dq.AnalysisRunner.onData(t1).addAnalyzers(analyzers).saveStatesWith(provider).run()
+        inc = dq.AnalysisRunner.onData(t2).addAnalyzers(analyzers).aggregateWith(provider).run()
+        both = dq.AnalysisRunner.onData([t1, t2]).addAnalyzers(analyzers).run()
+        for a in analyzers:
+            x, y = inc.metric(a).value.get(), both.metric(a).value.get()
+            assert close(x, y, 1e-12), (a, x, y)
