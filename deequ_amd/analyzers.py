@@ -154,9 +154,15 @@ class Analyzer:
     # ---- metric computation --------------------------------------------------------------
     def computeStateFrom(self, data) -> Optional[State]:
         """Runs this analyzer's aggregation alone (ScanShareableAnalyzer.computeStateFrom)."""
+        from .predicates import UnsupportedPredicate
+        from .metrics import UnsupportedOnGpuPathException
         from .runner import scan_states
 
-        return scan_states(data, [self])[self]
+        try:
+            return scan_states(data, [self])[self]
+        except UnsupportedPredicate as e:
+            raise UnsupportedOnGpuPathException(
+                f"{self} is outside the GPU-eligible set ({e}); a Spark integration keeps it on data.agg") from e
 
     def computeMetricFrom(self, state: Optional[State]) -> DoubleMetric:
         if state is not None:

@@ -3,9 +3,9 @@
 // HBM layout of one plan (all device-resident, allocated once at dq_plan_create):
 //   ColTask[ncol_tasks], PairTask[npair_tasks], PredProgram        (static task tables)
 //   ColPartial[ncol_tasks][kMaxWG]     per-workgroup partial states of the current scan
-//   uint8 hll[nhll][kMaxWG][512]       per-workgroup HLL registers (one byte per register)
 //   CorrPartial[npair][kMaxWG], PredPartial[kMaxWG]
-//   ColPartial / hll[512] / CorrPartial / PredPartial accumulators (merged over chunks, in order)
+//   ColPartial / CorrPartial / PredPartial accumulators (merged over chunks, in order)
+//   uint32 hll[nhll][512]              HLL registers, merged in by atomicMax (order-free)
 //   where bitmaps: uint64[n_rows/64] TRUE bits per `where` root used by column / pair tasks
 #pragma once
 
@@ -18,10 +18,11 @@ constexpr int kWaves = kBlock / 64;
 constexpr int kRowsPerLane = 8;
 constexpr int kRowsPerIter = kBlock * kRowsPerLane;  // 2048 rows per workgroup iteration
 constexpr int kMaxWG = 2048;                // max row ranges (workgroups) per task per scan
+constexpr int kTargetWGs = 8192;            // column/pair launch: aim for ~32 workgroups per CU
 constexpr int kMaxCols = 64;
 constexpr int kMaxWhere = 8;
 constexpr int kMaxRoots = 32;
-constexpr int kMaxCounters = 16;
+constexpr int kMaxCounters = 32;
 constexpr int kMaxInstr = 96;
 constexpr int kPredRowsPerIter = kBlock;    // predicate pass: one row per lane per iteration
 

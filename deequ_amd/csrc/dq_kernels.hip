@@ -382,7 +382,7 @@ __device__ void run_numeric(const ColTask& t, const ScanCols& cols, const ScanBi
 __global__ __launch_bounds__(kBlock) void dq_column_scan(const ColTask* __restrict__ tasks, int32_t ntasks,
                                                          ScanCols cols, ScanBitmaps bm, int64_t n_rows,
                                                          int64_t rows_per_range, ColPartial* __restrict__ partials,
-                                                         uint8_t* __restrict__ hll_partials) {
+                                                         uint32_t* __restrict__ hll_acc) {
   __shared__ uint32_t regs[512];
   __shared__ ColStats red[kWaves];
   const int32_t ti = blockIdx.x % ntasks;
@@ -424,9 +424,15 @@ __global__ __launch_bounds__(kBlock) void dq_column_scan(const ColTask* __restri
   }
   block_reduce_store(s, partials + (size_t)ti * kMaxWG + range, red);
   if (hll) {
+    // registers only grow: merge into the plan accumulator with device-scope atomicMax, skipping
+    // registers the (possibly stale) accumulator already covers -- max is order-free, so the
+    // result is deterministic.
     __syncthreads();
-    uint8_t* dst = hll_partials + ((size_t)t.hll_slot * kMaxWG + range) * 512;
-    for (int i = threadIdx.x; i < 512; i += kBlock) dst[i] = (uint8_t)regs[i];
+    uint32_t* dst = hll_acc + (size_t)t.hll_slot * 512;
+    for (int i = threadIdx.x; i < 512; i += kBlock) {
+      const uint32_t v = regs[i];
+      if (v > __builtin_nontemporal_load(dst + i)) atomicMax(dst + i, v);
+    }
   }
 }
 
@@ -677,10 +683,9 @@ __global__ __launch_bounds__(kBlock) void dq_pred_scan(const PredProgram* __rest
 // Kernel 4: fixed-order merge of per-workgroup partials into the plan accumulators.
 // blockIdx.x: [0, ncol) column tasks, [ncol, ncol + npair) pairs, then one block for counters.
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void dq_finalize(const ColTask* __restrict__ col_tasks, int32_t ncol, int32_t nranges_col,
+__global__ __launch_bounds__(kBlock) void dq_finalize(int32_t ncol, int32_t nranges_col,
                                                       const ColPartial* __restrict__ col_part,
-                                                      const uint8_t* __restrict__ hll_part, ColPartial* __restrict__ col_acc,
-                                                      uint8_t* __restrict__ hll_acc, int32_t npair, int32_t nranges_pair,
+                                                      ColPartial* __restrict__ col_acc, int32_t npair, int32_t nranges_pair,
                                                       const CorrPartial* __restrict__ pair_part,
                                                       CorrPartial* __restrict__ pair_acc, int32_t has_pred,
                                                       int32_t nranges_pred, const PredPartial* __restrict__ pred_part,
@@ -702,17 +707,6 @@ __global__ __launch_bounds__(kBlock) void dq_finalize(const ColTask* __restrict_
       ColStats acc = stats_load(col_acc + b);
       stats_merge(acc, cs[0]);
       stats_store(col_acc + b, acc);
-    }
-    const int hs = col_tasks[b].hll_slot;
-    if (hs >= 0) {
-      for (int i = tid; i < 512; i += kBlock) {
-        uint32_t m = hll_acc[(size_t)hs * 512 + i];
-        for (int r = 0; r < nranges_col; ++r) {
-          uint32_t v = hll_part[((size_t)hs * kMaxWG + r) * 512 + i];
-          m = v > m ? v : m;
-        }
-        hll_acc[(size_t)hs * 512 + i] = (uint8_t)m;
-      }
     }
   } else if (b < ncol + npair) {
     const int p = b - ncol;
@@ -768,9 +762,9 @@ hipError_t launch_pred_scan(const PredProgram* prog, const ScanCols& cols, const
 
 hipError_t launch_column_scan(const ColTask* tasks, int32_t ntasks, const ScanCols& cols, const ScanBitmaps& bm,
                               int64_t n_rows, int64_t rows_per_range, int32_t nranges, ColPartial* partials,
-                              uint8_t* hll_partials, hipStream_t st) {
+                              uint32_t* hll_acc, hipStream_t st) {
   hipLaunchKernelGGL(dq_column_scan, dim3((uint32_t)ntasks * (uint32_t)nranges), dim3(kBlock), 0, st, tasks, ntasks,
-                     cols, bm, n_rows, rows_per_range, partials, hll_partials);
+                     cols, bm, n_rows, rows_per_range, partials, hll_acc);
   return hipGetLastError();
 }
 
@@ -782,15 +776,14 @@ hipError_t launch_pair_scan(const PairTask* tasks, int32_t ntasks, const ScanCol
   return hipGetLastError();
 }
 
-hipError_t launch_finalize(const ColTask* col_tasks, int32_t ncol, int32_t nranges_col, const ColPartial* col_part,
-                           const uint8_t* hll_part, ColPartial* col_acc, uint8_t* hll_acc, int32_t npair,
-                           int32_t nranges_pair, const CorrPartial* pair_part, CorrPartial* pair_acc, int32_t has_pred,
-                           int32_t nranges_pred, const PredPartial* pred_part, PredPartial* pred_acc, hipStream_t st) {
+hipError_t launch_finalize(int32_t ncol, int32_t nranges_col, const ColPartial* col_part, ColPartial* col_acc,
+                           int32_t npair, int32_t nranges_pair, const CorrPartial* pair_part, CorrPartial* pair_acc,
+                           int32_t has_pred, int32_t nranges_pred, const PredPartial* pred_part, PredPartial* pred_acc,
+                           hipStream_t st) {
   const uint32_t nb = (uint32_t)(ncol + npair + (has_pred ? 1 : 0));
   if (nb == 0) return hipSuccess;
-  hipLaunchKernelGGL(dq_finalize, dim3(nb), dim3(kBlock), 0, st, col_tasks, ncol, nranges_col, col_part, hll_part,
-                     col_acc, hll_acc, npair, nranges_pair, pair_part, pair_acc, has_pred, nranges_pred, pred_part,
-                     pred_acc);
+  hipLaunchKernelGGL(dq_finalize, dim3(nb), dim3(kBlock), 0, st, ncol, nranges_col, col_part, col_acc, npair,
+                     nranges_pair, pair_part, pair_acc, has_pred, nranges_pred, pred_part, pred_acc);
   return hipGetLastError();
 }
 

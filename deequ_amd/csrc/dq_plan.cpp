@@ -30,14 +30,14 @@ hipError_t launch_pred_scan(const PredProgram* prog, const ScanCols& cols, const
                             int64_t rows_per_range, int32_t nranges, PredPartial* partials, hipStream_t st);
 hipError_t launch_column_scan(const ColTask* tasks, int32_t ntasks, const ScanCols& cols, const ScanBitmaps& bm,
                               int64_t n_rows, int64_t rows_per_range, int32_t nranges, ColPartial* partials,
-                              uint8_t* hll_partials, hipStream_t st);
+                              uint32_t* hll_acc, hipStream_t st);
 hipError_t launch_pair_scan(const PairTask* tasks, int32_t ntasks, const ScanCols& cols, const ScanBitmaps& bm,
                             int64_t n_rows, int64_t rows_per_range, int32_t nranges, CorrPartial* partials,
                             hipStream_t st);
-hipError_t launch_finalize(const ColTask* col_tasks, int32_t ncol, int32_t nranges_col, const ColPartial* col_part,
-                           const uint8_t* hll_part, ColPartial* col_acc, uint8_t* hll_acc, int32_t npair,
-                           int32_t nranges_pair, const CorrPartial* pair_part, CorrPartial* pair_acc, int32_t has_pred,
-                           int32_t nranges_pred, const PredPartial* pred_part, PredPartial* pred_acc, hipStream_t st);
+hipError_t launch_finalize(int32_t ncol, int32_t nranges_col, const ColPartial* col_part, ColPartial* col_acc,
+                           int32_t npair, int32_t nranges_pair, const CorrPartial* pair_part, CorrPartial* pair_acc,
+                           int32_t has_pred, int32_t nranges_pred, const PredPartial* pred_part, PredPartial* pred_acc,
+                           hipStream_t st);
 hipError_t launch_init_acc(ColPartial* col_acc, int32_t ncol, CorrPartial* pair_acc, int32_t npair, hipStream_t st);
 
 static thread_local char g_err[1024] = "";
@@ -394,11 +394,10 @@ struct dq_plan {
   PairTask* d_pair_tasks = nullptr;
   PredProgram* d_prog = nullptr;
   ColPartial* d_col_part = nullptr;
-  uint8_t* d_hll_part = nullptr;
   CorrPartial* d_pair_part = nullptr;
   PredPartial* d_pred_part = nullptr;
   ColPartial* d_col_acc = nullptr;
-  uint8_t* d_hll_acc = nullptr;
+  uint32_t* d_hll_acc = nullptr;
   CorrPartial* d_pair_acc = nullptr;
   PredPartial* d_pred_acc = nullptr;
   uint64_t* d_where_bits[kMaxWhere] = {nullptr};
@@ -461,7 +460,7 @@ static dq_status free_plan_mem(dq_plan* p) {
   p->pending.clear();
   for (hipEvent_t e : p->ev_pool) (void)hipEventDestroy(e);
   p->ev_pool.clear();
-  void* ptrs[] = {p->d_col_tasks, p->d_pair_tasks, p->d_prog, p->d_col_part, p->d_hll_part, p->d_pair_part,
+  void* ptrs[] = {p->d_col_tasks, p->d_pair_tasks, p->d_prog, p->d_col_part, p->d_pair_part,
                   p->d_pred_part, p->d_col_acc, p->d_hll_acc, p->d_pair_acc, p->d_pred_acc};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
@@ -473,7 +472,7 @@ static dq_status free_plan_mem(dq_plan* p) {
 static dq_status reset_acc(dq_plan* p) {
   HIP_TRY(launch_init_acc(p->d_col_acc, (int32_t)p->col_tasks.size(), p->d_pair_acc, (int32_t)p->pair_tasks.size(),
                           p->stream));
-  if (p->n_hll) HIP_TRY(hipMemsetAsync(p->d_hll_acc, 0, (size_t)p->n_hll * 512, p->stream));
+  if (p->n_hll) HIP_TRY(hipMemsetAsync(p->d_hll_acc, 0, (size_t)p->n_hll * 512 * sizeof(uint32_t), p->stream));
   if (p->has_pred) HIP_TRY(hipMemsetAsync(p->d_pred_acc, 0, sizeof(PredPartial), p->stream));
   p->total_rows = 0;
   p->next_chunk = 0;
@@ -715,11 +714,10 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
   if (dq_status s = dmalloc(&p->d_pair_tasks, npt * sizeof(PairTask))) return s;
   if (dq_status s = dmalloc(&p->d_prog, sizeof(PredProgram))) return s;
   if (dq_status s = dmalloc(&p->d_col_part, nct * kMaxWG * sizeof(ColPartial))) return s;
-  if (dq_status s = dmalloc(&p->d_hll_part, (size_t)p->n_hll * kMaxWG * 512)) return s;
   if (dq_status s = dmalloc(&p->d_pair_part, npt * kMaxWG * sizeof(CorrPartial))) return s;
   if (dq_status s = dmalloc(&p->d_pred_part, (p->has_pred ? kMaxWG : 1) * sizeof(PredPartial))) return s;
   if (dq_status s = dmalloc(&p->d_col_acc, nct * sizeof(ColPartial))) return s;
-  if (dq_status s = dmalloc(&p->d_hll_acc, (size_t)p->n_hll * 512)) return s;
+  if (dq_status s = dmalloc(&p->d_hll_acc, (size_t)p->n_hll * 512 * sizeof(uint32_t))) return s;
   if (dq_status s = dmalloc(&p->d_pair_acc, npt * sizeof(CorrPartial))) return s;
   if (dq_status s = dmalloc(&p->d_pred_acc, sizeof(PredPartial))) return s;
   if (nct) HIP_TRY(hipMemcpyAsync(p->d_col_tasks, p->col_tasks.data(), nct * sizeof(ColTask), hipMemcpyHostToDevice, p->stream));
@@ -830,7 +828,9 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
   for (int b = 0; b < kMaxWhere; ++b) bm.where_bits[b] = p->d_where_bits[b];
 
   // row ranges: column / pair passes in multiples of 2048 rows, predicate pass in multiples of 256
-  int32_t nr_col = (int32_t)std::min<int64_t>(kMaxWG, ceil_div(n_rows, kRowsPerIter));
+  const int64_t ntask_col = std::max<int64_t>(1, (int64_t)(p->col_tasks.size() + p->pair_tasks.size()));
+  const int64_t want = std::max<int64_t>(64, std::min<int64_t>(kMaxWG, kTargetWGs / ntask_col));
+  int32_t nr_col = (int32_t)std::min<int64_t>(want, ceil_div(n_rows, kRowsPerIter));
   int64_t rpr_col = ceil_div(ceil_div(n_rows, nr_col), kRowsPerIter) * kRowsPerIter;
   nr_col = (int32_t)ceil_div(n_rows, rpr_col);
   int32_t nr_pred = (int32_t)std::min<int64_t>(kMaxWG, ceil_div(n_rows, kPredRowsPerIter));
@@ -845,7 +845,7 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
   if (!p->col_tasks.empty())
     if (dq_status s = timed(p, 1, [&] {
           return launch_column_scan(p->d_col_tasks, (int32_t)p->col_tasks.size(), sc, bm, n_rows, rpr_col, nr_col,
-                                    p->d_col_part, p->d_hll_part, p->stream);
+                                    p->d_col_part, p->d_hll_acc, p->stream);
         }))
       return s;
   if (!p->pair_tasks.empty())
@@ -855,9 +855,9 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
         }))
       return s;
   if (dq_status s = timed(p, 3, [&] {
-        return launch_finalize(p->d_col_tasks, (int32_t)p->col_tasks.size(), nr_col, p->d_col_part, p->d_hll_part,
-                               p->d_col_acc, p->d_hll_acc, (int32_t)p->pair_tasks.size(), nr_col, p->d_pair_part,
-                               p->d_pair_acc, p->has_pred ? 1 : 0, nr_pred, p->d_pred_part, p->d_pred_acc, p->stream);
+        return launch_finalize((int32_t)p->col_tasks.size(), nr_col, p->d_col_part, p->d_col_acc,
+                               (int32_t)p->pair_tasks.size(), nr_col, p->d_pair_part, p->d_pair_acc,
+                               p->has_pred ? 1 : 0, nr_pred, p->d_pred_part, p->d_pred_acc, p->stream);
       }))
     return s;
   p->total_rows += n_rows;
@@ -869,11 +869,12 @@ dq_status dq_finish(dq_plan* p, dq_state* out) {
   if (!out && !p->specs.empty()) return set_error(DQ_E_INVALID, "dq_finish: out is NULL");
   HIP_TRY(hipSetDevice(p->device));
   std::vector<ColPartial> col(p->col_tasks.size());
-  std::vector<uint8_t> hll((size_t)p->n_hll * 512);
+  std::vector<uint32_t> hll((size_t)p->n_hll * 512);
   std::vector<CorrPartial> pair(p->pair_tasks.size());
   PredPartial pred{};
   if (!col.empty()) HIP_TRY(hipMemcpyAsync(col.data(), p->d_col_acc, col.size() * sizeof(ColPartial), hipMemcpyDeviceToHost, p->stream));
-  if (!hll.empty()) HIP_TRY(hipMemcpyAsync(hll.data(), p->d_hll_acc, hll.size(), hipMemcpyDeviceToHost, p->stream));
+  if (!hll.empty())
+    HIP_TRY(hipMemcpyAsync(hll.data(), p->d_hll_acc, hll.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, p->stream));
   if (!pair.empty()) HIP_TRY(hipMemcpyAsync(pair.data(), p->d_pair_acc, pair.size() * sizeof(CorrPartial), hipMemcpyDeviceToHost, p->stream));
   if (p->has_pred) HIP_TRY(hipMemcpyAsync(&pred, p->d_pred_acc, sizeof(PredPartial), hipMemcpyDeviceToHost, p->stream));
   HIP_TRY(hipStreamSynchronize(p->stream));
@@ -945,7 +946,12 @@ dq_status dq_finish(dq_plan* p, dq_state* out) {
         break;
       }
       case DQ_OP_APPROX_COUNT_DISTINCT:
-        hll_registers_to_words(hll.data() + (size_t)p->col_tasks[o.col_task].hll_slot * 512, s.u.hll.words);
+        {
+          uint8_t regs[512];
+          const uint32_t* r = hll.data() + (size_t)p->col_tasks[o.col_task].hll_slot * 512;
+          for (int k = 0; k < 512; ++k) regs[k] = (uint8_t)r[k];
+          hll_registers_to_words(regs, s.u.hll.words);
+        }
         set1(true);  // nullable = false (StatefulHyperloglogPlus.scala:59)
         break;
     }
