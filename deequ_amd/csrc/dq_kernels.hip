@@ -4,10 +4,10 @@
 // per-partition partial aggregate followed by a final merge.  Here one scan of a row chunk is:
 //   1. dq_pred_scan   (only if predicates exist): three-valued predicate program per row ->
 //                     Compliance / conditional-count counters, and `where` TRUE bitmaps.
-//   2. dq_column_scan: ONE launch for every single-column task (Completeness, Sum, Mean,
-//                     StandardDeviation, Minimum, Maximum, ApproxCountDistinct).  Workgroups are
-//                     interleaved task-fastest (blockIdx % ntasks) so HBM-bound and VALU-bound
-//                     (XXH64) column tasks run side by side on all 256 CUs.
+//   2. dq_column_scan<V>: single-column tasks (Completeness, Sum, Mean, StandardDeviation,
+//                     Minimum, Maximum, ApproxCountDistinct), one launch per variant V (column kind x
+//                     accumulators), optionally spread over several HIP streams so HBM-bound and
+//                     VALU-bound (XXH64) variants run side by side on the 256 CUs.
 //   3. dq_pair_scan   (only if Correlations exist): co-moments per column pair.
 //   4. dq_finalize:   fixed-order merge of the per-workgroup partials, then in-order merge into
 //                     the plan's accumulators (chunk order) -> results are deterministic.
@@ -328,11 +328,55 @@ __device__ void numeric_range(const void* values, const uint32_t* validity, cons
   }
 }
 
-// UTF8 column: one row per lane per step (rows base + 64*j + lane), offsets int32 or int64.
+// XXH64.hashUnsafeBytes of a string of len <= 28 bytes held in w[0..6] (little-endian dwords of the
+// string itself).  Branch-free: every lane runs 3 stripe rounds, one 4-byte round and 3 byte rounds
+// and keeps the ones its length needs, so a wave of mixed lengths does not diverge.
+__device__ __forceinline__ uint64_t xxh64_short(const uint32_t (&w)[7], uint32_t len) {
+  uint64_t h = kSeed + XP5 + (uint64_t)len;
+  const uint32_t nw = len >> 3;
+#pragma unroll
+  for (uint32_t k = 0; k < 3; ++k) {
+    const uint64_t k1 = ((uint64_t)w[2 * k + 1] << 32) | w[2 * k];
+    uint64_t hn = h ^ (rotl64(k1 * XP2, 31) * XP1);
+    hn = rotl64(hn, 27) * XP1 + XP4;
+    h = k < nw ? hn : h;
+  }
+  // 4-byte round on dword 2*nw
+  const uint32_t d4 = nw == 0 ? w[0] : (nw == 1 ? w[2] : (nw == 2 ? w[4] : w[6]));
+  uint64_t h4 = h ^ ((uint64_t)d4 * XP1);
+  h4 = rotl64(h4, 23) * XP2 + XP3;
+  h = (len & 4u) ? h4 : h;
+  // byte rounds on dword len >> 2
+  const uint32_t pb = len >> 2;
+  uint32_t db = w[0];
+#pragma unroll
+  for (uint32_t k = 1; k < 7; ++k) db = pb == k ? w[k] : db;
+  const uint32_t nb = len & 3u;
+#pragma unroll
+  for (uint32_t j = 0; j < 3; ++j) {
+    const uint64_t b = (db >> (8 * j)) & 0xFFu;
+    uint64_t hb = h ^ (b * XP5);
+    hb = rotl64(hb, 11) * XP1;
+    h = j < nb ? hb : h;
+  }
+  return fmix64(h);
+}
+
+// UTF8 column: one row per lane per step (rows base + 64*j + lane).  Offsets are read coalesced;
+// each string of <= 28 bytes is fetched with two 16-byte buffer loads (dword-aligned, bounded by
+// the range's last offset so nothing past the data is touched) and hashed branch-free; longer
+// strings take the general XXH64 loop.
 template <typename OffT>
 __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint32_t* validity,
                            const uint32_t* mask, int64_t row0, int64_t row1, ColStats& s, uint32_t* regs) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (row0 >= row1) return;
+  // byte window of this range, addressed by a 32-bit buffer offset from a dword-aligned base
+  const int64_t lo = (int64_t)offsets[row0] & ~int64_t(3);
+  const int64_t hi = (int64_t)offsets[row1];
+  const bool fast_ok = (hi - lo) < (int64_t)0x7FFFFFF0;
+  const __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(data + lo), (short)0, fast_ok ? (int)(hi - lo) : 0, 0x00020000);
   for (int64_t blk = row0; blk < row1; blk += kRowsPerIter) {
     const int64_t base = blk + (int64_t)wave * 512;
 #pragma unroll 2
@@ -347,7 +391,22 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
       s.count += b ? 1 : 0;
       if (b) {
         const int64_t o0 = (int64_t)offsets[row], o1 = (int64_t)offsets[row + 1];
-        hll_update(regs, xxh64_bytes(data, o0, o1 - o0));
+        const int64_t len = o1 - o0;
+        uint64_t h;
+        if (fast_ok && len <= 28) {
+          const int32_t off = (int32_t)((o0 - lo) & ~int64_t(3));
+          const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0);
+          const u32x4 c = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off + 16, 0, 0);
+          const uint32_t d[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+          const uint32_t sh = (uint32_t)(o0 & 3) * 8u;
+          uint32_t wv[7];
+#pragma unroll
+          for (int k = 0; k < 7; ++k) wv[k] = sh ? __builtin_amdgcn_alignbit(d[k + 1], d[k], sh) : d[k];
+          h = xxh64_short(wv, (uint32_t)len);
+        } else {
+          h = xxh64_bytes(data, o0, len);
+        }
+        hll_update(regs, h);
       }
     }
   }
@@ -376,14 +435,41 @@ __device__ void run_numeric(const ColTask& t, const ScanCols& cols, const ScanBi
 }
 
 // ------------------------------------------------------------------------------------------
-// Kernel 2: all single-column tasks of one chunk in one launch.
-// grid = ntasks * nranges; workgroup b -> task b % ntasks, row range b / ntasks.
+// Kernel 2: single-column tasks.  One kernel instantiation per variant (kind x accumulators), so
+// each launch carries only its own inner loop (small I-cache footprint); the tasks of one variant
+// share a launch, interleaved task-fastest: workgroup b -> task b % ntasks, row range b / ntasks.
 // ------------------------------------------------------------------------------------------
+template <int V>
+__device__ __forceinline__ void run_variant(const ColTask& t, const ScanCols& cols, const uint32_t* mask, int64_t row0,
+                                            int64_t row1, ColStats& s, uint32_t* regs) {
+  const void* v = cols.values[t.col];
+  const uint32_t* val = cols.validity[t.col];
+  if constexpr (V == CV_VALIDITY) validity_range(val, mask, row0, row1, s);
+  else if constexpr (V == CV_F64_S) numeric_range<CK_F64, true, false>(v, val, mask, row0, row1, s, regs);
+  else if constexpr (V == CV_F64_SH) numeric_range<CK_F64, true, true>(v, val, mask, row0, row1, s, regs);
+  else if constexpr (V == CV_F64_H) numeric_range<CK_F64, false, true>(v, val, mask, row0, row1, s, regs);
+  else if constexpr (V == CV_I64_S) numeric_range<CK_I64, true, false>(v, val, mask, row0, row1, s, regs);
+  else if constexpr (V == CV_I64_SH) numeric_range<CK_I64, true, true>(v, val, mask, row0, row1, s, regs);
+  else if constexpr (V == CV_I64_H) numeric_range<CK_I64, false, true>(v, val, mask, row0, row1, s, regs);
+  else if constexpr (V == CV_I32_S) numeric_range<CK_I32, true, false>(v, val, mask, row0, row1, s, regs);
+  else if constexpr (V == CV_I32_SH) numeric_range<CK_I32, true, true>(v, val, mask, row0, row1, s, regs);
+  else if constexpr (V == CV_I32_H) numeric_range<CK_I32, false, true>(v, val, mask, row0, row1, s, regs);
+  else if constexpr (V == CV_UTF8_H)
+    utf8_range<int32_t>(reinterpret_cast<const uint8_t*>(v), reinterpret_cast<const int32_t*>(cols.offsets[t.col]),
+                        val, mask, row0, row1, s, regs);
+  else
+    utf8_range<int64_t>(reinterpret_cast<const uint8_t*>(v), reinterpret_cast<const int64_t*>(cols.offsets[t.col]),
+                        val, mask, row0, row1, s, regs);
+}
+
+template <int V>
 __global__ __launch_bounds__(kBlock) void dq_column_scan(const ColTask* __restrict__ tasks, int32_t ntasks,
-                                                         ScanCols cols, ScanBitmaps bm, int64_t n_rows,
-                                                         int64_t rows_per_range, ColPartial* __restrict__ partials,
+                                                         int32_t part_base, ScanCols cols, ScanBitmaps bm,
+                                                         int64_t n_rows, int64_t rows_per_range,
+                                                         ColPartial* __restrict__ partials,
                                                          uint32_t* __restrict__ hll_acc) {
-  __shared__ uint32_t regs[512];
+  constexpr bool kHll = !(V == CV_VALIDITY || V == CV_F64_S || V == CV_I64_S || V == CV_I32_S);
+  __shared__ uint32_t regs[kHll ? 512 : 1];
   __shared__ ColStats red[kWaves];
   const int32_t ti = blockIdx.x % ntasks;
   const int32_t range = blockIdx.x / ntasks;
@@ -391,39 +477,16 @@ __global__ __launch_bounds__(kBlock) void dq_column_scan(const ColTask* __restri
   const int64_t row0 = (int64_t)range * rows_per_range;
   int64_t row1 = row0 + rows_per_range;
   if (row1 > n_rows) row1 = n_rows;
-  const bool hll = t.hll_slot >= 0;
-  if (hll) {
+  if constexpr (kHll) {
     for (int i = threadIdx.x; i < 512; i += kBlock) regs[i] = 0;
     __syncthreads();
   }
   ColStats s;
   stats_init(s);
   const uint32_t* mask = t.where >= 0 ? reinterpret_cast<const uint32_t*>(bm.where_bits[t.where]) : nullptr;
-  switch (t.variant) {
-    case CV_VALIDITY: validity_range(cols.validity[t.col], mask, row0, row1, s); break;
-    case CV_F64_S: run_numeric<CK_F64, true, false>(t, cols, bm, row0, row1, s, regs); break;
-    case CV_F64_SH: run_numeric<CK_F64, true, true>(t, cols, bm, row0, row1, s, regs); break;
-    case CV_F64_H: run_numeric<CK_F64, false, true>(t, cols, bm, row0, row1, s, regs); break;
-    case CV_I64_S: run_numeric<CK_I64, true, false>(t, cols, bm, row0, row1, s, regs); break;
-    case CV_I64_SH: run_numeric<CK_I64, true, true>(t, cols, bm, row0, row1, s, regs); break;
-    case CV_I64_H: run_numeric<CK_I64, false, true>(t, cols, bm, row0, row1, s, regs); break;
-    case CV_I32_S: run_numeric<CK_I32, true, false>(t, cols, bm, row0, row1, s, regs); break;
-    case CV_I32_SH: run_numeric<CK_I32, true, true>(t, cols, bm, row0, row1, s, regs); break;
-    case CV_I32_H: run_numeric<CK_I32, false, true>(t, cols, bm, row0, row1, s, regs); break;
-    case CV_UTF8_H:
-      utf8_range<int32_t>(reinterpret_cast<const uint8_t*>(cols.values[t.col]),
-                          reinterpret_cast<const int32_t*>(cols.offsets[t.col]), cols.validity[t.col], mask, row0,
-                          row1, s, regs);
-      break;
-    case CV_LUTF8_H:
-      utf8_range<int64_t>(reinterpret_cast<const uint8_t*>(cols.values[t.col]),
-                          reinterpret_cast<const int64_t*>(cols.offsets[t.col]), cols.validity[t.col], mask, row0,
-                          row1, s, regs);
-      break;
-    default: break;
-  }
-  block_reduce_store(s, partials + (size_t)ti * kMaxWG + range, red);
-  if (hll) {
+  run_variant<V>(t, cols, mask, row0, row1, s, regs);
+  block_reduce_store(s, partials + (size_t)(part_base + ti) * kMaxWG + range, red);
+  if constexpr (kHll) {
     // registers only grow: merge into the plan accumulator with device-scope atomicMax, skipping
     // registers the (possibly stale) accumulator already covers -- max is order-free, so the
     // result is deterministic.
@@ -729,11 +792,21 @@ __global__ __launch_bounds__(kBlock) void dq_finalize(int32_t ncol, int32_t nran
       q.n = acc.n; q.xa = acc.xa; q.ya = acc.ya; q.ck = acc.ck; q.xm = acc.xm; q.ym = acc.ym;
     }
   } else if (has_pred) {
+    // 256 threads = kMaxCounters counters x 8 range groups; integer sums are order-free
+    static_assert(kBlock % kMaxCounters == 0, "counter layout");
+    constexpr int G = kBlock / kMaxCounters;
+    __shared__ int64_t st[G][kMaxCounters], sn[G][kMaxCounters];
+    const int c = tid % kMaxCounters, g = tid / kMaxCounters;
+    int64_t t = 0, nn = 0;
+    for (int r = g; r < nranges_pred; r += G) { t += pred_part[r].t[c]; nn += pred_part[r].nn[c]; }
+    st[g][c] = t;
+    sn[g][c] = nn;
+    __syncthreads();
     if (tid < kMaxCounters) {
-      int64_t t = pred_acc->t[tid], nn = pred_acc->nn[tid];
-      for (int r = 0; r < nranges_pred; ++r) { t += pred_part[r].t[tid]; nn += pred_part[r].nn[tid]; }
-      pred_acc->t[tid] = t;
-      pred_acc->nn[tid] = nn;
+      int64_t a = pred_acc->t[tid], b = pred_acc->nn[tid];
+      for (int k = 0; k < G; ++k) { a += st[k][tid]; b += sn[k][tid]; }
+      pred_acc->t[tid] = a;
+      pred_acc->nn[tid] = b;
     }
   }
 }
@@ -760,11 +833,26 @@ hipError_t launch_pred_scan(const PredProgram* prog, const ScanCols& cols, const
   return hipGetLastError();
 }
 
-hipError_t launch_column_scan(const ColTask* tasks, int32_t ntasks, const ScanCols& cols, const ScanBitmaps& bm,
-                              int64_t n_rows, int64_t rows_per_range, int32_t nranges, ColPartial* partials,
-                              uint32_t* hll_acc, hipStream_t st) {
-  hipLaunchKernelGGL(dq_column_scan, dim3((uint32_t)ntasks * (uint32_t)nranges), dim3(kBlock), 0, st, tasks, ntasks,
-                     cols, bm, n_rows, rows_per_range, partials, hll_acc);
+template <int V>
+static void launch_v(const ColTask* tasks, int32_t ntasks, int32_t part_base, const ScanCols& cols,
+                     const ScanBitmaps& bm, int64_t n_rows, int64_t rows_per_range, int32_t nranges,
+                     ColPartial* partials, uint32_t* hll_acc, hipStream_t st) {
+  hipLaunchKernelGGL(dq_column_scan<V>, dim3((uint32_t)ntasks * (uint32_t)nranges), dim3(kBlock), 0, st, tasks, ntasks,
+                     part_base, cols, bm, n_rows, rows_per_range, partials, hll_acc);
+}
+
+// tasks [first, first + ntasks) of the plan's task table all have variant `variant`
+hipError_t launch_column_scan(int32_t variant, const ColTask* tasks, int32_t ntasks, int32_t part_base,
+                              const ScanCols& cols, const ScanBitmaps& bm, int64_t n_rows, int64_t rows_per_range,
+                              int32_t nranges, ColPartial* partials, uint32_t* hll_acc, hipStream_t st) {
+#define DQ_V(V)                                                                                             \
+  case V: launch_v<V>(tasks, ntasks, part_base, cols, bm, n_rows, rows_per_range, nranges, partials, hll_acc, st); break;
+  switch (variant) {
+    DQ_V(CV_VALIDITY) DQ_V(CV_F64_S) DQ_V(CV_F64_SH) DQ_V(CV_F64_H) DQ_V(CV_I64_S) DQ_V(CV_I64_SH) DQ_V(CV_I64_H)
+    DQ_V(CV_I32_S) DQ_V(CV_I32_SH) DQ_V(CV_I32_H) DQ_V(CV_UTF8_H) DQ_V(CV_LUTF8_H)
+    default: return hipErrorInvalidValue;
+  }
+#undef DQ_V
   return hipGetLastError();
 }
 

@@ -28,9 +28,9 @@ namespace dq {
 
 hipError_t launch_pred_scan(const PredProgram* prog, const ScanCols& cols, const ScanBitmaps& bm, int64_t n_rows,
                             int64_t rows_per_range, int32_t nranges, PredPartial* partials, hipStream_t st);
-hipError_t launch_column_scan(const ColTask* tasks, int32_t ntasks, const ScanCols& cols, const ScanBitmaps& bm,
-                              int64_t n_rows, int64_t rows_per_range, int32_t nranges, ColPartial* partials,
-                              uint32_t* hll_acc, hipStream_t st);
+hipError_t launch_column_scan(int32_t variant, const ColTask* tasks, int32_t ntasks, int32_t part_base,
+                              const ScanCols& cols, const ScanBitmaps& bm, int64_t n_rows, int64_t rows_per_range,
+                              int32_t nranges, ColPartial* partials, uint32_t* hll_acc, hipStream_t st);
 hipError_t launch_pair_scan(const PairTask* tasks, int32_t ntasks, const ScanCols& cols, const ScanBitmaps& bm,
                             int64_t n_rows, int64_t rows_per_range, int32_t nranges, CorrPartial* partials,
                             hipStream_t st);
@@ -383,8 +383,14 @@ struct dq_plan {
   std::vector<dq_analyzer_spec> specs;
   std::vector<SpecOut> outs;
 
-  std::vector<ColTask> col_tasks;
+  std::vector<ColTask> col_tasks;        // sorted by variant
+  struct Group { int32_t variant, first, count; };
+  std::vector<Group> groups;              // one column-scan launch per variant group
   std::vector<PairTask> pair_tasks;
+  int32_t concurrency = 1;                // HIP streams the variant launches are spread over
+  std::vector<hipStream_t> side;          // concurrency - 1 extra streams
+  std::vector<hipEvent_t> side_done;
+  hipEvent_t fork_ev = nullptr;
   PredProgram prog{};
   int32_t n_hll = 0;
   bool has_pred = false;
@@ -440,22 +446,27 @@ static dq_status resolve_timing(dq_plan* p) {
 
 // launch `fn` bracketed by timing events when enabled
 template <typename F>
-static dq_status timed(dq_plan* p, int kernel, F fn) {
+static dq_status timed(dq_plan* p, int kernel, hipStream_t st, F fn) {
   hipEvent_t a = nullptr, b = nullptr;
   if (p->timing) {
     if (dq_status s = take_event(p, &a)) return s;
     if (dq_status s = take_event(p, &b)) return s;
-    HIP_TRY(hipEventRecord(a, p->stream));
+    HIP_TRY(hipEventRecord(a, st));
   }
   HIP_TRY(fn());
   if (p->timing) {
-    HIP_TRY(hipEventRecord(b, p->stream));
+    HIP_TRY(hipEventRecord(b, st));
     p->pending.push_back({kernel, a, b});
   }
   return DQ_OK;
 }
 
 static dq_status free_plan_mem(dq_plan* p) {
+  for (hipStream_t st : p->side) (void)hipStreamDestroy(st);
+  for (hipEvent_t ev : p->side_done) (void)hipEventDestroy(ev);
+  if (p->fork_ev) (void)hipEventDestroy(p->fork_ev);
+  p->side.clear();
+  p->side_done.clear();
   for (auto& q : p->pending) { p->ev_pool.push_back(q.a); p->ev_pool.push_back(q.b); }
   p->pending.clear();
   for (hipEvent_t e : p->ev_pool) (void)hipEventDestroy(e);
@@ -659,6 +670,28 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
     }
   }
 
+  // sort column tasks by variant (stable), remap the analyzers' task indices, form launch groups
+  {
+    std::vector<int32_t> order(p->col_tasks.size());
+    for (size_t t = 0; t < order.size(); ++t) order[t] = (int32_t)t;
+    std::stable_sort(order.begin(), order.end(),
+                     [&](int32_t a, int32_t b) { return p->col_tasks[a].variant < p->col_tasks[b].variant; });
+    std::vector<int32_t> new_index(order.size());
+    std::vector<ColTask> sorted(order.size());
+    for (size_t k = 0; k < order.size(); ++k) {
+      sorted[k] = p->col_tasks[order[k]];
+      new_index[order[k]] = (int32_t)k;
+    }
+    p->col_tasks.swap(sorted);
+    for (SpecOut& o : p->outs)
+      if (o.col_task >= 0) o.col_task = new_index[o.col_task];
+    for (int32_t k = 0; k < (int32_t)p->col_tasks.size(); ++k) {
+      if (p->groups.empty() || p->groups.back().variant != p->col_tasks[k].variant)
+        p->groups.push_back({p->col_tasks[k].variant, k, 0});
+      p->groups.back().count++;
+    }
+  }
+
   // predicate program: roots in slot order, each followed by STORE
   p->has_pred = !root_code.empty() && (!counter_of.empty() || !bitmap_of.empty());
   PredProgram& prog = p->prog;
@@ -705,7 +738,7 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
     if (need_validity[c] && p->schema[c].nullable) b1000 += 125;
   }
   p->bytes_per_row_x1000 = b1000;
-  p->launches_per_scan = (p->has_pred ? 1 : 0) + (p->col_tasks.empty() ? 0 : 1) + (p->pair_tasks.empty() ? 0 : 1) +
+  p->launches_per_scan = (p->has_pred ? 1 : 0) + (int32_t)p->groups.size() + (p->pair_tasks.empty() ? 0 : 1) +
                          ((p->col_tasks.size() + p->pair_tasks.size() + (p->has_pred ? 1 : 0)) ? 1 : 0);
 
   // device allocations
@@ -725,6 +758,18 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
   HIP_TRY(hipMemcpyAsync(p->d_prog, &p->prog, sizeof(PredProgram), hipMemcpyHostToDevice, p->stream));
   if (dq_status s = reset_acc(p)) return s;
   HIP_TRY(hipStreamSynchronize(p->stream));
+  // concurrency: DQ_COLUMN_STREAMS (default 1) streams for the variant launches
+  if (const char* e = std::getenv("DQ_COLUMN_STREAMS")) p->concurrency = std::max(1, std::min(8, std::atoi(e)));
+  p->concurrency = std::min<int32_t>(p->concurrency, std::max<int32_t>(1, (int32_t)p->groups.size() + (npt ? 1 : 0)));
+  HIP_TRY(hipEventCreateWithFlags(&p->fork_ev, hipEventDisableTiming));
+  for (int32_t k = 1; k < p->concurrency; ++k) {
+    hipStream_t st;
+    hipEvent_t ev;
+    HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    p->side.push_back(st);
+    p->side_done.push_back(ev);
+  }
   return DQ_OK;
 }
 
@@ -838,23 +883,41 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
   nr_pred = (int32_t)ceil_div(n_rows, rpr_pred);
 
   if (p->has_pred)
-    if (dq_status s = timed(p, 0, [&] {
+    if (dq_status s = timed(p, 0, p->stream, [&] {
           return launch_pred_scan(p->d_prog, sc, bm, n_rows, rpr_pred, nr_pred, p->d_pred_part, p->stream);
         }))
       return s;
-  if (!p->col_tasks.empty())
-    if (dq_status s = timed(p, 1, [&] {
-          return launch_column_scan(p->d_col_tasks, (int32_t)p->col_tasks.size(), sc, bm, n_rows, rpr_col, nr_col,
-                                    p->d_col_part, p->d_hll_acc, p->stream);
+  // fork: variant launches (and the pair pass) round-robin over the plan stream + side streams
+  const int32_t K = p->concurrency;
+  if (K > 1) {
+    HIP_TRY(hipEventRecord(p->fork_ev, p->stream));
+    for (hipStream_t st : p->side) HIP_TRY(hipStreamWaitEvent(st, p->fork_ev, 0));
+  }
+  int32_t li = 0;
+  auto stream_for = [&](int32_t i) { return (K > 1 && i % K) ? p->side[i % K - 1] : p->stream; };
+  for (const auto& g : p->groups) {
+    hipStream_t st = stream_for(li++);
+    if (dq_status s = timed(p, 1, st, [&] {
+          return launch_column_scan(g.variant, p->d_col_tasks + g.first, g.count, g.first, sc, bm, n_rows, rpr_col,
+                                    nr_col, p->d_col_part, p->d_hll_acc, st);
         }))
       return s;
-  if (!p->pair_tasks.empty())
-    if (dq_status s = timed(p, 2, [&] {
+  }
+  if (!p->pair_tasks.empty()) {
+    hipStream_t st = stream_for(li++);
+    if (dq_status s = timed(p, 2, st, [&] {
           return launch_pair_scan(p->d_pair_tasks, (int32_t)p->pair_tasks.size(), sc, bm, n_rows, rpr_col, nr_col,
-                                  p->d_pair_part, p->stream);
+                                  p->d_pair_part, st);
         }))
       return s;
-  if (dq_status s = timed(p, 3, [&] {
+  }
+  if (K > 1) {  // join
+    for (int32_t k = 1; k < K; ++k) {
+      HIP_TRY(hipEventRecord(p->side_done[k - 1], p->side[k - 1]));
+      HIP_TRY(hipStreamWaitEvent(p->stream, p->side_done[k - 1], 0));
+    }
+  }
+  if (dq_status s = timed(p, 3, p->stream, [&] {
         return launch_finalize((int32_t)p->col_tasks.size(), nr_col, p->d_col_part, p->d_col_acc,
                                (int32_t)p->pair_tasks.size(), nr_col, p->d_pair_part, p->d_pair_acc,
                                p->has_pred ? 1 : 0, nr_pred, p->d_pred_part, p->d_pred_acc, p->stream);

@@ -771,6 +771,8 @@ class OracleExpr:
 
     def eval_bool(self, cols: dict, n: int):
         vals, typ, nn = self._ev(self.ast, cols, n)
+        if typ == "null":  # a bare NULL literal is a NULL boolean
+            return np.zeros(n, dtype=bool), np.zeros(n, dtype=bool)
         assert typ == "bool", f"predicate {self.text!r} is not boolean"
         return np.array([bool(x) for x in vals], dtype=bool) & nn, nn
 

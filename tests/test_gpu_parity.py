@@ -355,45 +355,55 @@ def test_configs_vs_oracle(dq, cfg):
     got = scan_states(t, analyzers)
     host = {name: host_column(c, n) for name, c in t.columns.items()}
     nparts = 8
+    errors = []
     for a in analyzers:
-        name = type(a).__name__
-        prod = got[a]
-        if name == "Size":
-            assert prod.numMatches == n
-        elif name == "Completeness":
-            assert prod.numMatches == int(host[a.column][1].sum()) and prod.count == n
-        elif name == "ApproxCountDistinct":
-            vals, valid, bm = host[a.column]
-            col = t.columns[a.column]
-            if col.dtype == "utf8":
-                offs = col.offsets.cpu().numpy()[: (n + 1) * 4].view(np.int32)
-                data = np.frombuffer(col.values.cpu().numpy().tobytes(), dtype=np.uint8)
-                regs = C.hll_registers("utf8", data, offs, bm, None, n)
-            else:
-                regs = C.hll_registers(col.dtype, vals, None, bm, None, n)
-            assert prod.words == tuple(O.registers_to_words(regs.tolist())), a
-        elif name == "Compliance":
-            cols = {k: O.OColumn(t.columns[k].dtype, host[k][0], host[k][1]) for k in ("i0", "i1", "i2", "i3")}
-            sub = 200_000  # python oracle evaluator on a prefix; the full count via numpy below
-            ref = O.compute_state(("Compliance", a.instance, a.predicate, None),
-                                  {k: O.OColumn(v.dtype, v.values[:sub], v.valid[:sub]) for k, v in cols.items()}, sub)
-            pre = dq.Compliance(a.instance, a.predicate)
-            from deequ_amd.table import column_from_numpy
-            dev_sub = dq.Table([column_from_numpy(k, "i64", cols[k].values[:sub], cols[k].valid[:sub]) for k in cols])
-            assert pre.computeStateFrom(dev_sub) == dq.NumMatchesAndCount(ref.numMatches, ref.count), a
-        elif name == "Correlation":
-            x, vx, bx = host[a.firstColumn]
-            y, vy, by = host[a.secondColumn]
-            r = C.corr("f64", x, bx, "f64", y, by, None, nparts)
-            assert_state_close(prod, O.CorrelationState(*r))
+        try:
+            _check_config_analyzer(dq, t, a, got[a], host, n, nparts)
+        except AssertionError as e:
+            errors.append(f"{a}: {e}")
+    assert not errors, "\n".join(errors[:20]) + f"\n({len(errors)} mismatches)"
+
+
+def _check_config_analyzer(dq, t, a, prod, host, n, nparts):
+    name = type(a).__name__
+    if name == "Size":
+        assert prod.numMatches == n
+    elif name == "Completeness":
+        assert prod.numMatches == int(host[a.column][1].sum()) and prod.count == n
+    elif name == "ApproxCountDistinct":
+        vals, valid, bm = host[a.column]
+        col = t.columns[a.column]
+        if col.dtype == "utf8":
+            offs = col.offsets.cpu().numpy()[: (n + 1) * 4].view(np.int32)
+            data = np.frombuffer(col.values.cpu().numpy().tobytes(), dtype=np.uint8)
+            regs = C.hll_registers("utf8", data, offs, bm, None, n)
         else:
-            vals, valid, bm = host[a.column]
-            dtype = t.columns[a.column].dtype
-            s = C.column_stats(dtype, vals, bm, None, nparts)
-            ref = {"Sum": lambda: O.SumState(s.sum_f64), "Mean": lambda: O.MeanState(s.sum_f64, s.count),
-                   "StandardDeviation": lambda: O.StandardDeviationState(s.n, s.avg, s.m2),
-                   "Minimum": lambda: O.MinState(s.min), "Maximum": lambda: O.MaxState(s.max)}[name]()
-            assert_state_close(prod, ref, scale=float(np.abs(vals.astype(np.float64)[valid]).sum()))
+            regs = C.hll_registers(col.dtype, vals, None, bm, None, n)
+        assert prod.words == tuple(O.registers_to_words(regs.tolist())), "HLL words differ"
+    elif name == "Compliance":
+        cols = {k: O.OColumn(t.columns[k].dtype, host[k][0], host[k][1]) for k in ("i0", "i1", "i2", "i3")}
+        sub = 200_000  # python oracle evaluator on a prefix
+        ref = O.compute_state(("Compliance", a.instance, a.predicate, None),
+                              {k: O.OColumn(v.dtype, v.values[:sub], v.valid[:sub]) for k, v in cols.items()}, sub)
+        from deequ_amd.table import column_from_numpy
+        dev_sub = dq.Table([column_from_numpy(k, "i64", cols[k].values[:sub], cols[k].valid[:sub]) for k in cols])
+        got = dq.Compliance(a.instance, a.predicate).computeStateFrom(dev_sub)
+        assert got == dq.NumMatchesAndCount(ref.numMatches, ref.count), (got, ref)
+    elif name == "Correlation":
+        x, vx, bx = host[a.firstColumn]
+        y, vy, by = host[a.secondColumn]
+        r = C.corr("f64", x, bx, "f64", y, by, None, nparts)
+        both = int((vx & vy).sum())
+        assert r[0] == both, f"oracle n {r[0]} != numpy both-valid {both}"
+        assert_state_close(prod, O.CorrelationState(*r))
+    else:
+        vals, valid, bm = host[a.column]
+        dtype = t.columns[a.column].dtype
+        s = C.column_stats(dtype, vals, bm, None, nparts)
+        ref = {"Sum": lambda: O.SumState(s.sum_f64), "Mean": lambda: O.MeanState(s.sum_f64, s.count),
+               "StandardDeviation": lambda: O.StandardDeviationState(s.n, s.avg, s.m2),
+               "Minimum": lambda: O.MinState(s.min), "Maximum": lambda: O.MaxState(s.max)}[name]()
+        assert_state_close(prod, ref, scale=float(np.abs(vals.astype(np.float64)[valid]).sum()))
 
 
 def test_incremental_state_provider_roundtrip(dq, tmp_path):
