@@ -19,6 +19,7 @@
 #include <type_traits>
 
 #include "dq_device.h"
+#include "dq_hash.h"
 
 namespace dq {
 
@@ -27,30 +28,6 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // ------------------------------------------------------------------------------------------
 // XXH64 (Spark XxHash64Function, seed 42) -- StatefulHyperloglogPlus.scala:93
 // ------------------------------------------------------------------------------------------
-constexpr uint64_t XP1 = 0x9E3779B185EBCA87ull;
-constexpr uint64_t XP2 = 0xC2B2AE3D27D4EB4Full;
-constexpr uint64_t XP3 = 0x165667B19E3779F9ull;
-constexpr uint64_t XP4 = 0x85EBCA77C2B2AE63ull;
-constexpr uint64_t XP5 = 0x27D4EB2F165667C5ull;
-constexpr uint64_t kSeed = 42;
-
-__device__ __forceinline__ uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
-__device__ __forceinline__ uint64_t fmix64(uint64_t h) {
-  h ^= h >> 33; h *= XP2; h ^= h >> 29; h *= XP3; h ^= h >> 32; return h;
-}
-__device__ __forceinline__ uint64_t xxh64_long(uint64_t v) {
-  uint64_t h = kSeed + XP5 + 8;
-  h ^= rotl64(v * XP2, 31) * XP1;
-  h = rotl64(h, 27) * XP1 + XP4;
-  return fmix64(h);
-}
-__device__ __forceinline__ uint64_t xxh64_int(uint32_t v) {
-  uint64_t h = kSeed + XP5 + 4;
-  h ^= (uint64_t)v * XP1;
-  h = rotl64(h, 23) * XP2 + XP3;
-  return fmix64(h);
-}
-
 // Byte reads from a 4-byte aligned buffer at an arbitrary byte position, via aligned dwords.
 __device__ __forceinline__ uint32_t ld32(const uint8_t* base, int64_t a) {
   return *reinterpret_cast<const uint32_t*>(base + a);
@@ -61,7 +38,7 @@ __device__ __forceinline__ uint32_t read4(const uint8_t* base, int64_t pos) {
   uint32_t w0 = ld32(base, a);
   if (sh == 0) return w0;
   uint32_t w1 = ld32(base, a + 4);
-  return __builtin_amdgcn_alignbit(w1, w0, sh);
+  return alignbit32(w1, w0, sh);
 }
 __device__ __forceinline__ uint64_t read8(const uint8_t* base, int64_t pos) {
   int64_t a = pos & ~int64_t(3);
@@ -69,8 +46,8 @@ __device__ __forceinline__ uint64_t read8(const uint8_t* base, int64_t pos) {
   uint32_t w0 = ld32(base, a), w1 = ld32(base, a + 4);
   if (sh == 0) return ((uint64_t)w1 << 32) | w0;
   uint32_t w2 = ld32(base, a + 8);
-  uint32_t lo = __builtin_amdgcn_alignbit(w1, w0, sh);
-  uint32_t hi = __builtin_amdgcn_alignbit(w2, w1, sh);
+  uint32_t lo = alignbit32(w1, w0, sh);
+  uint32_t hi = alignbit32(w2, w1, sh);
   return ((uint64_t)hi << 32) | lo;
 }
 
@@ -264,7 +241,13 @@ __device__ void block_reduce_store(ColStats s, ColPartial* out, ColStats* lds) {
   }
 }
 
-__device__ __forceinline__ uint32_t word_or_ones(const uint32_t* p, int64_t i) { return p ? p[i] : 0xFFFFFFFFu; }
+// Branch-free optional bitmap word: a missing bitmap reads word 0 of an all-ones buffer (the
+// pointer / index selects are wave-uniform scalar ops, so the loop body has no branches).
+__device__ const uint32_t kAllOnes[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+__device__ __forceinline__ uint32_t word_or_ones(const uint32_t* p, int64_t i) {
+  const uint32_t* q = p ? p : kAllOnes;
+  return q[p ? i : 0];
+}
 
 // 8-/4-byte numeric column: 16-byte loads, lane l of wave w holds rows
 //   base + k*64*R + l*R + [0, R)  (R = 16 / sizeof(T) rows per load, 8 / R loads)
@@ -290,8 +273,7 @@ __device__ void numeric_range(const void* values, const uint32_t* validity, cons
 #pragma unroll
       for (int k = 0; k < L; ++k) {
         const int64_t widx = (base + (int64_t)k * 64 * R) / 32 + (lane * R) / 32;
-        uint32_t w = word_or_ones(validity, widx);
-        if (mask) w &= mask[widx];
+        const uint32_t w = word_or_ones(validity, widx) & word_or_ones(mask, widx);
         uint32_t b = (w >> ((lane * R) & 31)) & ((1u << R) - 1u);
         bits |= b << (k * R);
         const T* e = reinterpret_cast<const T*>(&raw[k]);
@@ -328,40 +310,6 @@ __device__ void numeric_range(const void* values, const uint32_t* validity, cons
   }
 }
 
-// XXH64.hashUnsafeBytes of a string of len <= 28 bytes held in w[0..6] (little-endian dwords of the
-// string itself).  Branch-free: every lane runs 3 stripe rounds, one 4-byte round and 3 byte rounds
-// and keeps the ones its length needs, so a wave of mixed lengths does not diverge.
-__device__ __forceinline__ uint64_t xxh64_short(const uint32_t (&w)[7], uint32_t len) {
-  uint64_t h = kSeed + XP5 + (uint64_t)len;
-  const uint32_t nw = len >> 3;
-#pragma unroll
-  for (uint32_t k = 0; k < 3; ++k) {
-    const uint64_t k1 = ((uint64_t)w[2 * k + 1] << 32) | w[2 * k];
-    uint64_t hn = h ^ (rotl64(k1 * XP2, 31) * XP1);
-    hn = rotl64(hn, 27) * XP1 + XP4;
-    h = k < nw ? hn : h;
-  }
-  // 4-byte round on dword 2*nw
-  const uint32_t d4 = nw == 0 ? w[0] : (nw == 1 ? w[2] : (nw == 2 ? w[4] : w[6]));
-  uint64_t h4 = h ^ ((uint64_t)d4 * XP1);
-  h4 = rotl64(h4, 23) * XP2 + XP3;
-  h = (len & 4u) ? h4 : h;
-  // byte rounds on dword len >> 2
-  const uint32_t pb = len >> 2;
-  uint32_t db = w[0];
-#pragma unroll
-  for (uint32_t k = 1; k < 7; ++k) db = pb == k ? w[k] : db;
-  const uint32_t nb = len & 3u;
-#pragma unroll
-  for (uint32_t j = 0; j < 3; ++j) {
-    const uint64_t b = (db >> (8 * j)) & 0xFFu;
-    uint64_t hb = h ^ (b * XP5);
-    hb = rotl64(hb, 11) * XP1;
-    h = j < nb ? hb : h;
-  }
-  return fmix64(h);
-}
-
 // UTF8 column: one row per lane per step (rows base + 64*j + lane).  Offsets are read coalesced;
 // each string of <= 28 bytes is fetched with two 16-byte buffer loads (dword-aligned, bounded by
 // the range's last offset so nothing past the data is touched) and hashed branch-free; longer
@@ -393,7 +341,9 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
         const int64_t o0 = (int64_t)offsets[row], o1 = (int64_t)offsets[row + 1];
         const int64_t len = o1 - o0;
         uint64_t h;
-        if (fast_ok && len <= 28) {
+        // fast path only when both 16-byte loads lie inside [lo, hi): never rely on partially
+        // out-of-range buffer loads
+        if (fast_ok && len <= 28 && (o0 & ~int64_t(3)) + 32 <= hi) {
           const int32_t off = (int32_t)((o0 - lo) & ~int64_t(3));
           const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0);
           const u32x4 c = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off + 16, 0, 0);
@@ -401,7 +351,7 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
           const uint32_t sh = (uint32_t)(o0 & 3) * 8u;
           uint32_t wv[7];
 #pragma unroll
-          for (int k = 0; k < 7; ++k) wv[k] = sh ? __builtin_amdgcn_alignbit(d[k + 1], d[k], sh) : d[k];
+          for (int k = 0; k < 7; ++k) wv[k] = sh ? alignbit32(d[k + 1], d[k], sh) : d[k];
           h = xxh64_short(wv, (uint32_t)len);
         } else {
           h = xxh64_bytes(data, o0, len);

@@ -1,0 +1,29 @@
+// Host build of the kernels' XXH64 formulations (deequ_amd/csrc/dq_hash.h), driven by
+// tests/test_hash_formulation.py against the golden vectors.  Reads "len hex" lines on stdin and
+// prints the signed hash of xxh64_short() for every byte alignment 0..3 of the string.
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "../deequ_amd/csrc/dq_hash.h"
+
+int main() {
+  int len;
+  char hex[256];
+  while (std::scanf("%d %255s", &len, hex) == 2) {
+    unsigned char bytes[64] = {0};
+    for (int i = 0; i < len; ++i) std::sscanf(hex + 2 * i, "%2hhx", &bytes[i]);
+    for (int align = 0; align < 4; ++align) {
+      unsigned char buf[96] = {0};
+      std::memcpy(buf + align, bytes, len);
+      uint32_t d[8];
+      std::memcpy(d, buf, 32);
+      const uint32_t sh = align * 8u;
+      uint32_t w[7];
+      for (int k = 0; k < 7; ++k) w[k] = sh ? dq::alignbit32(d[k + 1], d[k], sh) : d[k];
+      std::printf("%lld%c", (long long)dq::xxh64_short(w, (uint32_t)len), align == 3 ? '\n' : ' ');
+    }
+  }
+  std::printf("LONG %lld INT %lld\n", (long long)dq::xxh64_long(42u), (long long)dq::xxh64_int(7u));
+  return 0;
+}

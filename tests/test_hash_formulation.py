@@ -1,0 +1,22 @@
+"""The kernels' branch-free short-string XXH64 (deequ_amd/csrc/dq_hash.h), built for the host,
+equals the golden vectors (independent `xxhash` package) for every length <= 28 and byte alignment."""
+import os
+import subprocess
+
+from tests.conftest import ROOT
+
+
+def test_short_string_formulation(tmp_path, hash_vectors):
+    exe = tmp_path / "hash_check"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-o", str(exe), os.path.join(ROOT, "tests", "hash_check.cpp")],
+                   check=True)
+    cases = [(len(bytes.fromhex(h)) if h else 0, h, v) for h, v in hash_vectors["bytes"]]
+    cases = [c for c in cases if c[0] <= 28]
+    inp = "".join(f"{n} {h or '00'}\n" for n, h, _ in cases)
+    out = subprocess.run([str(exe)], input=inp, capture_output=True, text=True, check=True).stdout.splitlines()
+    for (n, h, v), line in zip(cases, out):
+        assert [int(x) for x in line.split()] == [v] * 4, (n, h)
+    longs = dict((a, b) for a, b in hash_vectors["long"])
+    ints = dict((a, b) for a, b in hash_vectors["int"])
+    last = out[-1].split()
+    assert int(last[1]) == longs[42] and int(last[3]) == ints[7]
