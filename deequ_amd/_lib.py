@@ -21,6 +21,11 @@ DQ_E_STATE = -6
 
 TYPE_F64, TYPE_I64, TYPE_I32, TYPE_UTF8, TYPE_LARGE_UTF8 = 1, 2, 3, 4, 5
 
+# column-pass kernel variants (deequ_amd/csrc/dq_device.h ColVariant)
+VARIANT_NAMES = {0: "validity", 1: "f64_stats", 2: "f64_stats_hll", 3: "f64_hll", 4: "i64_stats",
+                 5: "i64_stats_hll", 6: "i64_hll", 7: "i32_stats", 8: "i32_stats_hll", 9: "i32_hll",
+                 10: "utf8_hll", 11: "large_utf8_hll"}
+
 OP_SIZE = 1
 OP_COMPLETENESS = 2
 OP_COMPLIANCE = 3
@@ -152,6 +157,8 @@ def _load():
     L.dq_plan_enable_timing.argtypes = [c.c_void_p, c.c_int32]
     L.dq_plan_kernel_time.restype = c.c_int32
     L.dq_plan_kernel_time.argtypes = [c.c_void_p, c.c_int32, P(c.c_double), P(c.c_int64)]
+    L.dq_plan_variant_bytes_per_row_x1000.restype = c.c_int64
+    L.dq_plan_variant_bytes_per_row_x1000.argtypes = [c.c_void_p, c.c_int32]
     L.dq_state_merge.restype = c.c_int32
     L.dq_state_merge.argtypes = [P(State), P(State), P(State)]
     L.dq_state_combine.restype = c.c_int32
@@ -179,7 +186,7 @@ lib = _load()
 EXPORTED = [
     "dq_abi_version", "dq_last_error", "dq_plan_create", "dq_plan_set_stream", "dq_scan", "dq_finish",
     "dq_plan_reset", "dq_plan_destroy", "dq_plan_bytes_per_row_x1000", "dq_plan_num_launches",
-    "dq_plan_enable_timing", "dq_plan_kernel_time",
+    "dq_plan_enable_timing", "dq_plan_kernel_time", "dq_plan_variant_bytes_per_row_x1000",
     "dq_state_merge", "dq_state_combine", "dq_state_is_defined", "dq_state_metric", "dq_hll_estimate",
     "dq_state_to_bytes", "dq_state_from_bytes", "dq_state_identifier",
 ]

@@ -417,8 +417,8 @@ struct dq_plan {
   std::vector<hipEvent_t> ev_pool;
   struct Pending { int kernel; hipEvent_t a, b; };
   std::vector<Pending> pending;
-  double kernel_ms[4] = {0, 0, 0, 0};
-  int64_t kernel_launches[4] = {0, 0, 0, 0};
+  double kernel_ms[32] = {0};       // 0 pred, 2 pair, 3 finalize, 16 + v column variant v
+  int64_t kernel_launches[32] = {0};
   int64_t bytes_per_row_x1000 = 0;
   int32_t launches_per_scan = 0;
 };
@@ -897,7 +897,7 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
   auto stream_for = [&](int32_t i) { return (K > 1 && i % K) ? p->side[i % K - 1] : p->stream; };
   for (const auto& g : p->groups) {
     hipStream_t st = stream_for(li++);
-    if (dq_status s = timed(p, 1, st, [&] {
+    if (dq_status s = timed(p, 16 + g.variant, st, [&] {
           return launch_column_scan(g.variant, p->d_col_tasks + g.first, g.count, g.first, sc, bm, n_rows, rpr_col,
                                     nr_col, p->d_col_part, p->d_hll_acc, st);
         }))
@@ -1044,18 +1044,39 @@ dq_status dq_plan_enable_timing(dq_plan* p, int32_t on) {
   HIP_TRY(hipSetDevice(p->device));
   if (dq_status s = resolve_timing(p)) return s;
   p->timing = on != 0;
-  for (int k = 0; k < 4; ++k) { p->kernel_ms[k] = 0; p->kernel_launches[k] = 0; }
+  for (int k = 0; k < 32; ++k) { p->kernel_ms[k] = 0; p->kernel_launches[k] = 0; }
   return DQ_OK;
 }
 
 dq_status dq_plan_kernel_time(dq_plan* p, int32_t kernel, double* total_ms, int64_t* launches) {
-  if (!p || kernel < 0 || kernel > 3 || !total_ms || !launches)
+  if (!p || kernel < 0 || kernel >= 32 || !total_ms || !launches)
     return set_error(DQ_E_INVALID, "dq_plan_kernel_time: bad argument");
   HIP_TRY(hipSetDevice(p->device));
   if (dq_status s = resolve_timing(p)) return s;
-  *total_ms = p->kernel_ms[kernel];
-  *launches = p->kernel_launches[kernel];
+  if (kernel == 1) {  // all column-scan variants
+    double ms = 0;
+    int64_t n = 0;
+    for (int k = 16; k < 32; ++k) { ms += p->kernel_ms[k]; n += p->kernel_launches[k]; }
+    *total_ms = ms;
+    *launches = n;
+  } else {
+    *total_ms = p->kernel_ms[kernel];
+    *launches = p->kernel_launches[kernel];
+  }
   return DQ_OK;
+}
+
+int64_t dq_plan_variant_bytes_per_row_x1000(const dq_plan* p, int32_t variant) {
+  if (!p) return 0;
+  int64_t b = 0;
+  for (const ColTask& t : p->col_tasks) {
+    if (t.variant != variant) continue;
+    const dq_column_desc& cd = p->schema[t.col];
+    if (t.variant != CV_VALIDITY) b += (cd.type == DQ_TYPE_I32 || cd.type == DQ_TYPE_UTF8) ? 4000 : 8000;
+    if (cd.nullable) b += 125;
+    if (t.where >= 0) b += 125;
+  }
+  return b;
 }
 int32_t dq_plan_num_launches(const dq_plan* p) { return p ? p->launches_per_scan : 0; }
 

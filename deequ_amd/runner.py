@@ -66,8 +66,12 @@ class ScanPlan:
     def enable_timing(self, on: bool = True) -> None:
         L.check(L.lib.dq_plan_enable_timing(self.handle, 1 if on else 0))
 
+    def variant_bytes_per_row(self, variant: int) -> float:
+        return L.lib.dq_plan_variant_bytes_per_row_x1000(self.handle, variant) / 1000.0
+
     def kernel_time(self, kernel: int):
-        """(total ms, launches) of kernel 0 pred / 1 column / 2 pair / 3 finalize since enable_timing."""
+        """(total ms, launches) of kernel 0 pred / 1 column (all) / 2 pair / 3 finalize / 16+v column
+        variant v, since enable_timing."""
         ms, n = ctypes.c_double(), ctypes.c_int64()
         L.check(L.lib.dq_plan_kernel_time(self.handle, kernel, ctypes.byref(ms), ctypes.byref(n)))
         return ms.value, n.value

@@ -165,12 +165,15 @@ void dq_plan_destroy(dq_plan* plan);
 int64_t dq_plan_bytes_per_row_x1000(const dq_plan* plan);
 /* Number of kernel launches one dq_scan issues. */
 int32_t dq_plan_num_launches(const dq_plan* plan);
-/* Optional per-kernel timing (hipEvents recorded on the plan's stream around every launch).
- * kernel: 0 = predicate pass, 1 = column pass, 2 = pair (correlation) pass, 3 = finalize.
+/* Optional per-kernel timing (hipEvents recorded on the launch stream around every launch).
+ * kernel: 0 = predicate pass, 1 = all column-pass launches, 2 = pair (correlation) pass,
+ * 3 = finalize, 16 + v = column-pass launches of variant v (see deequ_amd/csrc/dq_device.h).
  * dq_plan_kernel_time synchronises, then returns the summed duration and launch count since
  * timing was (re-)enabled. */
 dq_status dq_plan_enable_timing(dq_plan* plan, int32_t on);
 dq_status dq_plan_kernel_time(dq_plan* plan, int32_t kernel, double* total_ms, int64_t* launches);
+/* Algorithmic bytes per row (x1000) the column-pass launch of variant v reads (excl. UTF8 data). */
+int64_t dq_plan_variant_bytes_per_row_x1000(const dq_plan* plan, int32_t variant);
 
 /* State algebra.
  * dq_state_merge:   Analyzers.merge / State.sum on Option[State] (Analyzer.scala:343-362):

@@ -420,3 +420,21 @@ def test_incremental_state_provider_roundtrip(dq, tmp_path):
         for a in analyzers:
             x, y = inc.metric(a).value.get(), both.metric(a).value.get()
             assert close(x, y, 1e-12), (a, x, y)
+
+
+@pytest.mark.parametrize("cfg", ["c4", "c5"])
+def test_deterministic_repeat(dq, cfg):
+    """Fixed merge order everywhere: repeated scans are bitwise identical."""
+    from deequ_amd import synth
+    from deequ_amd.runner import scan_states
+
+    t = getattr(synth, f"{cfg}_table")(700_001, seed=8)
+    if cfg == "c4":
+        names = list(t.columns)
+        analyzers = [dq.Correlation(names[i], names[j]) for i in range(8) for j in range(i + 1, 8)]
+        analyzers += [dq.StandardDeviation(c) for c in names]
+    else:
+        analyzers = synth.profile_analyzers(t)
+    runs = [scan_states(t, analyzers) for _ in range(3)]
+    for a in analyzers:
+        assert repr(runs[0][a]) == repr(runs[1][a]) == repr(runs[2][a]), a

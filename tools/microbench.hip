@@ -1,0 +1,101 @@
+// microbench.hip -- ablation of the numeric column-scan inner loop on gfx950 (diagnostic only).
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I deequ_amd/csrc tools/microbench.hip -o /tmp/mb
+// Each kernel streams N doubles with the production load pattern (16 B per lane, 8 rows per lane per
+// iteration) and does a different amount of the per-value work; prints GB/s per variant.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdint>
+#include <vector>
+
+#include "dq_hash.h"
+
+using namespace dq;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+enum { LOAD_ONLY = 0, HASH_NOLDS = 1, HASH_LDS = 2, HASH_LDS_SKIP = 3, MUL_ONLY = 4 };
+
+template <int MODE>
+__global__ __launch_bounds__(256) void k(const double* __restrict__ v, int64_t n, int64_t rows_per_wg,
+                                         unsigned long long* out) {
+  __shared__ uint32_t regs[512];
+  for (int i = threadIdx.x; i < 512; i += 256) regs[i] = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t r0 = blockIdx.x * rows_per_wg, r1 = min(n, r0 + rows_per_wg);
+  uint64_t acc = 0;
+  for (int64_t blk = r0; blk + 2048 <= r1; blk += 2048) {
+    const int64_t base = blk + wave * 512;
+    u32x4 raw[4];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+      raw[kk] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(v + base + kk * 128) + lane);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        uint64_t x = ((uint64_t)raw[kk][2 * r + 1] << 32) | raw[kk][2 * r];
+        if (MODE == LOAD_ONLY) {
+          acc += x;
+        } else if (MODE == MUL_ONLY) {
+          acc += x * XP2;
+        } else {
+          uint64_t h = xxh64_long(x);
+          if (MODE == HASH_NOLDS) {
+            acc ^= h;
+          } else {
+            uint32_t idx = (uint32_t)(h >> 55);
+            uint32_t pw = (uint32_t)__clzll((long long)((h << 9) | 256ull)) + 1u;
+            if (MODE == HASH_LDS_SKIP) {
+              if (pw > 2) atomicMax(&regs[idx], pw);
+            } else {
+              atomicMax(&regs[idx], pw);
+            }
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (MODE >= HASH_LDS) acc += regs[threadIdx.x] + regs[threadIdx.x + 256];
+  if (acc == 0x123456789ull) out[0] = acc;  // keep live
+}
+
+__global__ void init(double* v, int64_t n) {
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    v[i] = (double)(i * 2654435761ull % 1000003ull) * 1.5;
+}
+
+template <int MODE>
+float run(const double* d, int64_t n, unsigned long long* out, int wgs) {
+  int64_t rpw = ((n + wgs - 1) / wgs + 2047) / 2048 * 2048;
+  int g = (int)((n + rpw - 1) / rpw);
+  hipEvent_t a, b;
+  hipEventCreate(&a);
+  hipEventCreate(&b);
+  hipLaunchKernelGGL(k<MODE>, dim3(g), dim3(256), 0, 0, d, n, rpw, out);
+  hipEventRecord(a);
+  for (int i = 0; i < 10; ++i) hipLaunchKernelGGL(k<MODE>, dim3(g), dim3(256), 0, 0, d, n, rpw, out);
+  hipEventRecord(b);
+  hipEventSynchronize(b);
+  float ms;
+  hipEventElapsedTime(&ms, a, b);
+  return ms / 10;
+}
+
+int main() {
+  const int64_t n = 500'000'000;
+  double* d;
+  unsigned long long* out;
+  hipMalloc(&d, n * 8);
+  hipMalloc(&out, 8);
+  hipLaunchKernelGGL(init, dim3(8192), dim3(256), 0, 0, d, n);
+  const char* names[] = {"load_only", "hash_nolds", "hash_lds", "hash_lds_skip", "mul_only"};
+  for (int wgs : {2048, 8192}) {
+    float t[5] = {run<0>(d, n, out, wgs), run<1>(d, n, out, wgs), run<2>(d, n, out, wgs), run<3>(d, n, out, wgs),
+                  run<4>(d, n, out, wgs)};
+    for (int m = 0; m < 5; ++m)
+      std::printf("{\"wgs\": %d, \"mode\": \"%s\", \"ms\": %.3f, \"GBps\": %.0f}\n", wgs, names[m], t[m], n * 8 / t[m] / 1e6);
+  }
+  return 0;
+}
