@@ -52,6 +52,20 @@ struct PairTask {
   int32_t pad[3];
 };
 
+// Correlation pairs sharing <= 8 distinct columns and one `where`: one LDS row tile serves them all.
+constexpr int kTileCols = 8;
+constexpr int kTilePairs = 32;
+constexpr int kTileRows = 512;
+struct PairGroup {
+  int32_t ncols;
+  int32_t npairs;
+  int32_t first_pair;               // pairs [first_pair, first_pair + npairs) of the pair-task table
+  int32_t where;                    // where-bitmap index or -1
+  int32_t cols[kTileCols];          // plan column indices
+  int32_t kinds[kTileCols];         // CK_F64 / CK_I64 / CK_I32
+  int8_t pi[kTilePairs], pj[kTilePairs];  // local column index of x / y per pair
+};
+
 // Per-workgroup partial of one column task.  Moments are Chan-mergeable (n, mean, m2).
 struct alignas(16) ColPartial {
   double n, mean, m2;   // over selected rows, values converted to double

@@ -8,7 +8,8 @@
 //                     Minimum, Maximum, ApproxCountDistinct), one launch per variant V (column kind x
 //                     accumulators), optionally spread over several HIP streams so HBM-bound and
 //                     VALU-bound (XXH64) variants run side by side on the 256 CUs.
-//   3. dq_pair_scan   (only if Correlations exist): co-moments per column pair.
+//   3. dq_pair_tile_scan (only if Correlations exist): co-moments of up to 32 column pairs per
+//                     launch group from one LDS tile of their (<= 8) columns.
 //   4. dq_finalize:   fixed-order merge of the per-workgroup partials, then in-order merge into
 //                     the plan's accumulators (chunk order) -> results are deterministic.
 // Streaming loads are 16 B per lane (global_load_dwordx4) for 8-/4-byte columns; there are no
@@ -101,6 +102,19 @@ __device__ __forceinline__ uint64_t f64_hash_bits(double d) {
   return d != d ? 0x7FF8000000000000ull : (uint64_t)__double_as_longlong(d);
 }
 
+// Hardware v_min_f64 / v_max_f64 (IEEE mode: a NaN operand yields the other operand).  Inline asm
+// keeps the compiler from canonicalising both inputs first (two extra v_max_f64 per call).
+__device__ __forceinline__ double hw_min(double a, double b) {
+  double r;
+  asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ double hw_max(double a, double b) {
+  double r;
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
 // ------------------------------------------------------------------------------------------
 // Chan-mergeable column statistics
 // ------------------------------------------------------------------------------------------
@@ -137,8 +151,8 @@ __device__ __forceinline__ void stats_merge(ColStats& a, const ColStats& b) {
   a.isum = (int64_t)((uint64_t)a.isum + (uint64_t)b.isum);
   a.count += b.count;
   a.nan_count += b.nan_count;
-  a.fmin = fmin(a.fmin, b.fmin);
-  a.fmax = fmax(a.fmax, b.fmax);
+  a.fmin = hw_min(a.fmin, b.fmin);
+  a.fmax = hw_max(a.fmax, b.fmax);
   a.imin = b.imin < a.imin ? b.imin : a.imin;
   a.imax = b.imax > a.imax ? b.imax : a.imax;
 }
@@ -166,46 +180,49 @@ __device__ __forceinline__ ColStats stats_load(const ColPartial* p) {
 }
 
 // Fold up to 8 values (bit j of `bits` = row j selected) into the running statistics:
-// per-chunk shifted sums around the running mean, one division per chunk.
+// per-chunk shifted sums around the running mean (first valid value for an empty state), one
+// division per chunk; the fp64 sum is recovered as sum(d) + k * shift.  NaN values propagate into
+// the moments (as Spark's per-row Welford does), are ignored by min / max and counted.
 template <int KIND>
 __device__ __forceinline__ void stats_chunk(ColStats& s, const double (&x)[8], const int64_t (&xi)[8], uint32_t bits) {
-  int k = __popc(bits);
+  const int k = __popc(bits);
   if (k == 0) return;
   double shift = s.mean;
   if (s.n == 0.0) {
 #pragma unroll
     for (int j = 7; j >= 0; --j) shift = ((bits >> j) & 1u) ? x[j] : shift;
   }
-  double sd = 0.0, sdd = 0.0, sm = 0.0;
+  const double pinf = __longlong_as_double(0x7FF0000000000000ll);
+  const double ninf = __longlong_as_double((long long)0xFFF0000000000000ull);
+  double sd = 0.0, sdd = 0.0;
   double lo = s.fmin, hi = s.fmax;
   int64_t is = 0, imn = s.imin, imx = s.imax;
   int nn = 0;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    bool b = (bits >> j) & 1u;
-    double d = b ? x[j] - shift : 0.0;
+    const bool b = (bits >> j) & 1u;
+    const double d = b ? x[j] - shift : 0.0;
     sd += d;
     sdd = __builtin_fma(d, d, sdd);
     if (KIND == CK_F64) {
-      sm += b ? x[j] : 0.0;
-      bool isn = b && (x[j] != x[j]);
-      nn += isn ? 1 : 0;
-      lo = (b && !isn) ? fmin(lo, x[j]) : lo;
-      hi = (b && !isn) ? fmax(hi, x[j]) : hi;
+      lo = hw_min(lo, b ? x[j] : pinf);
+      hi = hw_max(hi, b ? x[j] : ninf);
+      nn += (b && (x[j] != x[j])) ? 1 : 0;
     } else {
       is += b ? xi[j] : 0;
       imn = (b && xi[j] < imn) ? xi[j] : imn;
       imx = (b && xi[j] > imx) ? xi[j] : imx;
     }
   }
-  double n2 = s.n + (double)k;
-  double q = sd / n2;
+  const double n2 = s.n + (double)k;
+  const double q = sd / n2;
   s.mean = shift + q;
   s.m2 = s.m2 + (sdd - sd * q);
   s.n = n2;
   s.count += k;
   if (KIND == CK_F64) {
-    s.sum += sm; s.nan_count += nn; s.fmin = lo; s.fmax = hi;
+    s.sum += __builtin_fma((double)k, shift, sd);
+    s.nan_count += nn; s.fmin = lo; s.fmax = hi;
   } else {
     s.isum = (int64_t)((uint64_t)s.isum + (uint64_t)is); s.imin = imn; s.imax = imx;
   }
@@ -450,7 +467,7 @@ __global__ __launch_bounds__(kBlock) void dq_column_scan(const ColTask* __restri
 }
 
 // ------------------------------------------------------------------------------------------
-// Kernel 3: Correlation co-moments, one task per column pair (Corr update/merge algebra).
+// Correlation co-moment state (Corr update/merge algebra, Correlation.scala:37-52).
 // ------------------------------------------------------------------------------------------
 struct CorrStats { double n, xa, ya, ck, xm, ym; };
 
@@ -478,84 +495,131 @@ __device__ __forceinline__ double load_as_double(const void* p, int kind, int64_
   return (double)reinterpret_cast<const int32_t*>(p)[row];
 }
 
-__global__ __launch_bounds__(kBlock) void dq_pair_scan(const PairTask* __restrict__ tasks, int32_t ntasks, ScanCols cols,
-                                                       ScanBitmaps bm, int64_t n_rows, int64_t rows_per_range,
-                                                       CorrPartial* __restrict__ partials) {
-  __shared__ CorrStats red[kWaves];
-  const int32_t ti = blockIdx.x % ntasks;
-  const int32_t range = blockIdx.x / ntasks;
-  const PairTask t = tasks[ti];
+// ------------------------------------------------------------------------------------------
+// Kernel 3b: Correlation pair groups over an LDS row tile.  Each 512-row tile of the group's
+// (<= 8) columns is read from HBM once (16-byte loads, converted to double, validity & where
+// folded into per-column bit rows); then thread t owns pair t % 32 over the 64 tile rows of
+// group t / 32 and folds them in 8-row chunks (shifted co-moment sums, Chan merge, one division
+// per chunk).  Column stride kTileStride (516 doubles) puts the 8 columns of one tile row on
+// distinct LDS banks.
+// ------------------------------------------------------------------------------------------
+constexpr int kTileStride = kTileRows + 4;
+
+__global__ __launch_bounds__(kBlock) void dq_pair_tile_scan(const PairGroup* __restrict__ groups, int32_t ngroups,
+                                                            ScanCols cols, ScanBitmaps bm, int64_t n_rows,
+                                                            int64_t rows_per_range, CorrPartial* __restrict__ partials) {
+  __shared__ double tile[kTileCols * kTileStride];
+  __shared__ uint32_t vbits[kTileCols][kTileRows / 32];
+  __shared__ CorrStats red[kWaves][kTilePairs];
+  const int32_t gi = blockIdx.x % ngroups;
+  const int32_t range = blockIdx.x / ngroups;
+  const PairGroup& g = groups[gi];
+  const int ncols = g.ncols, npairs = g.npairs;
   const int64_t row0 = (int64_t)range * rows_per_range;
   int64_t row1 = row0 + rows_per_range;
   if (row1 > n_rows) row1 = n_rows;
-  const void* xv = cols.values[t.col_x];
-  const void* yv = cols.values[t.col_y];
-  const uint32_t* vx = cols.validity[t.col_x];
-  const uint32_t* vy = cols.validity[t.col_y];
-  const uint32_t* mask = t.where >= 0 ? reinterpret_cast<const uint32_t*>(bm.where_bits[t.where]) : nullptr;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t* mask = g.where >= 0 ? reinterpret_cast<const uint32_t*>(bm.where_bits[g.where]) : nullptr;
+  const int tid = threadIdx.x;
+  const int p = tid % kTilePairs, grp = tid / kTilePairs;  // 8 row groups of 64 tile rows
+  const bool active = p < npairs;
+  const int ci = active ? g.pi[p] : 0, cj = active ? g.pj[p] : 0;
   CorrStats s = {0, 0, 0, 0, 0, 0};
-  for (int64_t blk = row0; blk < row1; blk += kRowsPerIter) {
-    const int64_t base = blk + (int64_t)wave * 512;
-    double x[8], y[8];
-    uint32_t bits = 0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int64_t row = base + j * 64 + lane;
-      bool b = false;
-      x[j] = 0.0; y[j] = 0.0;
-      if (row < row1) {
-        uint32_t w = word_or_ones(vx, row >> 5) & word_or_ones(vy, row >> 5);
-        if (mask) w &= mask[row >> 5];
-        b = (w >> (row & 31)) & 1u;
-        x[j] = load_as_double(xv, t.kind_x, row);
-        y[j] = load_as_double(yv, t.kind_y, row);
+
+  for (int64_t t0 = row0; t0 < row1; t0 += kTileRows) {
+    const bool full = t0 + kTileRows <= row1;
+    // ---- stage the tile: each thread converts rows 2*tid, 2*tid+1 of every column
+    for (int c = 0; c < ncols; ++c) {
+      const void* src = cols.values[g.cols[c]];
+      const int kind = g.kinds[c];
+      const int64_t r = t0 + 2 * tid;
+      double a = 0.0, b = 0.0;
+      if (full) {
+        if (kind == CK_F64 || kind == CK_I64) {
+          const u32x4 v4 = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(reinterpret_cast<const int64_t*>(src) + r));
+          const uint64_t ua = ((uint64_t)v4.y << 32) | v4.x, ub = ((uint64_t)v4.w << 32) | v4.z;
+          if (kind == CK_F64) { a = __longlong_as_double((long long)ua); b = __longlong_as_double((long long)ub); }
+          else { a = (double)(int64_t)ua; b = (double)(int64_t)ub; }
+        } else {
+          const int2 v2 = *reinterpret_cast<const int2*>(reinterpret_cast<const int32_t*>(src) + r);
+          a = (double)v2.x; b = (double)v2.y;
+        }
+      } else {
+        if (r < row1) a = load_as_double(src, kind, r);
+        if (r + 1 < row1) b = load_as_double(src, kind, r + 1);
       }
-      bits |= (uint32_t)b << j;
+      tile[c * kTileStride + 2 * tid] = a;
+      tile[c * kTileStride + 2 * tid + 1] = b;
     }
-    int k = __popc(bits);
-    if (k == 0) continue;
-    double sx = s.xa, sy = s.ya;
-    if (s.n == 0.0) {
-#pragma unroll
-      for (int j = 7; j >= 0; --j) {
-        bool b = (bits >> j) & 1u;
-        sx = b ? x[j] : sx;
-        sy = b ? y[j] : sy;
+    if (tid < kTileCols * (kTileRows / 32)) {
+      const int c = tid / (kTileRows / 32), w = tid % (kTileRows / 32);
+      if (c < ncols) {
+        const int64_t widx = (t0 >> 5) + w;
+        uint32_t bits = word_or_ones(cols.validity[g.cols[c]], widx) & word_or_ones(mask, widx);
+        const int64_t r = t0 + 32 * w;
+        if (r >= row1) bits = 0;
+        else if (r + 32 > row1) bits &= (1u << (row1 - r)) - 1u;
+        vbits[c][w] = bits;
       }
     }
-    double Sx = 0, Sy = 0, Sxy = 0, Sxx = 0, Syy = 0;
+    __syncthreads();
+    // ---- fold: this thread's pair over its 64 rows, 8 rows per chunk
+    if (active) {
+#pragma unroll 1
+      for (int k = 0; k < 8; ++k) {
+        const int rr = grp * 64 + k * 8;
+        const uint32_t bits = ((vbits[ci][rr >> 5] & vbits[cj][rr >> 5]) >> (rr & 31)) & 0xFFu;
+        if (bits == 0) continue;
+        double x[8], y[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      bool b = (bits >> j) & 1u;
-      double dx = b ? x[j] - sx : 0.0, dy = b ? y[j] - sy : 0.0;
-      Sx += dx; Sy += dy;
-      Sxy = __builtin_fma(dx, dy, Sxy);
-      Sxx = __builtin_fma(dx, dx, Sxx);
-      Syy = __builtin_fma(dy, dy, Syy);
+        for (int j = 0; j < 8; ++j) {
+          x[j] = tile[ci * kTileStride + rr + j];
+          y[j] = tile[cj * kTileStride + rr + j];
+        }
+        double sx = s.xa, sy = s.ya;
+        if (s.n == 0.0) {
+#pragma unroll
+          for (int j = 7; j >= 0; --j) {
+            const bool b = (bits >> j) & 1u;
+            sx = b ? x[j] : sx;
+            sy = b ? y[j] : sy;
+          }
+        }
+        double Sx = 0, Sy = 0, Sxy = 0, Sxx = 0, Syy = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const bool b = (bits >> j) & 1u;
+          const double dx = b ? x[j] - sx : 0.0, dy = b ? y[j] - sy : 0.0;
+          Sx += dx; Sy += dy;
+          Sxy = __builtin_fma(dx, dy, Sxy);
+          Sxx = __builtin_fma(dx, dx, Sxx);
+          Syy = __builtin_fma(dy, dy, Syy);
+        }
+        const double n2 = s.n + (double)__popc(bits);
+        const double qx = Sx / n2, qy = Sy / n2;
+        s.xa = sx + qx; s.ya = sy + qy;
+        s.ck = s.ck + (Sxy - Sx * qy);
+        s.xm = s.xm + (Sxx - Sx * qx);
+        s.ym = s.ym + (Syy - Sy * qy);
+        s.n = n2;
+      }
     }
-    double n2 = s.n + (double)k;
-    double qx = Sx / n2, qy = Sy / n2;
-    s.xa = sx + qx; s.ya = sy + qy;
-    s.ck = s.ck + (Sxy - Sx * qy);
-    s.xm = s.xm + (Sxx - Sx * qx);
-    s.ym = s.ym + (Syy - Sy * qy);
-    s.n = n2;
+    __syncthreads();
   }
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) {
+  // ---- reduce the 8 row groups of each pair in fixed order: lanes p and p + 32 of a wave, then waves
+  {
     CorrStats o;
-    o.n = __shfl_xor(s.n, m); o.xa = __shfl_xor(s.xa, m); o.ya = __shfl_xor(s.ya, m);
-    o.ck = __shfl_xor(s.ck, m); o.xm = __shfl_xor(s.xm, m); o.ym = __shfl_xor(s.ym, m);
+    o.n = __shfl_xor(s.n, 32); o.xa = __shfl_xor(s.xa, 32); o.ya = __shfl_xor(s.ya, 32);
+    o.ck = __shfl_xor(s.ck, 32); o.xm = __shfl_xor(s.xm, 32); o.ym = __shfl_xor(s.ym, 32);
     corr_merge(s, o);
   }
-  if (lane == 0) red[wave] = s;
+  const int lane = tid & 63, wave = tid >> 6;
+  if (lane < kTilePairs) red[wave][lane] = s;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    CorrStats a = red[0];
-    for (int w = 1; w < kWaves; ++w) corr_merge(a, red[w]);
-    CorrPartial* p = partials + (size_t)ti * kMaxWG + range;
-    p->n = a.n; p->xa = a.xa; p->ya = a.ya; p->ck = a.ck; p->xm = a.xm; p->ym = a.ym; p->pad0 = 0; p->pad1 = 0;
+  if (tid < npairs) {
+    CorrStats a = red[0][tid];
+    for (int w = 1; w < kWaves; ++w) corr_merge(a, red[w][tid]);
+    CorrPartial* q = partials + (size_t)(g.first_pair + tid) * kMaxWG + range;
+    q->n = a.n; q->xa = a.xa; q->ya = a.ya; q->ck = a.ck; q->xm = a.xm; q->ym = a.ym; q->pad0 = 0; q->pad1 = 0;
   }
 }
 
@@ -806,11 +870,11 @@ hipError_t launch_column_scan(int32_t variant, const ColTask* tasks, int32_t nta
   return hipGetLastError();
 }
 
-hipError_t launch_pair_scan(const PairTask* tasks, int32_t ntasks, const ScanCols& cols, const ScanBitmaps& bm,
-                            int64_t n_rows, int64_t rows_per_range, int32_t nranges, CorrPartial* partials,
-                            hipStream_t st) {
-  hipLaunchKernelGGL(dq_pair_scan, dim3((uint32_t)ntasks * (uint32_t)nranges), dim3(kBlock), 0, st, tasks, ntasks, cols,
-                     bm, n_rows, rows_per_range, partials);
+hipError_t launch_pair_tile_scan(const PairGroup* groups, int32_t ngroups, const ScanCols& cols,
+                                 const ScanBitmaps& bm, int64_t n_rows, int64_t rows_per_range, int32_t nranges,
+                                 CorrPartial* partials, hipStream_t st) {
+  hipLaunchKernelGGL(dq_pair_tile_scan, dim3((uint32_t)ngroups * (uint32_t)nranges), dim3(kBlock), 0, st, groups,
+                     ngroups, cols, bm, n_rows, rows_per_range, partials);
   return hipGetLastError();
 }
 

@@ -31,9 +31,9 @@ hipError_t launch_pred_scan(const PredProgram* prog, const ScanCols& cols, const
 hipError_t launch_column_scan(int32_t variant, const ColTask* tasks, int32_t ntasks, int32_t part_base,
                               const ScanCols& cols, const ScanBitmaps& bm, int64_t n_rows, int64_t rows_per_range,
                               int32_t nranges, ColPartial* partials, uint32_t* hll_acc, hipStream_t st);
-hipError_t launch_pair_scan(const PairTask* tasks, int32_t ntasks, const ScanCols& cols, const ScanBitmaps& bm,
-                            int64_t n_rows, int64_t rows_per_range, int32_t nranges, CorrPartial* partials,
-                            hipStream_t st);
+hipError_t launch_pair_tile_scan(const PairGroup* groups, int32_t ngroups, const ScanCols& cols,
+                                 const ScanBitmaps& bm, int64_t n_rows, int64_t rows_per_range, int32_t nranges,
+                                 CorrPartial* partials, hipStream_t st);
 hipError_t launch_finalize(int32_t ncol, int32_t nranges_col, const ColPartial* col_part, ColPartial* col_acc,
                            int32_t npair, int32_t nranges_pair, const CorrPartial* pair_part, CorrPartial* pair_acc,
                            int32_t has_pred, int32_t nranges_pred, const PredPartial* pred_part, PredPartial* pred_acc,
@@ -386,7 +386,8 @@ struct dq_plan {
   std::vector<ColTask> col_tasks;        // sorted by variant
   struct Group { int32_t variant, first, count; };
   std::vector<Group> groups;              // one column-scan launch per variant group
-  std::vector<PairTask> pair_tasks;
+  std::vector<PairTask> pair_tasks;      // sorted by pair group
+  std::vector<PairGroup> pair_groups;     // <= 8 columns / <= 32 pairs / one where each
   int32_t concurrency = 1;                // HIP streams the variant launches are spread over
   std::vector<hipStream_t> side;          // concurrency - 1 extra streams
   std::vector<hipEvent_t> side_done;
@@ -398,6 +399,7 @@ struct dq_plan {
   // device memory
   ColTask* d_col_tasks = nullptr;
   PairTask* d_pair_tasks = nullptr;
+  PairGroup* d_pair_groups = nullptr;
   PredProgram* d_prog = nullptr;
   ColPartial* d_col_part = nullptr;
   CorrPartial* d_pair_part = nullptr;
@@ -471,7 +473,7 @@ static dq_status free_plan_mem(dq_plan* p) {
   p->pending.clear();
   for (hipEvent_t e : p->ev_pool) (void)hipEventDestroy(e);
   p->ev_pool.clear();
-  void* ptrs[] = {p->d_col_tasks, p->d_pair_tasks, p->d_prog, p->d_col_part, p->d_pair_part,
+  void* ptrs[] = {p->d_col_tasks, p->d_pair_tasks, p->d_pair_groups, p->d_prog, p->d_col_part, p->d_pair_part,
                   p->d_pred_part, p->d_col_acc, p->d_hll_acc, p->d_pair_acc, p->d_pred_acc};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
@@ -692,6 +694,50 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
     }
   }
 
+  // correlation pairs -> groups sharing one LDS row tile (greedy, per where bitmap)
+  {
+    std::vector<int32_t> order;
+    std::vector<PairGroup> groups;
+    std::vector<bool> taken(p->pair_tasks.size(), false);
+    for (size_t a = 0; a < p->pair_tasks.size(); ++a) {
+      if (taken[a]) continue;
+      PairGroup g{};
+      g.where = p->pair_tasks[a].where;
+      g.first_pair = (int32_t)order.size();
+      auto local = [&](int32_t col, int32_t kind) -> int32_t {
+        for (int c = 0; c < g.ncols; ++c)
+          if (g.cols[c] == col) return c;
+        if (g.ncols == kTileCols) return -1;
+        g.cols[g.ncols] = col;
+        g.kinds[g.ncols] = kind;
+        return g.ncols++;
+      };
+      for (size_t b = a; b < p->pair_tasks.size() && g.npairs < kTilePairs; ++b) {
+        const PairTask& t = p->pair_tasks[b];
+        if (taken[b] || t.where != g.where) continue;
+        PairGroup save = g;
+        int32_t x = local(t.col_x, t.kind_x), y = local(t.col_y, t.kind_y);
+        if (x < 0 || y < 0) { g = save; continue; }
+        g.pi[g.npairs] = (int8_t)x;
+        g.pj[g.npairs] = (int8_t)y;
+        g.npairs++;
+        taken[b] = true;
+        order.push_back((int32_t)b);
+      }
+      groups.push_back(g);
+    }
+    std::vector<PairTask> sorted(order.size());
+    std::vector<int32_t> new_index(order.size());
+    for (size_t k = 0; k < order.size(); ++k) {
+      sorted[k] = p->pair_tasks[order[k]];
+      new_index[order[k]] = (int32_t)k;
+    }
+    p->pair_tasks.swap(sorted);
+    p->pair_groups.swap(groups);
+    for (SpecOut& o : p->outs)
+      if (o.pair_task >= 0) o.pair_task = new_index[o.pair_task];
+  }
+
   // predicate program: roots in slot order, each followed by STORE
   p->has_pred = !root_code.empty() && (!counter_of.empty() || !bitmap_of.empty());
   PredProgram& prog = p->prog;
@@ -745,6 +791,7 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
   const size_t nct = p->col_tasks.size(), npt = p->pair_tasks.size();
   if (dq_status s = dmalloc(&p->d_col_tasks, nct * sizeof(ColTask))) return s;
   if (dq_status s = dmalloc(&p->d_pair_tasks, npt * sizeof(PairTask))) return s;
+  if (dq_status s = dmalloc(&p->d_pair_groups, p->pair_groups.size() * sizeof(PairGroup))) return s;
   if (dq_status s = dmalloc(&p->d_prog, sizeof(PredProgram))) return s;
   if (dq_status s = dmalloc(&p->d_col_part, nct * kMaxWG * sizeof(ColPartial))) return s;
   if (dq_status s = dmalloc(&p->d_pair_part, npt * kMaxWG * sizeof(CorrPartial))) return s;
@@ -755,6 +802,9 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
   if (dq_status s = dmalloc(&p->d_pred_acc, sizeof(PredPartial))) return s;
   if (nct) HIP_TRY(hipMemcpyAsync(p->d_col_tasks, p->col_tasks.data(), nct * sizeof(ColTask), hipMemcpyHostToDevice, p->stream));
   if (npt) HIP_TRY(hipMemcpyAsync(p->d_pair_tasks, p->pair_tasks.data(), npt * sizeof(PairTask), hipMemcpyHostToDevice, p->stream));
+  if (!p->pair_groups.empty())
+    HIP_TRY(hipMemcpyAsync(p->d_pair_groups, p->pair_groups.data(), p->pair_groups.size() * sizeof(PairGroup),
+                           hipMemcpyHostToDevice, p->stream));
   HIP_TRY(hipMemcpyAsync(p->d_prog, &p->prog, sizeof(PredProgram), hipMemcpyHostToDevice, p->stream));
   if (dq_status s = reset_acc(p)) return s;
   HIP_TRY(hipStreamSynchronize(p->stream));
@@ -873,7 +923,7 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
   for (int b = 0; b < kMaxWhere; ++b) bm.where_bits[b] = p->d_where_bits[b];
 
   // row ranges: column / pair passes in multiples of 2048 rows, predicate pass in multiples of 256
-  const int64_t ntask_col = std::max<int64_t>(1, (int64_t)(p->col_tasks.size() + p->pair_tasks.size()));
+  const int64_t ntask_col = std::max<int64_t>(1, (int64_t)(p->col_tasks.size() + p->pair_groups.size()));
   const int64_t want = std::max<int64_t>(64, std::min<int64_t>(kMaxWG, kTargetWGs / ntask_col));
   int32_t nr_col = (int32_t)std::min<int64_t>(want, ceil_div(n_rows, kRowsPerIter));
   int64_t rpr_col = ceil_div(ceil_div(n_rows, nr_col), kRowsPerIter) * kRowsPerIter;
@@ -906,8 +956,8 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
   if (!p->pair_tasks.empty()) {
     hipStream_t st = stream_for(li++);
     if (dq_status s = timed(p, 2, st, [&] {
-          return launch_pair_scan(p->d_pair_tasks, (int32_t)p->pair_tasks.size(), sc, bm, n_rows, rpr_col, nr_col,
-                                  p->d_pair_part, st);
+          return launch_pair_tile_scan(p->d_pair_groups, (int32_t)p->pair_groups.size(), sc, bm, n_rows, rpr_col,
+                                       nr_col, p->d_pair_part, st);
         }))
       return s;
   }
