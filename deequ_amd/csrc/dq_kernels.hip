@@ -179,67 +179,6 @@ __device__ __forceinline__ ColStats stats_load(const ColPartial* p) {
   return s;
 }
 
-// Fold up to 8 values (bit j of `bits` = row j selected) into the running statistics:
-// per-chunk shifted sums around the running mean (first valid value for an empty state), one
-// division per chunk; the fp64 sum is recovered as sum(d) + k * shift.  NaN values propagate into
-// the moments (as Spark's per-row Welford does), are ignored by min / max and counted.
-template <int KIND>
-__device__ __forceinline__ void stats_chunk(ColStats& s, const double (&x)[8], const int64_t (&xi)[8], uint32_t bits) {
-  const int k = __popc(bits);
-  if (k == 0) return;
-  double shift = s.mean;
-  if (s.n == 0.0) {
-#pragma unroll
-    for (int j = 7; j >= 0; --j) shift = ((bits >> j) & 1u) ? x[j] : shift;
-  }
-  const double pinf = __longlong_as_double(0x7FF0000000000000ll);
-  const double ninf = __longlong_as_double((long long)0xFFF0000000000000ull);
-  double sd = 0.0, sdd = 0.0;
-  double lo = s.fmin, hi = s.fmax;
-  int64_t is = 0, imn = s.imin, imx = s.imax;
-  int nn = 0;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const bool b = (bits >> j) & 1u;
-    const double d = b ? x[j] - shift : 0.0;
-    sd += d;
-    sdd = __builtin_fma(d, d, sdd);
-    if (KIND == CK_F64) {
-      lo = hw_min(lo, b ? x[j] : pinf);
-      hi = hw_max(hi, b ? x[j] : ninf);
-      nn += (b && (x[j] != x[j])) ? 1 : 0;
-    } else {
-      is += b ? xi[j] : 0;
-      imn = (b && xi[j] < imn) ? xi[j] : imn;
-      imx = (b && xi[j] > imx) ? xi[j] : imx;
-    }
-  }
-  const double n2 = s.n + (double)k;
-  const double q = sd / n2;
-  s.mean = shift + q;
-  s.m2 = s.m2 + (sdd - sd * q);
-  s.n = n2;
-  s.count += k;
-  if (KIND == CK_F64) {
-    s.sum += __builtin_fma((double)k, shift, sd);
-    s.nan_count += nn; s.fmin = lo; s.fmax = hi;
-  } else {
-    s.isum = (int64_t)((uint64_t)s.isum + (uint64_t)is); s.imin = imn; s.imax = imx;
-  }
-}
-
-template <int KIND>
-__device__ __forceinline__ void hash_chunk(uint32_t* regs, const double (&x)[8], const int64_t (&xi)[8], uint32_t bits) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    uint64_t h;
-    if (KIND == CK_F64) h = xxh64_long(f64_hash_bits(x[j]));
-    else if (KIND == CK_I64) h = xxh64_long((uint64_t)xi[j]);
-    else h = xxh64_int((uint32_t)xi[j]);
-    if ((bits >> j) & 1u) hll_update(regs, h);
-  }
-}
-
 // Reduce the 256 threads' statistics -> one ColPartial (fixed order: lanes by butterfly, waves 0..3).
 __device__ void block_reduce_store(ColStats s, ColPartial* out, ColStats* lds) {
 #pragma unroll
@@ -266,6 +205,63 @@ __device__ __forceinline__ uint32_t word_or_ones(const uint32_t* p, int64_t i) {
   return q[p ? i : 0];
 }
 
+// Streaming accumulator of one 8-row chunk: values are folded one at a time as they come out of the
+// 16-byte loads (no 8-value arrays held across the chunk), shifted around the running mean -- or,
+// for a still-empty state, around the chunk's first selected value -- and merged into the running
+// state with one division per chunk.
+template <int KIND>
+struct Chunk {
+  double shift, sd, sdd, lo, hi;
+  int64_t is, imn, imx;
+  int nn;
+  bool need_shift;
+
+  __device__ __forceinline__ void begin(const ColStats& s) {
+    shift = s.mean; need_shift = s.n == 0.0;
+    sd = 0.0; sdd = 0.0; lo = s.fmin; hi = s.fmax; is = 0; imn = s.imin; imx = s.imax; nn = 0;
+  }
+  __device__ __forceinline__ void add(double x, int64_t xi, bool b) {
+    shift = (need_shift && b) ? x : shift;
+    need_shift = need_shift && !b;
+    const double d = b ? x - shift : 0.0;
+    sd += d;
+    sdd = __builtin_fma(d, d, sdd);
+    if (KIND == CK_F64) {
+      lo = hw_min(lo, b ? x : __longlong_as_double(0x7FF0000000000000ll));
+      hi = hw_max(hi, b ? x : __longlong_as_double((long long)0xFFF0000000000000ull));
+      nn += (b && (x != x)) ? 1 : 0;
+    } else {
+      is += b ? xi : 0;
+      imn = (b && xi < imn) ? xi : imn;
+      imx = (b && xi > imx) ? xi : imx;
+    }
+  }
+  __device__ __forceinline__ void end(ColStats& s, int k) {
+    if (k == 0) return;
+    const double n2 = s.n + (double)k;
+    const double q = sd / n2;
+    s.mean = shift + q;
+    s.m2 = s.m2 + (sdd - sd * q);
+    s.n = n2;
+    s.count += k;
+    if (KIND == CK_F64) {
+      s.sum += __builtin_fma((double)k, shift, sd);
+      s.nan_count += nn; s.fmin = lo; s.fmax = hi;
+    } else {
+      s.isum = (int64_t)((uint64_t)s.isum + (uint64_t)is); s.imin = imn; s.imax = imx;
+    }
+  }
+};
+
+template <int KIND>
+__device__ __forceinline__ void hash_one(uint32_t* regs, double x, int64_t xi, bool b) {
+  uint64_t h;
+  if (KIND == CK_F64) h = xxh64_long(f64_hash_bits(x));
+  else if (KIND == CK_I64) h = xxh64_long((uint64_t)xi);
+  else h = xxh64_int((uint32_t)xi);
+  if (b) hll_update(regs, h);
+}
+
 // 8-/4-byte numeric column: 16-byte loads, lane l of wave w holds rows
 //   base + k*64*R + l*R + [0, R)  (R = 16 / sizeof(T) rows per load, 8 / R loads)
 template <int KIND, bool STATS, bool HLL>
@@ -276,28 +272,34 @@ __device__ void numeric_range(const void* values, const uint32_t* validity, cons
   constexpr int L = 8 / R;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const T* v = reinterpret_cast<const T*>(values);
+  Chunk<KIND> c;
   for (int64_t blk = row0; blk < row1; blk += kRowsPerIter) {
     const int64_t base = blk + (int64_t)wave * 512;
-    double x[8];
-    int64_t xi[8];
-    uint32_t bits = 0;
+    if (STATS) c.begin(s);
+    int k8 = 0;
     if (blk + kRowsPerIter <= row1) {
-      // fast path: whole 2048-row block in range
+      // fast path: whole 2048-row block in range; issue all loads first
       u32x4 raw[L];
+      uint32_t w[L];
 #pragma unroll
       for (int k = 0; k < L; ++k)
         raw[k] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(v + base + (int64_t)k * 64 * R) + lane);
 #pragma unroll
       for (int k = 0; k < L; ++k) {
         const int64_t widx = (base + (int64_t)k * 64 * R) / 32 + (lane * R) / 32;
-        const uint32_t w = word_or_ones(validity, widx) & word_or_ones(mask, widx);
-        uint32_t b = (w >> ((lane * R) & 31)) & ((1u << R) - 1u);
-        bits |= b << (k * R);
+        w[k] = (word_or_ones(validity, widx) & word_or_ones(mask, widx)) >> ((lane * R) & 31);
+      }
+#pragma unroll
+      for (int k = 0; k < L; ++k) {
         const T* e = reinterpret_cast<const T*>(&raw[k]);
+        k8 += __popc(w[k] & ((1u << R) - 1u));
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-          if (KIND == CK_F64) { x[k * R + r] = (double)e[r]; xi[k * R + r] = 0; }
-          else { xi[k * R + r] = (int64_t)e[r]; x[k * R + r] = (double)xi[k * R + r]; }
+          const bool b = (w[k] >> r) & 1u;
+          const int64_t xi = KIND == CK_F64 ? 0 : (int64_t)e[r];
+          const double x = KIND == CK_F64 ? (double)e[r] : (double)xi;
+          if (STATS) c.add(x, xi, b);
+          if (HLL) hash_one<KIND>(regs, x, xi, b);
         }
       }
     } else {
@@ -307,23 +309,22 @@ __device__ void numeric_range(const void* values, const uint32_t* validity, cons
 #pragma unroll
         for (int r = 0; r < R; ++r) {
           const int64_t row = base + (int64_t)k * 64 * R + (int64_t)lane * R + r;
-          const int j = k * R + r;
+          bool b = false;
+          T e = 0;
           if (row < row1) {
-            uint32_t w = word_or_ones(validity, row >> 5);
-            if (mask) w &= mask[row >> 5];
-            bits |= ((w >> (row & 31)) & 1u) << j;
-            T e = v[row];
-            if (KIND == CK_F64) { x[j] = (double)e; xi[j] = 0; }
-            else { xi[j] = (int64_t)e; x[j] = (double)xi[j]; }
-          } else {
-            x[j] = 0.0; xi[j] = 0;
+            b = ((word_or_ones(validity, row >> 5) & word_or_ones(mask, row >> 5)) >> (row & 31)) & 1u;
+            e = v[row];
           }
+          k8 += b ? 1 : 0;
+          const int64_t xi = KIND == CK_F64 ? 0 : (int64_t)e;
+          const double x = KIND == CK_F64 ? (double)e : (double)xi;
+          if (STATS) c.add(x, xi, b);
+          if (HLL) hash_one<KIND>(regs, x, xi, b);
         }
       }
     }
-    if (STATS) stats_chunk<KIND>(s, x, xi, bits);
-    else s.count += __popc(bits);
-    if (HLL) hash_chunk<KIND>(regs, x, xi, bits);
+    if (STATS) c.end(s, k8);
+    else s.count += k8;
   }
 }
 
