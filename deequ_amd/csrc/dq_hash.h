@@ -28,7 +28,18 @@ constexpr uint64_t XP4 = 0x85EBCA77C2B2AE63ull;
 constexpr uint64_t XP5 = 0x27D4EB2F165667C5ull;
 constexpr uint64_t kSeed = 42;
 
-DQ_HD uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+// 64-bit rotate by a constant 0 < r < 32.  On the device it is two v_alignbit_b32 on the halves:
+// written as 64-bit shifts, LLVM folds `rotl(x * P, r)` into extra multiplies by P << r.
+DQ_HD uint64_t rotl64(uint64_t x, int r) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  const uint32_t nhi = __builtin_amdgcn_alignbit(hi, lo, 32 - r);
+  const uint32_t nlo = __builtin_amdgcn_alignbit(lo, hi, 32 - r);
+  return ((uint64_t)nhi << 32) | nlo;
+#else
+  return (x << r) | (x >> (64 - r));
+#endif
+}
 DQ_HD uint64_t fmix64(uint64_t h) {
   h ^= h >> 33; h *= XP2; h ^= h >> 29; h *= XP3; h ^= h >> 32; return h;
 }

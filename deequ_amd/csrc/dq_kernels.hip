@@ -97,6 +97,14 @@ __device__ __forceinline__ void hll_update(uint32_t* regs, uint64_t x) {
   atomicMax(&regs[idx], pw);
 }
 
+// Branch-free predicated update: an unselected row does ds_max(reg, 0), a no-op.
+__device__ __forceinline__ void hll_update_if(uint32_t* regs, uint64_t x, bool b) {
+  uint32_t idx = (uint32_t)(x >> 55);
+  uint64_t w = (x << 9) | 256ull;
+  uint32_t pw = (uint32_t)__clzll((long long)w) + 1u;
+  atomicMax(&regs[idx], b ? pw : 0u);
+}
+
 __device__ __forceinline__ uint64_t f64_hash_bits(double d) {
   // doubleToLongBits: canonical NaN
   return d != d ? 0x7FF8000000000000ull : (uint64_t)__double_as_longlong(d);
@@ -205,6 +213,24 @@ __device__ __forceinline__ uint32_t word_or_ones(const uint32_t* p, int64_t i) {
   return q[p ? i : 0];
 }
 
+// Validity / `where` words of one workgroup row range [row0, row1) (row0 a multiple of 32) through a
+// raw buffer resource.  A missing bitmap is a zero-size resource (loads return 0) OR-ed with an
+// all-ones wave-uniform fill: no pointer selects, no flat loads, and a word past the range reads 0.
+struct RangeBits {
+  __amdgpu_buffer_rsrc_t r;
+  uint32_t fill;
+  __device__ __forceinline__ RangeBits(const uint32_t* p, int64_t row0, int64_t row1) {
+    const int32_t nbytes = p ? (int32_t)(((row1 - row0 + 31) >> 5) * 4) : 0;
+    r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(p ? p + (row0 >> 5) : nullptr), (short)0, nbytes,
+                                          0x00020000);
+    fill = p ? 0u : 0xFFFFFFFFu;
+  }
+  // word i of the range (rows row0 + 32 i .. + 31)
+  __device__ __forceinline__ uint32_t word(int32_t i) const {
+    return __builtin_amdgcn_raw_buffer_load_b32(r, i * 4, 0, 0) | fill;
+  }
+};
+
 // Streaming accumulator of one 8-row chunk: values are folded one at a time as they come out of the
 // 16-byte loads (no 8-value arrays held across the chunk), shifted around the running mean -- or,
 // for a still-empty state, around the chunk's first selected value -- and merged into the running
@@ -259,7 +285,7 @@ __device__ __forceinline__ void hash_one(uint32_t* regs, double x, int64_t xi, b
   if (KIND == CK_F64) h = xxh64_long(f64_hash_bits(x));
   else if (KIND == CK_I64) h = xxh64_long((uint64_t)xi);
   else h = xxh64_int((uint32_t)xi);
-  if (b) hll_update(regs, h);
+  hll_update_if(regs, h, b);
 }
 
 // 8-/4-byte numeric column: 16-byte loads, lane l of wave w holds rows
@@ -272,6 +298,7 @@ __device__ void numeric_range(const void* values, const uint32_t* validity, cons
   constexpr int L = 8 / R;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const T* v = reinterpret_cast<const T*>(values);
+  const RangeBits vb(validity, row0, row1), mb(mask, row0, row1);
   Chunk<KIND> c;
   for (int64_t blk = row0; blk < row1; blk += kRowsPerIter) {
     const int64_t base = blk + (int64_t)wave * 512;
@@ -286,8 +313,8 @@ __device__ void numeric_range(const void* values, const uint32_t* validity, cons
         raw[k] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(v + base + (int64_t)k * 64 * R) + lane);
 #pragma unroll
       for (int k = 0; k < L; ++k) {
-        const int64_t widx = (base + (int64_t)k * 64 * R) / 32 + (lane * R) / 32;
-        w[k] = (word_or_ones(validity, widx) & word_or_ones(mask, widx)) >> ((lane * R) & 31);
+        const int32_t widx = (int32_t)((base - row0 + (int64_t)k * 64 * R) / 32) + (lane * R) / 32;
+        w[k] = (vb.word(widx) & mb.word(widx)) >> ((lane * R) & 31);
       }
 #pragma unroll
       for (int k = 0; k < L; ++k) {
@@ -312,7 +339,8 @@ __device__ void numeric_range(const void* values, const uint32_t* validity, cons
           bool b = false;
           T e = 0;
           if (row < row1) {
-            b = ((word_or_ones(validity, row >> 5) & word_or_ones(mask, row >> 5)) >> (row & 31)) & 1u;
+            const int32_t wi = (int32_t)((row - row0) >> 5);
+            b = ((vb.word(wi) & mb.word(wi)) >> (row & 31)) & 1u;
             e = v[row];
           }
           k8 += b ? 1 : 0;
@@ -329,9 +357,12 @@ __device__ void numeric_range(const void* values, const uint32_t* validity, cons
 }
 
 // UTF8 column: one row per lane per step (rows base + 64*j + lane).  Offsets are read coalesced;
-// each string of <= 28 bytes is fetched with two 16-byte buffer loads (dword-aligned, bounded by
-// the range's last offset so nothing past the data is touched) and hashed branch-free; longer
-// strings take the general XXH64 loop.
+// every lane fetches its string with two 16-byte buffer loads (dword-aligned, bounded by the
+// range's last offset, so nothing past the data is touched and a lane whose window is out of range
+// reads zeros) and hashes it branch-free as a string of <= 28 bytes.  Lanes whose string is longer,
+// or whose 32-byte window crosses the range end, rehash with the general XXH64 loop (a divergent
+// branch that is almost never taken).  The body has no other branches, so the compiler can overlap
+// the loads of consecutive rows.
 template <typename OffT>
 __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint32_t* validity,
                            const uint32_t* mask, int64_t row0, int64_t row1, ColStats& s, uint32_t* regs) {
@@ -343,41 +374,36 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
   const bool fast_ok = (hi - lo) < (int64_t)0x7FFFFFF0;
   const __amdgpu_buffer_rsrc_t rsrc =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(data + lo), (short)0, fast_ok ? (int)(hi - lo) : 0, 0x00020000);
+  const RangeBits vb(validity, row0, row1), mb(mask, row0, row1);
+  int64_t cnt = 0;
   for (int64_t blk = row0; blk < row1; blk += kRowsPerIter) {
     const int64_t base = blk + (int64_t)wave * 512;
-#pragma unroll 2
+#pragma unroll 4
     for (int j = 0; j < 8; ++j) {
       const int64_t row = base + j * 64 + lane;
-      bool b = false;
-      if (row < row1) {
-        uint32_t w = word_or_ones(validity, row >> 5);
-        if (mask) w &= mask[row >> 5];
-        b = (w >> (row & 31)) & 1u;
-      }
-      s.count += b ? 1 : 0;
-      if (b) {
-        const int64_t o0 = (int64_t)offsets[row], o1 = (int64_t)offsets[row + 1];
-        const int64_t len = o1 - o0;
-        uint64_t h;
-        // fast path only when both 16-byte loads lie inside [lo, hi): never rely on partially
-        // out-of-range buffer loads
-        if (fast_ok && len <= 28 && (o0 & ~int64_t(3)) + 32 <= hi) {
-          const int32_t off = (int32_t)((o0 - lo) & ~int64_t(3));
-          const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0);
-          const u32x4 c = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off + 16, 0, 0);
-          const uint32_t d[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
-          const uint32_t sh = (uint32_t)(o0 & 3) * 8u;
-          uint32_t wv[7];
+      const bool in = row < row1;
+      const int32_t wi = (int32_t)((row - row0) >> 5);
+      const bool b = in && (((vb.word(wi) & mb.word(wi)) >> (row & 31)) & 1u);
+      const int64_t rr = in ? row : row1 - 1;  // keep the offset reads inside [row0, row1]
+      const int64_t o0 = (int64_t)offsets[rr], o1 = (int64_t)offsets[rr + 1];
+      const int64_t len = o1 - o0;
+      const int32_t off = (int32_t)((o0 - lo) & ~int64_t(3));
+      const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0);
+      const u32x4 c = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off + 16, 0, 0);
+      const uint32_t d[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+      const uint32_t sh = (uint32_t)(o0 & 3) * 8u;
+      uint32_t wv[7];
 #pragma unroll
-          for (int k = 0; k < 7; ++k) wv[k] = sh ? alignbit32(d[k + 1], d[k], sh) : d[k];
-          h = xxh64_short(wv, (uint32_t)len);
-        } else {
-          h = xxh64_bytes(data, o0, len);
-        }
-        hll_update(regs, h);
-      }
+      for (int k = 0; k < 7; ++k) wv[k] = alignbit32(d[k + 1], d[k], sh);  // sh == 0 -> d[k]
+      uint64_t h = xxh64_short(wv, (uint32_t)len);
+      // fast path only when both 16-byte loads lie inside [lo, hi)
+      const bool fast = fast_ok && len <= 28 && (o0 & ~int64_t(3)) + 32 <= hi;
+      if (b && !fast) h = xxh64_bytes(data, o0, len);
+      hll_update_if(regs, h, b);
+      cnt += b ? 1 : 0;
     }
   }
+  s.count += cnt;
 }
 
 // Only the count of selected rows (Completeness): popcount of validity (& where) words.

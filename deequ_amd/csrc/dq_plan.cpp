@@ -869,14 +869,11 @@ dq_status dq_plan_set_stream(dq_plan* p, void* hip_stream) {
   if (!p) return set_error(DQ_E_INVALID, "dq_plan_set_stream: plan is NULL");
   HIP_TRY(hipSetDevice(p->device));
   HIP_TRY(hipStreamSynchronize(p->stream));
-  if (hip_stream) {
-    if (p->own_stream) (void)hipStreamDestroy(p->stream);
-    p->stream = (hipStream_t)hip_stream;
-    p->own_stream = false;
-  } else if (!p->own_stream) {
-    HIP_TRY(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
-    p->own_stream = true;
-  }
+  // NULL is the device's null stream (what torch's default stream reports), not "keep the plan's
+  // own stream": the plan's own stream is non-blocking and would not wait for producers on it.
+  if (p->own_stream) (void)hipStreamDestroy(p->stream);
+  p->stream = (hipStream_t)hip_stream;
+  p->own_stream = false;
   return DQ_OK;
 }
 

@@ -150,7 +150,8 @@ const char* dq_last_error(void);
 dq_status dq_plan_create(const dq_analyzer_spec* specs, int32_t n_specs, const dq_column_desc* schema,
                          int32_t n_cols, const dq_pred_node* pred_pool, int32_t n_pred, int32_t device,
                          dq_plan** out);
-/* Launch on this hipStream_t (NULL = the plan's own stream). */
+/* Launch on this hipStream_t from now on (NULL = the device null stream).  A new plan launches on its
+   own non-blocking stream, which does not order against other streams: set the producer's stream. */
 dq_status dq_plan_set_stream(dq_plan* plan, void* hip_stream);
 /* Scan one chunk of rows (asynchronous on the plan's stream).  chunk_index must increase by one
  * per call starting at 0: chunk results are merged in that order, so results are deterministic. */

@@ -438,3 +438,22 @@ def test_deterministic_repeat(dq, cfg):
     runs = [scan_states(t, analyzers) for _ in range(3)]
     for a in analyzers:
         assert repr(runs[0][a]) == repr(runs[1][a]) == repr(runs[2][a]), a
+
+
+def test_scan_orders_after_producer_on_torch_stream(dq):
+    """The plan launches on torch's current stream (the null stream by default): a column whose values
+    are still being written by a queued kernel must be scanned after that kernel, not before."""
+    import torch
+
+    from deequ_amd.runner import scan_states
+    from deequ_amd.table import Column
+
+    n = 4_000_000
+    for _ in range(3):
+        raw = torch.zeros(n * 8 + 16, dtype=torch.uint8, device="cuda")
+        torch.cuda._sleep(50_000_000)  # keep the stream busy so an unordered scan would read the zeros
+        raw[: n * 8].view(torch.float64).fill_(1.5)
+        t = dq.Table([Column("x", "f64", n, raw, None, None, nullable=False)])
+        got = scan_states(t, [dq.Sum("x"), dq.Maximum("x")])
+        assert got[dq.Sum("x")].sum_ == 1.5 * n
+        assert got[dq.Maximum("x")].maxValue == 1.5
