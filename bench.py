@@ -20,6 +20,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md (HBM3E peak 8.0 TB/s)
+# FETCH_SIZE summary of this round's kernels (tools/profile_round.sh -> tools/summarize_prof.py):
+# per-dispatch HBM read bytes of each kernel at the default 62.5 M-row chunk, gfx950-corrected
+PMC_FILE = os.path.join(ROOT, "profiles", "r1_pmc.json")
+DEFAULT_CHUNK = 62_500_000
 
 
 def parse():
@@ -28,7 +32,7 @@ def parse():
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--rows", type=int, default=1_000_000_000, help="rows per GPU")
-    p.add_argument("--chunk", type=int, default=62_500_000, help="rows per chunk")
+    p.add_argument("--chunk", type=int, default=DEFAULT_CHUNK, help="rows per chunk")
     p.add_argument("--cpu-sample", type=int, default=62_500_000, help="rows timed on the CPU baseline (0 = skip)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="repeat the CPU sample for at least this long")
     p.add_argument("--cpu-threads", type=int, default=16)
@@ -43,9 +47,9 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local % max(1, torch.cuda.device_count())))
 
     import deequ_amd as dq
     from deequ_amd import distributed, synth
@@ -113,7 +117,9 @@ def main():
     value = rows_all / elapsed
     # roofline of the dominant kernel (largest total time): algorithmic bytes per launch / avg duration
     dom_name, dom = max(per_variant.items(), key=lambda kv: kv[1]["ms_total"])
+    dom_v = {name: v for v, name in L.VARIANT_NAMES.items()}[dom_name]
     achieved = dom["GBps"]
+    traffic = pmc_traffic(f"dq::dq_column_scan<{dom_v}>") if chunk == DEFAULT_CHUNK else None
     out = {
         "metric": "rows/sec (whole node) for fused 16-col profile scan; % of HBM peak BW",
         "value": value,
@@ -132,7 +138,8 @@ def main():
                    "parallelism": f"row-shard x{world}"},
         "hbm_frac_of_step": (algo_bytes_per_step / (elapsed / args.steps)) / 1e9 / HBM_PEAK_GBS,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_source": os.path.relpath(PMC_FILE, ROOT) if traffic is not None else None,
                      "kernel": f"dq_column_scan<{dom_name}>", "bytes_per_launch": dom["bytes_per_launch"],
                      "avg_launch_ms": dom["avg_ms"], "launches": dom["launches"],
                      "column_pass_ms_per_step": col_ms / args.steps,
@@ -147,6 +154,19 @@ def main():
     plan.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed FETCH_SIZE pass (None if not profiled)."""
+    try:
+        with open(PMC_FILE) as f:
+            recs = json.load(f)["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None
+    for r in recs:
+        if r["kernel"] == kernel:
+            return r["hbm_read_bytes_per_call_corrected"]
+    return None
 
 
 def cpu_baseline(table, n, threads, min_seconds=10.0):

@@ -17,7 +17,7 @@ constexpr int kBlock = 256;                 // threads per workgroup (4 waves of
 constexpr int kWaves = kBlock / 64;
 constexpr int kRowsPerLane = 8;
 constexpr int kRowsPerIter = kBlock * kRowsPerLane;  // 2048 rows per workgroup iteration
-constexpr int kMaxWG = 2048;                // max row ranges (workgroups) per task per scan
+constexpr int kMaxWG = 4096;                // max row ranges (workgroups) per task per scan
 constexpr int kTargetWGs = 8192;            // column/pair launch: aim for ~32 workgroups per CU
 constexpr int kMaxCols = 64;
 constexpr int kMaxWhere = 8;

@@ -231,38 +231,85 @@ struct RangeBits {
   }
 };
 
-// Streaming accumulator of one 8-row chunk: values are folded one at a time as they come out of the
-// 16-byte loads (no 8-value arrays held across the chunk), shifted around the running mean -- or,
-// for a still-empty state, around the chunk's first selected value -- and merged into the running
-// state with one division per chunk.
+// ------------------------------------------------------------------------------------------
+// Row masks as scalar lane masks.  Lane l of a wave handles rows r + l (r a multiple of 64), so the
+// selection of 64 rows is one 64-bit word of the validity (& where) bitmap: it is loaded with scalar
+// loads into SGPRs and used directly as the lane mask of v_cndmask (inverse ballot) -- no VALU work
+// per row for validity, and counts come from s_bcnt1.
+// ------------------------------------------------------------------------------------------
+typedef const __attribute__((address_space(4))) uint32_t* const_u32s;
+
+__device__ __forceinline__ uint64_t load_word64(const uint32_t* p, int64_t w) {
+  return ((uint64_t)((const_u32s)p)[w + 1] << 32) | ((const_u32s)p)[w];
+}
+
+// selected-row masks of the 8 lane groups [base + 64 j, + 64) of a wave's block (base a multiple of
+// 64; `full`: the whole block lies below row1).  All branches are wave-uniform.
+__device__ __forceinline__ void block_masks(const uint32_t* validity, const uint32_t* mask, int64_t base, int64_t row1,
+                                            bool full, uint64_t (&m)[8]) {
+  const int64_t w0 = base >> 5;
+  if (full) {
+    if (validity) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m[j] = load_word64(validity, w0 + 2 * j);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m[j] = ~0ull;
+    }
+    if (mask) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m[j] &= load_word64(mask, w0 + 2 * j);
+    }
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int64_t r = base + 64 * j, w = w0 + 2 * j;
+    uint64_t x = 0;
+    if (r < row1) {
+      const bool two = r + 32 < row1;  // the second dword holds rows below row1
+      x = ~0ull;
+      if (validity) x = ((uint64_t)(two ? ((const_u32s)validity)[w + 1] : 0u) << 32) | ((const_u32s)validity)[w];
+      if (mask) x &= ((uint64_t)(two ? ((const_u32s)mask)[w + 1] : 0u) << 32) | ((const_u32s)mask)[w];
+      if (r + 64 > row1) x &= (1ull << (row1 - r)) - 1ull;
+    }
+    m[j] = x;
+  }
+}
+
+__device__ __forceinline__ bool lane_bit(uint64_t m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
+
+// Streaming accumulator of one 8-row chunk of a lane (its rows r + 64 j + lane, j < 8): values are
+// shifted around the lane's running mean -- or, for a still-empty lane, around the chunk's first
+// selected value -- and merged into the running state with one division per chunk.
 template <int KIND>
 struct Chunk {
   double shift, sd, sdd, lo, hi;
   int64_t is, imn, imx;
-  int nn;
-  bool need_shift;
+  int k;
 
-  __device__ __forceinline__ void begin(const ColStats& s) {
-    shift = s.mean; need_shift = s.n == 0.0;
-    sd = 0.0; sdd = 0.0; lo = s.fmin; hi = s.fmax; is = 0; imn = s.imin; imx = s.imax; nn = 0;
+  __device__ __forceinline__ void begin(const ColStats& s, double first) {
+    shift = s.n == 0.0 ? first : s.mean;
+    sd = 0.0; sdd = 0.0; lo = s.fmin; hi = s.fmax; is = 0; imn = s.imin; imx = s.imax; k = 0;
   }
-  __device__ __forceinline__ void add(double x, int64_t xi, bool b) {
-    shift = (need_shift && b) ? x : shift;
-    need_shift = need_shift && !b;
+  // b: row selected; bnum: selected and not NaN (F64)
+  __device__ __forceinline__ void add(double x, int64_t xi, bool b, bool bnum) {
     const double d = b ? x - shift : 0.0;
     sd += d;
     sdd = __builtin_fma(d, d, sdd);
+    k += b ? 1 : 0;
     if (KIND == CK_F64) {
-      lo = hw_min(lo, b ? x : __longlong_as_double(0x7FF0000000000000ll));
-      hi = hw_max(hi, b ? x : __longlong_as_double((long long)0xFFF0000000000000ull));
-      nn += (b && (x != x)) ? 1 : 0;
+      // quiet NaN is the neutral operand of v_min_f64 / v_max_f64 (IEEE mode)
+      const double xm = bnum ? x : __longlong_as_double(0x7FF8000000000000ll);
+      lo = hw_min(lo, xm);
+      hi = hw_max(hi, xm);
     } else {
       is += b ? xi : 0;
       imn = (b && xi < imn) ? xi : imn;
       imx = (b && xi > imx) ? xi : imx;
     }
   }
-  __device__ __forceinline__ void end(ColStats& s, int k) {
+  __device__ __forceinline__ void end(ColStats& s) {
     if (k == 0) return;
     const double n2 = s.n + (double)k;
     const double q = sd / n2;
@@ -272,88 +319,90 @@ struct Chunk {
     s.count += k;
     if (KIND == CK_F64) {
       s.sum += __builtin_fma((double)k, shift, sd);
-      s.nan_count += nn; s.fmin = lo; s.fmax = hi;
+      s.fmin = lo; s.fmax = hi;
     } else {
       s.isum = (int64_t)((uint64_t)s.isum + (uint64_t)is); s.imin = imn; s.imax = imx;
     }
   }
 };
 
-template <int KIND>
-__device__ __forceinline__ void hash_one(uint32_t* regs, double x, int64_t xi, bool b) {
-  uint64_t h;
-  if (KIND == CK_F64) h = xxh64_long(f64_hash_bits(x));
-  else if (KIND == CK_I64) h = xxh64_long((uint64_t)xi);
-  else h = xxh64_int((uint32_t)xi);
-  hll_update_if(regs, h, b);
-}
-
-// 8-/4-byte numeric column: 16-byte loads, lane l of wave w holds rows
-//   base + k*64*R + l*R + [0, R)  (R = 16 / sizeof(T) rows per load, 8 / R loads)
+// Numeric column (f64 / i64 / i32): each wave takes 512-row blocks, lane l holding rows
+// base + 64 j + l (j < 8): coalesced 512-byte (8-byte types) loads per instruction, selection masks
+// in SGPRs.  Per row: stats as shifted sums (STATS), XXH64 + predicated LDS register max (HLL).
 template <int KIND, bool STATS, bool HLL>
 __device__ void numeric_range(const void* values, const uint32_t* validity, const uint32_t* mask,
                               int64_t row0, int64_t row1, ColStats& s, uint32_t* regs) {
   using T = typename std::conditional<KIND == CK_I32, int32_t, typename std::conditional<KIND == CK_I64, int64_t, double>::type>::type;
-  constexpr int R = 16 / sizeof(T);
-  constexpr int L = 8 / R;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const T* v = reinterpret_cast<const T*>(values);
-  const RangeBits vb(validity, row0, row1), mb(mask, row0, row1);
-  Chunk<KIND> c;
+  // values of [row0, row1) through a bounds-checked buffer resource: lane offset in one VGPR, the
+  // row-group offset in an SGPR, and rows past row1 read 0 (they are masked out) -- no address math
+  // per row.  dq_scan bounds a chunk to < 2^31 rows, so a range is < 2^31 bytes.
+  const __amdgpu_buffer_rsrc_t vr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<T*>(v + row0), (short)0, (int)((row1 - row0) * (int64_t)sizeof(T)), 0x00020000);
+  int64_t nan_w = 0;  // wave-uniform count of selected NaN values
+  int kcount = 0;     // per-lane selected rows (HLL-only variant)
   for (int64_t blk = row0; blk < row1; blk += kRowsPerIter) {
     const int64_t base = blk + (int64_t)wave * 512;
-    if (STATS) c.begin(s);
-    int k8 = 0;
-    if (blk + kRowsPerIter <= row1) {
-      // fast path: whole 2048-row block in range; issue all loads first
-      u32x4 raw[L];
-      uint32_t w[L];
+    const bool full = blk + kRowsPerIter <= row1;
+    T e[8];
+    uint64_t m[8];
 #pragma unroll
-      for (int k = 0; k < L; ++k)
-        raw[k] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(v + base + (int64_t)k * 64 * R) + lane);
-#pragma unroll
-      for (int k = 0; k < L; ++k) {
-        const int32_t widx = (int32_t)((base - row0 + (int64_t)k * 64 * R) / 32) + (lane * R) / 32;
-        w[k] = (vb.word(widx) & mb.word(widx)) >> ((lane * R) & 31);
-      }
-#pragma unroll
-      for (int k = 0; k < L; ++k) {
-        const T* e = reinterpret_cast<const T*>(&raw[k]);
-        k8 += __popc(w[k] & ((1u << R) - 1u));
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-          const bool b = (w[k] >> r) & 1u;
-          const int64_t xi = KIND == CK_F64 ? 0 : (int64_t)e[r];
-          const double x = KIND == CK_F64 ? (double)e[r] : (double)xi;
-          if (STATS) c.add(x, xi, b);
-          if (HLL) hash_one<KIND>(regs, x, xi, b);
-        }
-      }
-    } else {
-      // tail: same row mapping, guarded scalar loads
-#pragma unroll
-      for (int k = 0; k < L; ++k) {
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-          const int64_t row = base + (int64_t)k * 64 * R + (int64_t)lane * R + r;
-          bool b = false;
-          T e = 0;
-          if (row < row1) {
-            const int32_t wi = (int32_t)((row - row0) >> 5);
-            b = ((vb.word(wi) & mb.word(wi)) >> (row & 31)) & 1u;
-            e = v[row];
-          }
-          k8 += b ? 1 : 0;
-          const int64_t xi = KIND == CK_F64 ? 0 : (int64_t)e;
-          const double x = KIND == CK_F64 ? (double)e : (double)xi;
-          if (STATS) c.add(x, xi, b);
-          if (HLL) hash_one<KIND>(regs, x, xi, b);
-        }
+    for (int j = 0; j < 8; ++j) {
+      const int soff = (int)((base - row0 + j * 64) * (int64_t)sizeof(T));
+      if constexpr (sizeof(T) == 8) {
+        const auto w2 = __builtin_amdgcn_raw_buffer_load_b64(vr, lane * 8, soff, 2 /* nt */);
+        const uint64_t u = ((uint64_t)w2[1] << 32) | w2[0];
+        e[j] = __builtin_bit_cast(T, u);
+      } else {
+        e[j] = (T)__builtin_amdgcn_raw_buffer_load_b32(vr, lane * 4, soff, 2 /* nt */);
       }
     }
-    if (STATS) c.end(s, k8);
-    else s.count += k8;
+    block_masks(validity, mask, base, row1, full, m);
+    double x[8];
+    uint64_t nanm[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      x[j] = KIND == CK_F64 ? (double)e[j] : (double)(int64_t)e[j];
+      nanm[j] = KIND == CK_F64 ? __builtin_amdgcn_ballot_w64(x[j] != x[j]) & m[j] : 0ull;
+      if (KIND == CK_F64) nan_w += __builtin_popcountll(nanm[j]);
+    }
+    if (STATS) {
+      // first selected value of still-empty lanes (rare: a wave-uniform branch)
+      double first = 0.0;
+      if (__builtin_amdgcn_ballot_w64(s.n == 0.0) != 0) {
+#pragma unroll
+        for (int j = 7; j >= 0; --j) first = lane_bit(m[j]) ? x[j] : first;
+      }
+      Chunk<KIND> c;
+      c.begin(s, first);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) c.add(x[j], (int64_t)e[j], lane_bit(m[j]), lane_bit(m[j] & ~nanm[j]));
+      c.end(s);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) kcount += lane_bit(m[j]) ? 1 : 0;
+    }
+    if (HLL) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        uint64_t h;
+        if (KIND == CK_F64) {
+          uint64_t bits = (uint64_t)__double_as_longlong(x[j]);
+          if (nanm[j] != 0) bits = lane_bit(nanm[j]) ? 0x7FF8000000000000ull : bits;  // doubleToLongBits
+          h = xxh64_long(bits);
+        } else if (KIND == CK_I64) {
+          h = xxh64_long((uint64_t)(int64_t)e[j]);
+        } else {
+          h = xxh64_int((uint32_t)e[j]);
+        }
+        hll_update_if(regs, h, lane_bit(m[j]));
+      }
+    }
   }
+  if (!STATS) s.count += kcount;
+  if (KIND == CK_F64 && lane == 0) s.nan_count += nan_w;
 }
 
 // UTF8 column: one row per lane per step (rows base + 64*j + lane).  Offsets are read coalesced;

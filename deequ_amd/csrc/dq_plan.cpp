@@ -880,6 +880,8 @@ dq_status dq_plan_set_stream(dq_plan* p, void* hip_stream) {
 dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_t chunk_index) {
   if (!p) return set_error(DQ_E_INVALID, "dq_scan: plan is NULL");
   if (n_rows < 0) return set_error(DQ_E_INVALID, "dq_scan: n_rows < 0");
+  if (n_rows >= (int64_t(1) << 31))
+    return set_error(DQ_E_INVALID, "dq_scan: a chunk holds at most 2^31 - 1 rows (split larger inputs into chunks)");
   if (chunk_index != p->next_chunk)
     return set_error(DQ_E_INVALID, "dq_scan: chunk_index %lld out of order (expected %lld)", (long long)chunk_index,
                      (long long)p->next_chunk);
@@ -920,8 +922,13 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
   for (int b = 0; b < kMaxWhere; ++b) bm.where_bits[b] = p->d_where_bits[b];
 
   // row ranges: column / pair passes in multiples of 2048 rows, predicate pass in multiples of 256
-  const int64_t ntask_col = std::max<int64_t>(1, (int64_t)(p->col_tasks.size() + p->pair_groups.size()));
-  const int64_t want = std::max<int64_t>(64, std::min<int64_t>(kMaxWG, kTargetWGs / ntask_col));
+  // each variant (and the pair pass) is its own launch of (tasks x ranges) workgroups: size the ranges
+  // so the smallest launch still has ~kTargetWGs workgroups (load balance over 256 CUs)
+  int64_t min_launch = 0;
+  for (const auto& g : p->groups) min_launch = min_launch ? std::min<int64_t>(min_launch, g.count) : g.count;
+  if (!p->pair_groups.empty())
+    min_launch = min_launch ? std::min<int64_t>(min_launch, (int64_t)p->pair_groups.size()) : (int64_t)p->pair_groups.size();
+  const int64_t want = std::max<int64_t>(64, std::min<int64_t>(kMaxWG, kTargetWGs / std::max<int64_t>(1, min_launch)));
   int32_t nr_col = (int32_t)std::min<int64_t>(want, ceil_div(n_rows, kRowsPerIter));
   int64_t rpr_col = ceil_div(ceil_div(n_rows, nr_col), kRowsPerIter) * kRowsPerIter;
   nr_col = (int32_t)ceil_div(n_rows, rpr_col);

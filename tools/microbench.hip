@@ -116,6 +116,102 @@ float run(const double* d, int64_t n, unsigned long long* out, int wgs) {
   return ms / 10;
 }
 
+
+// ---- UTF8: strings of length 8..24 (uniform), production utf8_range vs a loads-only body
+__global__ void init_str(int32_t* offs, uint8_t* data, int64_t n) {
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    uint64_t h = (uint64_t)i * 0x9E3779B97F4A7C15ull;
+    offs[i + 1] = (int32_t)(8 + (h >> 59) % 17);  // lengths; prefix-summed on the host
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void kutf8(const uint8_t* data, const int32_t* offs, int64_t n, int64_t rpw,
+                                             ColPartial* out) {
+  __shared__ uint32_t regs[512];
+  __shared__ ColStats red[4];
+  for (int i = threadIdx.x; i < 512; i += 256) regs[i] = 0;
+  __syncthreads();
+  const int64_t r0 = blockIdx.x * rpw, r1 = min(n, r0 + rpw);
+  ColStats s;
+  stats_init(s);
+  if (MODE == 1) {
+    utf8_range<int32_t>(data, offs, nullptr, nullptr, r0, r1, s, regs);
+  } else {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t lo = offs[r0] & ~3, hi = offs[r1];
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(data + lo), (short)0, (int)(hi - lo), 0x00020000);
+    uint32_t acc = 0;
+    for (int64_t blk = r0; blk < r1; blk += kRowsPerIter) {
+      const int64_t base = blk + (int64_t)wave * 512;
+#pragma unroll 4
+      for (int j = 0; j < 8; ++j) {
+        const int64_t row = min(base + j * 64 + lane, r1 - 1);
+        const int64_t o0 = offs[row], o1 = offs[row + 1];
+        const int32_t off = (int32_t)((o0 - lo) & ~3);
+        const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0);
+        const u32x4 c = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off + 16, 0, 0);
+        if (MODE == 0) acc ^= a.x ^ a.y ^ a.z ^ a.w ^ c.x ^ c.y ^ c.z ^ c.w ^ (uint32_t)(o1 - o0);
+        else {  // MODE 2: + hash, no HLL
+          const uint32_t d[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+          const uint32_t sh = (uint32_t)(o0 & 3) * 8u;
+          uint32_t wv[7];
+#pragma unroll
+          for (int k = 0; k < 7; ++k) wv[k] = alignbit32(d[k + 1], d[k], sh);
+          acc ^= (uint32_t)xxh64_short(wv, (uint32_t)(o1 - o0));
+        }
+      }
+    }
+    s.count = acc;
+  }
+  block_reduce_store(s, out + blockIdx.x, red);
+  __syncthreads();
+  if (regs[threadIdx.x] == 0x12345u) out[0].pad = 1;
+}
+
+template <int MODE>
+float run_utf8(const uint8_t* data, const int32_t* offs, int64_t n, ColPartial* out, int wgs) {
+  int64_t rpw = ((n + wgs - 1) / wgs + 2047) / 2048 * 2048;
+  int g = (int)((n + rpw - 1) / rpw);
+  hipEvent_t a, b;
+  (void)hipEventCreate(&a);
+  (void)hipEventCreate(&b);
+  hipLaunchKernelGGL((kutf8<MODE>), dim3(g), dim3(256), 0, 0, data, offs, n, rpw, out);
+  (void)hipEventRecord(a);
+  for (int i = 0; i < 10; ++i) hipLaunchKernelGGL((kutf8<MODE>), dim3(g), dim3(256), 0, 0, data, offs, n, rpw, out);
+  (void)hipEventRecord(b);
+  (void)hipEventSynchronize(b);
+  float ms;
+  (void)hipEventElapsedTime(&ms, a, b);
+  return ms / 10;
+}
+
+void utf8_bench(ColPartial* part) {
+  const int64_t n = 100'000'000;  // <= 24 B each: offsets stay below 2^31
+  int32_t* offs;
+  (void)hipMalloc(&offs, (n + 1) * 4);
+  (void)hipMemset(offs, 0, 4);
+  hipLaunchKernelGGL(init_str, dim3(8192), dim3(256), 0, 0, offs, nullptr, n);
+  std::vector<int32_t> h(n + 1);
+  (void)hipMemcpy(h.data(), offs, (n + 1) * 4, hipMemcpyDeviceToHost);
+  h[0] = 0;
+  int64_t tot = 0;
+  for (int64_t i = 0; i < n; ++i) { tot += h[i + 1]; h[i + 1] = (int32_t)tot; }
+  if (tot > 0x7FFFFF00ll) { std::printf("utf8 bench: offsets overflow\n"); return; }
+  (void)hipMemcpy(offs, h.data(), (n + 1) * 4, hipMemcpyHostToDevice);
+  const int64_t bytes = h[n];
+  uint8_t* data;
+  (void)hipMalloc(&data, bytes + 64);
+  (void)hipMemset(data, 0x5A, bytes + 64);
+  const char* names[] = {"utf8_loads", "utf8_full", "utf8_hash_nohll"};
+  for (int wgs : {2048, 8192}) {
+    float t[3] = {run_utf8<0>(data, offs, n, part, wgs), run_utf8<1>(data, offs, n, part, wgs), run_utf8<2>(data, offs, n, part, wgs)};
+    for (int m = 0; m < 3; ++m)
+      std::printf("{\"wgs\": %d, \"mode\": \"%s\", \"ms\": %.3f, \"Gstr_per_s\": %.1f, \"GBps\": %.0f}\n", wgs, names[m], t[m],
+                  n / t[m] / 1e6, (n * 4.0 + bytes) / t[m] / 1e6);
+  }
+}
+
 int main() {
   const int64_t n = 500'000'000;
   double* d;
@@ -146,5 +242,7 @@ int main() {
     for (auto& x : r)
       std::printf("{\"wgs\": %d, \"mode\": \"%s\", \"ms\": %.3f, \"GBps\": %.0f}\n", wgs, x.name, x.ms, n * 8 / x.ms / 1e6);
   }
+  (void)hipFree(d);
+  utf8_bench(part);
   return 0;
 }

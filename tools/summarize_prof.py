@@ -1,0 +1,88 @@
+"""Summarise rocprofv3 CSV output into profiles/<tag>_kernel_stats.csv and profiles/<tag>_pmc.json.
+
+usage: summarize_prof.py <tag> <kernel-trace dir> <FETCH_SIZE pmc dir> [<SQ pmc dir>]
+
+FETCH_SIZE is corrected for gfx950 as /opt/skills/guides/MI355X_MICROARCH.md (HBM section) says:
+FETCH_SIZE reports 1/2 of the bytes of wide coalesced streaming reads, so bytes = FETCH_SIZE[KB]*1024*2.
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+
+def find(d, pattern):
+    hits = sorted(glob.glob(os.path.join(d, "**", pattern), recursive=True))
+    return hits[0] if hits else None
+
+
+def short(name):
+    return name.split("(")[0].replace("void ", "").strip()
+
+
+def counters(d):
+    """{kernel: {counter: [per-dispatch values]}} from a rocprofv3 counter_collection.csv"""
+    path = find(d, "*counter_collection.csv")
+    out = defaultdict(lambda: defaultdict(list))
+    durs = defaultdict(list)
+    if not path:
+        return out, durs
+    per_dispatch = defaultdict(lambda: defaultdict(float))
+    meta = {}
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            k = (row.get("Dispatch_Id") or row.get("Correlation_Id"), short(row["Kernel_Name"]))
+            per_dispatch[k][row["Counter_Name"]] += float(row["Counter_Value"])
+            if "Start_Timestamp" in row and row.get("End_Timestamp"):
+                meta[k] = (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e6
+    for (did, kname), cs in per_dispatch.items():
+        for c, v in cs.items():
+            out[kname][c].append(v)
+        if (did, kname) in meta:
+            durs[kname].append(meta[(did, kname)])
+    return out, durs
+
+
+def main():
+    tag, kt_dir, pmc_dir = sys.argv[1:4]
+    sq_dir = sys.argv[4] if len(sys.argv) > 4 else None
+    os.makedirs("profiles", exist_ok=True)
+    stats = find(kt_dir, "*kernel_stats.csv")
+    if stats:
+        shutil.copy(stats, f"profiles/{tag}_bench_kernel_stats.csv")
+    bench = {}
+    try:
+        with open("gpurun_out/prof_kt_bench.json") as f:
+            bench = json.loads([l for l in f if l.startswith("{")][-1])
+    except Exception:
+        pass
+    res = {"tag": tag,
+           "kernel_trace_command": "rocprofv3 --kernel-trace --stats -- python3 bench.py --cpu-sample 0 --steps 3 --warmup 1",
+           "pmc_command": "rocprofv3 --pmc FETCH_SIZE -- python3 bench.py --cpu-sample 0 --rows 250000000 --steps 1 --warmup 0",
+           "correction": "gfx950 FETCH_SIZE reports 1/2 of the bytes of wide coalesced streaming reads "
+                         "(MI355X_MICROARCH.md, HBM section): hbm_read_bytes = FETCH_SIZE[KB] * 1024 * 2",
+           "bench_line_under_kernel_trace": bench, "kernels": []}
+    fetch, durs = counters(pmc_dir)
+    sq, _ = counters(sq_dir) if sq_dir else ({}, {})
+    for kname, cs in sorted(fetch.items(), key=lambda kv: -sum(kv[1].get("FETCH_SIZE", [0]))):
+        vals = cs.get("FETCH_SIZE", [])
+        if not vals or "dq_" not in kname:
+            continue
+        rec = {"kernel": kname, "calls": len(vals), "FETCH_SIZE_KB_per_call": sum(vals) / len(vals),
+               "hbm_read_bytes_per_call_corrected": sum(vals) / len(vals) * 1024 * 2}
+        if durs.get(kname):
+            rec["avg_ms_under_pmc"] = sum(durs[kname]) / len(durs[kname])
+        if kname in sq:
+            for c, v in sq[kname].items():
+                rec[f"{c}_per_call"] = sum(v) / len(v)
+        res["kernels"].append(rec)
+    with open(f"profiles/{tag}_pmc.json", "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps([{k: v for k, v in r.items()} for r in res["kernels"]], indent=1)[:4000])
+
+
+if __name__ == "__main__":
+    main()
