@@ -58,27 +58,30 @@ DQ_HD uint64_t xxh64_int(uint32_t v) {
 
 // XXH64.hashUnsafeBytes of a string of len <= 28 bytes held in w[0..6] (little-endian dwords of the
 // string itself).  Branch-free: every lane runs 3 stripe rounds, one 4-byte round and 3 byte rounds
-// and keeps the ones its length needs, so a wave of mixed lengths does not diverge.
+// and keeps the ones its length needs, so a wave of mixed lengths does not diverge.  The 4-byte
+// round's dword w[2 nw] and the byte rounds' dword w[len >> 2] = w[2 nw + (len >> 2 & 1)] are
+// picked up by the same predicates as the stripe rounds (no dynamic register indexing).
 DQ_HD uint64_t xxh64_short(const uint32_t (&w)[7], uint32_t len) {
   uint64_t h = kSeed + XP5 + (uint64_t)len;
   const uint32_t nw = len >> 3;
+  uint32_t d4 = w[0], d4n = w[1];  // w[2 nw], w[2 nw + 1] after the stripe rounds
 #pragma unroll
   for (uint32_t k = 0; k < 3; ++k) {
     const uint64_t k1 = ((uint64_t)w[2 * k + 1] << 32) | w[2 * k];
     uint64_t hn = h ^ (rotl64(k1 * XP2, 31) * XP1);
     hn = rotl64(hn, 27) * XP1 + XP4;
-    h = k < nw ? hn : h;
+    const bool take = k < nw;
+    h = take ? hn : h;
+    d4 = take ? w[2 * k + 2] : d4;
+    d4n = take ? (k < 2 ? w[2 * k + 3] : 0u) : d4n;  // w[7] only for len 28, which has no byte rounds
   }
-  // 4-byte round on dword 2*nw
-  const uint32_t d4 = nw == 0 ? w[0] : (nw == 1 ? w[2] : (nw == 2 ? w[4] : w[6]));
+  // 4-byte round on dword 2 nw
+  const bool has4 = (len & 4u) != 0;
   uint64_t h4 = h ^ ((uint64_t)d4 * XP1);
   h4 = rotl64(h4, 23) * XP2 + XP3;
-  h = (len & 4u) ? h4 : h;
+  h = has4 ? h4 : h;
   // byte rounds on dword len >> 2
-  const uint32_t pb = len >> 2;
-  uint32_t db = w[0];
-#pragma unroll
-  for (uint32_t k = 1; k < 7; ++k) db = pb == k ? w[k] : db;
+  const uint32_t db = has4 ? d4n : d4;
   const uint32_t nb = len & 3u;
 #pragma unroll
   for (uint32_t j = 0; j < 3; ++j) {

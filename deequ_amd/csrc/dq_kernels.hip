@@ -405,38 +405,56 @@ __device__ void numeric_range(const void* values, const uint32_t* validity, cons
   if (KIND == CK_F64 && lane == 0) s.nan_count += nan_w;
 }
 
-// UTF8 column: one row per lane per step (rows base + 64*j + lane).  Offsets are read coalesced;
-// every lane fetches its string with two 16-byte buffer loads (dword-aligned, bounded by the
-// range's last offset, so nothing past the data is touched and a lane whose window is out of range
-// reads zeros) and hashes it branch-free as a string of <= 28 bytes.  Lanes whose string is longer,
-// or whose 32-byte window crosses the range end, rehash with the general XXH64 loop (a divergent
-// branch that is almost never taken).  The body has no other branches, so the compiler can overlap
-// the loads of consecutive rows.
+// UTF8 column: lane l of a wave takes rows base + 64 j + l (j < 8) of its 512-row block, so the
+// selection masks are scalar bitmap words (as in numeric_range).  Offsets come through a
+// bounds-checked buffer resource over offsets[row0 .. row1]; every lane fetches its string with two
+// 16-byte buffer loads (dword-aligned, bounded by the range's last offset, so nothing past the data
+// is touched and an out-of-range window reads zeros) and hashes it branch-free as a string of
+// <= 28 bytes.  Lanes whose string is longer, or whose 32-byte window crosses the range end, rehash
+// with the general XXH64 loop (a divergent branch that is almost never taken).
 template <typename OffT>
 __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint32_t* validity,
                            const uint32_t* mask, int64_t row0, int64_t row1, ColStats& s, uint32_t* regs) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (row0 >= row1) return;
+  constexpr int W = (int)sizeof(OffT);
   // byte window of this range, addressed by a 32-bit buffer offset from a dword-aligned base
   const int64_t lo = (int64_t)offsets[row0] & ~int64_t(3);
   const int64_t hi = (int64_t)offsets[row1];
   const bool fast_ok = (hi - lo) < (int64_t)0x7FFFFFF0;
   const __amdgpu_buffer_rsrc_t rsrc =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(data + lo), (short)0, fast_ok ? (int)(hi - lo) : 0, 0x00020000);
-  const RangeBits vb(validity, row0, row1), mb(mask, row0, row1);
-  int64_t cnt = 0;
+  const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<OffT*>(offsets + row0), (short)0, (int)((row1 - row0 + 1) * W), 0x00020000);
+  const int32_t win = fast_ok ? (int32_t)(hi - lo) : 0;
+  int64_t cnt_w = 0;  // wave-uniform count of selected rows
   for (int64_t blk = row0; blk < row1; blk += kRowsPerIter) {
     const int64_t base = blk + (int64_t)wave * 512;
-#pragma unroll 4
+    const bool full = blk + kRowsPerIter <= row1;
+    uint64_t m[8];
+    block_masks(validity, mask, base, row1, full, m);
+    uint32_t slow = 0;  // bit j: this lane's row j needs the general hash
+#pragma unroll
+    for (int j = 0; j < 8; ++j) cnt_w += __builtin_popcountll(m[j]);
+#pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int64_t row = base + j * 64 + lane;
-      const bool in = row < row1;
-      const int32_t wi = (int32_t)((row - row0) >> 5);
-      const bool b = in && (((vb.word(wi) & mb.word(wi)) >> (row & 31)) & 1u);
-      const int64_t rr = in ? row : row1 - 1;  // keep the offset reads inside [row0, row1]
-      const int64_t o0 = (int64_t)offsets[rr], o1 = (int64_t)offsets[rr + 1];
+      const bool b = lane_bit(m[j]);
+      const int soff = (int)((base - row0 + j * 64) * W);
+      int64_t o0, o1;
+      if constexpr (W == 4) {
+        o0 = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(orsrc, lane * 4, soff, 0);
+        o1 = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(orsrc, lane * 4 + 4, soff, 0);
+      } else {
+        const auto a0 = __builtin_amdgcn_raw_buffer_load_b64(orsrc, lane * 8, soff, 0);
+        const auto a1 = __builtin_amdgcn_raw_buffer_load_b64(orsrc, lane * 8 + 8, soff, 0);
+        o0 = (int64_t)(((uint64_t)a0[1] << 32) | a0[0]);
+        o1 = (int64_t)(((uint64_t)a1[1] << 32) | a1[0]);
+      }
+      // 32-bit window arithmetic: when fast_ok, every offset of the range lies in [lo, lo + 2^31)
+      const int32_t rel = (int32_t)(o0 - lo);
       const int64_t len = o1 - o0;
-      const int32_t off = (int32_t)((o0 - lo) & ~int64_t(3));
+      const int32_t off = rel & ~3;
       const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0);
       const u32x4 c = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off + 16, 0, 0);
       const uint32_t d[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
@@ -446,13 +464,23 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
       for (int k = 0; k < 7; ++k) wv[k] = alignbit32(d[k + 1], d[k], sh);  // sh == 0 -> d[k]
       uint64_t h = xxh64_short(wv, (uint32_t)len);
       // fast path only when both 16-byte loads lie inside [lo, hi)
-      const bool fast = fast_ok && len <= 28 && (o0 & ~int64_t(3)) + 32 <= hi;
-      if (b && !fast) h = xxh64_bytes(data, o0, len);
-      hll_update_if(regs, h, b);
-      cnt += b ? 1 : 0;
+      const bool fast = fast_ok && (uint32_t)len <= 28u && (uint32_t)len == len && off + 32 <= win;
+      slow |= (b && !fast) ? (1u << j) : 0u;
+      hll_update_if(regs, h, b && fast);
+    }
+    // the rare long / window-crossing strings: one general XXH64 per flagged row (a single copy of
+    // the loop, outside the unrolled body)
+    if (__builtin_amdgcn_ballot_w64(slow != 0) != 0) {
+      while (slow) {
+        const int j = __builtin_ctz(slow);
+        slow &= slow - 1;
+        const int64_t row = base + j * 64 + lane;
+        const int64_t o0 = (int64_t)offsets[row], o1 = (int64_t)offsets[row + 1];
+        hll_update_if(regs, xxh64_bytes(data, o0, o1 - o0), true);
+      }
     }
   }
-  s.count += cnt;
+  if (lane == 0) s.count += cnt_w;
 }
 
 // Only the count of selected rows (Completeness): popcount of validity (& where) words.
