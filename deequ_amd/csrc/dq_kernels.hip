@@ -89,20 +89,68 @@ __device__ uint64_t xxh64_bytes(const uint8_t* data, int64_t pos, int64_t n) {
   return fmix64(h);
 }
 
-// HLL++ update (StatefulHyperloglogPlus.scala:96-113) on LDS registers (one u32 per register).
-__device__ __forceinline__ void hll_update(uint32_t* regs, uint64_t x) {
-  uint32_t idx = (uint32_t)(x >> 55);
-  uint64_t w = (x << 9) | 256ull;
-  uint32_t pw = (uint32_t)__clzll((long long)w) + 1u;
-  atomicMax(&regs[idx], pw);
+// HLL++ registers (StatefulHyperloglogPlus.scala:96-113) live in LDS as int32 q = pw - 1, with -1 for
+// an empty register: pw = nlz((x << 9) | 256) + 1, so q = nlz(...) is the leading-zero count itself and
+// an update is one ds_max_i32; the workgroup merge writes q + 1 (0 for empty) to the accumulator.
+__device__ __forceinline__ int32_t hll_q_exact(uint64_t x) {
+  return (int32_t)__clzll((long long)((x << 9) | 256ull));
 }
 
-// Branch-free predicated update: an unselected row does ds_max(reg, 0), a no-op.
-__device__ __forceinline__ void hll_update_if(uint32_t* regs, uint64_t x, bool b) {
-  uint32_t idx = (uint32_t)(x >> 55);
-  uint64_t w = (x << 9) | 256ull;
-  uint32_t pw = (uint32_t)__clzll((long long)w) + 1u;
-  atomicMax(&regs[idx], b ? pw : 0u);
+__device__ __forceinline__ void hll_update(int32_t* regs, uint64_t x) {
+  atomicMax(&regs[(uint32_t)(x >> 55)], hll_q_exact(x));
+}
+
+// Branch-free predicated update: an unselected row does ds_max(reg, -1), a no-op.
+__device__ __forceinline__ void hll_update_if(int32_t* regs, uint64_t x, bool b) {
+  atomicMax(&regs[(uint32_t)(x >> 55)], b ? hll_q_exact(x) : -1);
+}
+
+// v_ffbh_u32 as the hardware defines it: leading-zero count, 0xFFFFFFFF (= -1) for a zero input.
+__device__ __forceinline__ int32_t ffbh_raw(uint32_t x) {
+  int32_t r;
+  asm("v_ffbh_u32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+
+// x * c + a (mod 2^64) for constants c, a: one v_mad_u64_u32 (low product + addend), two
+// v_mul_lo_u32 (cross products) and one add3 -- the shortest CDNA sequence for a 64-bit multiply.
+__device__ __forceinline__ uint64_t mul_add_c(uint64_t x, uint64_t c, uint64_t a) {
+  const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
+  const uint64_t p = (uint64_t)xl * (uint32_t)c + a;
+  const uint32_t hi = (uint32_t)(p >> 32) + xl * (uint32_t)(c >> 32) + xh * (uint32_t)c;
+  return ((uint64_t)hi << 32) | (uint32_t)p;
+}
+
+// HLL key of a finished-but-for-the-last-multiply XXH64 state b (after `h ^= h >> 29` of fmix64):
+// the final hash's high word is hi32(b * P3) (the closing `h ^= h >> 32` only changes the low word),
+// which carries the register index (bits 63..55) and, unless its bits 54..32 are all zero
+// (probability 2^-23), the rank.  `addr` is the LDS byte offset of register idx; `q` = pw - 1, or -1
+// when the rank needs the low word (the caller then recomputes that value exactly).
+struct HllKey {
+  uint32_t addr;
+  int32_t q;
+};
+__device__ __forceinline__ HllKey hll_key_from_fmix(uint64_t b) {
+  const uint32_t bl = (uint32_t)b, bh = (uint32_t)(b >> 32);
+  const uint32_t hi = __umulhi(bl, (uint32_t)XP3) + bl * (uint32_t)(XP3 >> 32) + bh * (uint32_t)XP3;
+  return {(hi >> 21) & 0x7FCu, ffbh_raw(hi << 9)};
+}
+// XXH64.hashLong(v, 42) -> HLL key (hashLong: StatefulHyperloglogPlus.scala:93 via XxHash64Function)
+__device__ __forceinline__ HllKey hll_key_long(uint64_t v) {
+  const uint64_t k = rotl64(mul_add_c(v, XP2, 0), 31);
+  uint64_t h = mul_add_c(k, XP1, 0) ^ (kSeed + XP5 + 8);
+  h = mul_add_c(rotl64(h, 27), XP1, XP4);
+  h ^= h >> 33;
+  h = mul_add_c(h, XP2, 0);
+  return hll_key_from_fmix(h ^ (h >> 29));
+}
+// XXH64.hashInt(v, 42) -> HLL key
+__device__ __forceinline__ HllKey hll_key_int(uint32_t v) {
+  uint64_t h = ((uint64_t)v * XP1) ^ (kSeed + XP5 + 4);
+  h = mul_add_c(rotl64(h, 23), XP2, XP3);
+  h ^= h >> 33;
+  h = mul_add_c(h, XP2, 0);
+  return hll_key_from_fmix(h ^ (h >> 29));
 }
 
 __device__ __forceinline__ uint64_t f64_hash_bits(double d) {
@@ -279,59 +327,155 @@ __device__ __forceinline__ void block_masks(const uint32_t* validity, const uint
 
 __device__ __forceinline__ bool lane_bit(uint64_t m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
 
-// Streaming accumulator of one 8-row chunk of a lane (its rows r + 64 j + lane, j < 8): values are
-// shifted around the lane's running mean -- or, for a still-empty lane, around the chunk's first
-// selected value -- and merged into the running state with one division per chunk.
-template <int KIND>
-struct Chunk {
-  double shift, sd, sdd, lo, hi;
-  int64_t is, imn, imx;
-  int k;
+// Per-lane streaming moments of a numeric column (lane l of a wave owns rows base + 64 j + l).  Values
+// are accumulated as shifted sums sd = sum(x - shift), sdd = sum((x - shift)^2), k under the selection
+// mask -- exec-masked updates, so an unselected row costs no VALU work -- and merged into the lane's
+// running (n, mean, m2) with Chan's formula (StandardDeviation.scala:37-44) every kChunkBlocks blocks:
+// one reciprocal per 32 values.  shift is the lane's running mean, so the shifted sums stay small;
+// a lane with nothing yet takes its first selected value.
+constexpr int kChunkBlocks = 4;
 
-  __device__ __forceinline__ void begin(const ColStats& s, double first) {
-    shift = s.n == 0.0 ? first : s.mean;
-    sd = 0.0; sdd = 0.0; lo = s.fmin; hi = s.fmax; is = 0; imn = s.imin; imx = s.imax; k = 0;
-  }
-  // b: row selected; bnum: selected and not NaN (F64)
-  __device__ __forceinline__ void add(double x, int64_t xi, bool b, bool bnum) {
-    const double d = b ? x - shift : 0.0;
-    sd += d;
-    sdd = __builtin_fma(d, d, sdd);
-    k += b ? 1 : 0;
-    if (KIND == CK_F64) {
-      // quiet NaN is the neutral operand of v_min_f64 / v_max_f64 (IEEE mode)
-      const double xm = bnum ? x : __longlong_as_double(0x7FF8000000000000ll);
-      lo = hw_min(lo, xm);
-      hi = hw_max(hi, xm);
-    } else {
-      is += b ? xi : 0;
-      imn = (b && xi < imn) ? xi : imn;
-      imx = (b && xi > imx) ? xi : imx;
-    }
-  }
-  __device__ __forceinline__ void end(ColStats& s) {
-    if (k == 0) return;
-    const double n2 = s.n + (double)k;
-    const double q = sd / n2;
-    s.mean = shift + q;
-    s.m2 = s.m2 + (sdd - sd * q);
-    s.n = n2;
-    s.count += k;
-    if (KIND == CK_F64) {
-      s.sum += __builtin_fma((double)k, shift, sd);
-      s.fmin = lo; s.fmax = hi;
-    } else {
-      s.isum = (int64_t)((uint64_t)s.isum + (uint64_t)is); s.imin = imn; s.imax = imx;
-    }
-  }
+struct LaneMoments {
+  double shift, sd, sdd;
+  int32_t k;
+  int64_t is;  // wrapping int64 sum (integral kinds; Spark Sum on LongType)
 };
+
+// v_rcp_f64 + one Newton step: within an ulp of 1/a (a is a positive count; deterministic)
+__device__ __forceinline__ double rcp_nr(double a) {
+  const double r = __builtin_amdgcn_rcp(a);
+  return __builtin_fma(r, __builtin_fma(-a, r, 1.0), r);
+}
+
+template <int KIND>
+__device__ __forceinline__ void moments_flush(ColStats& s, LaneMoments& a) {
+  if (a.k != 0) {
+    const double kd = (double)a.k;
+    const double n2 = s.n + kd;
+    const double q = a.sd * rcp_nr(n2);
+    s.mean = a.shift + q;
+    s.m2 = s.m2 + __builtin_fma(-a.sd, q, a.sdd);
+    s.n = n2;
+    s.count += a.k;
+    if (KIND == CK_F64) s.sum += __builtin_fma(kd, a.shift, a.sd);
+    else s.isum = (int64_t)((uint64_t)s.isum + (uint64_t)a.is);
+  }
+  a.shift = s.mean;
+  a.sd = 0.0;
+  a.sdd = 0.0;
+  a.k = 0;
+  a.is = 0;
+}
+
+// Exec-masked moment / min / max update of one value (inline asm so the accumulators are plain
+// read-write operands: a C++ `if` on a lane mask makes the compiler copy every accumulator into
+// its phi register before the branch).  exec &= ma for the moments, exec &= mb for min / max
+// (MINMAX_SEP: mb excludes NaN rows), then restored; the outer exec is respected (s_and_saveexec).
+template <bool INTEGRAL, bool MINMAX_SEP>
+__device__ __forceinline__ void masked_moments(LaneMoments& a, double& lo, double& hi, double x, uint64_t b,
+                                               uint64_t ma, uint64_t mb) {
+  double d;
+  uint64_t save;
+  if constexpr (INTEGRAL) {
+    asm volatile(
+        "s_and_saveexec_b64 %[save], %[ma]\n\t"
+        "v_add_f64 %[d], %[x], -%[sh]\n\t"
+        "v_lshl_add_u64 %[is], %[b], 0, %[is]\n\t"
+        "v_add_u32 %[k], 1, %[k]\n\t"
+        "v_add_f64 %[sd], %[sd], %[d]\n\t"
+        "v_fma_f64 %[sdd], %[d], %[d], %[sdd]\n\t"
+        "v_min_f64 %[lo], %[lo], %[x]\n\t"
+        "v_max_f64 %[hi], %[hi], %[x]\n\t"
+        "s_mov_b64 exec, %[save]"
+        : [sd] "+v"(a.sd), [sdd] "+v"(a.sdd), [k] "+v"(a.k), [is] "+v"(a.is), [lo] "+v"(lo), [hi] "+v"(hi),
+          [d] "=&v"(d), [save] "=&s"(save)
+        : [x] "v"(x), [sh] "v"(a.shift), [b] "v"(b), [ma] "s"(ma));
+  } else if constexpr (!MINMAX_SEP) {
+    asm volatile(
+        "s_and_saveexec_b64 %[save], %[ma]\n\t"
+        "v_add_f64 %[d], %[x], -%[sh]\n\t"
+        "v_add_u32 %[k], 1, %[k]\n\t"
+        "v_min_f64 %[lo], %[lo], %[x]\n\t"
+        "v_max_f64 %[hi], %[hi], %[x]\n\t"
+        "v_add_f64 %[sd], %[sd], %[d]\n\t"
+        "v_fma_f64 %[sdd], %[d], %[d], %[sdd]\n\t"
+        "s_mov_b64 exec, %[save]"
+        : [sd] "+v"(a.sd), [sdd] "+v"(a.sdd), [k] "+v"(a.k), [lo] "+v"(lo), [hi] "+v"(hi), [d] "=&v"(d),
+          [save] "=&s"(save)
+        : [x] "v"(x), [sh] "v"(a.shift), [ma] "s"(ma));
+  } else {
+    asm volatile(
+        "s_and_saveexec_b64 %[save], %[ma]\n\t"
+        "v_add_f64 %[d], %[x], -%[sh]\n\t"
+        "v_add_u32 %[k], 1, %[k]\n\t"
+        "v_add_f64 %[sd], %[sd], %[d]\n\t"
+        "v_fma_f64 %[sdd], %[d], %[d], %[sdd]\n\t"
+        "s_and_b64 exec, %[save], %[mb]\n\t"
+        "v_min_f64 %[lo], %[lo], %[x]\n\t"
+        "v_max_f64 %[hi], %[hi], %[x]\n\t"
+        "s_mov_b64 exec, %[save]"
+        : [sd] "+v"(a.sd), [sdd] "+v"(a.sdd), [k] "+v"(a.k), [lo] "+v"(lo), [hi] "+v"(hi), [d] "=&v"(d),
+          [save] "=&s"(save)
+        : [x] "v"(x), [sh] "v"(a.shift), [ma] "s"(ma), [mb] "s"(mb));
+  }
+}
+
+// One 512-row block of a wave: x[j] the lane's value of row group j as a double, bits[j] its raw
+// 64-bit pattern (i32: sign-extended), m[j] the selection masks, nanm[j] the selected NaN rows (F64).
+// NANS (the block holds a selected NaN, rare): NaN rows hash as the canonical NaN (doubleToLongBits)
+// and stay out of min / max (Spark orders NaN above every value; the caller counts them).
+template <int KIND, bool STATS, bool HLL, bool NANS>
+__device__ __forceinline__ void numeric_block(const double (&x)[8], const uint64_t (&bits)[8], const uint64_t (&m)[8],
+                                              const uint64_t (&nanm)[8], ColStats& s, LaneMoments& a, int32_t* regs,
+                                              int32_t& qmin) {
+  if (STATS) {
+    // still-empty lanes take the block's first selected value as their shift (wave-uniform branch)
+    if (__builtin_amdgcn_ballot_w64(s.n == 0.0 && a.k == 0) != 0) {
+      double first = a.shift;
+#pragma unroll
+      for (int j = 7; j >= 0; --j) first = lane_bit(m[j]) ? x[j] : first;
+      if (s.n == 0.0 && a.k == 0) a.shift = first;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    if (STATS) masked_moments<KIND != CK_F64, NANS>(a, s.fmin, s.fmax, x[j], bits[j], m[j], m[j] & ~nanm[j]);
+    if (HLL) {
+      HllKey key;
+      if (KIND == CK_I32) {
+        key = hll_key_int((uint32_t)bits[j]);
+      } else {
+        uint64_t b = bits[j];
+        if (NANS) b = lane_bit(nanm[j]) ? 0x7FF8000000000000ull : b;
+        key = hll_key_long(b);
+      }
+      qmin = min(qmin, key.q);
+      if (lane_bit(m[j])) atomicMax(reinterpret_cast<int32_t*>(reinterpret_cast<char*>(regs) + key.addr), key.q);
+    }
+  }
+  if (HLL) {
+    // rare (2^-23 per value): a rank that needs the hash's low word -- redo the block's selected
+    // values exactly (register max is idempotent)
+    if (__builtin_amdgcn_ballot_w64(qmin < 0) != 0) {
+#pragma unroll 1
+      for (int j = 0; j < 8; ++j) {
+        if (lane_bit(m[j])) {
+          uint64_t b = bits[j];
+          if (KIND == CK_F64 && x[j] != x[j]) b = 0x7FF8000000000000ull;
+          hll_update(regs, KIND == CK_I32 ? xxh64_int((uint32_t)b) : xxh64_long(b));
+        }
+      }
+      qmin = 0;
+    }
+  }
+}
 
 // Numeric column (f64 / i64 / i32): each wave takes 512-row blocks, lane l holding rows
 // base + 64 j + l (j < 8): coalesced 512-byte (8-byte types) loads per instruction, selection masks
-// in SGPRs.  Per row: stats as shifted sums (STATS), XXH64 + predicated LDS register max (HLL).
+// in SGPRs.  Per row: stats as shifted sums (STATS), XXH64 + exec-masked LDS register max (HLL).
 template <int KIND, bool STATS, bool HLL>
 __device__ void numeric_range(const void* values, const uint32_t* validity, const uint32_t* mask,
-                              int64_t row0, int64_t row1, ColStats& s, uint32_t* regs) {
+                              int64_t row0, int64_t row1, ColStats& s, int32_t* regs) {
   using T = typename std::conditional<KIND == CK_I32, int32_t, typename std::conditional<KIND == CK_I64, int64_t, double>::type>::type;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -342,66 +486,48 @@ __device__ void numeric_range(const void* values, const uint32_t* validity, cons
   const __amdgpu_buffer_rsrc_t vr = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<T*>(v + row0), (short)0, (int)((row1 - row0) * (int64_t)sizeof(T)), 0x00020000);
   int64_t nan_w = 0;  // wave-uniform count of selected NaN values
-  int kcount = 0;     // per-lane selected rows (HLL-only variant)
-  for (int64_t blk = row0; blk < row1; blk += kRowsPerIter) {
+  int64_t cnt_w = 0;  // wave-uniform count of selected rows (HLL-only variant)
+  LaneMoments a{0.0, 0.0, 0.0, 0, 0};
+  int32_t qmin = 0;
+  int nb = 0;
+  for (int64_t blk = row0; blk < row1; blk += kRowsPerIter, ++nb) {
     const int64_t base = blk + (int64_t)wave * 512;
     const bool full = blk + kRowsPerIter <= row1;
-    T e[8];
-    uint64_t m[8];
+    uint64_t bits[8], m[8], nanm[8];
+    double x[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int soff = (int)((base - row0 + j * 64) * (int64_t)sizeof(T));
       if constexpr (sizeof(T) == 8) {
         const auto w2 = __builtin_amdgcn_raw_buffer_load_b64(vr, lane * 8, soff, 2 /* nt */);
-        const uint64_t u = ((uint64_t)w2[1] << 32) | w2[0];
-        e[j] = __builtin_bit_cast(T, u);
+        bits[j] = ((uint64_t)w2[1] << 32) | w2[0];
+        if (KIND == CK_F64) x[j] = __builtin_bit_cast(double, bits[j]);
+        else x[j] = __builtin_fma((double)(int32_t)w2[1], 4294967296.0, (double)w2[0]);  // exact int64 -> double
       } else {
-        e[j] = (T)__builtin_amdgcn_raw_buffer_load_b32(vr, lane * 4, soff, 2 /* nt */);
+        const int32_t w = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(vr, lane * 4, soff, 2 /* nt */);
+        bits[j] = (uint64_t)(int64_t)w;
+        x[j] = (double)w;
       }
     }
     block_masks(validity, mask, base, row1, full, m);
-    double x[8];
-    uint64_t nanm[8];
+    uint64_t nan_any = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      x[j] = KIND == CK_F64 ? (double)e[j] : (double)(int64_t)e[j];
       nanm[j] = KIND == CK_F64 ? __builtin_amdgcn_ballot_w64(x[j] != x[j]) & m[j] : 0ull;
-      if (KIND == CK_F64) nan_w += __builtin_popcountll(nanm[j]);
+      nan_any |= nanm[j];
+      if (!STATS) cnt_w += __builtin_popcountll(m[j]);
     }
-    if (STATS) {
-      // first selected value of still-empty lanes (rare: a wave-uniform branch)
-      double first = 0.0;
-      if (__builtin_amdgcn_ballot_w64(s.n == 0.0) != 0) {
+    if (KIND == CK_F64 && nan_any != 0) {
 #pragma unroll
-        for (int j = 7; j >= 0; --j) first = lane_bit(m[j]) ? x[j] : first;
-      }
-      Chunk<KIND> c;
-      c.begin(s, first);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) c.add(x[j], (int64_t)e[j], lane_bit(m[j]), lane_bit(m[j] & ~nanm[j]));
-      c.end(s);
+      for (int j = 0; j < 8; ++j) nan_w += __builtin_popcountll(nanm[j]);
+      numeric_block<KIND, STATS, HLL, true>(x, bits, m, nanm, s, a, regs, qmin);
     } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) kcount += lane_bit(m[j]) ? 1 : 0;
+      numeric_block<KIND, STATS, HLL, false>(x, bits, m, nanm, s, a, regs, qmin);
     }
-    if (HLL) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        uint64_t h;
-        if (KIND == CK_F64) {
-          uint64_t bits = (uint64_t)__double_as_longlong(x[j]);
-          if (nanm[j] != 0) bits = lane_bit(nanm[j]) ? 0x7FF8000000000000ull : bits;  // doubleToLongBits
-          h = xxh64_long(bits);
-        } else if (KIND == CK_I64) {
-          h = xxh64_long((uint64_t)(int64_t)e[j]);
-        } else {
-          h = xxh64_int((uint32_t)e[j]);
-        }
-        hll_update_if(regs, h, lane_bit(m[j]));
-      }
-    }
+    if (STATS && (nb % kChunkBlocks) == kChunkBlocks - 1) moments_flush<KIND>(s, a);
   }
-  if (!STATS) s.count += kcount;
+  if (STATS) moments_flush<KIND>(s, a);
+  if (!STATS && lane == 0) s.count += cnt_w;
   if (KIND == CK_F64 && lane == 0) s.nan_count += nan_w;
 }
 
@@ -414,7 +540,7 @@ __device__ void numeric_range(const void* values, const uint32_t* validity, cons
 // with the general XXH64 loop (a divergent branch that is almost never taken).
 template <typename OffT>
 __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint32_t* validity,
-                           const uint32_t* mask, int64_t row0, int64_t row1, ColStats& s, uint32_t* regs) {
+                           const uint32_t* mask, int64_t row0, int64_t row1, ColStats& s, int32_t* regs) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (row0 >= row1) return;
@@ -500,7 +626,7 @@ __device__ void validity_range(const uint32_t* validity, const uint32_t* mask, i
 
 template <int KIND, bool STATS, bool HLL>
 __device__ void run_numeric(const ColTask& t, const ScanCols& cols, const ScanBitmaps& bm, int64_t row0, int64_t row1,
-                            ColStats& s, uint32_t* regs) {
+                            ColStats& s, int32_t* regs) {
   const uint32_t* mask = t.where >= 0 ? reinterpret_cast<const uint32_t*>(bm.where_bits[t.where]) : nullptr;
   numeric_range<KIND, STATS, HLL>(cols.values[t.col], cols.validity[t.col], mask, row0, row1, s, regs);
 }
@@ -512,7 +638,7 @@ __device__ void run_numeric(const ColTask& t, const ScanCols& cols, const ScanBi
 // ------------------------------------------------------------------------------------------
 template <int V>
 __device__ __forceinline__ void run_variant(const ColTask& t, const ScanCols& cols, const uint32_t* mask, int64_t row0,
-                                            int64_t row1, ColStats& s, uint32_t* regs) {
+                                            int64_t row1, ColStats& s, int32_t* regs) {
   const void* v = cols.values[t.col];
   const uint32_t* val = cols.validity[t.col];
   if constexpr (V == CV_VALIDITY) validity_range(val, mask, row0, row1, s);
@@ -540,7 +666,7 @@ __global__ __launch_bounds__(kBlock) void dq_column_scan(const ColTask* __restri
                                                          ColPartial* __restrict__ partials,
                                                          uint32_t* __restrict__ hll_acc) {
   constexpr bool kHll = !(V == CV_VALIDITY || V == CV_F64_S || V == CV_I64_S || V == CV_I32_S);
-  __shared__ uint32_t regs[kHll ? 512 : 1];
+  __shared__ int32_t regs[kHll ? 512 : 1];  // q = pw - 1, -1 = empty (see hll_q_exact)
   __shared__ ColStats red[kWaves];
   const int32_t ti = blockIdx.x % ntasks;
   const int32_t range = blockIdx.x / ntasks;
@@ -549,7 +675,7 @@ __global__ __launch_bounds__(kBlock) void dq_column_scan(const ColTask* __restri
   int64_t row1 = row0 + rows_per_range;
   if (row1 > n_rows) row1 = n_rows;
   if constexpr (kHll) {
-    for (int i = threadIdx.x; i < 512; i += kBlock) regs[i] = 0;
+    for (int i = threadIdx.x; i < 512; i += kBlock) regs[i] = -1;
     __syncthreads();
   }
   ColStats s;
@@ -564,7 +690,7 @@ __global__ __launch_bounds__(kBlock) void dq_column_scan(const ColTask* __restri
     __syncthreads();
     uint32_t* dst = hll_acc + (size_t)t.hll_slot * 512;
     for (int i = threadIdx.x; i < 512; i += kBlock) {
-      const uint32_t v = regs[i];
+      const uint32_t v = (uint32_t)(regs[i] + 1);
       if (v > __builtin_nontemporal_load(dst + i)) atomicMax(dst + i, v);
     }
   }

@@ -1046,12 +1046,13 @@ dq_status dq_finish(dq_plan* p, dq_state* out) {
       case DQ_OP_MIN:
       case DQ_OP_MAX: {
         set1(c->count > 0);
-        if (o.col_type == DQ_TYPE_F64) {
+        // fmin / fmax hold the min / max of the selected non-NaN values as doubles for every numeric
+        // kind: for integral columns min(double(x)) == double(min(x)), Spark's CAST(min(col) AS DOUBLE),
+        // because the int -> double cast is monotone.  nan_count is 0 for integral columns.
+        {
           const bool all_nan = c->nan_count == c->count;
           if (o.op == DQ_OP_MIN) s.u.minmax.value = all_nan ? nan : c->fmin;
           else s.u.minmax.value = c->nan_count > 0 ? nan : c->fmax;  // NaN is the largest value
-        } else {
-          s.u.minmax.value = (double)(o.op == DQ_OP_MIN ? c->imin : c->imax);
         }
         break;
       }

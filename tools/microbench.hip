@@ -64,9 +64,9 @@ __global__ __launch_bounds__(256) void k(const double* __restrict__ v, int64_t n
 template <bool STATS, bool HLL>
 __global__ __launch_bounds__(256) void kreal(const double* __restrict__ v, const uint32_t* validity, int64_t n,
                                              int64_t rows_per_wg, ColPartial* out) {
-  __shared__ uint32_t regs[512];
+  __shared__ int32_t regs[512];
   __shared__ ColStats red[4];
-  for (int i = threadIdx.x; i < 512; i += 256) regs[i] = 0;
+  for (int i = threadIdx.x; i < 512; i += 256) regs[i] = -1;
   __syncthreads();
   const int64_t r0 = blockIdx.x * rows_per_wg, r1 = min(n, r0 + rows_per_wg);
   ColStats s;
@@ -74,7 +74,7 @@ __global__ __launch_bounds__(256) void kreal(const double* __restrict__ v, const
   numeric_range<CK_F64, STATS, HLL>(v, validity, nullptr, r0, r1, s, regs);
   block_reduce_store(s, out + blockIdx.x, red);
   __syncthreads();
-  if (HLL && regs[threadIdx.x] == 0x12345u) out[0].pad = 1;
+  if (HLL && regs[threadIdx.x] == 0x12345) out[0].pad = 1;
 }
 
 template <bool STATS, bool HLL>
@@ -128,9 +128,9 @@ __global__ void init_str(int32_t* offs, uint8_t* data, int64_t n) {
 template <int MODE>
 __global__ __launch_bounds__(256) void kutf8(const uint8_t* data, const int32_t* offs, int64_t n, int64_t rpw,
                                              ColPartial* out) {
-  __shared__ uint32_t regs[512];
+  __shared__ int32_t regs[512];
   __shared__ ColStats red[4];
-  for (int i = threadIdx.x; i < 512; i += 256) regs[i] = 0;
+  for (int i = threadIdx.x; i < 512; i += 256) regs[i] = -1;
   __syncthreads();
   const int64_t r0 = blockIdx.x * rpw, r1 = min(n, r0 + rpw);
   ColStats s;
@@ -166,7 +166,7 @@ __global__ __launch_bounds__(256) void kutf8(const uint8_t* data, const int32_t*
   }
   block_reduce_store(s, out + blockIdx.x, red);
   __syncthreads();
-  if (regs[threadIdx.x] == 0x12345u) out[0].pad = 1;
+  if (regs[threadIdx.x] == 0x12345) out[0].pad = 1;
 }
 
 template <int MODE>
