@@ -40,58 +40,88 @@ DQ_HD uint64_t rotl64(uint64_t x, int r) {
   return (x << r) | (x >> (64 - r));
 #endif
 }
-DQ_HD uint64_t fmix64(uint64_t h) {
-  h ^= h >> 33; h *= XP2; h ^= h >> 29; h *= XP3; h ^= h >> 32; return h;
-}
-DQ_HD uint64_t xxh64_long(uint64_t v) {
-  uint64_t h = kSeed + XP5 + 8;
-  h ^= rotl64(v * XP2, 31) * XP1;
-  h = rotl64(h, 27) * XP1 + XP4;
-  return fmix64(h);
-}
-DQ_HD uint64_t xxh64_int(uint32_t v) {
-  uint64_t h = kSeed + XP5 + 4;
-  h ^= (uint64_t)v * XP1;
-  h = rotl64(h, 23) * XP2 + XP3;
-  return fmix64(h);
+// x * c + a (mod 2^64) for constants c, a, written so the device code is one v_mad_u64_u32 (low
+// product + addend), two v_mul_lo_u32 (cross products) and one add3.
+DQ_HD uint64_t mul_add_c(uint64_t x, uint64_t c, uint64_t a) {
+  const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
+#if defined(__HIP_DEVICE_COMPILE__)
+  // The three multiplies are pinned in asm: left to itself LLVM re-associates the cross products
+  // into extra v_mad_u64_u32 + v_mov chains (up to 7 instructions).  The addend is a VGPR pair (a
+  // loop-invariant constant; the VOP3 constant bus takes only the SGPR multiplier).
+  uint64_t p, carry;
+  uint32_t t1, t2;
+  asm("v_mad_u64_u32 %[p], %[cy], %[xl], %[cl], %[a]\n\t"
+      "v_mul_lo_u32 %[t1], %[xl], %[ch]\n\t"
+      "v_mul_lo_u32 %[t2], %[xh], %[cl]"
+      : [p] "=&v"(p), [cy] "=&s"(carry), [t1] "=&v"(t1), [t2] "=&v"(t2)
+      : [xl] "v"(xl), [xh] "v"(xh), [cl] "s"((uint32_t)c), [ch] "s"((uint32_t)(c >> 32)), [a] "v"(a));
+  (void)carry;
+  const uint32_t hi = (uint32_t)(p >> 32) + t1 + t2;
+#else
+  const uint64_t p = (uint64_t)xl * (uint32_t)c + a;
+  const uint32_t hi = (uint32_t)(p >> 32) + xl * (uint32_t)(c >> 32) + xh * (uint32_t)c;
+#endif
+  return ((uint64_t)hi << 32) | (uint32_t)p;
 }
 
-// XXH64.hashUnsafeBytes of a string of len <= 28 bytes held in w[0..6] (little-endian dwords of the
-// string itself).  Branch-free: every lane runs 3 stripe rounds, one 4-byte round and 3 byte rounds
-// and keeps the ones its length needs, so a wave of mixed lengths does not diverge.  The 4-byte
-// round's dword w[2 nw] and the byte rounds' dword w[len >> 2] = w[2 nw + (len >> 2 & 1)] are
-// picked up by the same predicates as the stripe rounds (no dynamic register indexing).
-DQ_HD uint64_t xxh64_short(const uint32_t (&w)[7], uint32_t len) {
+// fmix64 split in two: fmix_head(h) is the state before the last multiply; the final hash is
+// fmix_tail(fmix_head(h)).  The HLL kernels only need the high word of fmix_tail, hi32(b * P3).
+DQ_HD uint64_t fmix_head(uint64_t h) {
+  h ^= h >> 33;
+  h = mul_add_c(h, XP2, 0);
+  return h ^ (h >> 29);
+}
+DQ_HD uint64_t fmix_tail(uint64_t b) {
+  const uint64_t h = b * XP3;
+  return h ^ (h >> 32);
+}
+DQ_HD uint64_t fmix64(uint64_t h) { return fmix_tail(fmix_head(h)); }
+
+// XXH64.hashLong / hashInt (seed 42) up to fmix_head
+DQ_HD uint64_t xxh64_long_head(uint64_t v) {
+  const uint64_t k = rotl64(mul_add_c(v, XP2, 0), 31);
+  const uint64_t h = mul_add_c(k, XP1, 0) ^ (kSeed + XP5 + 8);
+  return fmix_head(mul_add_c(rotl64(h, 27), XP1, XP4));
+}
+DQ_HD uint64_t xxh64_int_head(uint32_t v) {
+  const uint64_t h = ((uint64_t)v * XP1) ^ (kSeed + XP5 + 4);
+  return fmix_head(mul_add_c(rotl64(h, 23), XP2, XP3));
+}
+DQ_HD uint64_t xxh64_long(uint64_t v) { return fmix_tail(xxh64_long_head(v)); }
+DQ_HD uint64_t xxh64_int(uint32_t v) { return fmix_tail(xxh64_int_head(v)); }
+
+// XXH64.hashUnsafeBytes of a string of len <= 28 bytes, up to fmix_head.  w[0..6]: the string's
+// bytes as little-endian dwords (bytes past len may hold anything).  Branch-free: every lane runs 3
+// stripe rounds, one 4-byte round and 3 byte rounds and keeps the ones its length needs, so a wave
+// of mixed lengths does not diverge.  The 4-byte round's dword w[2 nw] and the byte rounds' dword
+// w[len >> 2] = w[2 nw + (len >> 2 & 1)] ride along the stripe rounds' predicates (no dynamic
+// register indexing).
+DQ_HD uint64_t xxh64_short_head(const uint32_t (&w)[7], uint32_t len) {
   uint64_t h = kSeed + XP5 + (uint64_t)len;
   const uint32_t nw = len >> 3;
   uint32_t d4 = w[0], d4n = w[1];  // w[2 nw], w[2 nw + 1] after the stripe rounds
 #pragma unroll
   for (uint32_t k = 0; k < 3; ++k) {
     const uint64_t k1 = ((uint64_t)w[2 * k + 1] << 32) | w[2 * k];
-    uint64_t hn = h ^ (rotl64(k1 * XP2, 31) * XP1);
-    hn = rotl64(hn, 27) * XP1 + XP4;
+    uint64_t hn = h ^ mul_add_c(rotl64(mul_add_c(k1, XP2, 0), 31), XP1, 0);
+    hn = mul_add_c(rotl64(hn, 27), XP1, XP4);
     const bool take = k < nw;
     h = take ? hn : h;
     d4 = take ? w[2 * k + 2] : d4;
     d4n = take ? (k < 2 ? w[2 * k + 3] : 0u) : d4n;  // w[7] only for len 28, which has no byte rounds
   }
-  // 4-byte round on dword 2 nw
   const bool has4 = (len & 4u) != 0;
-  uint64_t h4 = h ^ ((uint64_t)d4 * XP1);
-  h4 = rotl64(h4, 23) * XP2 + XP3;
+  const uint64_t h4 = mul_add_c(rotl64(h ^ ((uint64_t)d4 * XP1), 23), XP2, XP3);
   h = has4 ? h4 : h;
-  // byte rounds on dword len >> 2
   const uint32_t db = has4 ? d4n : d4;
   const uint32_t nb = len & 3u;
 #pragma unroll
   for (uint32_t j = 0; j < 3; ++j) {
     const uint64_t b = (db >> (8 * j)) & 0xFFu;
-    uint64_t hb = h ^ (b * XP5);
-    hb = rotl64(hb, 11) * XP1;
+    const uint64_t hb = mul_add_c(rotl64(h ^ (b * XP5), 11), XP1, 0);
     h = j < nb ? hb : h;
   }
-  return fmix64(h);
+  return fmix_head(h);
 }
-
 
 }  // namespace dq

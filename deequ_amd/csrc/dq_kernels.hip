@@ -112,16 +112,7 @@ __device__ __forceinline__ int32_t ffbh_raw(uint32_t x) {
   return r;
 }
 
-// x * c + a (mod 2^64) for constants c, a: one v_mad_u64_u32 (low product + addend), two
-// v_mul_lo_u32 (cross products) and one add3 -- the shortest CDNA sequence for a 64-bit multiply.
-__device__ __forceinline__ uint64_t mul_add_c(uint64_t x, uint64_t c, uint64_t a) {
-  const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
-  const uint64_t p = (uint64_t)xl * (uint32_t)c + a;
-  const uint32_t hi = (uint32_t)(p >> 32) + xl * (uint32_t)(c >> 32) + xh * (uint32_t)c;
-  return ((uint64_t)hi << 32) | (uint32_t)p;
-}
-
-// HLL key of a finished-but-for-the-last-multiply XXH64 state b (after `h ^= h >> 29` of fmix64):
+// HLL key of an XXH64 state b = fmix_head(h) (dq_hash.h), i.e. before fmix64's last multiply:
 // the final hash's high word is hi32(b * P3) (the closing `h ^= h >> 32` only changes the low word),
 // which carries the register index (bits 63..55) and, unless its bits 54..32 are all zero
 // (probability 2^-23), the rank.  `addr` is the LDS byte offset of register idx; `q` = pw - 1, or -1
@@ -135,28 +126,9 @@ __device__ __forceinline__ HllKey hll_key_from_fmix(uint64_t b) {
   const uint32_t hi = __umulhi(bl, (uint32_t)XP3) + bl * (uint32_t)(XP3 >> 32) + bh * (uint32_t)XP3;
   return {(hi >> 21) & 0x7FCu, ffbh_raw(hi << 9)};
 }
-// XXH64.hashLong(v, 42) -> HLL key (hashLong: StatefulHyperloglogPlus.scala:93 via XxHash64Function)
-__device__ __forceinline__ HllKey hll_key_long(uint64_t v) {
-  const uint64_t k = rotl64(mul_add_c(v, XP2, 0), 31);
-  uint64_t h = mul_add_c(k, XP1, 0) ^ (kSeed + XP5 + 8);
-  h = mul_add_c(rotl64(h, 27), XP1, XP4);
-  h ^= h >> 33;
-  h = mul_add_c(h, XP2, 0);
-  return hll_key_from_fmix(h ^ (h >> 29));
-}
-// XXH64.hashInt(v, 42) -> HLL key
-__device__ __forceinline__ HllKey hll_key_int(uint32_t v) {
-  uint64_t h = ((uint64_t)v * XP1) ^ (kSeed + XP5 + 4);
-  h = mul_add_c(rotl64(h, 23), XP2, XP3);
-  h ^= h >> 33;
-  h = mul_add_c(h, XP2, 0);
-  return hll_key_from_fmix(h ^ (h >> 29));
-}
-
-__device__ __forceinline__ uint64_t f64_hash_bits(double d) {
-  // doubleToLongBits: canonical NaN
-  return d != d ? 0x7FF8000000000000ull : (uint64_t)__double_as_longlong(d);
-}
+// XXH64.hashLong / hashInt (seed 42) -> HLL key (StatefulHyperloglogPlus.scala:93 via XxHash64Function)
+__device__ __forceinline__ HllKey hll_key_long(uint64_t v) { return hll_key_from_fmix(xxh64_long_head(v)); }
+__device__ __forceinline__ HllKey hll_key_int(uint32_t v) { return hll_key_from_fmix(xxh64_int_head(v)); }
 
 // Hardware v_min_f64 / v_max_f64 (IEEE mode: a NaN operand yields the other operand).  Inline asm
 // keeps the compiler from canonicalising both inputs first (two extra v_max_f64 per call).
@@ -534,38 +506,41 @@ __device__ void numeric_range(const void* values, const uint32_t* validity, cons
 // UTF8 column: lane l of a wave takes rows base + 64 j + l (j < 8) of its 512-row block, so the
 // selection masks are scalar bitmap words (as in numeric_range).  Offsets come through a
 // bounds-checked buffer resource over offsets[row0 .. row1]; every lane fetches its string with two
-// 16-byte buffer loads (dword-aligned, bounded by the range's last offset, so nothing past the data
-// is touched and an out-of-range window reads zeros) and hashes it branch-free as a string of
-// <= 28 bytes.  Lanes whose string is longer, or whose 32-byte window crosses the range end, rehash
-// with the general XXH64 loop (a divergent branch that is almost never taken).
+// dword-aligned 16-byte buffer loads (byte-granular loads are exact on gfx950 but run at ~60% of the
+// aligned rate) from a window over the chunk's string bytes, realigns them with v_alignbit and hashes
+// the string branch-free as one of <= 28 bytes (xxh64_short_head).  A string that is longer, or whose
+// 32-byte window would cross the end of the chunk's bytes, is flagged in an SGPR mask and rehashed by
+// the general XXH64 loop after the block (rare; ds_max is idempotent, so the block's selected rows
+// are simply redone there).
 template <typename OffT>
 __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint32_t* validity,
-                           const uint32_t* mask, int64_t row0, int64_t row1, ColStats& s, int32_t* regs) {
+                           const uint32_t* mask, int64_t row0, int64_t row1, int64_t n_rows, ColStats& s,
+                           int32_t* regs) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (row0 >= row1) return;
   constexpr int W = (int)sizeof(OffT);
-  // byte window of this range, addressed by a 32-bit buffer offset from a dword-aligned base
+  // byte window [lo, end of the chunk's strings) from a dword-aligned lo, 32-bit offsets
   const int64_t lo = (int64_t)offsets[row0] & ~int64_t(3);
-  const int64_t hi = (int64_t)offsets[row1];
-  const bool fast_ok = (hi - lo) < (int64_t)0x7FFFFFF0;
+  const int64_t span = (int64_t)offsets[n_rows] - lo;
+  const bool fast_ok = span < (int64_t)0x7FFFFF00;
   const __amdgpu_buffer_rsrc_t rsrc =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(data + lo), (short)0, fast_ok ? (int)(hi - lo) : 0, 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(data + lo), (short)0, fast_ok ? (int)span : 0, 0x00020000);
   const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<OffT*>(offsets + row0), (short)0, (int)((row1 - row0 + 1) * W), 0x00020000);
-  const int32_t win = fast_ok ? (int32_t)(hi - lo) : 0;
+  const int32_t win = fast_ok ? (int32_t)span - 32 : -1;  // fast iff off <= win: both loads in range
   int64_t cnt_w = 0;  // wave-uniform count of selected rows
+  int32_t qmin = 0;
   for (int64_t blk = row0; blk < row1; blk += kRowsPerIter) {
     const int64_t base = blk + (int64_t)wave * 512;
     const bool full = blk + kRowsPerIter <= row1;
     uint64_t m[8];
     block_masks(validity, mask, base, row1, full, m);
-    uint32_t slow = 0;  // bit j: this lane's row j needs the general hash
+    uint64_t slow = 0;  // OR of the rows that need the general hash
 #pragma unroll
     for (int j = 0; j < 8; ++j) cnt_w += __builtin_popcountll(m[j]);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const bool b = lane_bit(m[j]);
       const int soff = (int)((base - row0 + j * 64) * W);
       int64_t o0, o1;
       if constexpr (W == 4) {
@@ -577,10 +552,11 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
         o0 = (int64_t)(((uint64_t)a0[1] << 32) | a0[0]);
         o1 = (int64_t)(((uint64_t)a1[1] << 32) | a1[0]);
       }
-      // 32-bit window arithmetic: when fast_ok, every offset of the range lies in [lo, lo + 2^31)
-      const int32_t rel = (int32_t)(o0 - lo);
-      const int64_t len = o1 - o0;
-      const int32_t off = rel & ~3;
+      // 32-bit window arithmetic: when fast_ok, every offset of the chunk lies in [lo, lo + 2^31)
+      const int32_t off = (int32_t)(o0 - lo) & ~3;
+      const uint32_t len = (uint32_t)(o1 - o0);
+      const uint64_t fastm = __builtin_amdgcn_ballot_w64(len <= 28u && off <= win);
+      slow |= m[j] & ~fastm;
       const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0);
       const u32x4 c = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off + 16, 0, 0);
       const uint32_t d[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
@@ -588,22 +564,21 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
       uint32_t wv[7];
 #pragma unroll
       for (int k = 0; k < 7; ++k) wv[k] = alignbit32(d[k + 1], d[k], sh);  // sh == 0 -> d[k]
-      uint64_t h = xxh64_short(wv, (uint32_t)len);
-      // fast path only when both 16-byte loads lie inside [lo, hi)
-      const bool fast = fast_ok && (uint32_t)len <= 28u && (uint32_t)len == len && off + 32 <= win;
-      slow |= (b && !fast) ? (1u << j) : 0u;
-      hll_update_if(regs, h, b && fast);
+      const HllKey key = hll_key_from_fmix(xxh64_short_head(wv, len));
+      qmin = min(qmin, key.q);
+      if (lane_bit(m[j] & fastm)) atomicMax(reinterpret_cast<int32_t*>(reinterpret_cast<char*>(regs) + key.addr), key.q);
     }
-    // the rare long / window-crossing strings: one general XXH64 per flagged row (a single copy of
-    // the loop, outside the unrolled body)
-    if (__builtin_amdgcn_ballot_w64(slow != 0) != 0) {
-      while (slow) {
-        const int j = __builtin_ctz(slow);
-        slow &= slow - 1;
-        const int64_t row = base + j * 64 + lane;
-        const int64_t o0 = (int64_t)offsets[row], o1 = (int64_t)offsets[row + 1];
-        hll_update_if(regs, xxh64_bytes(data, o0, o1 - o0), true);
+    // rare: long / window-crossing strings, or a rank that needs the hash's low word (2^-23)
+    if ((slow | __builtin_amdgcn_ballot_w64(qmin < 0)) != 0) {
+#pragma unroll 1
+      for (int j = 0; j < 8; ++j) {
+        if (lane_bit(m[j])) {
+          const int64_t row = base + j * 64 + lane;
+          const int64_t o0 = (int64_t)offsets[row], o1 = (int64_t)offsets[row + 1];
+          hll_update(regs, xxh64_bytes(data, o0, o1 - o0));
+        }
       }
+      qmin = 0;
     }
   }
   if (lane == 0) s.count += cnt_w;
@@ -638,7 +613,7 @@ __device__ void run_numeric(const ColTask& t, const ScanCols& cols, const ScanBi
 // ------------------------------------------------------------------------------------------
 template <int V>
 __device__ __forceinline__ void run_variant(const ColTask& t, const ScanCols& cols, const uint32_t* mask, int64_t row0,
-                                            int64_t row1, ColStats& s, int32_t* regs) {
+                                            int64_t row1, int64_t n_rows, ColStats& s, int32_t* regs) {
   const void* v = cols.values[t.col];
   const uint32_t* val = cols.validity[t.col];
   if constexpr (V == CV_VALIDITY) validity_range(val, mask, row0, row1, s);
@@ -653,10 +628,10 @@ __device__ __forceinline__ void run_variant(const ColTask& t, const ScanCols& co
   else if constexpr (V == CV_I32_H) numeric_range<CK_I32, false, true>(v, val, mask, row0, row1, s, regs);
   else if constexpr (V == CV_UTF8_H)
     utf8_range<int32_t>(reinterpret_cast<const uint8_t*>(v), reinterpret_cast<const int32_t*>(cols.offsets[t.col]),
-                        val, mask, row0, row1, s, regs);
+                        val, mask, row0, row1, n_rows, s, regs);
   else
     utf8_range<int64_t>(reinterpret_cast<const uint8_t*>(v), reinterpret_cast<const int64_t*>(cols.offsets[t.col]),
-                        val, mask, row0, row1, s, regs);
+                        val, mask, row0, row1, n_rows, s, regs);
 }
 
 template <int V>
@@ -681,7 +656,7 @@ __global__ __launch_bounds__(kBlock) void dq_column_scan(const ColTask* __restri
   ColStats s;
   stats_init(s);
   const uint32_t* mask = t.where >= 0 ? reinterpret_cast<const uint32_t*>(bm.where_bits[t.where]) : nullptr;
-  run_variant<V>(t, cols, mask, row0, row1, s, regs);
+  run_variant<V>(t, cols, mask, row0, row1, n_rows, s, regs);
   block_reduce_store(s, partials + (size_t)(part_base + ti) * kMaxWG + range, red);
   if constexpr (kHll) {
     // registers only grow: merge into the plan accumulator with device-scope atomicMax, skipping

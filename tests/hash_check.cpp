@@ -1,6 +1,8 @@
 // Host build of the kernels' XXH64 formulations (deequ_amd/csrc/dq_hash.h), driven by
 // tests/test_hash_formulation.py against the golden vectors.  Reads "len hex" lines on stdin and
-// prints the signed hash of xxh64_short() for every byte alignment 0..3 of the string.
+// prints the signed hash of fmix_tail(xxh64_short_head()) for every byte alignment 0..3 of the string,
+// fed as the UTF8 kernel feeds it: two aligned 16-byte loads realigned with alignbit, and garbage
+// (0xA5) in the bytes past the string.
 #include <cstdio>
 #include <cstring>
 #include <vector>
@@ -14,14 +16,16 @@ int main() {
     unsigned char bytes[64] = {0};
     for (int i = 0; i < len; ++i) std::sscanf(hex + 2 * i, "%2hhx", &bytes[i]);
     for (int align = 0; align < 4; ++align) {
-      unsigned char buf[96] = {0};
+      unsigned char buf[96];
+      std::memset(buf, 0xA5, sizeof(buf));
       std::memcpy(buf + align, bytes, len);
       uint32_t d[8];
       std::memcpy(d, buf, 32);
       const uint32_t sh = align * 8u;
       uint32_t w[7];
-      for (int k = 0; k < 7; ++k) w[k] = sh ? dq::alignbit32(d[k + 1], d[k], sh) : d[k];
-      std::printf("%lld%c", (long long)dq::xxh64_short(w, (uint32_t)len), align == 3 ? '\n' : ' ');
+      for (int k = 0; k < 7; ++k) w[k] = dq::alignbit32(d[k + 1], d[k], sh);
+      const uint64_t h = dq::fmix_tail(dq::xxh64_short_head(w, (uint32_t)len));
+      std::printf("%lld%c", (long long)h, align == 3 ? '\n' : ' ');
     }
   }
   std::printf("LONG %lld INT %lld\n", (long long)dq::xxh64_long(42u), (long long)dq::xxh64_int(7u));

@@ -136,7 +136,7 @@ __global__ __launch_bounds__(256) void kutf8(const uint8_t* data, const int32_t*
   ColStats s;
   stats_init(s);
   if (MODE == 1) {
-    utf8_range<int32_t>(data, offs, nullptr, nullptr, r0, r1, s, regs);
+    utf8_range<int32_t>(data, offs, nullptr, nullptr, r0, r1, n, s, regs);
   } else {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t lo = offs[r0] & ~3, hi = offs[r1];
@@ -158,7 +158,7 @@ __global__ __launch_bounds__(256) void kutf8(const uint8_t* data, const int32_t*
           uint32_t wv[7];
 #pragma unroll
           for (int k = 0; k < 7; ++k) wv[k] = alignbit32(d[k + 1], d[k], sh);
-          acc ^= (uint32_t)xxh64_short(wv, (uint32_t)(o1 - o0));
+          acc ^= (uint32_t)(xxh64_short_head(wv, (uint32_t)(o1 - o0)) >> 32);
         }
       }
     }
