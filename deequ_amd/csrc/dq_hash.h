@@ -64,6 +64,22 @@ DQ_HD uint64_t mul_add_c(uint64_t x, uint64_t c, uint64_t a) {
   return ((uint64_t)hi << 32) | (uint32_t)p;
 }
 
+// x * c (mod 2^64) for a 32-bit x: one v_mad_u64_u32, one v_mul_lo_u32, one add.
+DQ_HD uint64_t mul32_c(uint32_t x, uint64_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint64_t p, carry;
+  uint32_t t;
+  asm("v_mad_u64_u32 %[p], %[cy], %[x], %[cl], 0\n\t"
+      "v_mul_lo_u32 %[t], %[x], %[ch]"
+      : [p] "=&v"(p), [cy] "=&s"(carry), [t] "=&v"(t)
+      : [x] "v"(x), [cl] "s"((uint32_t)c), [ch] "s"((uint32_t)(c >> 32)));
+  (void)carry;
+  return ((uint64_t)((uint32_t)(p >> 32) + t) << 32) | (uint32_t)p;
+#else
+  return (uint64_t)x * c;
+#endif
+}
+
 // fmix64 split in two: fmix_head(h) is the state before the last multiply; the final hash is
 // fmix_tail(fmix_head(h)).  The HLL kernels only need the high word of fmix_tail, hi32(b * P3).
 DQ_HD uint64_t fmix_head(uint64_t h) {
@@ -84,43 +100,60 @@ DQ_HD uint64_t xxh64_long_head(uint64_t v) {
   return fmix_head(mul_add_c(rotl64(h, 27), XP1, XP4));
 }
 DQ_HD uint64_t xxh64_int_head(uint32_t v) {
-  const uint64_t h = ((uint64_t)v * XP1) ^ (kSeed + XP5 + 4);
+  const uint64_t h = mul32_c(v, XP1) ^ (kSeed + XP5 + 4);
   return fmix_head(mul_add_c(rotl64(h, 23), XP2, XP3));
 }
 DQ_HD uint64_t xxh64_long(uint64_t v) { return fmix_tail(xxh64_long_head(v)); }
 DQ_HD uint64_t xxh64_int(uint32_t v) { return fmix_tail(xxh64_int_head(v)); }
 
-// XXH64.hashUnsafeBytes of a string of len <= 28 bytes, up to fmix_head.  w[0..6]: the string's
-// bytes as little-endian dwords (bytes past len may hold anything).  Branch-free: every lane runs 3
-// stripe rounds, one 4-byte round and 3 byte rounds and keeps the ones its length needs, so a wave
-// of mixed lengths does not diverge.  The 4-byte round's dword w[2 nw] and the byte rounds' dword
-// w[len >> 2] = w[2 nw + (len >> 2 & 1)] ride along the stripe rounds' predicates (no dynamic
-// register indexing).
-DQ_HD uint64_t xxh64_short_head(const uint32_t (&w)[7], uint32_t len) {
+// Predicated 64-bit move dst = cond ? src : dst.  On the device it is one exec-masked v_mov_b64
+// (s_and_saveexec / s_mov exec around it) instead of two v_cndmask_b32.
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ void sel64(uint64_t& dst, uint64_t src, bool cond) {
+  uint64_t save;
+  asm("s_and_saveexec_b64 %[s], %[m]\n\t"
+      "v_mov_b64 %[d], %[x]\n\t"
+      "s_mov_b64 exec, %[s]"
+      : [d] "+v"(dst), [s] "=&s"(save)
+      : [x] "v"(src), [m] "s"(__builtin_amdgcn_ballot_w64(cond))
+      : "scc");  // s_and_saveexec writes SCC
+}
+#else
+inline void sel64(uint64_t& dst, uint64_t src, bool cond) { dst = cond ? src : dst; }
+#endif
+
+struct MulP5 {  // b * P5 for a byte b (host; the kernels read a 256-entry LDS table instead)
+  DQ_HD uint64_t operator()(uint32_t b) const { return (uint64_t)b * XP5; }
+};
+
+// XXH64.hashUnsafeBytes of a string of len <= 28 bytes, up to fmix_head.  w[0..7]: the string's
+// bytes as little-endian dwords (bytes past len may hold anything; w[7] is never read for a value
+// that matters).  Branch-free: every lane runs 3 stripe rounds, one 4-byte round and 3 byte rounds
+// and keeps the ones its length needs, so a wave of mixed lengths does not diverge.  The 4-byte
+// round's dword w[2 nw] and the byte rounds' dword w[len >> 2] = w[2 nw + (len >> 2 & 1)] ride
+// along the stripe rounds' predicates as one 64-bit pair (no dynamic register indexing).
+// bp(b) = b * P5 for a byte b.
+template <typename BP>
+DQ_HD uint64_t xxh64_short_head(const uint32_t (&w)[8], uint32_t len, BP bp) {
   uint64_t h = kSeed + XP5 + (uint64_t)len;
   const uint32_t nw = len >> 3;
-  uint32_t d4 = w[0], d4n = w[1];  // w[2 nw], w[2 nw + 1] after the stripe rounds
+  uint64_t d4p = ((uint64_t)w[1] << 32) | w[0];  // {w[2 nw], w[2 nw + 1]} after the stripe rounds
 #pragma unroll
   for (uint32_t k = 0; k < 3; ++k) {
     const uint64_t k1 = ((uint64_t)w[2 * k + 1] << 32) | w[2 * k];
     uint64_t hn = h ^ mul_add_c(rotl64(mul_add_c(k1, XP2, 0), 31), XP1, 0);
     hn = mul_add_c(rotl64(hn, 27), XP1, XP4);
     const bool take = k < nw;
-    h = take ? hn : h;
-    d4 = take ? w[2 * k + 2] : d4;
-    d4n = take ? (k < 2 ? w[2 * k + 3] : 0u) : d4n;  // w[7] only for len 28, which has no byte rounds
+    sel64(h, hn, take);
+    sel64(d4p, ((uint64_t)w[2 * k + 3] << 32) | w[2 * k + 2], take);
   }
+  const uint32_t d4 = (uint32_t)d4p, d4n = (uint32_t)(d4p >> 32);
   const bool has4 = (len & 4u) != 0;
-  const uint64_t h4 = mul_add_c(rotl64(h ^ ((uint64_t)d4 * XP1), 23), XP2, XP3);
-  h = has4 ? h4 : h;
+  sel64(h, mul_add_c(rotl64(h ^ mul32_c(d4, XP1), 23), XP2, XP3), has4);
   const uint32_t db = has4 ? d4n : d4;
   const uint32_t nb = len & 3u;
 #pragma unroll
-  for (uint32_t j = 0; j < 3; ++j) {
-    const uint64_t b = (db >> (8 * j)) & 0xFFu;
-    const uint64_t hb = mul_add_c(rotl64(h ^ (b * XP5), 11), XP1, 0);
-    h = j < nb ? hb : h;
-  }
+  for (uint32_t j = 0; j < 3; ++j) sel64(h, mul_add_c(rotl64(h ^ bp((db >> (8 * j)) & 0xFFu), 11), XP1, 0), j < nb);
   return fmix_head(h);
 }
 

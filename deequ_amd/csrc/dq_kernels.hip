@@ -361,7 +361,8 @@ __device__ __forceinline__ void masked_moments(LaneMoments& a, double& lo, doubl
         "s_mov_b64 exec, %[save]"
         : [sd] "+v"(a.sd), [sdd] "+v"(a.sdd), [k] "+v"(a.k), [is] "+v"(a.is), [lo] "+v"(lo), [hi] "+v"(hi),
           [d] "=&v"(d), [save] "=&s"(save)
-        : [x] "v"(x), [sh] "v"(a.shift), [b] "v"(b), [ma] "s"(ma));
+        : [x] "v"(x), [sh] "v"(a.shift), [b] "v"(b), [ma] "s"(ma)
+        : "scc");
   } else if constexpr (!MINMAX_SEP) {
     asm volatile(
         "s_and_saveexec_b64 %[save], %[ma]\n\t"
@@ -374,7 +375,8 @@ __device__ __forceinline__ void masked_moments(LaneMoments& a, double& lo, doubl
         "s_mov_b64 exec, %[save]"
         : [sd] "+v"(a.sd), [sdd] "+v"(a.sdd), [k] "+v"(a.k), [lo] "+v"(lo), [hi] "+v"(hi), [d] "=&v"(d),
           [save] "=&s"(save)
-        : [x] "v"(x), [sh] "v"(a.shift), [ma] "s"(ma));
+        : [x] "v"(x), [sh] "v"(a.shift), [ma] "s"(ma)
+        : "scc");
   } else {
     asm volatile(
         "s_and_saveexec_b64 %[save], %[ma]\n\t"
@@ -388,7 +390,8 @@ __device__ __forceinline__ void masked_moments(LaneMoments& a, double& lo, doubl
         "s_mov_b64 exec, %[save]"
         : [sd] "+v"(a.sd), [sdd] "+v"(a.sdd), [k] "+v"(a.k), [lo] "+v"(lo), [hi] "+v"(hi), [d] "=&v"(d),
           [save] "=&s"(save)
-        : [x] "v"(x), [sh] "v"(a.shift), [ma] "s"(ma), [mb] "s"(mb));
+        : [x] "v"(x), [sh] "v"(a.shift), [ma] "s"(ma), [mb] "s"(mb)
+        : "scc");
   }
 }
 
@@ -508,20 +511,22 @@ __device__ void numeric_range(const void* values, const uint32_t* validity, cons
 // bounds-checked buffer resource over offsets[row0 .. row1]; every lane fetches its string with two
 // dword-aligned 16-byte buffer loads (byte-granular loads are exact on gfx950 but run at ~60% of the
 // aligned rate) from a window over the chunk's string bytes, realigns them with v_alignbit and hashes
-// the string branch-free as one of <= 28 bytes (xxh64_short_head).  A string that is longer, or whose
-// 32-byte window would cross the end of the chunk's bytes, is flagged in an SGPR mask and rehashed by
-// the general XXH64 loop after the block (rare; ds_max is idempotent, so the block's selected rows
-// are simply redone there).
+// the string branch-free as one of <= 28 bytes (xxh64_short_head; byte rounds read b * P5 from the
+// LDS table p5).  A string that is longer, or whose 32-byte window would cross the end of the chunk's
+// bytes, is flagged in an SGPR mask and rehashed by the general XXH64 loop after the block (rare;
+// ds_max is idempotent, so the block's selected rows are simply redone there).
 template <typename OffT>
 __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint32_t* validity,
                            const uint32_t* mask, int64_t row0, int64_t row1, int64_t n_rows, ColStats& s,
-                           int32_t* regs) {
+                           int32_t* regs, const uint64_t* p5) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (row0 >= row1) return;
   constexpr int W = (int)sizeof(OffT);
-  // byte window [lo, end of the chunk's strings) from a dword-aligned lo, 32-bit offsets
-  const int64_t lo = (int64_t)offsets[row0] & ~int64_t(3);
+  // byte window [lo, end of the chunk's strings) with 32-bit offsets from lo: int32 offsets address
+  // the chunk's bytes directly (lo = 0, a UTF8 chunk holds < 2 GiB); int64 offsets from this range's
+  // first string (dword-aligned)
+  const int64_t lo = W == 4 ? 0 : ((int64_t)offsets[row0] & ~int64_t(3));
   const int64_t span = (int64_t)offsets[n_rows] - lo;
   const bool fast_ok = span < (int64_t)0x7FFFFF00;
   const __amdgpu_buffer_rsrc_t rsrc =
@@ -531,45 +536,73 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
   const int32_t win = fast_ok ? (int32_t)span - 32 : -1;  // fast iff off <= win: both loads in range
   int64_t cnt_w = 0;  // wave-uniform count of selected rows
   int32_t qmin = 0;
+  const auto bp = [p5](uint32_t b) { return p5[b]; };
+  // Software pipeline: string j + 1's 32 bytes are in flight while string j is hashed, and right
+  // after row j is hashed its registers take the next block's offsets of row j (a whole block of
+  // slack; vmcnt retires in order, so every load is awaited about one row after it was issued).
+  // Each row's exec-masked ds_max ends a basic block, so the order written here is the issue order;
+  // the prefetch is unconditional (a conditional one makes the wait counts of both paths merge).
+  OffT ra[8], rb[8];  // offsets o0, o1 of the lane's 8 rows (then: o0 and len)
+  auto load_offsets = [&](int64_t blk, int j) {
+    const int soff = (int)((blk + (int64_t)wave * 512 - row0 + j * 64) * W);
+    if constexpr (W == 4) {
+      ra[j] = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(orsrc, lane * 4, soff, 0);
+      rb[j] = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(orsrc, lane * 4 + 4, soff, 0);
+    } else {
+      const auto a0 = __builtin_amdgcn_raw_buffer_load_b64(orsrc, lane * 8, soff, 0);
+      const auto a1 = __builtin_amdgcn_raw_buffer_load_b64(orsrc, lane * 8 + 8, soff, 0);
+      ra[j] = (int64_t)(((uint64_t)a0[1] << 32) | a0[0]);
+      rb[j] = (int64_t)(((uint64_t)a1[1] << 32) | a1[0]);
+    }
+  };
+#pragma unroll
+  for (int j = 0; j < 8; ++j) load_offsets(row0, j);
+  // o0 rel. to the window (low 2 bits = the string's byte alignment) and len of row j
+  auto rel_of = [&](int j) -> uint32_t { return W == 4 ? (uint32_t)ra[j] : (uint32_t)((int64_t)ra[j] - lo); };
+  auto len_of = [&](int j) -> uint32_t {
+    const int64_t l = (int64_t)rb[j] - (int64_t)ra[j];
+    return W == 4 ? (uint32_t)l : (l > 28 ? 29u : (uint32_t)l);
+  };
+  const int32_t win3 = win < 0 ? -1 : (win | 3);  // (rel & ~3) <= win  <=>  rel <= win | 3
   for (int64_t blk = row0; blk < row1; blk += kRowsPerIter) {
     const int64_t base = blk + (int64_t)wave * 512;
     const bool full = blk + kRowsPerIter <= row1;
-    uint64_t m[8];
+    uint64_t m[8];  // selected rows that take the fast path (SGPR budget: the rare path reloads the masks)
     block_masks(validity, mask, base, row1, full, m);
-    uint64_t slow = 0;  // OR of the rows that need the general hash
-#pragma unroll
-    for (int j = 0; j < 8; ++j) cnt_w += __builtin_popcountll(m[j]);
+    uint64_t slow = 0;  // OR of the selected rows that need the general hash
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int soff = (int)((base - row0 + j * 64) * W);
-      int64_t o0, o1;
-      if constexpr (W == 4) {
-        o0 = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(orsrc, lane * 4, soff, 0);
-        o1 = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(orsrc, lane * 4 + 4, soff, 0);
-      } else {
-        const auto a0 = __builtin_amdgcn_raw_buffer_load_b64(orsrc, lane * 8, soff, 0);
-        const auto a1 = __builtin_amdgcn_raw_buffer_load_b64(orsrc, lane * 8 + 8, soff, 0);
-        o0 = (int64_t)(((uint64_t)a0[1] << 32) | a0[0]);
-        o1 = (int64_t)(((uint64_t)a1[1] << 32) | a1[0]);
-      }
-      // 32-bit window arithmetic: when fast_ok, every offset of the chunk lies in [lo, lo + 2^31)
-      const int32_t off = (int32_t)(o0 - lo) & ~3;
-      const uint32_t len = (uint32_t)(o1 - o0);
-      const uint64_t fastm = __builtin_amdgcn_ballot_w64(len <= 28u && off <= win);
+      cnt_w += __builtin_popcountll(m[j]);
+      const uint64_t fastm = __builtin_amdgcn_ballot_w64(len_of(j) <= 28u && (int32_t)rel_of(j) <= win3);
       slow |= m[j] & ~fastm;
-      const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0);
-      const u32x4 c = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off + 16, 0, 0);
-      const uint32_t d[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
-      const uint32_t sh = (uint32_t)(o0 & 3) * 8u;
-      uint32_t wv[7];
+      m[j] &= fastm;
+    }
+    u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int32_t)(rel_of(0) & ~3u), 0, 0);
+    u32x4 c = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int32_t)(rel_of(0) & ~3u) + 16, 0, 0);
 #pragma unroll
-      for (int k = 0; k < 7; ++k) wv[k] = alignbit32(d[k + 1], d[k], sh);  // sh == 0 -> d[k]
-      const HllKey key = hll_key_from_fmix(xxh64_short_head(wv, len));
+    for (int j = 0; j < 8; ++j) {
+      u32x4 an = a, cn = c;
+      if (j < 7) {
+        const int32_t offn = (int32_t)(rel_of(j + 1) & ~3u);
+        an = __builtin_amdgcn_raw_buffer_load_b128(rsrc, offn, 0, 0);
+        cn = __builtin_amdgcn_raw_buffer_load_b128(rsrc, offn + 16, 0, 0);
+      }
+      const uint32_t d[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+      const uint32_t sh = rel_of(j) << 3;  // v_alignbit reads the low 5 bits: (o0 & 3) * 8
+      uint32_t wv[8];
+#pragma unroll
+      for (int k = 0; k < 7; ++k) wv[k] = alignbit32(d[k + 1], d[k], sh);
+      wv[7] = d[7];  // only ever feeds the unused half of the tail pair for len >= 24
+      const HllKey key = hll_key_from_fmix(xxh64_short_head(wv, len_of(j), bp));
       qmin = min(qmin, key.q);
-      if (lane_bit(m[j] & fastm)) atomicMax(reinterpret_cast<int32_t*>(reinterpret_cast<char*>(regs) + key.addr), key.q);
+      if (lane_bit(m[j])) atomicMax(reinterpret_cast<int32_t*>(reinterpret_cast<char*>(regs) + key.addr), key.q);
+      load_offsets(blk + kRowsPerIter, j);  // unconditional: past row1 the descriptor reads 0
+      a = an;
+      c = cn;
     }
     // rare: long / window-crossing strings, or a rank that needs the hash's low word (2^-23)
     if ((slow | __builtin_amdgcn_ballot_w64(qmin < 0)) != 0) {
+      block_masks(validity, mask, base, row1, full, m);
 #pragma unroll 1
       for (int j = 0; j < 8; ++j) {
         if (lane_bit(m[j])) {
@@ -613,7 +646,8 @@ __device__ void run_numeric(const ColTask& t, const ScanCols& cols, const ScanBi
 // ------------------------------------------------------------------------------------------
 template <int V>
 __device__ __forceinline__ void run_variant(const ColTask& t, const ScanCols& cols, const uint32_t* mask, int64_t row0,
-                                            int64_t row1, int64_t n_rows, ColStats& s, int32_t* regs) {
+                                            int64_t row1, int64_t n_rows, ColStats& s, int32_t* regs,
+                                            const uint64_t* p5) {
   const void* v = cols.values[t.col];
   const uint32_t* val = cols.validity[t.col];
   if constexpr (V == CV_VALIDITY) validity_range(val, mask, row0, row1, s);
@@ -628,10 +662,10 @@ __device__ __forceinline__ void run_variant(const ColTask& t, const ScanCols& co
   else if constexpr (V == CV_I32_H) numeric_range<CK_I32, false, true>(v, val, mask, row0, row1, s, regs);
   else if constexpr (V == CV_UTF8_H)
     utf8_range<int32_t>(reinterpret_cast<const uint8_t*>(v), reinterpret_cast<const int32_t*>(cols.offsets[t.col]),
-                        val, mask, row0, row1, n_rows, s, regs);
+                        val, mask, row0, row1, n_rows, s, regs, p5);
   else
     utf8_range<int64_t>(reinterpret_cast<const uint8_t*>(v), reinterpret_cast<const int64_t*>(cols.offsets[t.col]),
-                        val, mask, row0, row1, n_rows, s, regs);
+                        val, mask, row0, row1, n_rows, s, regs, p5);
 }
 
 template <int V>
@@ -641,7 +675,9 @@ __global__ __launch_bounds__(kBlock) void dq_column_scan(const ColTask* __restri
                                                          ColPartial* __restrict__ partials,
                                                          uint32_t* __restrict__ hll_acc) {
   constexpr bool kHll = !(V == CV_VALIDITY || V == CV_F64_S || V == CV_I64_S || V == CV_I32_S);
+  constexpr bool kStr = V == CV_UTF8_H || V == CV_LUTF8_H;
   __shared__ int32_t regs[kHll ? 512 : 1];  // q = pw - 1, -1 = empty (see hll_q_exact)
+  __shared__ uint64_t p5[kStr ? 256 : 1];   // b * P5 for the byte rounds of the string hash
   __shared__ ColStats red[kWaves];
   const int32_t ti = blockIdx.x % ntasks;
   const int32_t range = blockIdx.x / ntasks;
@@ -651,12 +687,13 @@ __global__ __launch_bounds__(kBlock) void dq_column_scan(const ColTask* __restri
   if (row1 > n_rows) row1 = n_rows;
   if constexpr (kHll) {
     for (int i = threadIdx.x; i < 512; i += kBlock) regs[i] = -1;
+    if constexpr (kStr) p5[threadIdx.x] = (uint64_t)threadIdx.x * XP5;
     __syncthreads();
   }
   ColStats s;
   stats_init(s);
   const uint32_t* mask = t.where >= 0 ? reinterpret_cast<const uint32_t*>(bm.where_bits[t.where]) : nullptr;
-  run_variant<V>(t, cols, mask, row0, row1, n_rows, s, regs);
+  run_variant<V>(t, cols, mask, row0, row1, n_rows, s, regs, p5);
   block_reduce_store(s, partials + (size_t)(part_base + ti) * kMaxWG + range, red);
   if constexpr (kHll) {
     // registers only grow: merge into the plan accumulator with device-scope atomicMax, skipping

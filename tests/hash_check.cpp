@@ -22,9 +22,10 @@ int main() {
       uint32_t d[8];
       std::memcpy(d, buf, 32);
       const uint32_t sh = align * 8u;
-      uint32_t w[7];
+      uint32_t w[8];
       for (int k = 0; k < 7; ++k) w[k] = dq::alignbit32(d[k + 1], d[k], sh);
-      const uint64_t h = dq::fmix_tail(dq::xxh64_short_head(w, (uint32_t)len));
+      w[7] = d[7];
+      const uint64_t h = dq::fmix_tail(dq::xxh64_short_head(w, (uint32_t)len, dq::MulP5{}));
       std::printf("%lld%c", (long long)h, align == 3 ? '\n' : ' ');
     }
   }

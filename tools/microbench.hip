@@ -130,13 +130,15 @@ __global__ __launch_bounds__(256) void kutf8(const uint8_t* data, const int32_t*
                                              ColPartial* out) {
   __shared__ int32_t regs[512];
   __shared__ ColStats red[4];
+  __shared__ uint64_t p5[256];
+  p5[threadIdx.x] = (uint64_t)threadIdx.x * XP5;
   for (int i = threadIdx.x; i < 512; i += 256) regs[i] = -1;
   __syncthreads();
   const int64_t r0 = blockIdx.x * rpw, r1 = min(n, r0 + rpw);
   ColStats s;
   stats_init(s);
   if (MODE == 1) {
-    utf8_range<int32_t>(data, offs, nullptr, nullptr, r0, r1, n, s, regs);
+    utf8_range<int32_t>(data, offs, nullptr, nullptr, r0, r1, n, s, regs, p5);
   } else {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t lo = offs[r0] & ~3, hi = offs[r1];
@@ -146,19 +148,23 @@ __global__ __launch_bounds__(256) void kutf8(const uint8_t* data, const int32_t*
       const int64_t base = blk + (int64_t)wave * 512;
 #pragma unroll 4
       for (int j = 0; j < 8; ++j) {
-        const int64_t row = min(base + j * 64 + lane, r1 - 1);
+        // MODE 3: the loads of MODE 0 with rows permuted inside the wave's 512-row block (what a
+        // length-sorted slot assignment would issue): a lane-slot reads row base + (61 (64 j + lane)) % 512
+        const int64_t row = MODE == 3 ? min(base + (int64_t)((61 * (j * 64 + lane)) & 511), r1 - 1)
+                                      : min(base + j * 64 + lane, r1 - 1);
         const int64_t o0 = offs[row], o1 = offs[row + 1];
         const int32_t off = (int32_t)((o0 - lo) & ~3);
         const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0);
         const u32x4 c = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off + 16, 0, 0);
-        if (MODE == 0) acc ^= a.x ^ a.y ^ a.z ^ a.w ^ c.x ^ c.y ^ c.z ^ c.w ^ (uint32_t)(o1 - o0);
+        if (MODE == 0 || MODE == 3) acc ^= a.x ^ a.y ^ a.z ^ a.w ^ c.x ^ c.y ^ c.z ^ c.w ^ (uint32_t)(o1 - o0);
         else {  // MODE 2: + hash, no HLL
           const uint32_t d[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
           const uint32_t sh = (uint32_t)(o0 & 3) * 8u;
-          uint32_t wv[7];
+          uint32_t wv[8];
 #pragma unroll
           for (int k = 0; k < 7; ++k) wv[k] = alignbit32(d[k + 1], d[k], sh);
-          acc ^= (uint32_t)(xxh64_short_head(wv, (uint32_t)(o1 - o0)) >> 32);
+          wv[7] = d[7];
+          acc ^= (uint32_t)(xxh64_short_head(wv, (uint32_t)(o1 - o0), [&](uint32_t b) { return p5[b]; }) >> 32);
         }
       }
     }
@@ -203,16 +209,31 @@ void utf8_bench(ColPartial* part) {
   uint8_t* data;
   (void)hipMalloc(&data, bytes + 64);
   (void)hipMemset(data, 0x5A, bytes + 64);
-  const char* names[] = {"utf8_loads", "utf8_full", "utf8_hash_nohll"};
+  const char* names[] = {"utf8_loads", "utf8_full", "utf8_hash_nohll", "utf8_loads_permuted"};
   for (int wgs : {2048, 8192}) {
-    float t[3] = {run_utf8<0>(data, offs, n, part, wgs), run_utf8<1>(data, offs, n, part, wgs), run_utf8<2>(data, offs, n, part, wgs)};
-    for (int m = 0; m < 3; ++m)
+    float t[4];
+    t[0] = run_utf8<0>(data, offs, n, part, wgs);
+    std::printf("loads done\n");
+    t[1] = run_utf8<1>(data, offs, n, part, wgs);
+    std::printf("full done\n");
+    t[2] = run_utf8<2>(data, offs, n, part, wgs);
+    std::printf("hash done\n");
+    t[3] = run_utf8<3>(data, offs, n, part, wgs);
+    for (int m = 0; m < 4; ++m)
       std::printf("{\"wgs\": %d, \"mode\": \"%s\", \"ms\": %.3f, \"Gstr_per_s\": %.1f, \"GBps\": %.0f}\n", wgs, names[m], t[m],
                   n / t[m] / 1e6, (n * 4.0 + bytes) / t[m] / 1e6);
   }
 }
 
-int main() {
+int main(int argc, char** argv) {
+  setvbuf(stdout, nullptr, _IOLBF, 0);
+  const bool utf8_only = argc > 1 && argv[1][0] == 'u';
+  if (utf8_only) {
+    ColPartial* part;
+    (void)hipMalloc(&part, 16384 * sizeof(ColPartial));
+    utf8_bench(part);
+    return 0;
+  }
   const int64_t n = 500'000'000;
   double* d;
   unsigned long long* out;
