@@ -24,7 +24,7 @@ constexpr int kMaxWhere = 8;
 constexpr int kMaxRoots = 32;
 constexpr int kMaxCounters = 32;
 constexpr int kMaxInstr = 96;
-constexpr int kPredRowsPerIter = kBlock;    // predicate pass: one row per lane per iteration
+constexpr int kPredStack = 16;              // predicate pass: operand stack depth
 
 // column kinds seen by the kernels
 enum ColKind : int32_t { CK_F64 = 1, CK_I64 = 2, CK_I32 = 3, CK_UTF8 = 4, CK_LUTF8 = 5 };
@@ -128,7 +128,10 @@ struct PredProgram {
   int32_t n_instr;
   int32_t n_counters;
   int32_t n_bitmaps;
-  int32_t pad;
+  int32_t n_loads;                 // atoms (the instructions that read a column)
+  int32_t n_roots;                 // root slots stored by the program
+  int32_t stack_depth;             // max operand stack depth (<= kPredStack)
+  int16_t load_instr[kMaxInstr];   // their instruction indices, in program order
   int32_t bitmap_root[kMaxWhere];  // root slot whose TRUE bits fill where-bitmap i
   PredCounter counters[kMaxCounters];
   PredInstr instr[kMaxInstr];

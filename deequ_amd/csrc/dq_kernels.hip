@@ -866,11 +866,15 @@ __global__ __launch_bounds__(kBlock) void dq_pair_tile_scan(const PairGroup* __r
 }
 
 // ------------------------------------------------------------------------------------------
-// Kernel 1: predicate program (three-valued logic), one row per lane.
+// Kernel 1: predicate program (three-valued logic) -- Compliance / conditional counts and `where`
+// bitmaps (Compliance.scala:37-53, Analyzer.scala:404-408).  A wave takes 512-row blocks (lane l:
+// rows base + 64 j + l, j < 8).  Each atom of the postfix program is evaluated for the whole block:
+// its 8 (or 16) value loads are in flight together, the comparison is ballot-ed into TRUE / NULL
+// row masks (validity and COALESCE fallbacks applied on the scalar masks).  The logic then runs on
+// 32-row mask words: lanes 0..15 each own one word of the block, with the operand stack, the stored
+// roots and per-lane counter partials in the wave's LDS scratch.  Counters reach the accumulator by
+// 64-bit integer atomics (order-free, so the result is deterministic).
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ bool valid_bit(const uint32_t* v, int64_t row) {
-  return v ? ((v[row >> 5] >> (row & 31)) & 1u) : true;
-}
 __device__ __forceinline__ int64_t load_as_int(const void* p, int kind, int64_t row) {
   if (kind == CK_I64) return reinterpret_cast<const int64_t*>(p)[row];
   return (int64_t)reinterpret_cast<const int32_t*>(p)[row];
@@ -894,107 +898,211 @@ __device__ __forceinline__ bool apply_cmp(int op, int c) {
   }
 }
 
+// One wave's LDS scratch (dynamic, sized by the plan: pred_scratch_words per wave), 32-bit mask
+// words of the current 512-row block, each array [entry][16 word lanes]: operand stack (TRUE,
+// NULL), stored roots (TRUE, NULL), per-lane counter partials (TRUE, NOT NULL).
+struct PredScratch {
+  uint32_t *st, *sn, *rt, *rn, *ct, *cn;
+  __device__ PredScratch(uint32_t* w, int depth, int roots, int counters) {
+    st = w; sn = st + 16 * depth; rt = sn + 16 * depth; rn = rt + 16 * roots; ct = rn + 16 * roots; cn = ct + 16 * counters;
+  }
+};
+
+// raw values of one column for the block (all 8 row-group loads issued before any is used; i32
+// sign-extended), through a bounds-checked buffer descriptor over the workgroup's rows [row0, row1):
+// rows past row1 read 0
+__device__ __forceinline__ void pred_load(const void* p, int kind, int64_t row0, int64_t row1, int64_t base, int lane,
+                                          uint64_t (&v)[8]) {
+  const int sz = kind == CK_I32 ? 4 : 8;
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<char*>(reinterpret_cast<const char*>(p) + row0 * sz), (short)0, (int)((row1 - row0) * sz), 0x00020000);
+  if (kind == CK_I32) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      v[j] = (uint64_t)(int64_t)(int32_t)__builtin_amdgcn_raw_buffer_load_b32(r, lane * 4, (int)((base - row0 + 64 * j) * 4), 2);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const auto w2 = __builtin_amdgcn_raw_buffer_load_b64(r, lane * 8, (int)((base - row0 + 64 * j) * 8), 2);
+      v[j] = ((uint64_t)w2[1] << 32) | w2[0];
+    }
+  }
+}
+__device__ __forceinline__ double pred_as_double(uint64_t v, int kind) {
+  return kind == CK_F64 ? __builtin_bit_cast(double, v) : (double)(int64_t)v;
+}
+
+// validity word of the lane's 32 rows (lanes 0..15: rows base + 32 L .. + 31) through a bounds-checked
+// descriptor over the bitmap of [0, n_rows) (past it: 0); all ones without a bitmap
+__device__ __forceinline__ uint32_t pred_valid_word(const uint32_t* v, int64_t base, int64_t n_rows, int lane) {
+  if (!v) return ~0u;
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(v), (short)0,
+                                                                    (int)(((n_rows + 31) >> 5) * 4), 0x00020000);
+  return __builtin_amdgcn_raw_buffer_load_b32(r, (lane & 15) * 4, (int)((base >> 5) * 4), 0);
+}
+
+// Loads of one atom for a block: raw values of column a / b (ATOM_CMP) and the lane's validity words.
+struct AtomBuf {
+  uint64_t a[8], b[8];
+  uint32_t va, vb;
+};
+
+// One ATOM_CMP for a block from its loads: the lane's 32-bit TRUE / NULL words (lanes 0..15).
+__device__ __forceinline__ void pred_atom_cmp(const PredInstr& ins, const AtomBuf& L, int lane, uint32_t& wt,
+                                              uint32_t& wn) {
+  // result = (lt & Klt) | (eq & Keq) | (gt & Kgt) | NaN terms (Spark: NaN = NaN, NaN > all)
+  const int cmp = ins.cmp;
+  const uint64_t Klt = (cmp == C_LT || cmp == C_LE || cmp == C_NE || cmp == C_TRUE) ? ~0ull : 0ull;
+  const uint64_t Keq = (cmp == C_LE || cmp == C_GE || cmp == C_EQ || cmp == C_TRUE) ? ~0ull : 0ull;
+  const uint64_t Kgt = (cmp == C_GT || cmp == C_GE || cmp == C_NE || cmp == C_TRUE) ? ~0ull : 0ull;
+  const uint64_t Kbn = (cmp == C_LT || cmp == C_LE || cmp == C_NE || cmp == C_TRUE) ? ~0ull : 0ull;  // only b NaN
+  const uint64_t Kan = (cmp == C_GT || cmp == C_GE || cmp == C_NE || cmp == C_TRUE) ? ~0ull : 0ull;  // only a NaN
+  const uint64_t Kab = (cmp == C_LE || cmp == C_GE || cmp == C_EQ || cmp == C_TRUE) ? ~0ull : 0ull;  // both NaN
+  const bool two = ins.col_b >= 0;
+  const bool is_int = ins.ctype == CT_INT;
+  uint32_t wc = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    uint64_t lt, eq, gt, an = 0, bn = 0;
+    if (is_int) {
+      const int64_t x = (int64_t)L.a[j], y = two ? (int64_t)L.b[j] : ins.lit_i;
+      lt = __builtin_amdgcn_ballot_w64(x < y);
+      eq = __builtin_amdgcn_ballot_w64(x == y);
+      gt = __builtin_amdgcn_ballot_w64(x > y);
+    } else {
+      const double x = pred_as_double(L.a[j], ins.kind_a), y = two ? pred_as_double(L.b[j], ins.kind_b) : ins.lit_d;
+      lt = __builtin_amdgcn_ballot_w64(x < y);
+      eq = __builtin_amdgcn_ballot_w64(x == y);
+      gt = __builtin_amdgcn_ballot_w64(x > y);
+      an = __builtin_amdgcn_ballot_w64(x != x);
+      bn = __builtin_amdgcn_ballot_w64(y != y);
+    }
+    const uint64_t cm = (lt & Klt) | (eq & Keq) | (gt & Kgt) | (~an & bn & Kbn) | (an & ~bn & Kan) | (an & bn & Kab);
+    // fold row group j into the lane's word (lanes 0..15: word L = rows 32 L .. + 31 of the block)
+    if ((lane >> 1) == j) wc = (lane & 1) ? (uint32_t)(cm >> 32) : (uint32_t)cm;
+  }
+  // NULL operand b -> NULL; NULL a -> the COALESCE fallback result (NULL without one)
+  const uint32_t va = L.va, vb = two ? L.vb : ~0u;
+  const uint32_t nr_true = ins.null_res == NR_TRUE ? ~0u : 0u, nr_null = ins.null_res == NR_NULL ? ~0u : 0u;
+  wt = (va & vb & wc) | (~va & vb & nr_true);
+  wn = ~vb | (~va & nr_null);
+}
+
 __global__ __launch_bounds__(kBlock) void dq_pred_scan(const PredProgram* __restrict__ prog_g, ScanCols cols,
                                                        ScanBitmaps bm, int64_t n_rows, int64_t rows_per_range,
-                                                       PredPartial* __restrict__ partials) {
-  __shared__ int64_t red_t[kWaves][kMaxCounters];
-  __shared__ int64_t red_n[kWaves][kMaxCounters];
+                                                       PredPartial* __restrict__ acc) {
+  extern __shared__ uint32_t pred_lds[];
   const PredProgram& prog = *prog_g;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wave_words = 32 * (prog.stack_depth + prog.n_roots + prog.n_counters);
+  PredScratch S(pred_lds + wave * wave_words, prog.stack_depth, prog.n_roots, prog.n_counters);
+  const bool wl = lane < 16;  // word lanes
+  const int n_instr = prog.n_instr, n_counters = prog.n_counters, n_bitmaps = prog.n_bitmaps, n_loads = prog.n_loads;
+  if (wl) {
+    for (int c = 0; c < n_counters; ++c) { S.ct[(c) * 16 + lane] = 0; S.cn[(c) * 16 + lane] = 0; }
+  }
   const int64_t row0 = (int64_t)blockIdx.x * rows_per_range;
   int64_t row1 = row0 + rows_per_range;
   if (row1 > n_rows) row1 = n_rows;
-  const int n_instr = prog.n_instr, n_counters = prog.n_counters, n_bitmaps = prog.n_bitmaps;
-  if (lane < kMaxCounters) { red_t[wave][lane] = 0; red_n[wave][lane] = 0; }
-
-  for (int64_t blk = row0; blk < row1; blk += kPredRowsPerIter) {
-    const int64_t row = blk + wave * 64 + lane;
-    const bool in_range = row < row1;
-    uint32_t root_t = 0, root_n = 0;
-    if (in_range) {
-      uint32_t st_t = 0, st_n = 0;
-      for (int i = 0; i < n_instr; ++i) {
-        const PredInstr& ins = prog.instr[i];
-        uint32_t t = 0, nl = 0;
-        switch (ins.op) {
-          case PO_ATOM_CMP: {
-            const bool va = valid_bit(cols.validity[ins.col_a], row);
-            const bool vb = ins.col_b < 0 ? true : valid_bit(cols.validity[ins.col_b], row);
-            if (!vb) { nl = 1; }
-            else if (!va) { t = ins.null_res == NR_TRUE; nl = ins.null_res == NR_NULL; }
-            else {
-              int c;
-              if (ins.ctype == CT_INT) {
-                int64_t a = load_as_int(cols.values[ins.col_a], ins.kind_a, row);
-                int64_t b = ins.col_b < 0 ? ins.lit_i : load_as_int(cols.values[ins.col_b], ins.kind_b, row);
-                c = (a > b) - (a < b);
-              } else {
-                double a = load_as_double(cols.values[ins.col_a], ins.kind_a, row);
-                double b = ins.col_b < 0 ? ins.lit_d : load_as_double(cols.values[ins.col_b], ins.kind_b, row);
-                c = cmp_dbl(a, b);
-              }
-              t = apply_cmp(ins.cmp, c);
-            }
-            st_t = (st_t << 1) | t; st_n = (st_n << 1) | nl;
-            break;
-          }
-          case PO_ATOM_ISNULL:
-          case PO_ATOM_NOTNULL: {
-            const bool va = valid_bit(cols.validity[ins.col_a], row);
-            t = (ins.op == PO_ATOM_ISNULL) ? !va : va;
-            st_t = (st_t << 1) | t; st_n = (st_n << 1);
-            break;
-          }
-          case PO_CONST:
-            st_t = (st_t << 1) | (ins.null_res == NR_TRUE); st_n = (st_n << 1) | (ins.null_res == NR_NULL);
-            break;
-          case PO_AND:
-          case PO_OR: {
-            const uint32_t bt = st_t & 1u, bn = st_n & 1u, at = (st_t >> 1) & 1u, an = (st_n >> 1) & 1u;
-            st_t >>= 2; st_n >>= 2;
-            const uint32_t af = !at & !an, bf = !bt & !bn;
-            uint32_t rt, rf;
-            if (ins.op == PO_AND) { rt = at & bt; rf = af | bf; }
-            else { rt = at | bt; rf = af & bf; }
-            st_t = (st_t << 1) | rt; st_n = (st_n << 1) | (!rt & !rf);
-            break;
-          }
-          case PO_NOT: {
-            const uint32_t at = st_t & 1u, an = st_n & 1u;
-            st_t = (st_t & ~1u) | (!at & !an);
-            (void)an;
-            break;
-          }
-          case PO_STORE: {
-            root_t |= (st_t & 1u) << ins.slot; root_n |= (st_n & 1u) << ins.slot;
-            st_t >>= 1; st_n >>= 1;
-            break;
-          }
-          default: break;
-        }
+  // Two-deep pipeline over the atoms, across blocks: atom g (a wave-uniform running count) uses
+  // buffer g & 1, and the loads of atom g + 1 go into the other buffer before atom g is evaluated.
+  AtomBuf B0, B1;
+  auto issue = [&](int k, int64_t base, AtomBuf& L) {
+    const PredInstr& ins = prog.instr[prog.load_instr[k]];
+    if (ins.op == PO_ATOM_CMP) {
+      pred_load(cols.values[ins.col_a], ins.kind_a, row0, row1, base, lane, L.a);
+      if (ins.col_b >= 0) {
+        pred_load(cols.values[ins.col_b], ins.kind_b, row0, row1, base, lane, L.b);
+        L.vb = pred_valid_word(cols.validity[ins.col_b], base, n_rows, lane);
       }
     }
-    // outputs: where bitmaps (64 rows per word) and counters
-    for (int b = 0; b < n_bitmaps; ++b) {
-      const unsigned long long word = __ballot(in_range && ((root_t >> prog.bitmap_root[b]) & 1u));
-      if (lane == 0) bm.where_bits[b][(blk + wave * 64) >> 6] = word;
+    L.va = pred_valid_word(cols.validity[ins.col_a], base, n_rows, lane);
+  };
+  if (n_loads > 0) issue(0, row0 + (int64_t)wave * 512, B0);
+  uint32_t g = 0;
+
+  for (int64_t blk = row0; blk < row1; blk += kRowsPerIter) {
+    const int64_t base = blk + (int64_t)wave * 512;
+    if (base >= row1) break;  // wave-uniform
+    // in-range rows of this lane's word
+    const int64_t wr = base + 32 * (lane & 15);
+    const uint32_t inr = wr >= row1 ? 0u : (wr + 32 <= row1 ? ~0u : ((1u << (row1 - wr)) - 1u));
+    int sp = 0, k = 0;
+    for (int i = 0; i < n_instr; ++i) {
+      const PredInstr& ins = prog.instr[i];
+      const int op = ins.op;
+      if (op == PO_ATOM_CMP || op == PO_ATOM_ISNULL || op == PO_ATOM_NOTNULL) {
+        // next atom: the following one of this block, else the first of the next block
+        const int kn = k + 1 < n_loads ? k + 1 : 0;
+        const int64_t bn = k + 1 < n_loads ? base : base + kRowsPerIter;
+        uint32_t wt, wn;
+        const AtomBuf& cur = (g & 1u) ? B1 : B0;
+        if ((g & 1u) == 0) issue(kn, bn, B1);
+        else issue(kn, bn, B0);
+        if (op == PO_ATOM_CMP) {
+          if ((g & 1u) == 0) pred_atom_cmp(ins, B0, lane, wt, wn);
+          else pred_atom_cmp(ins, B1, lane, wt, wn);
+        } else {
+          const uint32_t va = (g & 1u) ? B1.va : B0.va;
+          wt = op == PO_ATOM_ISNULL ? ~va : va;
+          wn = 0u;
+        }
+        (void)cur;
+        ++g;
+        ++k;
+        if (wl) { S.st[(sp) * 16 + lane] = wt; S.sn[(sp) * 16 + lane] = wn; }
+        ++sp;
+      } else if (op == PO_CONST) {
+        if (wl) { S.st[(sp) * 16 + lane] = ins.null_res == NR_TRUE ? ~0u : 0u; S.sn[(sp) * 16 + lane] = ins.null_res == NR_NULL ? ~0u : 0u; }
+        ++sp;
+      } else if (op == PO_AND || op == PO_OR) {
+        if (wl) {
+          const uint32_t at = S.st[(sp - 2) * 16 + lane], an = S.sn[(sp - 2) * 16 + lane];
+          const uint32_t bt = S.st[(sp - 1) * 16 + lane], bn = S.sn[(sp - 1) * 16 + lane];
+          const uint32_t af = ~at & ~an, bf = ~bt & ~bn;
+          const uint32_t rt = op == PO_AND ? (at & bt) : (at | bt);
+          const uint32_t rf = op == PO_AND ? (af | bf) : (af & bf);
+          S.st[(sp - 2) * 16 + lane] = rt;
+          S.sn[(sp - 2) * 16 + lane] = ~rt & ~rf;
+        }
+        --sp;
+      } else if (op == PO_NOT) {
+        if (wl) {
+          const uint32_t at = S.st[(sp - 1) * 16 + lane], an = S.sn[(sp - 1) * 16 + lane];
+          S.st[(sp - 1) * 16 + lane] = ~at & ~an;
+        }
+      } else if (op == PO_STORE) {
+        if (wl) { S.rt[(ins.slot) * 16 + lane] = S.st[(sp - 1) * 16 + lane]; S.rn[(ins.slot) * 16 + lane] = S.sn[(sp - 1) * 16 + lane]; }
+        --sp;
+      }
     }
-    for (int c = 0; c < n_counters; ++c) {
-      const PredCounter pc = prog.counters[c];
-      const bool tw = pc.where < 0 ? true : ((root_t >> pc.where) & 1u);
-      const bool tp = (root_t >> pc.pred) & 1u;
-      const bool np = !((root_n >> pc.pred) & 1u);
-      const int64_t a = __popcll(__ballot(in_range && tp && tw));
-      const int64_t b = __popcll(__ballot(in_range && np && tw));
-      if (lane == 0) { red_t[wave][c] += a; red_n[wave][c] += b; }  // each wave owns its row
+    if (wl) {
+      for (int c = 0; c < n_counters; ++c) {
+        const PredCounter pc = prog.counters[c];
+        const uint32_t tw = (pc.where < 0 ? ~0u : S.rt[(pc.where) * 16 + lane]) & inr;
+        S.ct[(c) * 16 + lane] += __popc(S.rt[(pc.pred) * 16 + lane] & tw);
+        S.cn[(c) * 16 + lane] += __popc(~S.rn[(pc.pred) * 16 + lane] & tw);
+      }
+      if (wr < n_rows) {
+        for (int b = 0; b < n_bitmaps; ++b)
+          reinterpret_cast<uint32_t*>(bm.where_bits[b])[wr >> 5] = S.rt[prog.bitmap_root[b] * 16 + lane] & inr;
+      }
     }
   }
   __syncthreads();
-  if (threadIdx.x < kMaxCounters) {
-    int64_t a = 0, b = 0;
-    for (int w = 0; w < kWaves; ++w) { a += red_t[w][threadIdx.x]; b += red_n[w][threadIdx.x]; }
-    partials[blockIdx.x].t[threadIdx.x] = a;
-    partials[blockIdx.x].nn[threadIdx.x] = b;
+  // workgroup partials -> accumulator (integer atomics: order-free)
+  if (threadIdx.x < n_counters) {
+    const int c = threadIdx.x;
+    int64_t t = 0, nn = 0;
+    for (int w = 0; w < kWaves; ++w)
+      for (int l = 0; l < 16; ++l) {
+        const PredScratch W(pred_lds + w * wave_words, prog.stack_depth, prog.n_roots, prog.n_counters);
+        t += W.ct[c * 16 + l];
+        nn += W.cn[c * 16 + l];
+      }
+    atomicAdd(reinterpret_cast<unsigned long long*>(&acc->t[c]), (unsigned long long)t);
+    atomicAdd(reinterpret_cast<unsigned long long*>(&acc->nn[c]), (unsigned long long)nn);
   }
 }
 
@@ -1084,8 +1192,9 @@ __global__ void dq_init_acc(ColPartial* col_acc, int32_t ncol, CorrPartial* pair
 // host-side launchers (called from dq_plan.cpp)
 // ------------------------------------------------------------------------------------------
 hipError_t launch_pred_scan(const PredProgram* prog, const ScanCols& cols, const ScanBitmaps& bm, int64_t n_rows,
-                            int64_t rows_per_range, int32_t nranges, PredPartial* partials, hipStream_t st) {
-  hipLaunchKernelGGL(dq_pred_scan, dim3(nranges), dim3(kBlock), 0, st, prog, cols, bm, n_rows, rows_per_range, partials);
+                            int64_t rows_per_range, int32_t nranges, PredPartial* acc, int32_t lds_bytes, hipStream_t st) {
+  hipLaunchKernelGGL(dq_pred_scan, dim3(nranges), dim3(kBlock), (size_t)lds_bytes, st, prog, cols, bm, n_rows,
+                     rows_per_range, acc);
   return hipGetLastError();
 }
 

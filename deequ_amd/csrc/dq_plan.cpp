@@ -27,7 +27,7 @@
 namespace dq {
 
 hipError_t launch_pred_scan(const PredProgram* prog, const ScanCols& cols, const ScanBitmaps& bm, int64_t n_rows,
-                            int64_t rows_per_range, int32_t nranges, PredPartial* partials, hipStream_t st);
+                            int64_t rows_per_range, int32_t nranges, PredPartial* acc, int32_t lds_bytes, hipStream_t st);
 hipError_t launch_column_scan(int32_t variant, const ColTask* tasks, int32_t ntasks, int32_t part_base,
                               const ScanCols& cols, const ScanBitmaps& bm, int64_t n_rows, int64_t rows_per_range,
                               int32_t nranges, ColPartial* partials, uint32_t* hll_acc, hipStream_t st);
@@ -751,8 +751,20 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
       code.push_back(st);
     }
     if ((int32_t)code.size() > kMaxInstr) return set_error(DQ_E_UNSUPPORTED, "predicate program too long (%zu)", code.size());
+    int depth = 0, max_depth = 0;
+    for (const PredInstr& ins : code) {
+      depth += (ins.op == PO_AND || ins.op == PO_OR || ins.op == PO_STORE) ? -1 : (ins.op == PO_NOT ? 0 : 1);
+      max_depth = std::max(max_depth, depth);
+    }
+    if (max_depth > kPredStack)
+      return set_error(DQ_E_UNSUPPORTED, "predicate nesting needs a stack of %d (at most %d)", max_depth, kPredStack);
+    prog.stack_depth = std::max(1, max_depth);
+    prog.n_roots = (int32_t)root_code.size();
     prog.n_instr = (int32_t)code.size();
     std::copy(code.begin(), code.end(), prog.instr);
+    for (int32_t i = 0; i < prog.n_instr; ++i)
+      if (prog.instr[i].op == PO_ATOM_CMP || prog.instr[i].op == PO_ATOM_ISNULL || prog.instr[i].op == PO_ATOM_NOTNULL)
+        prog.load_instr[prog.n_loads++] = (int16_t)i;
     prog.n_counters = (int32_t)counter_of.size();
     for (auto& kv : counter_of) prog.counters[kv.second] = PredCounter{kv.first.first, kv.first.second};
     prog.n_bitmaps = (int32_t)bitmap_of.size();
@@ -785,7 +797,7 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
   }
   p->bytes_per_row_x1000 = b1000;
   p->launches_per_scan = (p->has_pred ? 1 : 0) + (int32_t)p->groups.size() + (p->pair_tasks.empty() ? 0 : 1) +
-                         ((p->col_tasks.size() + p->pair_tasks.size() + (p->has_pred ? 1 : 0)) ? 1 : 0);
+                         ((p->col_tasks.size() + p->pair_tasks.size()) ? 1 : 0);
 
   // device allocations
   const size_t nct = p->col_tasks.size(), npt = p->pair_tasks.size();
@@ -795,7 +807,7 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
   if (dq_status s = dmalloc(&p->d_prog, sizeof(PredProgram))) return s;
   if (dq_status s = dmalloc(&p->d_col_part, nct * kMaxWG * sizeof(ColPartial))) return s;
   if (dq_status s = dmalloc(&p->d_pair_part, npt * kMaxWG * sizeof(CorrPartial))) return s;
-  if (dq_status s = dmalloc(&p->d_pred_part, (p->has_pred ? kMaxWG : 1) * sizeof(PredPartial))) return s;
+  if (dq_status s = dmalloc(&p->d_pred_part, sizeof(PredPartial))) return s;  // unused (kept for the finalize ABI)
   if (dq_status s = dmalloc(&p->d_col_acc, nct * sizeof(ColPartial))) return s;
   if (dq_status s = dmalloc(&p->d_hll_acc, (size_t)p->n_hll * 512 * sizeof(uint32_t))) return s;
   if (dq_status s = dmalloc(&p->d_pair_acc, npt * sizeof(CorrPartial))) return s;
@@ -932,13 +944,15 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
   int32_t nr_col = (int32_t)std::min<int64_t>(want, ceil_div(n_rows, kRowsPerIter));
   int64_t rpr_col = ceil_div(ceil_div(n_rows, nr_col), kRowsPerIter) * kRowsPerIter;
   nr_col = (int32_t)ceil_div(n_rows, rpr_col);
-  int32_t nr_pred = (int32_t)std::min<int64_t>(kMaxWG, ceil_div(n_rows, kPredRowsPerIter));
-  int64_t rpr_pred = ceil_div(ceil_div(n_rows, nr_pred), kPredRowsPerIter) * kPredRowsPerIter;
+  // predicate pass: ~2048 workgroups of whole 2048-row iterations (HBM-bound; counters leave by atomics)
+  int32_t nr_pred = (int32_t)std::min<int64_t>(2048, ceil_div(n_rows, kRowsPerIter));
+  int64_t rpr_pred = ceil_div(ceil_div(n_rows, nr_pred), kRowsPerIter) * kRowsPerIter;
   nr_pred = (int32_t)ceil_div(n_rows, rpr_pred);
 
   if (p->has_pred)
     if (dq_status s = timed(p, 0, p->stream, [&] {
-          return launch_pred_scan(p->d_prog, sc, bm, n_rows, rpr_pred, nr_pred, p->d_pred_part, p->stream);
+          const int32_t lds = kWaves * 128 * (p->prog.stack_depth + p->prog.n_roots + p->prog.n_counters);
+          return launch_pred_scan(p->d_prog, sc, bm, n_rows, rpr_pred, nr_pred, p->d_pred_acc, lds, p->stream);
         }))
       return s;
   // fork: variant launches (and the pair pass) round-robin over the plan stream + side streams
@@ -974,7 +988,8 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
   if (dq_status s = timed(p, 3, p->stream, [&] {
         return launch_finalize((int32_t)p->col_tasks.size(), nr_col, p->d_col_part, p->d_col_acc,
                                (int32_t)p->pair_tasks.size(), nr_col, p->d_pair_part, p->d_pair_acc,
-                               p->has_pred ? 1 : 0, nr_pred, p->d_pred_part, p->d_pred_acc, p->stream);
+                               0 /* the predicate pass accumulates itself */, nr_pred, p->d_pred_part, p->d_pred_acc,
+                               p->stream);
       }))
     return s;
   p->total_rows += n_rows;
