@@ -5,7 +5,8 @@
 //   ColPartial[ncol_tasks][kMaxWG]     per-workgroup partial states of the current scan
 //   CorrPartial[npair][kMaxWG], PredPartial[kMaxWG]
 //   ColPartial / CorrPartial / PredPartial accumulators (merged over chunks, in order)
-//   uint32 hll[nhll][512]              HLL registers, merged in by atomicMax (order-free)
+//   uint32 hll[nhll][kHllCopies][512]  HLL registers, merged in by atomicMax (order-free); a
+//                                      workgroup merges into copy blockIdx % kHllCopies
 //   where bitmaps: uint64[n_rows/64] TRUE bits per `where` root used by column / pair tasks
 #pragma once
 
@@ -21,6 +22,7 @@ constexpr int kMaxWG = 4096;                // max row ranges (workgroups) per t
 constexpr int kTargetWGs = 8192;            // column/pair launch: aim for ~32 workgroups per CU
 constexpr int kMaxCols = 64;
 constexpr int kMaxWhere = 8;
+constexpr int kHllCopies = 8;             // accumulator copies per HLL column (spreads the merge atomics)
 constexpr int kMaxRoots = 32;
 constexpr int kMaxCounters = 32;
 constexpr int kMaxInstr = 96;

@@ -700,7 +700,9 @@ __global__ __launch_bounds__(kBlock) void dq_column_scan(const ColTask* __restri
     // registers the (possibly stale) accumulator already covers -- max is order-free, so the
     // result is deterministic.
     __syncthreads();
-    uint32_t* dst = hll_acc + (size_t)t.hll_slot * 512;
+    // one of kHllCopies accumulator copies per workgroup: a one-column launch otherwise funnels every
+    // workgroup's 512 atomics into the same 2 KB (dq_finish takes the max over the copies)
+    uint32_t* dst = hll_acc + ((size_t)t.hll_slot * kHllCopies + (blockIdx.x % kHllCopies)) * 512;
     for (int i = threadIdx.x; i < 512; i += kBlock) {
       const uint32_t v = (uint32_t)(regs[i] + 1);
       if (v > __builtin_nontemporal_load(dst + i)) atomicMax(dst + i, v);

@@ -485,7 +485,7 @@ static dq_status free_plan_mem(dq_plan* p) {
 static dq_status reset_acc(dq_plan* p) {
   HIP_TRY(launch_init_acc(p->d_col_acc, (int32_t)p->col_tasks.size(), p->d_pair_acc, (int32_t)p->pair_tasks.size(),
                           p->stream));
-  if (p->n_hll) HIP_TRY(hipMemsetAsync(p->d_hll_acc, 0, (size_t)p->n_hll * 512 * sizeof(uint32_t), p->stream));
+  if (p->n_hll) HIP_TRY(hipMemsetAsync(p->d_hll_acc, 0, (size_t)p->n_hll * kHllCopies * 512 * sizeof(uint32_t), p->stream));
   if (p->has_pred) HIP_TRY(hipMemsetAsync(p->d_pred_acc, 0, sizeof(PredPartial), p->stream));
   p->total_rows = 0;
   p->next_chunk = 0;
@@ -809,7 +809,7 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
   if (dq_status s = dmalloc(&p->d_pair_part, npt * kMaxWG * sizeof(CorrPartial))) return s;
   if (dq_status s = dmalloc(&p->d_pred_part, sizeof(PredPartial))) return s;  // unused (kept for the finalize ABI)
   if (dq_status s = dmalloc(&p->d_col_acc, nct * sizeof(ColPartial))) return s;
-  if (dq_status s = dmalloc(&p->d_hll_acc, (size_t)p->n_hll * 512 * sizeof(uint32_t))) return s;
+  if (dq_status s = dmalloc(&p->d_hll_acc, (size_t)p->n_hll * kHllCopies * 512 * sizeof(uint32_t))) return s;
   if (dq_status s = dmalloc(&p->d_pair_acc, npt * sizeof(CorrPartial))) return s;
   if (dq_status s = dmalloc(&p->d_pred_acc, sizeof(PredPartial))) return s;
   if (nct) HIP_TRY(hipMemcpyAsync(p->d_col_tasks, p->col_tasks.data(), nct * sizeof(ColTask), hipMemcpyHostToDevice, p->stream));
@@ -940,7 +940,11 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
   for (const auto& g : p->groups) min_launch = min_launch ? std::min<int64_t>(min_launch, g.count) : g.count;
   if (!p->pair_groups.empty())
     min_launch = min_launch ? std::min<int64_t>(min_launch, (int64_t)p->pair_groups.size()) : (int64_t)p->pair_groups.size();
-  const int64_t want = std::max<int64_t>(64, std::min<int64_t>(kMaxWG, kTargetWGs / std::max<int64_t>(1, min_launch)));
+  static const int64_t target = [] {
+    const char* e = std::getenv("DQ_TARGET_WGS");  // tuning override (diagnostic)
+    return e ? std::max<int64_t>(256, std::atoll(e)) : (int64_t)kTargetWGs;
+  }();
+  const int64_t want = std::max<int64_t>(64, std::min<int64_t>(kMaxWG, target / std::max<int64_t>(1, min_launch)));
   int32_t nr_col = (int32_t)std::min<int64_t>(want, ceil_div(n_rows, kRowsPerIter));
   int64_t rpr_col = ceil_div(ceil_div(n_rows, nr_col), kRowsPerIter) * kRowsPerIter;
   nr_col = (int32_t)ceil_div(n_rows, rpr_col);
@@ -1001,7 +1005,7 @@ dq_status dq_finish(dq_plan* p, dq_state* out) {
   if (!out && !p->specs.empty()) return set_error(DQ_E_INVALID, "dq_finish: out is NULL");
   HIP_TRY(hipSetDevice(p->device));
   std::vector<ColPartial> col(p->col_tasks.size());
-  std::vector<uint32_t> hll((size_t)p->n_hll * 512);
+  std::vector<uint32_t> hll((size_t)p->n_hll * kHllCopies * 512);
   std::vector<CorrPartial> pair(p->pair_tasks.size());
   PredPartial pred{};
   if (!col.empty()) HIP_TRY(hipMemcpyAsync(col.data(), p->d_col_acc, col.size() * sizeof(ColPartial), hipMemcpyDeviceToHost, p->stream));
@@ -1081,8 +1085,12 @@ dq_status dq_finish(dq_plan* p, dq_state* out) {
       case DQ_OP_APPROX_COUNT_DISTINCT:
         {
           uint8_t regs[512];
-          const uint32_t* r = hll.data() + (size_t)p->col_tasks[o.col_task].hll_slot * 512;
-          for (int k = 0; k < 512; ++k) regs[k] = (uint8_t)r[k];
+          const uint32_t* r = hll.data() + (size_t)p->col_tasks[o.col_task].hll_slot * kHllCopies * 512;
+          for (int k = 0; k < 512; ++k) {
+            uint32_t v = 0;
+            for (int c = 0; c < kHllCopies; ++c) v = std::max(v, r[c * 512 + k]);
+            regs[k] = (uint8_t)v;
+          }
           hll_registers_to_words(regs, s.u.hll.words);
         }
         set1(true);  // nullable = false (StatefulHyperloglogPlus.scala:59)
