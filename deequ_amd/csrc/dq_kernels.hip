@@ -806,44 +806,68 @@ __global__ __launch_bounds__(kBlock) void dq_pair_tile_scan(const PairGroup* __r
       }
     }
     __syncthreads();
-    // ---- fold: this thread's pair over its 64 rows, 8 rows per chunk
+    // ---- fold: this thread's pair over its 64 rows as shifted sums around the pair's running means
+    // (exec-masked accumulation: a row that is not valid in both columns costs no VALU work), then one
+    // Chan merge per tile (rcp + Newton step instead of a division)
     if (active) {
+      double sx = s.xa, sy = s.ya;
+      if (s.n == 0.0) {  // still-empty pair: its first valid row of this tile group is the shift
+        bool found = false;
+#pragma unroll 1
+        for (int k = 0; k < 8 && !found; ++k) {
+          const int rr = grp * 64 + k * 8;
+          const uint32_t bits = ((vbits[ci][rr >> 5] & vbits[cj][rr >> 5]) >> (rr & 31)) & 0xFFu;
+          if (bits) {
+            const int j = __builtin_ctz(bits);
+            sx = tile[ci * kTileStride + rr + j];
+            sy = tile[cj * kTileStride + rr + j];
+            found = true;
+          }
+        }
+      }
+      double Sx = 0.0, Sy = 0.0, Sxy = 0.0, Sxx = 0.0, Syy = 0.0;
+      int32_t kc = 0;
 #pragma unroll 1
       for (int k = 0; k < 8; ++k) {
         const int rr = grp * 64 + k * 8;
         const uint32_t bits = ((vbits[ci][rr >> 5] & vbits[cj][rr >> 5]) >> (rr & 31)) & 0xFFu;
-        if (bits == 0) continue;
+        if (__builtin_amdgcn_ballot_w64(bits != 0) == 0) continue;  // wave-uniform skip
         double x[8], y[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           x[j] = tile[ci * kTileStride + rr + j];
           y[j] = tile[cj * kTileStride + rr + j];
         }
-        double sx = s.xa, sy = s.ya;
-        if (s.n == 0.0) {
-#pragma unroll
-          for (int j = 7; j >= 0; --j) {
-            const bool b = (bits >> j) & 1u;
-            sx = b ? x[j] : sx;
-            sy = b ? y[j] : sy;
-          }
-        }
-        double Sx = 0, Sy = 0, Sxy = 0, Sxx = 0, Syy = 0;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const bool b = (bits >> j) & 1u;
-          const double dx = b ? x[j] - sx : 0.0, dy = b ? y[j] - sy : 0.0;
-          Sx += dx; Sy += dy;
-          Sxy = __builtin_fma(dx, dy, Sxy);
-          Sxx = __builtin_fma(dx, dx, Sxx);
-          Syy = __builtin_fma(dy, dy, Syy);
+          const uint64_t m = __builtin_amdgcn_ballot_w64((bits >> j) & 1u);
+          double dx, dy;
+          uint64_t save;
+          asm volatile(
+              "s_and_saveexec_b64 %[save], %[m]\n\t"
+              "v_add_f64 %[dx], %[x], -%[sx]\n\t"
+              "v_add_f64 %[dy], %[y], -%[sy]\n\t"
+              "v_add_u32 %[k], 1, %[k]\n\t"
+              "v_add_f64 %[Sx], %[Sx], %[dx]\n\t"
+              "v_add_f64 %[Sy], %[Sy], %[dy]\n\t"
+              "v_fma_f64 %[Sxy], %[dx], %[dy], %[Sxy]\n\t"
+              "v_fma_f64 %[Sxx], %[dx], %[dx], %[Sxx]\n\t"
+              "v_fma_f64 %[Syy], %[dy], %[dy], %[Syy]\n\t"
+              "s_mov_b64 exec, %[save]"
+              : [Sx] "+v"(Sx), [Sy] "+v"(Sy), [Sxy] "+v"(Sxy), [Sxx] "+v"(Sxx), [Syy] "+v"(Syy), [k] "+v"(kc),
+                [dx] "=&v"(dx), [dy] "=&v"(dy), [save] "=&s"(save)
+              : [x] "v"(x[j]), [y] "v"(y[j]), [sx] "v"(sx), [sy] "v"(sy), [m] "s"(m)
+              : "scc");
         }
-        const double n2 = s.n + (double)__popc(bits);
-        const double qx = Sx / n2, qy = Sy / n2;
+      }
+      if (kc != 0) {
+        const double n2 = s.n + (double)kc;
+        const double r = rcp_nr(n2);
+        const double qx = Sx * r, qy = Sy * r;
         s.xa = sx + qx; s.ya = sy + qy;
-        s.ck = s.ck + (Sxy - Sx * qy);
-        s.xm = s.xm + (Sxx - Sx * qx);
-        s.ym = s.ym + (Syy - Sy * qy);
+        s.ck = s.ck + __builtin_fma(-Sx, qy, Sxy);
+        s.xm = s.xm + __builtin_fma(-Sx, qx, Sxx);
+        s.ym = s.ym + __builtin_fma(-Sy, qy, Syy);
         s.n = n2;
       }
     }

@@ -315,6 +315,45 @@ def test_where_filters_vs_oracle(dq, pred_data):
             assert_state_close(prod, ref, scale=float(np.abs(ocols["b"].values).sum() + np.abs(ocols["a"].values).sum()))
 
 
+@pytest.mark.parametrize("n", [1, 31, 32, 33, 63, 64, 65, 511, 513, 2047, 2048, 2049, 4097, 100003])
+def test_predicates_ragged_sizes(dq, n):
+    """Row counts around the predicate pass's 32-row words, 64-row waves and 2048-row workgroup
+    slices, with NaNs in the f64 column (Spark orders NaN above every number and NaN = NaN)."""
+    from deequ_amd.runner import scan_states
+
+    rng = np.random.default_rng(n)
+    a = rng.integers(-8, 12, n).astype(np.int64)
+    b = np.round(rng.normal(0.5, 2.0, n), 2)
+    b[rng.random(n) < 0.05] = np.nan
+    c = rng.integers(-5, 10, n).astype(np.int32)
+    va, vb, vc = rng.random(n) > 0.15, rng.random(n) > 0.2, rng.random(n) > 0.1
+    _, dev, ocols = _tables(dq, (n, {"a": ("i64", a, va), "b": ("f64", b, vb), "c": ("i32", c, vc)}))
+    preds = ["a > 3", "b <= 0.25", "b = b", "b > 1e300", "a < b", "`b` IS NULL OR (`b` > -1.0 AND `b` < 8.0)",
+             "NOT (a > 2 AND b < 0.5)", "(a > 1 AND b > 0.1) OR (c < 0 AND a IS NULL)"]
+    analyzers = [dq.Compliance(f"r{i}", p) for i, p in enumerate(preds)]
+    analyzers += [dq.Size("b > 0.5"), dq.Compliance("w", "a < c", "b >= 0"), dq.Sum("a", "c > 0"),
+                  dq.Maximum("b", "a > 0")]
+    got = scan_states(dev, analyzers)
+    for an in analyzers:
+        name = type(an).__name__
+        if name == "Compliance":
+            spec = ("Compliance", an.instance, an.predicate, an.where)
+        elif name == "Size":
+            spec = ("Size", an.where)
+        else:
+            spec = (name, an.column, an.where)
+        ref = O.compute_state(spec, ocols, n)
+        prod = got[an]
+        if ref is None:
+            assert prod is None, (an, prod)
+        elif name == "Compliance":
+            assert prod == dq.NumMatchesAndCount(ref.numMatches, ref.count), (an, prod, ref)
+        elif name == "Size":
+            assert prod == dq.NumMatches(ref.numMatches), (an, prod, ref)
+        else:
+            assert_state_close(prod, ref, scale=float(np.abs(a).sum()) + 1.0)
+
+
 def test_unsupported_predicate_routes_to_fallback(dq, pred_data):
     from deequ_amd.metrics import UnsupportedOnGpuPathException
 
