@@ -9,7 +9,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdqscan.so")
+LIB_PATH = os.environ.get("DQ_LIB_PATH") or os.path.join(_HERE, "libdqscan.so")  # override: diagnostic A/B builds
 
 DQ_OK = 0
 DQ_E_INVALID = -1

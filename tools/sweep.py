@@ -1,5 +1,5 @@
 """Kernel sweep (diagnostic, GPU): column-scan time and algorithmic GB/s for analyzer subsets on one
-C5 chunk.  Usage: python tools/sweep.py [rows]"""
+C5 chunk.  Usage: python tools/sweep.py [rows [case-filter]]"""
 import json
 import os
 import sys
@@ -13,7 +13,12 @@ from deequ_amd import synth  # noqa: E402
 from deequ_amd.runner import ScanPlan  # noqa: E402
 
 
+ONLY = sys.argv[2] if len(sys.argv) > 2 else ""  # optional case-name filter
+
+
 def measure(name, table, analyzers, reps=5):
+    if ONLY and ONLY not in name:
+        return
     plan = ScanPlan(analyzers, table.schema)
     for _ in range(2):
         plan.reset(); plan.scan(table); plan.finish()
@@ -45,24 +50,25 @@ def measure(name, table, analyzers, reps=5):
 
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 62_500_000
-    t = synth.c5_table(n, seed=42)
-    torch.cuda.synchronize()
-    f = [c for c, d, _ in t.schema if d == "f64"]
-    i = [c for c, d, _ in t.schema if d == "i64"]
-    s = [c for c, d, _ in t.schema if d == "utf8"]
-    stats = lambda cs: [A(c) for c in cs for A in (dq.Mean, dq.StandardDeviation, dq.Minimum, dq.Maximum, dq.Sum)]
-    measure("completeness16", t, [dq.Completeness(c) for c, _, _ in t.schema])
-    measure("f64x1_stats", t, stats(f[:1]))
-    measure("f64x1_hll", t, [dq.ApproxCountDistinct(f[0])])
-    measure("f64x8_stats", t, stats(f))
-    measure("f64x8_hll", t, [dq.ApproxCountDistinct(c) for c in f])
-    measure("f64x8_stats_hll", t, stats(f) + [dq.ApproxCountDistinct(c) for c in f])
-    measure("i64x4_stats_hll", t, stats(i) + [dq.ApproxCountDistinct(c) for c in i])
-    measure("utf8x1_hll", t, [dq.ApproxCountDistinct(s[0])])
-    measure("utf8x4_hll", t, [dq.ApproxCountDistinct(c) for c in s])
-    measure("profile16", t, synth.profile_analyzers(t))
-    measure("compliance4", t, [dq.Compliance("p0", "i0 >= 0"), dq.Compliance("p1", "`i1` IS NULL OR (`i1` >= 10.0 AND `i1` <= 1000.0)"),
-                               dq.Compliance("p2", "i2 < i3"), dq.Compliance("p3", "COALESCE(i3, 0.0) >= 0")])
+    if not ONLY or not ONLY.startswith("corr"):
+        t = synth.c5_table(n, seed=42)
+        torch.cuda.synchronize()
+        f = [c for c, d, _ in t.schema if d == "f64"]
+        i = [c for c, d, _ in t.schema if d == "i64"]
+        s = [c for c, d, _ in t.schema if d == "utf8"]
+        stats = lambda cs: [A(c) for c in cs for A in (dq.Mean, dq.StandardDeviation, dq.Minimum, dq.Maximum, dq.Sum)]
+        measure("completeness16", t, [dq.Completeness(c) for c, _, _ in t.schema])
+        measure("f64x1_stats", t, stats(f[:1]))
+        measure("f64x1_hll", t, [dq.ApproxCountDistinct(f[0])])
+        measure("f64x8_stats", t, stats(f))
+        measure("f64x8_hll", t, [dq.ApproxCountDistinct(c) for c in f])
+        measure("f64x8_stats_hll", t, stats(f) + [dq.ApproxCountDistinct(c) for c in f])
+        measure("i64x4_stats_hll", t, stats(i) + [dq.ApproxCountDistinct(c) for c in i])
+        measure("utf8x1_hll", t, [dq.ApproxCountDistinct(s[0])])
+        measure("utf8x4_hll", t, [dq.ApproxCountDistinct(c) for c in s])
+        measure("profile16", t, synth.profile_analyzers(t))
+        measure("compliance4", t, [dq.Compliance("p0", "i0 >= 0"), dq.Compliance("p1", "`i1` IS NULL OR (`i1` >= 10.0 AND `i1` <= 1000.0)"),
+                                   dq.Compliance("p2", "i2 < i3"), dq.Compliance("p3", "COALESCE(i3, 0.0) >= 0")])
     c4 = synth.c4_table(n // 2, seed=42)
     names = list(c4.columns)
     measure("corr28_half", c4, [dq.Correlation(names[a], names[b]) for a in range(8) for b in range(a + 1, 8)])
