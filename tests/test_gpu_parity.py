@@ -195,6 +195,39 @@ def test_profile_vs_oracle(dq, n, null_frac):
         assert_state_close(prod, ref, scale=scale)
 
 
+UTF8_LENS = [0, 1, 3, 4, 7, 8, 9, 12, 15, 16, 17, 20, 23, 24, 25, 27, 28, 29, 31, 32, 33, 40, 63, 64, 65, 100]
+
+
+@pytest.mark.parametrize("large", [False, True])
+@pytest.mark.parametrize("n", [1, 5, 64, 513, 4099])
+def test_utf8_hll_edge_lengths(dq, n, large):
+    """HLL registers of strings of every round structure of the short hash (stripes, 4-byte and byte
+    rounds), empty strings, the > 28-byte general path, arbitrary bytes (incl. 0x00 / 0xFF, invalid
+    UTF-8) and both offset widths, with and without a `where` filter, vs the oracle."""
+    from deequ_amd.runner import scan_states
+    from deequ_amd.table import column_from_numpy, utf8_column
+
+    rng = np.random.default_rng(1000 + n + int(large))
+    strs = []
+    for i in range(n):
+        if rng.random() < 0.1:
+            strs.append(None)
+        else:
+            ln = int(UTF8_LENS[int(rng.integers(0, len(UTF8_LENS)))])
+            # a small alphabet keeps repeats (distinct counts well below n) next to unique values
+            strs.append(bytes(rng.integers(0, 256, ln, dtype=np.uint8)) if rng.random() < 0.5
+                        else bytes(rng.integers(0, 3, ln, dtype=np.uint8)))
+    a = rng.integers(-5, 5, n).astype(np.int64)
+    t = dq.Table([utf8_column("s", strs, large=large), column_from_numpy("a", "i64", a, np.ones(n, bool))])
+    analyzers = [dq.ApproxCountDistinct("s"), dq.ApproxCountDistinct("s", "a > 0"), dq.Completeness("s")]
+    got = scan_states(t, analyzers)
+    valid = np.array([s is not None for s in strs])
+    ocols = {"s": O.OColumn("utf8", strs, valid), "a": O.OColumn("i64", a, np.ones(n, bool))}  # (offset width: no effect on the hash)
+    for an in analyzers:
+        ref = O.compute_state((type(an).__name__, an.column, an.where), ocols, n)
+        assert_state_close(got[an], ref)
+
+
 def test_chunked_equals_single_scan(dq):
     """dq_scan over row chunks (chunk_index order) == one scan (PartitionedTableIntegrationTest analogue)."""
     from deequ_amd import synth
