@@ -5,11 +5,11 @@ libdqscan.so: hand-written gfx950 HIP kernels behind the C ABI in include/dqscan
 is the host-side mirror of the reference's analyzer / state / runner API over that ABI.
 """
 from ._lib import DQError, lib  # noqa: F401  (fails loudly if libdqscan.so is missing)
-from .analyzers import (ApproxCountDistinct, Completeness, Compliance, Correlation, Maximum, Mean,  # noqa: F401
-                        Minimum, Size, StandardDeviation, Sum)
-from .metrics import DoubleMetric, Entity  # noqa: F401
+from .analyzers import (ApproxCountDistinct, Completeness, Compliance, Correlation, DataType,  # noqa: F401
+                        DataTypeInstances, Maximum, Mean, Minimum, Size, StandardDeviation, Sum)
+from .metrics import DoubleMetric, Distribution, DistributionValue, Entity, HistogramMetric  # noqa: F401
 from .runner import AnalysisRunner, AnalyzerContext  # noqa: F401
 from .state_provider import HdfsStateProvider, InMemoryStateProvider  # noqa: F401
-from .states import (ApproxCountDistinctState, CorrelationState, MaxState, MeanState, MinState,  # noqa: F401
-                     NumMatches, NumMatchesAndCount, StandardDeviationState, SumState)
+from .states import (ApproxCountDistinctState, CorrelationState, DataTypeHistogram, MaxState, MeanState,  # noqa: F401
+                     MinState, NumMatches, NumMatchesAndCount, StandardDeviationState, SumState)
 from .table import Column, Table  # noqa: F401

@@ -24,7 +24,8 @@ TYPE_F64, TYPE_I64, TYPE_I32, TYPE_UTF8, TYPE_LARGE_UTF8 = 1, 2, 3, 4, 5
 # column-pass kernel variants (deequ_amd/csrc/dq_device.h ColVariant)
 VARIANT_NAMES = {0: "validity", 1: "f64_stats", 2: "f64_stats_hll", 3: "f64_hll", 4: "i64_stats",
                  5: "i64_stats_hll", 6: "i64_hll", 7: "i32_stats", 8: "i32_stats_hll", 9: "i32_hll",
-                 10: "utf8_hll", 11: "large_utf8_hll"}
+                 10: "utf8_hll", 11: "large_utf8_hll", 12: "utf8_dtype", 13: "utf8_hll_dtype",
+                 14: "large_utf8_dtype", 15: "large_utf8_hll_dtype", 16: "f64_dtype"}
 
 OP_SIZE = 1
 OP_COMPLETENESS = 2
@@ -36,6 +37,7 @@ OP_MIN = 7
 OP_MAX = 8
 OP_CORRELATION = 9
 OP_APPROX_COUNT_DISTINCT = 10
+OP_DATATYPE = 11
 
 PRED_COLUMN = 1
 PRED_LIT_INT = 2
@@ -106,9 +108,14 @@ class _Hll(ctypes.Structure):
     _fields_ = [("words", ctypes.c_int64 * 52)]
 
 
+class _DType(ctypes.Structure):
+    _fields_ = [("num_null", ctypes.c_int64), ("num_fractional", ctypes.c_int64), ("num_integral", ctypes.c_int64),
+                ("num_boolean", ctypes.c_int64), ("num_string", ctypes.c_int64)]
+
+
 class _StateUnion(ctypes.Union):
     _fields_ = [("size", _Size), ("ratio", _Ratio), ("sum", _Sum), ("mean", _Mean), ("stddev", _StdDev),
-                ("minmax", _MinMax), ("corr", _Corr), ("hll", _Hll)]
+                ("minmax", _MinMax), ("corr", _Corr), ("hll", _Hll), ("dtype", _DType)]
 
 
 class State(ctypes.Structure):

@@ -6,7 +6,7 @@ Reference (paths relative to src/main/scala/com/amazon/deequ/analyzers/):
   StandardScanShareableAnalyzer             Analyzer.scala:190-216
   Preconditions.hasColumn / isNumeric       Analyzer.scala:315-334
   Size.scala, Completeness.scala, Compliance.scala, Sum.scala, Mean.scala, StandardDeviation.scala,
-  Minimum.scala, Maximum.scala, Correlation.scala, ApproxCountDistinct.scala
+  Minimum.scala, Maximum.scala, Correlation.scala, ApproxCountDistinct.scala, DataType.scala
 
 Instead of `aggregationFunctions(): Seq[Column]` each analyzer lowers itself into one
 dq_analyzer_spec of the C ABI (`_lower`), and instead of `fromAggregationResult(row, offset)` it
@@ -14,6 +14,7 @@ receives the dq_state slot set libdqscan.so produced for that spec (`_from_resul
 """
 from __future__ import annotations
 
+import math
 from typing import Callable, List, Optional, Sequence
 
 from . import _lib as L
@@ -357,3 +358,68 @@ class Correlation(Analyzer):  # Correlation.scala:65-105
 
     def _lower(self, b):
         return (L.OP_CORRELATION, b.col(self.firstColumn), b.col(self.secondColumn), -1, b.pred(self.where))
+
+
+class DataTypeInstances:  # DataType.scala:32-38 (Enumeration: name -> id)
+    Unknown = "Unknown"
+    Fractional = "Fractional"
+    Integral = "Integral"
+    Boolean = "Boolean"
+    String = "String"
+    ALL = (Unknown, Fractional, Integral, Boolean, String)
+
+
+def _ratio(count: int, total: int) -> float:
+    # Long.toDouble / Long in the JVM: 0 / 0 -> NaN
+    return count / total if total != 0 else (float("nan") if count == 0 else math.copysign(float("inf"), count))
+
+
+def toDistribution(hist) -> "Distribution":
+    """DataTypeHistogram.toDistribution (DataType.scala:98-114)."""
+    from .metrics import Distribution, DistributionValue
+
+    total = hist.numNull + hist.numString + hist.numBoolean + hist.numIntegral + hist.numFractional
+    counts = {DataTypeInstances.Unknown: hist.numNull, DataTypeInstances.Fractional: hist.numFractional,
+              DataTypeInstances.Integral: hist.numIntegral, DataTypeInstances.Boolean: hist.numBoolean,
+              DataTypeInstances.String: hist.numString}
+    return Distribution({k: DistributionValue(v, _ratio(v, total)) for k, v in counts.items()}, numberOfBins=5)
+
+
+def determineType(dist) -> str:
+    """DataTypeHistogram.determineType (DataType.scala:116-143)."""
+    def ratio_of(key):
+        v = dist.values.get(key)
+        return 0.0 if v is None else v.ratio
+
+    I = DataTypeInstances
+    if ratio_of(I.Unknown) == 1.0:
+        return I.Unknown
+    if ratio_of(I.String) > 0.0 or (ratio_of(I.Boolean) > 0.0 and (ratio_of(I.Integral) > 0.0 or ratio_of(I.Fractional) > 0.0)):
+        return I.String
+    if ratio_of(I.Boolean) > 0.0:
+        return I.Boolean
+    if ratio_of(I.Fractional) > 0.0:
+        return I.Fractional
+    return I.Integral
+
+
+class DataType(_ColumnAnalyzer):  # DataType.scala:152-183
+    """stateful_datatype(conditionalSelection(column, where)): every row is NULL (null or `where` not
+    TRUE), or its string form is classified FRACTIONAL / INTEGRAL / BOOLEAN / STRING
+    (catalyst/StatefulDataType.scala:36-67).  The metric is a HistogramMetric."""
+    name = "Histogram"
+    OP = L.OP_DATATYPE
+    numeric = False
+
+    def computeMetricFrom(self, state):
+        from .metrics import HistogramMetric, Success
+
+        if state is not None:
+            return HistogramMetric(self.column, Success(toDistribution(state)))
+        return self.toFailureMetric(EmptyStateException(
+            f"Empty state for analyzer {self}, all input values were NULL."))
+
+    def toFailureMetric(self, e: BaseException):
+        from .metrics import HistogramMetric
+
+        return HistogramMetric(self.column, Failure(wrap_if_necessary(e)))

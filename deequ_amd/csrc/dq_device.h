@@ -38,7 +38,11 @@ enum ColVariant : int32_t {
   CV_I64_S = 4, CV_I64_SH = 5, CV_I64_H = 6,
   CV_I32_S = 7, CV_I32_SH = 8, CV_I32_H = 9,
   CV_UTF8_H = 10, CV_LUTF8_H = 11,
+  // DataType (StatefulDataType.scala:36-69): string columns classify every selected value (alone or
+  // fused with the HLL pass); double columns count the values whose Double.toString is fractional
+  CV_UTF8_D = 12, CV_UTF8_HD = 13, CV_LUTF8_D = 14, CV_LUTF8_HD = 15, CV_F64_D = 16,
 };
+constexpr int kNumVariants = 17;
 
 struct ColTask {
   int32_t variant;   // ColVariant

@@ -506,6 +506,83 @@ __device__ void numeric_range(const void* values, const uint32_t* validity, cons
   if (KIND == CK_F64 && lane == 0) s.nan_count += nan_w;
 }
 
+// ------------------------------------------------------------------------------------------
+// DataType classification of a string value (catalyst/StatefulDataType.scala:36-38, 62-67): the
+// first of FRACTIONAL ^(-|\+)? ?\d*\.\d*$, INTEGRAL ^(-|\+)? ?\d*$, BOOLEAN ^(true|false)$ that
+// matches the whole value, else STRING.  The patterns only accept ASCII and Java's \d is [0-9], so
+// matching the UTF-8 bytes is the same as matching the decoded Java string (any byte >= 0x80, an
+// invalid sequence, a NUL or a trailing newline makes the value a STRING).
+// ------------------------------------------------------------------------------------------
+enum DtClass : uint32_t { DT_FRACTIONAL = 1, DT_INTEGRAL = 2, DT_BOOLEAN = 3, DT_STRING = 4 };
+
+__device__ __forceinline__ uint32_t dt_class_of(bool numeric, uint32_t dots, bool boolean) {
+  return numeric && dots <= 1 ? (dots ? DT_FRACTIONAL : DT_INTEGRAL) : (boolean ? DT_BOOLEAN : DT_STRING);
+}
+
+// bit 7 of every byte i of a dword with lo <= i < hi
+__device__ __forceinline__ uint32_t dt_keep(int lo, int hi) {
+  const uint32_t below_hi = hi >= 4 ? 0x80808080u : (hi <= 0 ? 0u : 0x80808080u & ((1u << (8 * hi)) - 1u));
+  const uint32_t from_lo = lo <= 0 ? 0x80808080u : (lo >= 4 ? 0u : 0x80808080u & ~((1u << (8 * lo)) - 1u));
+  return below_hi & from_lo;
+}
+
+// A string of len <= 28 bytes given as little-endian dwords w[0..6] (bytes past len: anything).
+// SWAR per dword: bit 7 of ((t & 0x7F..) + 0x76..) | t, t = w ^ '0'.., is set for the bytes that are
+// not digits; the same with '.' and + 0x7F.. for the bytes that are not dots.  The dword loop stops as
+// soon as no lane of the wave can still be numeric (text columns: after one dword).
+__device__ __forceinline__ uint32_t dt_class_short(const uint32_t (&w)[8], uint32_t len, bool active) {
+  const uint32_t b0 = w[0] & 0xFFu;
+  const uint32_t sgn = (len > 0 && (b0 == 0x2Bu || b0 == 0x2Du)) ? 1u : 0u;  // '+' / '-'
+  const uint32_t start = sgn + ((sgn < len && ((w[0] >> (8 * sgn)) & 0xFFu) == 0x20u) ? 1u : 0u);  // ' '
+  uint32_t bad = 0, dots = 0;
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    if (k > 0 && __builtin_amdgcn_ballot_w64(active && bad == 0 && dots <= 1 && (uint32_t)(4 * k) < len) == 0) break;
+    const uint32_t keep = dt_keep((int)start - 4 * k, (int)len - 4 * k);
+    const uint32_t t = w[k] ^ 0x30303030u, z = w[k] ^ 0x2E2E2E2Eu;
+    const uint32_t nd = ((t & 0x7F7F7F7Fu) + 0x76767676u) | t;
+    const uint32_t nz = ((z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | z;
+    bad |= nd & nz & keep;
+    dots += __builtin_popcount(~nz & keep);
+  }
+  const bool boolean = (len == 4 && w[0] == 0x65757274u) ||                            // "true"
+                       (len == 5 && w[0] == 0x736C6166u && (w[1] & 0xFFu) == 0x65u);   // "false"
+  return dt_class_of(bad == 0, dots, boolean);
+}
+
+// Any length, byte by byte (the rare path: strings longer than 28 bytes or at the end of the data).
+__device__ uint32_t dt_class_bytes(const uint8_t* p, int64_t len) {
+  int64_t i = 0;
+  if (len > 0 && (p[0] == '+' || p[0] == '-')) i = 1;
+  if (i < len && p[i] == ' ') ++i;
+  bool numeric = true;
+  uint32_t dots = 0;
+  for (; i < len && numeric; ++i) {
+    const uint8_t c = p[i];
+    if (c == '.') ++dots;
+    else if (c < '0' || c > '9') numeric = false;
+  }
+  const bool boolean = (len == 4 && p[0] == 't' && p[1] == 'r' && p[2] == 'u' && p[3] == 'e') ||
+                       (len == 5 && p[0] == 'f' && p[1] == 'a' && p[2] == 'l' && p[3] == 's' && p[4] == 'e');
+  return dt_class_of(numeric, dots, boolean);
+}
+
+// Per-lane DataType counters of the selected values (STRING = count - the others, NULL = rows - count).
+struct DtCounts {
+  uint32_t frac = 0, integ = 0, boolean = 0;
+  __device__ __forceinline__ void add(uint32_t cls, bool sel) {
+    frac += sel && cls == DT_FRACTIONAL;
+    integ += sel && cls == DT_INTEGRAL;
+    boolean += sel && cls == DT_BOOLEAN;
+  }
+  // into the UTF8 task's otherwise unused additive ColStats fields (merged by stats_merge / finalize)
+  __device__ __forceinline__ void flush(ColStats& s) const {
+    s.isum += frac;
+    s.nan_count += integ;
+    s.sum += (double)boolean;
+  }
+};
+
 // UTF8 column: lane l of a wave takes rows base + 64 j + l (j < 8) of its 512-row block, so the
 // selection masks are scalar bitmap words (as in numeric_range).  Offsets come through a
 // bounds-checked buffer resource over offsets[row0 .. row1]; every lane fetches its string with two
@@ -515,7 +592,7 @@ __device__ void numeric_range(const void* values, const uint32_t* validity, cons
 // LDS table p5).  A string that is longer, or whose 32-byte window would cross the end of the chunk's
 // bytes, is flagged in an SGPR mask and rehashed by the general XXH64 loop after the block (rare;
 // ds_max is idempotent, so the block's selected rows are simply redone there).
-template <typename OffT>
+template <typename OffT, bool HLL, bool DT>
 __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint32_t* validity,
                            const uint32_t* mask, int64_t row0, int64_t row1, int64_t n_rows, ColStats& s,
                            int32_t* regs, const uint64_t* p5) {
@@ -536,6 +613,7 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
   const int32_t win = fast_ok ? (int32_t)span - 32 : -1;  // fast iff off <= win: both loads in range
   int64_t cnt_w = 0;  // wave-uniform count of selected rows
   int32_t qmin = 0;
+  DtCounts dtc;
   const auto bp = [p5](uint32_t b) { return p5[b]; };
   // Software pipeline: string j + 1's 32 bytes are in flight while string j is hashed, and right
   // after row j is hashed its registers take the next block's offsets of row j (a whole block of
@@ -593,14 +671,19 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
 #pragma unroll
       for (int k = 0; k < 7; ++k) wv[k] = alignbit32(d[k + 1], d[k], sh);
       wv[7] = d[7];  // only ever feeds the unused half of the tail pair for len >= 24
-      const HllKey key = hll_key_from_fmix(xxh64_short_head(wv, len_of(j), bp));
-      qmin = min(qmin, key.q);
-      if (lane_bit(m[j])) atomicMax(reinterpret_cast<int32_t*>(reinterpret_cast<char*>(regs) + key.addr), key.q);
+      if constexpr (DT) dtc.add(dt_class_short(wv, len_of(j), lane_bit(m[j])), lane_bit(m[j]));
+      if constexpr (HLL) {
+        const HllKey key = hll_key_from_fmix(xxh64_short_head(wv, len_of(j), bp));
+        qmin = min(qmin, key.q);
+        if (lane_bit(m[j])) atomicMax(reinterpret_cast<int32_t*>(reinterpret_cast<char*>(regs) + key.addr), key.q);
+      }
       load_offsets(blk + kRowsPerIter, j);  // unconditional: past row1 the descriptor reads 0
       a = an;
       c = cn;
     }
-    // rare: long / window-crossing strings, or a rank that needs the hash's low word (2^-23)
+    // rare: long / window-crossing strings, or a rank that needs the hash's low word (2^-23).  The
+    // HLL update is idempotent, so the block's selected rows are simply redone; DataType counts only
+    // the rows the fast path skipped.
     if ((slow | __builtin_amdgcn_ballot_w64(qmin < 0)) != 0) {
       block_masks(validity, mask, base, row1, full, m);
 #pragma unroll 1
@@ -608,13 +691,36 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
         if (lane_bit(m[j])) {
           const int64_t row = base + j * 64 + lane;
           const int64_t o0 = (int64_t)offsets[row], o1 = (int64_t)offsets[row + 1];
-          hll_update(regs, xxh64_bytes(data, o0, o1 - o0));
+          if constexpr (HLL) hll_update(regs, xxh64_bytes(data, o0, o1 - o0));
+          if constexpr (DT) {
+            const bool was_fast = o1 - o0 <= 28 && o0 - lo <= (int64_t)win3;
+            if (!was_fast) dtc.add(dt_class_bytes(data + o0, o1 - o0), true);
+          }
         }
       }
       qmin = 0;
     }
   }
   if (lane == 0) s.count += cnt_w;
+  if constexpr (DT) dtc.flush(s);
+}
+
+// DataType of a double column: Spark casts the value to a string with Double.toString, which is
+// plain decimal (matches FRACTIONAL) iff the value is finite and zero or 1e-3 <= |x| < 1e7, and
+// otherwise "NaN", "Infinity" or computerized scientific notation ("1.0E7": a STRING).  Counts the
+// selected rows (s.count) and the fractional ones (s.isum).
+__device__ void f64_dtype_range(const double* values, const uint32_t* validity, const uint32_t* mask, int64_t row0,
+                                int64_t row1, ColStats& s) {
+  uint32_t cnt = 0, frac = 0;
+  for (int64_t r = row0 + threadIdx.x; r < row1; r += kBlock) {
+    const uint32_t bit = (word_or_ones(validity, r >> 5) & word_or_ones(mask, r >> 5)) >> (r & 31);
+    const bool sel = bit & 1u;
+    const double x = __builtin_nontemporal_load(values + r), a = __builtin_fabs(x);
+    cnt += sel;
+    frac += sel && (x == 0.0 || (a >= 1e-3 && a < 1e7));
+  }
+  s.count += cnt;
+  s.isum += frac;
 }
 
 // Only the count of selected rows (Completeness): popcount of validity (& where) words.
@@ -660,12 +766,15 @@ __device__ __forceinline__ void run_variant(const ColTask& t, const ScanCols& co
   else if constexpr (V == CV_I32_S) numeric_range<CK_I32, true, false>(v, val, mask, row0, row1, s, regs);
   else if constexpr (V == CV_I32_SH) numeric_range<CK_I32, true, true>(v, val, mask, row0, row1, s, regs);
   else if constexpr (V == CV_I32_H) numeric_range<CK_I32, false, true>(v, val, mask, row0, row1, s, regs);
-  else if constexpr (V == CV_UTF8_H)
-    utf8_range<int32_t>(reinterpret_cast<const uint8_t*>(v), reinterpret_cast<const int32_t*>(cols.offsets[t.col]),
-                        val, mask, row0, row1, n_rows, s, regs, p5);
+  else if constexpr (V == CV_F64_D) f64_dtype_range(reinterpret_cast<const double*>(v), val, mask, row0, row1, s);
+  else if constexpr (V == CV_UTF8_H || V == CV_UTF8_D || V == CV_UTF8_HD)
+    utf8_range<int32_t, V != CV_UTF8_D, V != CV_UTF8_H>(
+        reinterpret_cast<const uint8_t*>(v), reinterpret_cast<const int32_t*>(cols.offsets[t.col]), val, mask, row0,
+        row1, n_rows, s, regs, p5);
   else
-    utf8_range<int64_t>(reinterpret_cast<const uint8_t*>(v), reinterpret_cast<const int64_t*>(cols.offsets[t.col]),
-                        val, mask, row0, row1, n_rows, s, regs, p5);
+    utf8_range<int64_t, V != CV_LUTF8_D, V != CV_LUTF8_H>(
+        reinterpret_cast<const uint8_t*>(v), reinterpret_cast<const int64_t*>(cols.offsets[t.col]), val, mask, row0,
+        row1, n_rows, s, regs, p5);
 }
 
 template <int V>
@@ -674,8 +783,9 @@ __global__ __launch_bounds__(kBlock) void dq_column_scan(const ColTask* __restri
                                                          int64_t n_rows, int64_t rows_per_range,
                                                          ColPartial* __restrict__ partials,
                                                          uint32_t* __restrict__ hll_acc) {
-  constexpr bool kHll = !(V == CV_VALIDITY || V == CV_F64_S || V == CV_I64_S || V == CV_I32_S);
-  constexpr bool kStr = V == CV_UTF8_H || V == CV_LUTF8_H;
+  constexpr bool kHll = !(V == CV_VALIDITY || V == CV_F64_S || V == CV_I64_S || V == CV_I32_S || V == CV_F64_D ||
+                         V == CV_UTF8_D || V == CV_LUTF8_D);
+  constexpr bool kStr = V == CV_UTF8_H || V == CV_LUTF8_H || V == CV_UTF8_HD || V == CV_LUTF8_HD;
   __shared__ int32_t regs[kHll ? 512 : 1];  // q = pw - 1, -1 = empty (see hll_q_exact)
   __shared__ uint64_t p5[kStr ? 256 : 1];   // b * P5 for the byte rounds of the string hash
   __shared__ ColStats red[kWaves];
@@ -1241,6 +1351,7 @@ hipError_t launch_column_scan(int32_t variant, const ColTask* tasks, int32_t nta
   switch (variant) {
     DQ_V(CV_VALIDITY) DQ_V(CV_F64_S) DQ_V(CV_F64_SH) DQ_V(CV_F64_H) DQ_V(CV_I64_S) DQ_V(CV_I64_SH) DQ_V(CV_I64_H)
     DQ_V(CV_I32_S) DQ_V(CV_I32_SH) DQ_V(CV_I32_H) DQ_V(CV_UTF8_H) DQ_V(CV_LUTF8_H)
+    DQ_V(CV_UTF8_D) DQ_V(CV_UTF8_HD) DQ_V(CV_LUTF8_D) DQ_V(CV_LUTF8_HD) DQ_V(CV_F64_D)
     default: return hipErrorInvalidValue;
   }
 #undef DQ_V

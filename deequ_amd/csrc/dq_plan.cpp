@@ -419,8 +419,9 @@ struct dq_plan {
   std::vector<hipEvent_t> ev_pool;
   struct Pending { int kernel; hipEvent_t a, b; };
   std::vector<Pending> pending;
-  double kernel_ms[32] = {0};       // 0 pred, 2 pair, 3 finalize, 16 + v column variant v
-  int64_t kernel_launches[32] = {0};
+  static constexpr int kTimers = 16 + kNumVariants;
+  double kernel_ms[kTimers] = {0};       // 0 pred, 2 pair, 3 finalize, 16 + v column variant v
+  int64_t kernel_launches[kTimers] = {0};
   int64_t bytes_per_row_x1000 = 0;
   int32_t launches_per_scan = 0;
 };
@@ -503,11 +504,12 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
   const int32_t ncols = (int32_t)p->schema.size();
   std::map<std::string, int32_t> root_slot;          // canonical predicate text -> root slot
   std::vector<std::vector<PredInstr>> root_code;
-  std::map<std::pair<int32_t, int32_t>, int32_t> col_task_of;      // (col, where bitmap) -> task
+  std::map<std::tuple<int32_t, int32_t, int32_t>, int32_t> col_task_of;  // (col, where bitmap, f64 DataType) -> task
   std::map<std::tuple<int32_t, int32_t, int32_t>, int32_t> pair_of; // (x, y, where bitmap) -> task
   std::map<std::pair<int32_t, int32_t>, int32_t> counter_of;      // (pred slot, where slot) -> counter
   std::map<int32_t, int32_t> bitmap_of;                             // where slot -> bitmap index
-  std::vector<std::pair<bool, bool>> col_task_needs;                // (stats, hll)
+  struct Needs { bool stats = false, hll = false, dtype = false; };
+  std::vector<Needs> col_task_needs;
   Lowering low{pool, n_pred, &p->schema, {}};
 
   auto root = [&](int32_t node, int32_t& slot) -> dq_status {
@@ -553,8 +555,9 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
     bitmap_of[where_slot] = b;
     return DQ_OK;
   };
-  auto col_task = [&](int32_t col, int32_t bm, bool stats, bool hll, int32_t& t) -> dq_status {
-    auto key = std::make_pair(col, bm);
+  auto col_task = [&](int32_t col, int32_t bm, bool stats, bool hll, int32_t& t, bool dtype = false) -> dq_status {
+    // a double column's DataType count is a variant of its own (CV_F64_D)
+    auto key = std::make_tuple(col, bm, dtype && p->schema[col].type == DQ_TYPE_F64 ? 1 : 0);
     auto it = col_task_of.find(key);
     if (it == col_task_of.end()) {
       if ((int32_t)p->col_tasks.size() >= 256) return set_error(DQ_E_UNSUPPORTED, "too many column tasks");
@@ -563,12 +566,13 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
       ColTask ct{};
       ct.col = col; ct.where = bm; ct.hll_slot = -1; ct.variant = CV_VALIDITY;
       p->col_tasks.push_back(ct);
-      col_task_needs.push_back({false, false});
+      col_task_needs.push_back(Needs{});
     } else {
       t = it->second;
     }
-    col_task_needs[t].first |= stats;
-    col_task_needs[t].second |= hll;
+    col_task_needs[t].stats |= stats;
+    col_task_needs[t].hll |= hll;
+    col_task_needs[t].dtype |= dtype;
     return DQ_OK;
   };
 
@@ -630,6 +634,15 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
         if (dq_status st = col_task(s.col_a, bm, !hll, hll, o.col_task)) return st;
         break;
       }
+      case DQ_OP_DATATYPE: {  // DataType.scala:157-159: stateful_datatype(conditionalSelection(column, where))
+        if (dq_status st = need_col(s.col_a)) return st;
+        o.col_type = p->schema[s.col_a].type;
+        int32_t bm;
+        if (dq_status st = bitmap(where_slot, bm)) return st;
+        // integral columns: Long/Int.toString always matches INTEGRAL -> the selected-row count suffices
+        if (dq_status st = col_task(s.col_a, bm, false, false, o.col_task, !is_integral(o.col_type))) return st;
+        break;
+      }
       case DQ_OP_CORRELATION: {
         if (dq_status st = need_col(s.col_a)) return st;
         if (dq_status st = need_col(s.col_b)) return st;
@@ -660,12 +673,13 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
   // column task variants
   for (size_t t = 0; t < p->col_tasks.size(); ++t) {
     ColTask& ct = p->col_tasks[t];
-    bool stats = col_task_needs[t].first, hll = col_task_needs[t].second;
+    const bool stats = col_task_needs[t].stats, hll = col_task_needs[t].hll, dtype = col_task_needs[t].dtype;
     int32_t type = p->schema[ct.col].type;
     if (hll) ct.hll_slot = p->n_hll++;
-    if (!stats && !hll) ct.variant = CV_VALIDITY;
-    else if (type == DQ_TYPE_UTF8) ct.variant = CV_UTF8_H;
-    else if (type == DQ_TYPE_LARGE_UTF8) ct.variant = CV_LUTF8_H;
+    if (dtype && type == DQ_TYPE_F64) ct.variant = CV_F64_D;
+    else if (!stats && !hll && !dtype) ct.variant = CV_VALIDITY;
+    else if (type == DQ_TYPE_UTF8) ct.variant = hll && dtype ? CV_UTF8_HD : (dtype ? CV_UTF8_D : CV_UTF8_H);
+    else if (type == DQ_TYPE_LARGE_UTF8) ct.variant = hll && dtype ? CV_LUTF8_HD : (dtype ? CV_LUTF8_D : CV_LUTF8_H);
     else {
       int base = type == DQ_TYPE_F64 ? CV_F64_S : (type == DQ_TYPE_I64 ? CV_I64_S : CV_I32_S);
       ct.variant = base + (stats && hll ? 1 : (stats ? 0 : 2));
@@ -1082,6 +1096,22 @@ dq_status dq_finish(dq_plan* p, dq_state* out) {
         set1(true);
         break;
       }
+      case DQ_OP_DATATYPE: {  // StatefulDataType: NULL (incl. where-false), FRACTIONAL, INTEGRAL, BOOLEAN, STRING
+        auto& d = s.u.dtype;
+        d.num_null = rows - c->count;
+        if (o.col_type == DQ_TYPE_UTF8 || o.col_type == DQ_TYPE_LARGE_UTF8) {
+          d.num_fractional = c->isum;
+          d.num_integral = c->nan_count;
+          d.num_boolean = (int64_t)c->sum;
+        } else if (o.col_type == DQ_TYPE_F64) {
+          d.num_fractional = c->isum;
+        } else {
+          d.num_integral = c->count;
+        }
+        d.num_string = c->count - d.num_fractional - d.num_integral - d.num_boolean;
+        set1(true);  // the UDAF result is never NULL
+        break;
+      }
       case DQ_OP_APPROX_COUNT_DISTINCT:
         {
           uint8_t regs[512];
@@ -1122,19 +1152,19 @@ dq_status dq_plan_enable_timing(dq_plan* p, int32_t on) {
   HIP_TRY(hipSetDevice(p->device));
   if (dq_status s = resolve_timing(p)) return s;
   p->timing = on != 0;
-  for (int k = 0; k < 32; ++k) { p->kernel_ms[k] = 0; p->kernel_launches[k] = 0; }
+  for (int k = 0; k < dq_plan::kTimers; ++k) { p->kernel_ms[k] = 0; p->kernel_launches[k] = 0; }
   return DQ_OK;
 }
 
 dq_status dq_plan_kernel_time(dq_plan* p, int32_t kernel, double* total_ms, int64_t* launches) {
-  if (!p || kernel < 0 || kernel >= 32 || !total_ms || !launches)
+  if (!p || kernel < 0 || kernel >= dq_plan::kTimers || !total_ms || !launches)
     return set_error(DQ_E_INVALID, "dq_plan_kernel_time: bad argument");
   HIP_TRY(hipSetDevice(p->device));
   if (dq_status s = resolve_timing(p)) return s;
   if (kernel == 1) {  // all column-scan variants
     double ms = 0;
     int64_t n = 0;
-    for (int k = 16; k < 32; ++k) { ms += p->kernel_ms[k]; n += p->kernel_launches[k]; }
+    for (int k = 16; k < dq_plan::kTimers; ++k) { ms += p->kernel_ms[k]; n += p->kernel_launches[k]; }
     *total_ms = ms;
     *launches = n;
   } else {

@@ -185,6 +185,15 @@ static void corr_sum(const dq_state& a, const dq_state& b, dq_state& o) {
   o.u.corr.ck = ck; o.u.corr.x_mk = xm; o.u.corr.y_mk = ym;
 }
 
+// DataTypeHistogram.sum (DataType.scala:48-51) == StatefulDataType.merge (StatefulDataType.scala:71-77).
+static void dtype_sum(const dq_state& a, const dq_state& b, dq_state& o) {
+  o.u.dtype.num_null = wrap_add(a.u.dtype.num_null, b.u.dtype.num_null);
+  o.u.dtype.num_fractional = wrap_add(a.u.dtype.num_fractional, b.u.dtype.num_fractional);
+  o.u.dtype.num_integral = wrap_add(a.u.dtype.num_integral, b.u.dtype.num_integral);
+  o.u.dtype.num_boolean = wrap_add(a.u.dtype.num_boolean, b.u.dtype.num_boolean);
+  o.u.dtype.num_string = wrap_add(a.u.dtype.num_string, b.u.dtype.num_string);
+}
+
 // Sum of two DEFINED states (State.sum).
 static void state_sum_defined(const dq_state& a, const dq_state& b, dq_state& o) {
   o = a;
@@ -205,6 +214,7 @@ static void state_sum_defined(const dq_state& a, const dq_state& b, dq_state& o)
     case DQ_OP_MAX: o.u.minmax.value = java_max(a.u.minmax.value, b.u.minmax.value); break;
     case DQ_OP_CORRELATION: corr_sum(a, b, o); break;
     case DQ_OP_APPROX_COUNT_DISTINCT: hll_merge_words(a.u.hll.words, b.u.hll.words, o.u.hll.words); break;
+    case DQ_OP_DATATYPE: dtype_sum(a, b, o); break;
   }
 }
 
@@ -266,6 +276,9 @@ dq_status state_combine(const dq_state& a, const dq_state& b, dq_state& o) {
     case DQ_OP_APPROX_COUNT_DISTINCT:
       hll_merge_words(a.u.hll.words, b.u.hll.words, o.u.hll.words);
       break;
+    case DQ_OP_DATATYPE:  // the UDAF buffer is never NULL: partial buffers add field by field
+      dtype_sum(a, b, o);
+      break;
     default:
       return set_error(DQ_E_STATE, "dq_state_combine: bad op %d", a.op);
   }
@@ -293,6 +306,8 @@ dq_status state_metric(const dq_state& s, double& out) {
     case DQ_OP_MAX: out = s.u.minmax.value; break;
     case DQ_OP_CORRELATION: out = s.u.corr.ck / std::sqrt(s.u.corr.x_mk * s.u.corr.y_mk); break;
     case DQ_OP_APPROX_COUNT_DISTINCT: out = hll_count(s.u.hll.words); break;
+    case DQ_OP_DATATYPE:
+      return set_error(DQ_E_STATE, "dq_state_metric: DataType yields a HistogramMetric, not a double");
     default: return set_error(DQ_E_STATE, "dq_state_metric: bad op %d", s.op);
   }
   return DQ_OK;
@@ -334,6 +349,13 @@ int64_t state_to_bytes(const dq_state& s, uint8_t* buf, int64_t cap) {
       tmp[0] = 0; tmp[1] = 0; tmp[2] = (416 >> 8) & 0xFF; tmp[3] = 416 & 0xFF;
       n = 4;
       for (int i = 0; i < kHllWords; ++i) w64((uint64_t)s.u.hll.words[i]);
+      break;
+    case DQ_OP_DATATYPE:  // persistBytes(DataTypeHistogram.toBytes(...)): int length 40 + 5 big-endian longs
+      tmp[0] = 0; tmp[1] = 0; tmp[2] = 0; tmp[3] = 40;
+      n = 4;
+      w64((uint64_t)s.u.dtype.num_null); w64((uint64_t)s.u.dtype.num_fractional);
+      w64((uint64_t)s.u.dtype.num_integral); w64((uint64_t)s.u.dtype.num_boolean);
+      w64((uint64_t)s.u.dtype.num_string);
       break;
     default: return set_error(DQ_E_STATE, "dq_state_to_bytes: bad op %d", s.op);
   }
@@ -381,6 +403,15 @@ dq_status state_from_bytes(int32_t op, const uint8_t* buf, int64_t len, dq_state
       if (l != 416) break;  // wordsFromBytes: require(bytes.length == NUM_WORDS * 8)
       p = 4;
       for (int i = 0; i < kHllWords; ++i) o.u.hll.words[i] = (int64_t)r64();
+      return DQ_OK;
+    }
+    case DQ_OP_DATATYPE: {
+      if (len != 4 + 40) break;
+      if (buf[0] != 0 || buf[1] != 0 || buf[2] != 0 || buf[3] != 40) break;  // fromBytes: require(length == 40)
+      p = 4;
+      o.u.dtype.num_null = (int64_t)r64(); o.u.dtype.num_fractional = (int64_t)r64();
+      o.u.dtype.num_integral = (int64_t)r64(); o.u.dtype.num_boolean = (int64_t)r64();
+      o.u.dtype.num_string = (int64_t)r64();
       return DQ_OK;
     }
     default:

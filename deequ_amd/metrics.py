@@ -1,6 +1,7 @@
 """Metric types and failure semantics.
 
-Mirrors metrics/Metric.scala:21-68 (Entity, DoubleMetric) and
+Mirrors metrics/Metric.scala:21-68 (Entity, DoubleMetric), metrics/HistogramMetric.scala:21-61
+(DistributionValue, Distribution, HistogramMetric) and
 analyzers/runners/MetricCalculationException.scala:19-78 plus the EmptyStateException message
 of analyzers/Analyzer.scala:420-422 (paths relative to src/main/scala/com/amazon/deequ/).
 """
@@ -9,7 +10,7 @@ from __future__ import annotations
 import math
 from dataclasses import dataclass
 from enum import Enum
-from typing import Optional
+from typing import Dict, Optional
 
 
 class Entity(Enum):  # Metric.scala:21-23 (the typo "Mutlicolumn" is the reference's)
@@ -126,3 +127,43 @@ class DoubleMetric:  # Metric.scala:41-49
 
     def flatten(self):
         return [self]
+
+
+@dataclass(frozen=True)
+class DistributionValue:  # HistogramMetric.scala:21
+    absolute: int
+    ratio: float
+
+
+@dataclass(eq=True)
+class Distribution:  # HistogramMetric.scala:23-35
+    values: Dict[str, DistributionValue]
+    numberOfBins: int
+
+    def __getitem__(self, key: str) -> DistributionValue:
+        return self.values[key]
+
+    def argmax(self) -> str:
+        return max(self.values.items(), key=lambda kv: kv[1].absolute)[0]
+
+
+@dataclass(eq=True)
+class HistogramMetric:  # HistogramMetric.scala:37-61
+    column: str
+    value: Try
+    entity: Entity = Entity.Column
+    name: str = "Histogram"
+
+    @property
+    def instance(self) -> str:
+        return self.column
+
+    def flatten(self):
+        if self.value.isFailure:
+            return [DoubleMetric(self.entity, f"{self.name}.bins", self.instance, self.value)]
+        d = self.value.get()
+        out = [DoubleMetric(self.entity, f"{self.name}.bins", self.instance, Success(float(d.numberOfBins)))]
+        for key, v in d.values.items():
+            out.append(DoubleMetric(self.entity, f"{self.name}.abs.{key}", self.instance, Success(float(v.absolute))))
+            out.append(DoubleMetric(self.entity, f"{self.name}.ratio.{key}", self.instance, Success(v.ratio)))
+        return out

@@ -174,7 +174,7 @@ class AnalyzerContext:
 
     def successMetricsAsJson(self) -> str:
         rows = []
-        for m in self.allMetrics:
+        for m in (d for metric in self.allMetrics for d in metric.flatten()):  # AnalyzerContext.scala:90
             if m.value.isSuccess:
                 rows.append({"entity": m.entity.value, "instance": m.instance, "name": m.name,
                              "value": m.value.get()})

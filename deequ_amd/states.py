@@ -5,7 +5,8 @@ NumMatches analyzers/Size.scala:23-33, NumMatchesAndCount analyzers/Analyzer.sca
 SumState analyzers/Sum.scala:25-34, MeanState analyzers/Mean.scala:25-34,
 StandardDeviationState analyzers/StandardDeviation.scala:25-45, MinState/MaxState
 analyzers/Minimum.scala:25-34 / analyzers/Maximum.scala:25-34, CorrelationState
-analyzers/Correlation.scala:26-57, ApproxCountDistinctState analyzers/ApproxCountDistinct.scala:26-40.
+analyzers/Correlation.scala:26-57, ApproxCountDistinctState analyzers/ApproxCountDistinct.scala:26-40,
+DataTypeHistogram analyzers/DataType.scala:40-52.
 `sum` and `metricValue` call dq_state_merge / dq_state_metric in libdqscan.so, so host-side
 merges (StateLoader aggregation, incremental runs) use exactly the library's algebra.
 """
@@ -151,6 +152,24 @@ class ApproxCountDistinctState(State):
         return f"ApproxCountDistinctState({','.join(str(w) for w in self.words)})"
 
 
+@dataclass(frozen=True)
+class DataTypeHistogram(State):  # DataType.scala:40-52
+    numNull: int
+    numFractional: int
+    numIntegral: int
+    numBoolean: int
+    numString: int
+    OP = L.OP_DATATYPE
+
+    def _fill(self, u):
+        d = u.dtype
+        d.num_null, d.num_fractional, d.num_integral = self.numNull, self.numFractional, self.numIntegral
+        d.num_boolean, d.num_string = self.numBoolean, self.numString
+
+    def metricValue(self) -> float:
+        raise TypeError("DataTypeHistogram yields a Distribution (DataTypeHistogram.toDistribution), not a double")
+
+
 _COMPLIANCE_LIKE = (L.OP_COMPLETENESS, L.OP_COMPLIANCE)
 
 
@@ -178,6 +197,10 @@ def state_from_c(s: L.State) -> Optional[State]:
         return CorrelationState(c.n, c.x_avg, c.y_avg, c.ck, c.x_mk, c.y_mk)
     if op == L.OP_APPROX_COUNT_DISTINCT:
         return ApproxCountDistinctState(tuple(int(w) for w in u.hll.words))
+    if op == L.OP_DATATYPE:
+        d = u.dtype
+        return DataTypeHistogram(int(d.num_null), int(d.num_fractional), int(d.num_integral), int(d.num_boolean),
+                                 int(d.num_string))
     raise ValueError(f"unknown op {op}")
 
 

@@ -62,7 +62,8 @@ enum dq_op {
   DQ_OP_MIN = 7,                  /* analyzers/Minimum.scala:36-53 */
   DQ_OP_MAX = 8,                  /* analyzers/Maximum.scala:36-53 */
   DQ_OP_CORRELATION = 9,          /* analyzers/Correlation.scala:65-105 */
-  DQ_OP_APPROX_COUNT_DISTINCT = 10 /* analyzers/ApproxCountDistinct.scala:47-64 */
+  DQ_OP_APPROX_COUNT_DISTINCT = 10,/* analyzers/ApproxCountDistinct.scala:47-64 */
+  DQ_OP_DATATYPE = 11             /* analyzers/DataType.scala:152-183, catalyst/StatefulDataType.scala:26-83 */
 };
 
 typedef struct dq_column_desc {
@@ -73,7 +74,7 @@ typedef struct dq_column_desc {
 /* One analyzer instance (a Scala case class).  Unused fields = -1. */
 typedef struct dq_analyzer_spec {
   int32_t op;         /* enum dq_op */
-  int32_t col_a;      /* column index (COMPLETENESS..MAX, ACD, CORRELATION first column) */
+  int32_t col_a;      /* column index (COMPLETENESS..MAX, ACD, DATATYPE, CORRELATION first column) */
   int32_t col_b;      /* CORRELATION second column */
   int32_t pred_root;  /* COMPLIANCE predicate: root index into the predicate node pool */
   int32_t where_root; /* optional `where` filter root, -1 = none */
@@ -137,6 +138,7 @@ typedef struct dq_state {
     struct { double value; } minmax;                          /* MinState / MaxState */
     struct { double n, x_avg, y_avg, ck, x_mk, y_mk; } corr;  /* CorrelationState */
     struct { int64_t words[52]; } hll;                        /* ApproxCountDistinctState */
+    struct { int64_t num_null, num_fractional, num_integral, num_boolean, num_string; } dtype;  /* DataTypeHistogram */
   } u;
 } dq_state;
 
@@ -186,7 +188,8 @@ dq_status dq_state_merge(const dq_state* a, const dq_state* b, dq_state* out);
 dq_status dq_state_combine(const dq_state* a, const dq_state* b, dq_state* out);
 /* 1 if fromAggregationResult would produce Some(state). */
 int32_t dq_state_is_defined(const dq_state* s);
-/* metricValue() of a defined state. */
+/* metricValue() of a defined state (DoubleMetric analyzers; DATATYPE has a histogram, not a double:
+   DQ_E_STATE). */
 dq_status dq_state_metric(const dq_state* s, double* out);
 /* HLL++ estimate of 52 packed words, bit-exact with DeequHyperLogLogPlusPlusUtils.count. */
 dq_status dq_hll_estimate(const int64_t* words52, double* out);

@@ -17,7 +17,12 @@ What it restates (reference = malcolmgreaves/deequ, paths relative to
   (``analyzers/catalyst/StatefulHyperloglogPlus.scala:89-297``, constants
   ``analyzers/catalyst/HLLConstants.scala:27-37,51,84``);
 * ``HdfsStateProvider`` byte formats and file identifiers
-  (``analyzers/StateProvider.scala:81-83, 176-294``).
+  (``analyzers/StateProvider.scala:81-83, 176-294``);
+* ``DataType`` (``analyzers/DataType.scala:40-183``) and its UDAF
+  ``analyzers/catalyst/StatefulDataType.scala:26-83``: Scala ``Regex`` extractors
+  (``Matcher.matches``, whole-value) over the value's Java string -- the UDAF's
+  input is ``StringType``, so Spark casts numeric columns with
+  ``Long/Integer.toString`` / ``Double.toString`` first.
 
 Spark 2.2.2 itself is not vendored in the reference (pom.xml:79-83), so the
 following are restated from Spark's published source and pinned by the
@@ -39,6 +44,7 @@ buffers in order into the zero buffer with the merge expressions.
 from __future__ import annotations
 
 import math
+import re
 import struct
 from dataclasses import dataclass
 from typing import List, Optional, Sequence, Tuple
@@ -577,6 +583,23 @@ class ApproxCountDistinctState:  # ApproxCountDistinct.scala:26-40
         return hll_count(self.words)
 
 
+@dataclass(frozen=True)
+class DataTypeHistogram:  # DataType.scala:40-52
+    numNull: int
+    numFractional: int
+    numIntegral: int
+    numBoolean: int
+    numString: int
+
+    def sum(self, o):
+        return DataTypeHistogram(self.numNull + o.numNull, self.numFractional + o.numFractional,
+                                 self.numIntegral + o.numIntegral, self.numBoolean + o.numBoolean,
+                                 self.numString + o.numString)
+
+    def metricValue(self):
+        raise TypeError("DataType has a HistogramMetric")
+
+
 def merge_states(*states):
     """Analyzers.merge (Analyzer.scala:343-362)."""
     acc = None
@@ -1053,6 +1076,61 @@ def hll_words_for(c: OColumn, sel: np.ndarray) -> Tuple[int, ...]:
 # --------------------------------------------------------------------------------------
 
 
+# StatefulDataType.scala:36-38.  Java's \\d is [0-9] (no UNICODE_CHARACTER_CLASS), and the Scala
+# extractor calls Matcher.matches(), i.e. re.fullmatch: a trailing line terminator does not match.
+_DT_FRACTIONAL = re.compile(rb"(-|\+)? ?[0-9]*\.[0-9]*")
+_DT_INTEGRAL = re.compile(rb"(-|\+)? ?[0-9]*")
+_DT_BOOLEAN = re.compile(rb"(true|false)")
+
+
+def java_double_to_string(d: float) -> str:
+    """java.lang.Double.toString: plain decimal for 1e-3 <= |d| < 1e7 (and zero), else computerized
+    scientific notation ("1.0E7", "1.234E-5"), "NaN", "Infinity".  The digits are Python's shortest
+    repr (Java's can differ in the last digit, which does not change the DataType class)."""
+    if math.isnan(d):
+        return "NaN"
+    if math.isinf(d):
+        return "Infinity" if d > 0 else "-Infinity"
+    if d == 0.0:
+        return "-0.0" if math.copysign(1.0, d) < 0 else "0.0"
+    a = abs(d)
+    if 1e-3 <= a < 1e7:
+        r = repr(d)  # Python uses positional notation throughout [1e-4, 1e16)
+        return r if "." in r else r + ".0"
+    mant, exp = ("%.16e" % d).split("e")
+    mant = mant.rstrip("0")
+    return f"{mant}0E{int(exp)}" if mant.endswith(".") else f"{mant}E{int(exp)}"
+
+
+def datatype_class(value: bytes) -> int:
+    """StatefulDataType.update (:58-69): 1 FRACTIONAL, 2 INTEGRAL, 3 BOOLEAN, 4 STRING, first match
+    wins.  `value` is the UTF-8 of the Java string; every pattern is ASCII-only, so a value with any
+    byte >= 0x80 (decoded to a non-ASCII char, or U+FFFD if invalid) is a STRING either way."""
+    if _DT_FRACTIONAL.fullmatch(value):
+        return 1
+    if _DT_INTEGRAL.fullmatch(value):
+        return 2
+    if _DT_BOOLEAN.fullmatch(value):
+        return 3
+    return 4
+
+
+def _value_string(c: "OColumn", i: int) -> bytes:
+    """CAST(value AS STRING) of a column value, as UTF-8."""
+    if c.dtype in ("utf8", "large_utf8"):
+        return c.values[i]
+    if c.dtype == "f64":
+        return java_double_to_string(float(c.values[i])).encode()
+    return str(int(c.values[i])).encode()
+
+
+def datatype_histogram(c: "OColumn", sel: np.ndarray) -> DataTypeHistogram:
+    counts = [0, 0, 0, 0, 0]  # NULL_POS, FRACTIONAL_POS, INTEGRAL_POS, BOOLEAN_POS, STRING_POS
+    for i in range(len(sel)):
+        counts[datatype_class(_value_string(c, i)) if sel[i] else 0] += 1
+    return DataTypeHistogram(*counts)
+
+
 def _where(cols, n, where: Optional[str]):
     """(where_true, where_notnull) masks; no where -> all true."""
     if where is None:
@@ -1114,6 +1192,10 @@ def compute_state(spec: tuple, cols: dict, n: int, n_partitions: int = 1):
                 return None
             return MinState(v) if op == "Minimum" else MaxState(v)
         return ApproxCountDistinctState(hll_words_for(c, sel))
+    if op == "DataType":  # stateful_datatype(conditionalSelection(column, where)); never NULL
+        col, where = spec[1], spec[2]
+        wt, _ = _where(cols, n, where)
+        return datatype_histogram(cols[col], cols[col].valid & wt)
     if op == "Correlation":
         a, b, where = spec[1], spec[2], spec[3]
         wt, _ = _where(cols, n, where)
@@ -1191,5 +1273,9 @@ def state_to_bytes(state) -> bytes:
         return struct.pack(">dddddd", state.n, state.xAvg, state.yAvg, state.ck, state.xMk, state.yMk)
     if isinstance(state, ApproxCountDistinctState):
         b = words_to_bytes(state.words)
+        return struct.pack(">i", len(b)) + b
+    if isinstance(state, DataTypeHistogram):  # persistBytes(DataTypeHistogram.toBytes(...))
+        b = struct.pack(">qqqqq", state.numNull, state.numFractional, state.numIntegral, state.numBoolean,
+                        state.numString)
         return struct.pack(">i", len(b)) + b
     raise TypeError(type(state))

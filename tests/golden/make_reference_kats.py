@@ -3,8 +3,10 @@
 Every dataset is transcribed from the reference's test fixtures and every expected value
 from an assertion in the reference's test suite (paths relative to
 src/test/scala/com/amazon/deequ/).  This is data only: tables + expected metrics.
-`expected` is a float, "NaN", or "EmptyState" (metric fails with EmptyStateException,
-Analyzer.scala:420-431).  `needs` lists GPU-path capabilities a case depends on beyond
+`expected` is a float, "NaN", "EmptyState" (metric fails with EmptyStateException,
+Analyzer.scala:420-431), or {"DataTypeHistogram": [numNull, numFractional, numIntegral,
+numBoolean, numString]} for DataType (its HistogramMetric is DataTypeHistogram.toDistribution of
+that state, DataType.scala:98-114).  `needs` lists GPU-path capabilities a case depends on beyond
 numeric columns (e.g. a string predicate), so tests can route/skip with a reason.
 """
 import json
@@ -40,6 +42,36 @@ datasets = {
             "att1": ["f64", [1.0, 2.0, 3.0, 4.0, 5.0, 6.0]],
             "att2": ["f64", [0.0, 0.0, 0.0, 5.0, 6.0, 7.0]],
         }
+    },
+    "dfWithNegativeNumbers": {  # utils/FixtureSupport.scala:75-84
+        "columns": {
+            "item": ["utf8", ["1", "2", "3", "4"]],
+            "att1": ["utf8", ["-1", "-2", "-3", "-4"]],
+            "att2": ["utf8", ["-1.0", "-2.0", "-3.0", "-4.0"]],
+        }
+    },
+    "dfFractionalIntegralTypes": {  # utils/FixtureSupport.scala:110-117
+        "columns": {"item": ["utf8", ["1", "2"]], "att1": ["utf8", ["1.0", "1"]]}
+    },
+    "dfFractionalStringTypes": {  # utils/FixtureSupport.scala:119-126
+        "columns": {"item": ["utf8", ["1", "2"]], "att1": ["utf8", ["1.0", "a"]]}
+    },
+    "dfIntegralStringTypes": {  # utils/FixtureSupport.scala:128-135
+        "columns": {"item": ["utf8", ["1", "2"]], "att1": ["utf8", ["1", "a"]]}
+    },
+    "dfWithNumericValuesAsString": {  # AnalyzerTests.scala:331-332: getDfWithNumericValues, att1 cast to string
+        "columns": {"item": ["utf8", ["1", "2", "3", "4", "5", "6"]],
+                    "att1_str": ["utf8", ["1", "2", "3", "4", "5", "6"]]}
+    },
+    "dfWithNumericFractionalValuesAsString": {  # AnalyzerTests.scala:338-339: Double att1 cast to string
+        "columns": {"item": ["utf8", ["1", "2", "3", "4", "5", "6"]],
+                    "att1_str": ["utf8", ["1.0", "2.0", "3.0", "4.0", "5.0", "6.0"]]}
+    },
+    "dfBoolean": {  # AnalyzerTests.scala:395-398
+        "columns": {"item": ["utf8", ["1", "2"]], "att1": ["utf8", ["true", "false"]]}
+    },
+    "dfBooleanNullFractional": {  # AnalyzerTests.scala:407-412
+        "columns": {"item": ["utf8", ["1", "2", "3", "4"]], "att1": ["utf8", ["true", "false", N, "2.0"]]}
     },
     "dfWithUniqueColumns": {  # utils/FixtureSupport.scala:162-175
         "columns": {
@@ -138,6 +170,20 @@ cases = [
     ("dfWithNumericValues", ["Compliance", "nr9", "`att2` IS NULL OR (`att2` > -1.0 AND `att2` <= 7.0)", N], 1.0, "checks/CheckTest.scala:259-275", []),
     ("dfWithNumericValues", ["Compliance", "att1 is non-negative", "COALESCE(att1, 0.0) >= 0", N], 1.0, "predicate form Check.scala:676 (isNonNegative); expected value computed by hand", []),
     ("dfWithNumericValues", ["Compliance", "att2 is positive", "COALESCE(att2, 1.0) > 0", N], 0.5, "predicate form Check.scala:687 (isPositive); expected value computed by hand", []),
+    # DataType (AnalyzerTests.scala:295-421; the FloatType case :322-328 needs a float column: not a GPU type)
+    ("dfFull", ["DataType", "att1", N], {"DataTypeHistogram": [0, 0, 0, 0, 4]}, S + ":295-300", []),
+    ("dfWithNumericValues", ["DataType", "att1", N], {"DataTypeHistogram": [0, 0, 6, 0, 0]}, S + ":302-306", []),
+    ("dfWithNegativeNumbers", ["DataType", "att1", N], {"DataTypeHistogram": [0, 0, 4, 0, 0]}, S + ":308-312", []),
+    ("dfWithNegativeNumbers", ["DataType", "att2", N], {"DataTypeHistogram": [0, 4, 0, 0, 0]}, S + ":314-319", []),
+    ("dfWithNumericValuesAsString", ["DataType", "att1_str", N], {"DataTypeHistogram": [0, 0, 6, 0, 0]}, S + ":330-335", []),
+    ("dfWithNumericFractionalValuesAsString", ["DataType", "att1_str", N], {"DataTypeHistogram": [0, 6, 0, 0, 0]}, S + ":337-344", []),
+    ("dfFractionalIntegralTypes", ["DataType", "att1", N], {"DataTypeHistogram": [0, 1, 1, 0, 0]}, S + ":353-361", []),
+    ("dfFractionalStringTypes", ["DataType", "att1", N], {"DataTypeHistogram": [0, 1, 0, 0, 1]}, S + ":363-371", []),
+    ("dfIntegralStringTypes", ["DataType", "att1", N], {"DataTypeHistogram": [0, 0, 1, 0, 1]}, S + ":373-381", []),
+    ("dfWithUniqueColumns", ["DataType", "uniqueWithNulls", N], {"DataTypeHistogram": [1, 0, 5, 0, 0]}, S + ":383-391", []),
+    ("dfBoolean", ["DataType", "att1", N], {"DataTypeHistogram": [0, 0, 0, 2, 0]}, S + ":393-403", []),
+    ("dfBooleanNullFractional", ["DataType", "att1", N], {"DataTypeHistogram": [1, 1, 0, 2, 0]}, S + ":405-421", []),
+    ("dataWithNullColumns", ["DataType", "stringCol", N], {"DataTypeHistogram": [8, 0, 0, 0, 0]}, "analyzers/NullHandlingTests.scala:69-70", []),
     # incremental (analyzers/IncrementalAnalyzerTest.scala:49-99)
     ("incrementalInitial", ["Size", N], 3.0, "analyzers/IncrementalAnalyzerTest.scala:58", []),
     ("incrementalInitial", ["Completeness", "att1", N], 0.6666666666666666, "analyzers/IncrementalAnalyzerTest.scala:96", []),

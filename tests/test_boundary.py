@@ -51,7 +51,8 @@ def _py(state):
          O.StandardDeviationState: lambda s: S.StandardDeviationState(s.n, s.avg, s.m2),
          O.MinState: lambda s: S.MinState(s.minValue), O.MaxState: lambda s: S.MaxState(s.maxValue),
          O.CorrelationState: lambda s: S.CorrelationState(s.n, s.xAvg, s.yAvg, s.ck, s.xMk, s.yMk),
-         O.ApproxCountDistinctState: lambda s: S.ApproxCountDistinctState(tuple(s.words))}
+         O.ApproxCountDistinctState: lambda s: S.ApproxCountDistinctState(tuple(s.words)),
+         O.DataTypeHistogram: lambda s: S.DataTypeHistogram(*s.__dict__.values())}
     return m[type(state)](state)
 
 
@@ -69,6 +70,7 @@ def _rand_states(rng):
         (O.MaxState(float(rng.normal())), O.MaxState(float(rng.normal()))),
         (O.CorrelationState(10.0, 1.0, 2.0, 3.0, 4.0, 5.0), O.CorrelationState(3.0, -1.0, 0.5, 0.25, 1.0, 2.0)),
         (O.ApproxCountDistinctState(words()), O.ApproxCountDistinctState(words())),
+        (O.DataTypeHistogram(*rng.integers(0, 1 << 40, 5).tolist()), O.DataTypeHistogram(0, 1, 2, 3, 4)),
     ]
 
 
@@ -86,6 +88,8 @@ def test_state_sum_equals_oracle(dq):
         ref = a.sum(b)
         got = _py(a).sum(_py(b))
         _same(got, ref)
+        if isinstance(ref, O.DataTypeHistogram):
+            continue
         va, vb = ref.metricValue(), got.metricValue()
         assert (math.isnan(va) and math.isnan(vb)) or va == vb
 
@@ -121,7 +125,7 @@ def test_state_bytes_roundtrip_and_format(dq):
     ops = {O.NumMatches: L.OP_SIZE, O.NumMatchesAndCount: L.OP_COMPLIANCE, O.SumState: L.OP_SUM,
            O.MeanState: L.OP_MEAN, O.StandardDeviationState: L.OP_STDDEV, O.MinState: L.OP_MIN,
            O.MaxState: L.OP_MAX, O.CorrelationState: L.OP_CORRELATION,
-           O.ApproxCountDistinctState: L.OP_APPROX_COUNT_DISTINCT}
+           O.ApproxCountDistinctState: L.OP_APPROX_COUNT_DISTINCT, O.DataTypeHistogram: L.OP_DATATYPE}
     for a, _ in _rand_states(rng):
         op = ops[type(a)]
         c = state_to_c(_py(a), op)
@@ -141,7 +145,7 @@ def test_identifier_is_scala_murmur3(dq):
 
     for a in (dq.Size(), dq.Completeness("att1"), dq.Compliance("rule1", "att1 > 3", "att2 < 4"),
               dq.Correlation("a", "b"), dq.Mean("numericCol"), dq.ApproxCountDistinct("ü名"),
-              dq.Completeness("att1", "item IN ('1', '2')")):
+              dq.Completeness("att1", "item IN ('1', '2')"), dq.DataType("item")):
         assert int(identifier(a)) == O.murmur3_string_hash(str(a)), str(a)
 
 

@@ -54,6 +54,8 @@ def assert_state_close(prod, ref, scale=None):
         for k in a:
             x, y = a[k], b[k]
             assert x == y or (isinstance(x, float) and math.isnan(x) and math.isnan(y)), (name, k, x, y)
+    elif name == "DataTypeHistogram":
+        assert tuple(prod.__dict__.values()) == tuple(ref.__dict__.values()), (prod, ref)
     elif name == "ApproxCountDistinctState":
         assert tuple(prod.words) == tuple(ref.words)
     elif name == "SumState":
@@ -101,7 +103,12 @@ def test_reference_kats_fused_and_single(dq, kats):
                     assert metric.value.isFailure
                     assert isinstance(metric.value.failed, UnsupportedOnGpuPathException), metric
                     continue
-                if exp == "EmptyState":
+                if isinstance(exp, dict):  # DataType -> HistogramMetric(column, Success(toDistribution(hist)))
+                    from deequ_amd.analyzers import toDistribution
+
+                    want = toDistribution(dq.DataTypeHistogram(*exp["DataTypeHistogram"]))
+                    assert metric.value.get() == want, (c["source"], a, metric)
+                elif exp == "EmptyState":
                     assert metric.value.isFailure and isinstance(metric.value.failed, EmptyStateException), (c, metric)
                 elif exp == "NaN":
                     assert math.isnan(metric.value.get()), (c, metric)
@@ -529,3 +536,61 @@ def test_scan_orders_after_producer_on_torch_stream(dq):
         got = scan_states(t, [dq.Sum("x"), dq.Maximum("x")])
         assert got[dq.Sum("x")].sum_ == 1.5 * n
         assert got[dq.Maximum("x")].maxValue == 1.5
+
+
+DT_ATOMS = [b"", b"-", b"+", b" ", b"- ", b"+ ", b"0", b"7", b"12", b"007", b".", b"..", b"1.5", b"-3.25", b"+ 0.",
+            b"true", b"false", b"True", b"fals", b"truee", b"a", b"1e5", b"1 ", b" 1", b"--1", b"1\n", b"\xff",
+            b"\xd9\xa1", b"\x00", b"/", b":", b"-", b"9" * 27 + b".", b"1" * 28, b"1" * 29, b"-" + b"2" * 40,
+            b"3." + b"4" * 30, b"5" * 31 + b".6", b"12345678901234567890.1234567"]
+
+
+def _dt_string(rng) -> bytes:
+    k = rng.random()
+    if k < 0.5:
+        return DT_ATOMS[int(rng.integers(0, len(DT_ATOMS)))]
+    # signed / spaced digit strings with 0-2 dots at random places, lengths 0..40
+    sign = [b"", b"-", b"+", b"- ", b" "][int(rng.integers(0, 5))]
+    body = bytearray(rng.choice(np.frombuffer(b"0123456789", np.uint8), int(rng.integers(0, 40))).tobytes())
+    for _ in range(int(rng.integers(0, 3))):
+        if body:
+            body[int(rng.integers(0, len(body)))] = ord(".")
+    if rng.random() < 0.05 and body:
+        body[int(rng.integers(0, len(body)))] = int(rng.integers(0, 256))
+    return sign + bytes(body)
+
+
+@pytest.mark.parametrize("large", [False, True])
+@pytest.mark.parametrize("n", [1, 64, 513, 4099, 70_001])
+def test_datatype_vs_oracle(dq, n, large):
+    """DataType (StatefulDataType.scala:36-67) on strings of every class and length (the <= 28-byte
+    SWAR path and the byte path), alone and fused with ApproxCountDistinct, with and without `where`;
+    on f64 values around the Double.toString boundaries (1e-3, 1e7, +-0, NaN, +-inf) and on integral
+    columns -- bit-exact histograms vs the oracle."""
+    from deequ_amd.runner import scan_states
+    from deequ_amd.table import column_from_numpy, utf8_column
+
+    rng = np.random.default_rng(77 + n + int(large))
+    strs = [None if rng.random() < 0.1 else _dt_string(rng) for _ in range(n)]
+    pool = np.array([0.0, -0.0, 1e-3, np.nextafter(1e-3, 0), 9999999.999, 1e7, np.nextafter(1e7, 0), -5e-4,
+                     float("nan"), float("inf"), -float("inf"), 1.5, -2.75e12, 3e-300])
+    f = np.where(rng.random(n) < 0.5, pool[rng.integers(0, len(pool), n)], rng.normal(0, 1e4, n) * 10.0 ** rng.integers(-6, 9, n))
+    fv = rng.random(n) >= 0.1
+    a = rng.integers(-5, 5, n).astype(np.int64)
+    i32 = rng.integers(-(1 << 31), 1 << 31, n).astype(np.int32)
+    t = dq.Table([utf8_column("s", strs, large=large), utf8_column("u", strs, large=not large),
+                  column_from_numpy("f", "f64", f, fv), column_from_numpy("a", "i64", a, rng.random(n) >= 0.2),
+                  column_from_numpy("i", "i32", i32, np.ones(n, bool))])
+    analyzers = [dq.DataType("s"), dq.ApproxCountDistinct("s"), dq.DataType("s", "a > 0"),
+                 dq.DataType("u"),  # alone: the classify-only variant
+                 dq.DataType("f"), dq.DataType("f", "a >= 0"), dq.Mean("f"), dq.DataType("a"), dq.DataType("i"),
+                 dq.DataType("a", "a < 2")]
+    got = scan_states(t, analyzers)
+    host = {name: host_column(c, n) for name, c in t.columns.items()}
+    ocols = {name: O.OColumn(t.columns[name].dtype.replace("large_", ""), host[name][0], host[name][1])
+             for name in t.columns}
+    for an in analyzers:
+        ref = O.compute_state((type(an).__name__, an.column, an.where), ocols, n)
+        if type(an).__name__ == "DataType":
+            assert tuple(got[an].__dict__.values()) == tuple(ref.__dict__.values()), (an, got[an], ref)
+        else:
+            assert_state_close(got[an], ref, scale=float(np.abs(f[fv]).sum()))

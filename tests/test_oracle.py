@@ -22,8 +22,11 @@ def test_reference_kats(kats):
         ds = kats["datasets"][case["dataset"]]
         cols, n = oracle_columns(ds)
         st = O.compute_state(tuple(case["analyzer"]), cols, n, ds.get("partitions", 1))
-        got = "EmptyState" if st is None else st.metricValue()
         exp = case["expected"]
+        if isinstance(exp, dict):  # DataType: the histogram state itself
+            assert st == O.DataTypeHistogram(*exp["DataTypeHistogram"]), (case["source"], st)
+            continue
+        got = "EmptyState" if st is None else st.metricValue()
         if exp == "NaN":
             assert isinstance(got, float) and math.isnan(got), case
         else:
@@ -139,11 +142,26 @@ def test_c_oracle_equals_python_oracle(nparts):
     assert tuple(O.registers_to_words(regs.tolist())) == ref.words
 
 
+def test_datatype_classes():
+    """StatefulDataType.scala:36-38 patterns, whole-value match, first match wins."""
+    cases = {b"": 2, b"-": 2, b"+ ": 2, b"- 12": 2, b"007": 2, b".": 1, b"-.5": 1, b"+ 3.": 1, b"1.2.3": 4,
+             b"true": 3, b"false": 3, b"TRUE": 4, b"1\n": 4, b"1 ": 4, b" -1": 4, b"--1": 4, b"1e5": 4,
+             "\u0661".encode(): 4, b"\xff": 4, b"tru": 4, b"falsee": 4}
+    for v, k in cases.items():
+        assert O.datatype_class(v) == k, v
+    # Double.toString: plain decimal on [1e-3, 1e7) and for zero, else scientific / NaN / Infinity
+    for d, k in ((0.0, 1), (-0.0, 1), (1e-3, 1), (0.000999, 4), (9999999.5, 1), (1e7, 4), (-2.5, 1),
+                 (float("nan"), 4), (float("-inf"), 4), (1e300, 4)):
+        assert O.datatype_class(O.java_double_to_string(d).encode()) == k, d
+
+
 def test_state_bytes_and_identifier():
     # HdfsStateProvider images are Java DataOutputStream big-endian (StateProvider.scala:176-245)
     assert O.state_to_bytes(O.NumMatches(3)) == bytes.fromhex("0000000000000003")
     assert O.state_to_bytes(O.MeanState(1.0, 2))[:8] == bytes.fromhex("3ff0000000000000")
     img = O.state_to_bytes(O.ApproxCountDistinctState(tuple(range(52))))
     assert img[:4] == bytes.fromhex("000001a0") and len(img) == 420
+    img = O.state_to_bytes(O.DataTypeHistogram(1, 2, 3, 4, 5))
+    assert img[:4] == bytes.fromhex("00000028") and len(img) == 44 and img[-1] == 5
     # scala.util.hashing.MurmurHash3.stringHash("", 42) == avalanche(42 ^ 0)
     assert isinstance(O.murmur3_string_hash("Size(None)"), int)
