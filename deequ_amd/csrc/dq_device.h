@@ -80,7 +80,8 @@ struct alignas(16) ColPartial {
   int64_t count;        // selected rows (non-null AND where-true)
   int64_t nan_count;    // selected NaN values (F64)
   double fmin, fmax;    // min / max over selected non-NaN values (F64)
-  int64_t imin, imax;   // min / max (I64 / I32)
+  int64_t pinf_count;   // selected +inf values (F64; kept out of the moments, added back in dq_finish)
+  int64_t ninf_count;   // selected -inf values (F64)
   int64_t pad;
 };
 static_assert(sizeof(ColPartial) == 96, "ColPartial layout");

@@ -150,7 +150,7 @@ struct ColStats {
   double n, mean, m2, sum;
   int64_t isum, count, nan_count;
   double fmin, fmax;
-  int64_t imin, imax;
+  int64_t pinf, ninf;  // selected +-inf values of an F64 column (outside n / mean / m2 / sum)
 };
 
 __device__ __forceinline__ void stats_init(ColStats& s) {
@@ -158,7 +158,7 @@ __device__ __forceinline__ void stats_init(ColStats& s) {
   s.isum = 0; s.count = 0; s.nan_count = 0;
   s.fmin = __longlong_as_double(0x7FF0000000000000ll);   // +inf
   s.fmax = __longlong_as_double((long long)0xFFF0000000000000ull);  // -inf
-  s.imin = INT64_MAX; s.imax = INT64_MIN;
+  s.pinf = 0; s.ninf = 0;
 }
 
 // a <- a (+) b ; exact Chan/Welford combination (same algebra as StandardDeviationState.sum)
@@ -181,8 +181,8 @@ __device__ __forceinline__ void stats_merge(ColStats& a, const ColStats& b) {
   a.nan_count += b.nan_count;
   a.fmin = hw_min(a.fmin, b.fmin);
   a.fmax = hw_max(a.fmax, b.fmax);
-  a.imin = b.imin < a.imin ? b.imin : a.imin;
-  a.imax = b.imax > a.imax ? b.imax : a.imax;
+  a.pinf += b.pinf;
+  a.ninf += b.ninf;
 }
 
 __device__ __forceinline__ ColStats stats_shfl_xor(const ColStats& s, int m) {
@@ -191,19 +191,19 @@ __device__ __forceinline__ ColStats stats_shfl_xor(const ColStats& s, int m) {
   o.sum = __shfl_xor(s.sum, m);
   o.isum = __shfl_xor(s.isum, m); o.count = __shfl_xor(s.count, m); o.nan_count = __shfl_xor(s.nan_count, m);
   o.fmin = __shfl_xor(s.fmin, m); o.fmax = __shfl_xor(s.fmax, m);
-  o.imin = __shfl_xor(s.imin, m); o.imax = __shfl_xor(s.imax, m);
+  o.pinf = __shfl_xor(s.pinf, m); o.ninf = __shfl_xor(s.ninf, m);
   return o;
 }
 
 __device__ __forceinline__ void stats_store(ColPartial* p, const ColStats& s) {
   p->n = s.n; p->mean = s.mean; p->m2 = s.m2; p->sum = s.sum; p->isum = s.isum; p->count = s.count;
-  p->nan_count = s.nan_count; p->fmin = s.fmin; p->fmax = s.fmax; p->imin = s.imin; p->imax = s.imax;
+  p->nan_count = s.nan_count; p->fmin = s.fmin; p->fmax = s.fmax; p->pinf_count = s.pinf; p->ninf_count = s.ninf;
   p->pad = 0;
 }
 __device__ __forceinline__ ColStats stats_load(const ColPartial* p) {
   ColStats s;
   s.n = p->n; s.mean = p->mean; s.m2 = p->m2; s.sum = p->sum; s.isum = p->isum; s.count = p->count;
-  s.nan_count = p->nan_count; s.fmin = p->fmin; s.fmax = p->fmax; s.imin = p->imin; s.imax = p->imax;
+  s.nan_count = p->nan_count; s.fmin = p->fmin; s.fmax = p->fmax; s.pinf = p->pinf_count; s.ninf = p->ninf_count;
   return s;
 }
 
@@ -397,24 +397,27 @@ __device__ __forceinline__ void masked_moments(LaneMoments& a, double& lo, doubl
 
 // One 512-row block of a wave: x[j] the lane's value of row group j as a double, bits[j] its raw
 // 64-bit pattern (i32: sign-extended), m[j] the selection masks, nanm[j] the selected NaN rows (F64).
-// NANS (the block holds a selected NaN, rare): NaN rows hash as the canonical NaN (doubleToLongBits)
-// and stay out of min / max (Spark orders NaN above every value; the caller counts them).
+// NANS (the block holds a selected NaN or +-inf, rare): NaN rows hash as the canonical NaN
+// (doubleToLongBits) and stay out of min / max (Spark orders NaN above every value; the caller counts
+// them); +-inf rows (mm = m without them) stay out of the shifted moments -- x - shift would be inf - inf
+// for the rest of the lane -- and are counted by the caller: dq_finish adds them back into the sum
+// (Spark's sequential sum is then +-inf, or NaN with both signs) and the moments become NaN.
 template <int KIND, bool STATS, bool HLL, bool NANS>
 __device__ __forceinline__ void numeric_block(const double (&x)[8], const uint64_t (&bits)[8], const uint64_t (&m)[8],
-                                              const uint64_t (&nanm)[8], ColStats& s, LaneMoments& a, int32_t* regs,
-                                              int32_t& qmin) {
+                                              const uint64_t (&mm)[8], const uint64_t (&nanm)[8], ColStats& s,
+                                              LaneMoments& a, int32_t* regs, int32_t& qmin) {
   if (STATS) {
     // still-empty lanes take the block's first selected value as their shift (wave-uniform branch)
     if (__builtin_amdgcn_ballot_w64(s.n == 0.0 && a.k == 0) != 0) {
       double first = a.shift;
 #pragma unroll
-      for (int j = 7; j >= 0; --j) first = lane_bit(m[j]) ? x[j] : first;
+      for (int j = 7; j >= 0; --j) first = lane_bit(mm[j]) ? x[j] : first;
       if (s.n == 0.0 && a.k == 0) a.shift = first;
     }
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    if (STATS) masked_moments<KIND != CK_F64, NANS>(a, s.fmin, s.fmax, x[j], bits[j], m[j], m[j] & ~nanm[j]);
+    if (STATS) masked_moments<KIND != CK_F64, NANS>(a, s.fmin, s.fmax, x[j], bits[j], mm[j], m[j] & ~nanm[j]);
     if (HLL) {
       HllKey key;
       if (KIND == CK_I32) {
@@ -461,6 +464,7 @@ __device__ void numeric_range(const void* values, const uint32_t* validity, cons
   const __amdgpu_buffer_rsrc_t vr = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<T*>(v + row0), (short)0, (int)((row1 - row0) * (int64_t)sizeof(T)), 0x00020000);
   int64_t nan_w = 0;  // wave-uniform count of selected NaN values
+  int64_t pinf_w = 0, ninf_w = 0;  // ... of selected +inf / -inf values
   int64_t cnt_w = 0;  // wave-uniform count of selected rows (HLL-only variant)
   LaneMoments a{0.0, 0.0, 0.0, 0, 0};
   int32_t qmin = 0;
@@ -485,25 +489,40 @@ __device__ void numeric_range(const void* values, const uint32_t* validity, cons
       }
     }
     block_masks(validity, mask, base, row1, full, m);
-    uint64_t nan_any = 0;
+    uint64_t nf_any = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      nanm[j] = KIND == CK_F64 ? __builtin_amdgcn_ballot_w64(x[j] != x[j]) & m[j] : 0ull;
-      nan_any |= nanm[j];
+      // one v_cmp_class per value: NaN or +-inf
+      nanm[j] = KIND == CK_F64 ? __builtin_amdgcn_ballot_w64(!__builtin_isfinite(x[j])) & m[j] : 0ull;
+      nf_any |= nanm[j];
       if (!STATS) cnt_w += __builtin_popcountll(m[j]);
     }
-    if (KIND == CK_F64 && nan_any != 0) {
+    if (KIND == CK_F64 && nf_any != 0) {
+      uint64_t mm[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) nan_w += __builtin_popcountll(nanm[j]);
-      numeric_block<KIND, STATS, HLL, true>(x, bits, m, nanm, s, a, regs, qmin);
+      for (int j = 0; j < 8; ++j) {
+        const uint64_t nf = nanm[j];
+        nanm[j] = __builtin_amdgcn_ballot_w64(x[j] != x[j]) & m[j];
+        const uint64_t inf = nf & ~nanm[j], pinf = __builtin_amdgcn_ballot_w64(x[j] > 0.0) & inf;
+        nan_w += __builtin_popcountll(nanm[j]);
+        pinf_w += __builtin_popcountll(pinf);
+        ninf_w += __builtin_popcountll(inf & ~pinf);
+        mm[j] = STATS ? m[j] & ~inf : m[j];
+      }
+      numeric_block<KIND, STATS, HLL, true>(x, bits, m, mm, nanm, s, a, regs, qmin);
     } else {
-      numeric_block<KIND, STATS, HLL, false>(x, bits, m, nanm, s, a, regs, qmin);
+      numeric_block<KIND, STATS, HLL, false>(x, bits, m, m, nanm, s, a, regs, qmin);
     }
     if (STATS && (nb % kChunkBlocks) == kChunkBlocks - 1) moments_flush<KIND>(s, a);
   }
   if (STATS) moments_flush<KIND>(s, a);
   if (!STATS && lane == 0) s.count += cnt_w;
-  if (KIND == CK_F64 && lane == 0) s.nan_count += nan_w;
+  if (KIND == CK_F64 && lane == 0) {
+    s.nan_count += nan_w;
+    s.pinf += pinf_w;
+    s.ninf += ninf_w;
+    if (STATS) s.count += pinf_w + ninf_w;  // the moments' k counted only the finite / NaN rows
+  }
 }
 
 // ------------------------------------------------------------------------------------------

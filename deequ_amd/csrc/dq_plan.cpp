@@ -1031,6 +1031,15 @@ dq_status dq_finish(dq_plan* p, dq_state* out) {
 
   const int64_t rows = p->total_rows;
   const double nan = std::numeric_limits<double>::quiet_NaN();
+  const double inf = std::numeric_limits<double>::infinity();
+  // Spark's sequential fp64 sum: the finite / NaN part plus the +-inf values kept out of the moments
+  // (+inf and -inf together give NaN, as inf + -inf in any order)
+  auto f64_sum = [&](const ColPartial& c) {
+    double v = c.sum;
+    if (c.pinf_count > 0) v += inf;
+    if (c.ninf_count > 0) v += -inf;
+    return v;
+  };
   for (size_t i = 0; i < p->specs.size(); ++i) {
     const SpecOut& o = p->outs[i];
     dq_state& s = out[i];
@@ -1063,17 +1072,22 @@ dq_status dq_finish(dq_plan* p, dq_state* out) {
         else { s.u.ratio.count = rows; s.has_value[1] = 1; }
         break;
       case DQ_OP_SUM:
-        s.u.sum.sum = o.col_type == DQ_TYPE_F64 ? c->sum : (double)c->isum;
+        s.u.sum.sum = o.col_type == DQ_TYPE_F64 ? f64_sum(*c) : (double)c->isum;
         set1(c->count > 0);
         break;
       case DQ_OP_MEAN:
-        s.u.mean.sum = o.col_type == DQ_TYPE_F64 ? c->sum : (double)c->isum;
+        s.u.mean.sum = o.col_type == DQ_TYPE_F64 ? f64_sum(*c) : (double)c->isum;
         s.u.mean.count = c->count;
         s.has_value[0] = c->count > 0;
         s.has_value[1] = 1;  // count(...) is never NULL
         break;
       case DQ_OP_STDDEV:
         s.u.stddev.n = c->n; s.u.stddev.avg = c->mean; s.u.stddev.m2 = c->m2;
+        if (c->pinf_count + c->ninf_count > 0) {
+          // an infinite value makes Spark's m2 NaN (delta * (x - avg) = inf * (inf - inf)) and its avg
+          // inf or NaN depending on the row order; the metric sqrt(m2 / n) is NaN either way
+          s.u.stddev.n = (double)c->count; s.u.stddev.avg = nan; s.u.stddev.m2 = nan;
+        }
         set1(true);  // the struct is never NULL; n == 0 -> None (StandardDeviation.scala:46-47)
         break;
       case DQ_OP_MIN:

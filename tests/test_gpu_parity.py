@@ -275,6 +275,45 @@ def test_nan_min_max_and_hash(dq):
     assert math.isnan(s2[dq.Minimum("y")].minValue) and math.isnan(s2[dq.Maximum("y")].maxValue)
 
 
+@pytest.mark.parametrize("kinds", ["pinf", "ninf", "both", "nan_inf"])
+@pytest.mark.parametrize("n", [1, 5, 300, 4099, 70_001])
+def test_infinities_vs_oracle(dq, n, kinds):
+    """+-inf values: Sum / Mean are Spark's sequential sum (+-inf, NaN with both signs or any NaN),
+    Min / Max include them, StdDev's metric is NaN (its m2 is NaN in Spark; its avg is order-dependent:
+    inf or NaN), counts and HLL registers stay exact."""
+    from deequ_amd.runner import scan_states
+    from deequ_amd.table import column_from_numpy
+
+    rng = np.random.default_rng(4000 + n + len(kinds))
+    x = rng.normal(10.0, 3.0, n)
+    k = max(1, n // 500)
+    pos = rng.choice(n, size=min(n, 3 * k), replace=False)
+    specials = {"pinf": [np.inf], "ninf": [-np.inf], "both": [np.inf, -np.inf], "nan_inf": [np.inf, np.nan]}[kinds]
+    x[pos] = np.array(specials)[rng.integers(0, len(specials), len(pos))]
+    valid = rng.random(n) >= 0.1
+    valid[pos[0]] = True
+    t = dq.Table([column_from_numpy("x", "f64", x, valid)])
+    an = [dq.Sum("x"), dq.Mean("x"), dq.Minimum("x"), dq.Maximum("x"), dq.StandardDeviation("x"),
+          dq.ApproxCountDistinct("x"), dq.Completeness("x")]
+    got = scan_states(t, an)
+    cols = {"x": O.OColumn("f64", x, valid)}
+
+    def same(a, b):
+        return (math.isnan(a) and math.isnan(b)) or a == b
+
+    for a in an:
+        name = type(a).__name__
+        ref = O.compute_state((name, "x", None), cols, n)
+        g = got[a]
+        if name == "StandardDeviation":
+            assert g.n == ref.n and math.isnan(g.metricValue()) and math.isnan(ref.metricValue()), (g, ref)
+        elif name in ("Sum", "Mean") and not math.isfinite(ref.sum_):
+            assert same(g.sum_, ref.sum_), (a, g, ref)
+            assert name == "Sum" or g.count == ref.count
+        else:
+            assert_state_close(g, ref, scale=float(np.abs(x[valid & np.isfinite(x)]).sum()))
+
+
 # ---------------------------------------------------------------------------------------------
 # 3. predicates (Compliance / where) vs the oracle's independent SQL evaluator
 # ---------------------------------------------------------------------------------------------
@@ -592,5 +631,8 @@ def test_datatype_vs_oracle(dq, n, large):
         ref = O.compute_state((type(an).__name__, an.column, an.where), ocols, n)
         if type(an).__name__ == "DataType":
             assert tuple(got[an].__dict__.values()) == tuple(ref.__dict__.values()), (an, got[an], ref)
-        else:
-            assert_state_close(got[an], ref, scale=float(np.abs(f[fv]).sum()))
+        elif math.isfinite(ref.sum_):
+            assert_state_close(got[an], ref, scale=float(np.abs(f[fv & np.isfinite(f)]).sum()))
+        else:  # +-inf / NaN in the column: Spark's sum is +-inf or NaN
+            g = got[an]
+            assert g.count == ref.count and ((math.isnan(g.sum_) and math.isnan(ref.sum_)) or g.sum_ == ref.sum_)
