@@ -6,7 +6,8 @@ is the host-side mirror of the reference's analyzer / state / runner API over th
 """
 from ._lib import DQError, lib  # noqa: F401  (fails loudly if libdqscan.so is missing)
 from .analyzers import (ApproxCountDistinct, Completeness, Compliance, Correlation, DataType,  # noqa: F401
-                        DataTypeInstances, Maximum, Mean, Minimum, Size, StandardDeviation, Sum)
+                        DataTypeInstances, Maximum, Mean, Minimum, PatternMatch, Patterns, Size, StandardDeviation,
+                        Sum)
 from .metrics import DoubleMetric, Distribution, DistributionValue, Entity, HistogramMetric  # noqa: F401
 from .runner import AnalysisRunner, AnalyzerContext  # noqa: F401
 from .state_provider import HdfsStateProvider, InMemoryStateProvider  # noqa: F401

@@ -38,6 +38,7 @@ OP_MAX = 8
 OP_CORRELATION = 9
 OP_APPROX_COUNT_DISTINCT = 10
 OP_DATATYPE = 11
+OP_PATTERN_MATCH = 12
 
 PRED_COLUMN = 1
 PRED_LIT_INT = 2
@@ -52,6 +53,10 @@ PRED_NOT = 10
 PRED_IS_NULL = 11
 PRED_IS_NOT_NULL = 12
 PRED_COALESCE = 13
+PRED_REGEX = 14
+
+REGEX_RLIKE = 0             # col RLIKE p: NULL on NULL, find()
+REGEX_EXTRACT_NONEMPTY = 1  # regexp_extract(col, p, 0) != '' as PatternMatch builds it: FALSE on NULL
 
 CMP_LT, CMP_LE, CMP_GT, CMP_GE, CMP_EQ, CMP_NE = 1, 2, 3, 4, 5, 6
 
@@ -146,6 +151,13 @@ def _load():
     L.dq_plan_create.restype = c.c_int32
     L.dq_plan_create.argtypes = [P(AnalyzerSpec), c.c_int32, P(ColumnDesc), c.c_int32, P(PredNode), c.c_int32,
                                  c.c_int32, P(c.c_void_p)]
+    L.dq_plan_create_ex.restype = c.c_int32
+    L.dq_plan_create_ex.argtypes = [P(AnalyzerSpec), c.c_int32, P(ColumnDesc), c.c_int32, P(PredNode), c.c_int32,
+                                    P(c.c_char_p), c.c_int32, c.c_int32, P(c.c_void_p)]
+    L.dq_regex_info.restype = c.c_int32
+    L.dq_regex_info.argtypes = [c.c_char_p, c.c_int32, P(c.c_int32), P(c.c_int32)]
+    L.dq_regex_match_host.restype = c.c_int32
+    L.dq_regex_match_host.argtypes = [c.c_char_p, c.c_int32, c.c_void_p, c.c_void_p, c.c_int64, c.c_void_p]
     L.dq_plan_set_stream.restype = c.c_int32
     L.dq_plan_set_stream.argtypes = [c.c_void_p, c.c_void_p]
     L.dq_scan.restype = c.c_int32
@@ -191,7 +203,8 @@ lib = _load()
 
 # every symbol include/dqscan.h declares (checked by tests/test_boundary.py)
 EXPORTED = [
-    "dq_abi_version", "dq_last_error", "dq_plan_create", "dq_plan_set_stream", "dq_scan", "dq_finish",
+    "dq_abi_version", "dq_last_error", "dq_plan_create", "dq_plan_create_ex", "dq_regex_info", "dq_regex_match_host",
+    "dq_plan_set_stream", "dq_scan", "dq_finish",
     "dq_plan_reset", "dq_plan_destroy", "dq_plan_bytes_per_row_x1000", "dq_plan_num_launches",
     "dq_plan_enable_timing", "dq_plan_kernel_time", "dq_plan_variant_bytes_per_row_x1000",
     "dq_state_merge", "dq_state_combine", "dq_state_is_defined", "dq_state_metric", "dq_hll_estimate",

@@ -332,6 +332,50 @@ class Compliance(Analyzer):  # Compliance.scala:37-53 (no additional preconditio
         return (L.OP_COMPLIANCE, -1, -1, b.pred(self.predicate), b.pred(self.where))
 
 
+class PatternMatch(_ColumnAnalyzer):  # PatternMatch.scala:37-56
+    """Fraction of rows whose value contains a match of `pattern` (java.util.regex find()):
+    sum(CASE WHEN where THEN (regexp_extract(column, pattern, 0) != '' ? 1 : 0) END) over
+    conditionalCount(where).  A NULL value counts as 0; state NumMatchesAndCount.  The pattern is
+    compiled into a byte-level search DFA walked on the GPU (deequ_amd/csrc/dq_regex.cpp)."""
+    name = "PatternMatch"
+    OP = L.OP_PATTERN_MATCH
+    numeric = False
+
+    def __init__(self, column: str, pattern, where: Optional[str] = None):
+        super().__init__(column, where)
+        self.pattern = pattern if isinstance(pattern, str) else pattern.pattern  # scala Regex / re.Pattern
+
+    def _fields(self):
+        return (self.column, self.pattern, self.where)
+
+    def _show(self):
+        return (self.column, self.pattern, ("opt", self.where))
+
+    def _lower(self, b):
+        from .predicates import UnsupportedPredicate
+        from .table import DTYPES
+
+        col = b.col(self.column)
+        if DTYPES[b.by_name[self.column][1]] not in (L.TYPE_UTF8, L.TYPE_LARGE_UTF8):
+            raise UnsupportedPredicate(f"PatternMatch on non-string column {self.column} (Spark casts it to string)")
+        root = b.pool.add_regex(col, self.pattern, L.REGEX_EXTRACT_NONEMPTY)
+        return (L.OP_PATTERN_MATCH, col, -1, root, b.pred(self.where))
+
+
+class Patterns:  # PatternMatch.scala:58-74
+    # http://emailregex.com
+    EMAIL = (r"""(?:[a-z0-9!#$%&'*+/=?^_`{|}~-]+(?:\.[a-z0-9!#$%&'*+/=?^_`{|}~-]+)*|"(?:[\x01-\x08\x0b\x0c\x0e-\x1f\x21\x23-\x5b\x5d-\x7f]|\\[\x01-\x09\x0b\x0c\x0e-\x7f])*")"""
+             r"""@(?:(?:[a-z0-9](?:[a-z0-9-]*[a-z0-9])?\.)+[a-z0-9](?:[a-z0-9-]*[a-z0-9])?|\[(?:(?:25[0-5]|2[0-4][0-9]|[01]?[0-9][0-9]?)\.){3}"""
+             r"""(?:25[0-5]|2[0-4][0-9]|[01]?[0-9][0-9]?|[a-z0-9-]*[a-z0-9]:(?:[\x01-\x08\x0b\x0c\x0e-\x1f\x21-\x5a\x53-\x7f]|\\[\x01-\x09\x0b\x0c\x0e-\x7f])+)\])""")
+    # https://mathiasbynens.be/demo/url-regex stephenhay
+    URL = r"""(https?|ftp)://[^\s/$.?#].[^\s]*"""
+    # look-ahead / backreference / \b: outside the GPU regex subset (UnsupportedPredicate -> fallback)
+    SOCIAL_SECURITY_NUMBER_US = (r"""((?!219-09-9999|078-05-1120)(?!666|000|9\d{2})\d{3}-(?!00)\d{2}-(?!0{4})\d{4})|"""
+                                 r"""((?!219 09 9999|078 05 1120)(?!666|000|9\d{2})\d{3} (?!00)\d{2} (?!0{4})\d{4})|"""
+                                 r"""((?!219099999|078051120)(?!666|000|9\d{2})\d{3}(?!00)\d{2}(?!0{4})\d{4})""")
+    CREDITCARD = (r"""\b(?:3[47]\d{2}([\ \-]?)\d{6}\1\d|(?:(?:4\d|5[1-5]|65)\d{2}|6011)([\ \-]?)\d{4}\2\d{4}\2)\d{4}\b""")
+
+
 class Correlation(Analyzer):  # Correlation.scala:65-105
     name = "Correlation"
     entity = Entity.Mutlicolumn

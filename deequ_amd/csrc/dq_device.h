@@ -27,6 +27,7 @@ constexpr int kMaxRoots = 32;
 constexpr int kMaxCounters = 32;
 constexpr int kMaxInstr = 96;
 constexpr int kPredStack = 16;              // predicate pass: operand stack depth
+constexpr int kMaxRegexWords = 32768;       // compiled regex DFAs of one plan (64 KB of LDS)
 
 // column kinds seen by the kernels
 enum ColKind : int32_t { CK_F64 = 1, CK_I64 = 2, CK_I32 = 3, CK_UTF8 = 4, CK_LUTF8 = 5 };
@@ -106,6 +107,8 @@ enum PredOp : int32_t {
   PO_OR = 6,
   PO_NOT = 7,
   PO_STORE = 8,        // pop into root slot `slot`
+  PO_ATOM_REGEX = 9,   // search DFA (lit_i = word offset in PredProgram::regex) over UTF8 column col_a;
+                       // NULL value -> null_res (RLIKE: NULL, PatternMatch: FALSE)
 };
 enum CmpOp : int32_t { C_LT = 1, C_LE = 2, C_GT = 3, C_GE = 4, C_EQ = 5, C_NE = 6, C_FALSE = 7, C_TRUE = 8 };
 enum CmpType : int32_t { CT_INT = 1, CT_DBL = 2 };
@@ -132,6 +135,9 @@ struct PredCounter {
 };
 
 struct PredProgram {
+  const uint16_t* regex;           // device: concatenated DFAs (n_states, n_classes, start, flags,
+                                   // cls[256], acc_end[n_states], trans[n_states][n_classes])
+  int32_t regex_words;             // its length (uint16 words); staged into LDS by dq_pred_scan
   int32_t n_instr;
   int32_t n_counters;
   int32_t n_bitmaps;

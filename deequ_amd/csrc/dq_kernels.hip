@@ -1143,6 +1143,51 @@ __device__ __forceinline__ void pred_atom_cmp(const PredInstr& ins, const AtomBu
   wn = ~vb | (~va & nr_null);
 }
 
+// One ATOM_REGEX for a block (PatternMatch.scala:48-49 / RLIKE): lane l walks the search DFA (staged in
+// LDS) over the UTF-8 bytes of rows base + 64 j + l, four bytes per aligned dword load; the walk stops
+// in the dead (0) or sticky-accept (1) state.  Rows past row1 and NULL rows are masked by the caller's
+// validity / in-range words.  The aligned dword holding a value byte never leaves the value's page.
+__device__ __forceinline__ void pred_atom_regex(const PredInstr& ins, const uint16_t* __restrict__ dfa,
+                                                const uint8_t* __restrict__ bytes, const void* __restrict__ offs,
+                                                int64_t row1, int64_t base, int lane, uint32_t va, uint32_t& wt,
+                                                uint32_t& wn) {
+  const int ns = dfa[0], nc = dfa[1], start = dfa[2];
+  const uint16_t* cls = dfa + 4;
+  const uint16_t* acc = cls + 256;
+  const uint16_t* tr = acc + ns;
+  const bool large = ins.kind_a == CK_LUTF8;
+  uint32_t wc = 0;
+  for (int j = 0; j < 8; ++j) {
+    const int64_t r = base + 64 * j + lane;
+    bool m = false;
+    if (r < row1) {
+      int64_t o0, o1;
+      if (large) {
+        o0 = reinterpret_cast<const int64_t*>(offs)[r];
+        o1 = reinterpret_cast<const int64_t*>(offs)[r + 1];
+      } else {
+        o0 = reinterpret_cast<const int32_t*>(offs)[r];
+        o1 = reinterpret_cast<const int32_t*>(offs)[r + 1];
+      }
+      int st = start;
+      int64_t i = o0;
+      while (i < o1 && st >= 2) {
+        const uint32_t w = *reinterpret_cast<const uint32_t*>(bytes + (i & ~(int64_t)3));
+        const int64_t end = (i | 3) + 1 < o1 ? (i | 3) + 1 : o1;
+        do {
+          st = tr[st * nc + cls[(w >> (8 * (i & 3))) & 0xFFu]];
+          ++i;
+        } while (i < end && st >= 2);
+      }
+      m = acc[st] != 0;
+    }
+    const uint64_t cm = __builtin_amdgcn_ballot_w64(m);
+    if ((lane >> 1) == j) wc = (lane & 1) ? (uint32_t)(cm >> 32) : (uint32_t)cm;
+  }
+  wt = va & wc;
+  wn = ins.null_res == NR_NULL ? ~va : 0u;
+}
+
 __global__ __launch_bounds__(kBlock) void dq_pred_scan(const PredProgram* __restrict__ prog_g, ScanCols cols,
                                                        ScanBitmaps bm, int64_t n_rows, int64_t rows_per_range,
                                                        PredPartial* __restrict__ acc) {
@@ -1156,6 +1201,12 @@ __global__ __launch_bounds__(kBlock) void dq_pred_scan(const PredProgram* __rest
   const int n_instr = prog.n_instr, n_counters = prog.n_counters, n_bitmaps = prog.n_bitmaps, n_loads = prog.n_loads;
   if (wl) {
     for (int c = 0; c < n_counters; ++c) { S.ct[(c) * 16 + lane] = 0; S.cn[(c) * 16 + lane] = 0; }
+  }
+  // compiled regex DFAs -> LDS after the waves' scratch
+  uint16_t* dfa_lds = reinterpret_cast<uint16_t*>(pred_lds + kWaves * wave_words);
+  if (prog.regex_words > 0) {
+    for (int k = threadIdx.x; k < prog.regex_words; k += kBlock) dfa_lds[k] = prog.regex[k];
+    __syncthreads();
   }
   const int64_t row0 = (int64_t)blockIdx.x * rows_per_range;
   int64_t row1 = row0 + rows_per_range;
@@ -1187,7 +1238,7 @@ __global__ __launch_bounds__(kBlock) void dq_pred_scan(const PredProgram* __rest
     for (int i = 0; i < n_instr; ++i) {
       const PredInstr& ins = prog.instr[i];
       const int op = ins.op;
-      if (op == PO_ATOM_CMP || op == PO_ATOM_ISNULL || op == PO_ATOM_NOTNULL) {
+      if (op == PO_ATOM_CMP || op == PO_ATOM_ISNULL || op == PO_ATOM_NOTNULL || op == PO_ATOM_REGEX) {
         // next atom: the following one of this block, else the first of the next block
         const int kn = k + 1 < n_loads ? k + 1 : 0;
         const int64_t bn = k + 1 < n_loads ? base : base + kRowsPerIter;
@@ -1198,6 +1249,10 @@ __global__ __launch_bounds__(kBlock) void dq_pred_scan(const PredProgram* __rest
         if (op == PO_ATOM_CMP) {
           if ((g & 1u) == 0) pred_atom_cmp(ins, B0, lane, wt, wn);
           else pred_atom_cmp(ins, B1, lane, wt, wn);
+        } else if (op == PO_ATOM_REGEX) {
+          const uint32_t va = (g & 1u) ? B1.va : B0.va;
+          pred_atom_regex(ins, dfa_lds + ins.lit_i, reinterpret_cast<const uint8_t*>(cols.values[ins.col_a]),
+                          cols.offsets[ins.col_a], row1, base, lane, va, wt, wn);
         } else {
           const uint32_t va = (g & 1u) ? B1.va : B0.va;
           wt = op == PO_ATOM_ISNULL ? ~va : va;

@@ -23,6 +23,7 @@
 
 #include "dq_device.h"
 #include "dq_internal.h"
+#include "dq_regex.h"
 
 namespace dq {
 
@@ -174,6 +175,9 @@ struct Lowering {
   int32_t n_pred;
   const std::vector<dq_column_desc>* schema;
   std::vector<PredInstr> out;
+  const std::vector<std::string>* patterns = nullptr;
+  std::vector<uint16_t>* regex_blob = nullptr;              // concatenated DFAs (dq_regex.h layout)
+  std::map<std::pair<int64_t, int32_t>, int64_t> regex_at;  // (pattern, mode) -> blob word offset
 
   dq_status lit_of(int32_t idx, Lit& l) {
     const dq_pred_node& n = pool[idx];
@@ -285,6 +289,37 @@ struct Lowering {
         out.push_back(p);
         return DQ_OK;
       }
+      case DQ_PRED_REGEX: {  // PatternMatch.scala:48-49 / RLIKE on a string column
+        if (dq_status s = check_idx(n.a)) return s;
+        const dq_pred_node& c = pool[n.a];
+        if (c.kind != DQ_PRED_COLUMN) return set_error(DQ_E_UNSUPPORTED, "regex on a non-column expression");
+        if (dq_status s = check_col(c.a)) return s;
+        const int32_t t = (*schema)[c.a].type;
+        if (t != DQ_TYPE_UTF8 && t != DQ_TYPE_LARGE_UTF8)
+          return set_error(DQ_E_UNSUPPORTED, "regex on a non-string column (%d)", c.a);
+        if (n.cmp != DQ_REGEX_RLIKE && n.cmp != DQ_REGEX_EXTRACT_NONEMPTY)
+          return set_error(DQ_E_INVALID, "regex mode %d", n.cmp);
+        if (!patterns || n.i64 < 0 || n.i64 >= (int64_t)patterns->size())
+          return set_error(DQ_E_INVALID, "regex pattern index %lld out of range", (long long)n.i64);
+        auto key = std::make_pair(n.i64, n.cmp);
+        auto it = regex_at.find(key);
+        int64_t off;
+        if (it != regex_at.end()) {
+          off = it->second;
+        } else {
+          RegexDfa d;
+          if (dq_status s = regex_compile((*patterns)[n.i64].c_str(), n.cmp, d)) return s;
+          off = (int64_t)regex_blob->size();
+          regex_serialize(d, *regex_blob);
+          regex_at[key] = off;
+        }
+        PredInstr p{};
+        p.op = PO_ATOM_REGEX; p.col_a = c.a; p.col_b = -1; p.kind_a = kind_of(t);
+        p.lit_i = off;
+        p.null_res = n.cmp == DQ_REGEX_RLIKE ? NR_NULL : NR_FALSE;
+        out.push_back(p);
+        return DQ_OK;
+      }
       case DQ_PRED_IS_NULL:
       case DQ_PRED_IS_NOT_NULL: {
         if (dq_status s = check_idx(n.a)) return s;
@@ -363,7 +398,8 @@ static std::string canon(const dq_pred_node* pool, int32_t n_pred, int32_t idx, 
   if (n.kind == DQ_PRED_COLUMN) s += ":c" + std::to_string(n.a);
   else {
     if (n.kind == DQ_PRED_CMP || n.kind == DQ_PRED_AND || n.kind == DQ_PRED_OR || n.kind == DQ_PRED_NOT ||
-        n.kind == DQ_PRED_IS_NULL || n.kind == DQ_PRED_IS_NOT_NULL || n.kind == DQ_PRED_COALESCE)
+        n.kind == DQ_PRED_IS_NULL || n.kind == DQ_PRED_IS_NOT_NULL || n.kind == DQ_PRED_COALESCE ||
+        n.kind == DQ_PRED_REGEX)
       s += canon(pool, n_pred, n.a, depth + 1);
     if (n.kind == DQ_PRED_CMP || n.kind == DQ_PRED_AND || n.kind == DQ_PRED_OR || n.kind == DQ_PRED_COALESCE)
       s += canon(pool, n_pred, n.b, depth + 1);
@@ -393,6 +429,9 @@ struct dq_plan {
   std::vector<hipEvent_t> side_done;
   hipEvent_t fork_ev = nullptr;
   PredProgram prog{};
+  std::vector<std::string> patterns;      // DQ_PRED_REGEX patterns (dq_plan_create_ex)
+  std::vector<uint16_t> regex_blob;       // their compiled DFAs
+  uint16_t* d_regex = nullptr;
   int32_t n_hll = 0;
   bool has_pred = false;
 
@@ -475,7 +514,7 @@ static dq_status free_plan_mem(dq_plan* p) {
   for (hipEvent_t e : p->ev_pool) (void)hipEventDestroy(e);
   p->ev_pool.clear();
   void* ptrs[] = {p->d_col_tasks, p->d_pair_tasks, p->d_pair_groups, p->d_prog, p->d_col_part, p->d_pair_part,
-                  p->d_pred_part, p->d_col_acc, p->d_hll_acc, p->d_pair_acc, p->d_pred_acc};
+                  p->d_pred_part, p->d_col_acc, p->d_hll_acc, p->d_pair_acc, p->d_pred_acc, p->d_regex};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   for (int i = 0; i < kMaxWhere; ++i)
@@ -511,6 +550,8 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
   struct Needs { bool stats = false, hll = false, dtype = false; };
   std::vector<Needs> col_task_needs;
   Lowering low{pool, n_pred, &p->schema, {}};
+  low.patterns = &p->patterns;
+  low.regex_blob = &p->regex_blob;
 
   auto root = [&](int32_t node, int32_t& slot) -> dq_status {
     if (node < 0 || node >= n_pred) return set_error(DQ_E_INVALID, "predicate root %d out of range", node);
@@ -609,9 +650,15 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
         }
         break;
       }
-      case DQ_OP_COMPLIANCE: {
+      case DQ_OP_COMPLIANCE:
+      case DQ_OP_PATTERN_MATCH: {  // PatternMatch = Compliance over the regexp_extract(...) != '' atom
         int32_t ps;
         if (s.pred_root < 0) return set_error(DQ_E_INVALID, "spec %zu: Compliance without predicate", i);
+        if (s.op == DQ_OP_PATTERN_MATCH) {
+          if (s.pred_root >= n_pred || pool[s.pred_root].kind != DQ_PRED_REGEX ||
+              pool[s.pred_root].cmp != DQ_REGEX_EXTRACT_NONEMPTY)
+            return set_error(DQ_E_INVALID, "spec %zu: PatternMatch needs a DQ_PRED_REGEX root (extract mode)", i);
+        }
         if (dq_status st = root(s.pred_root, ps)) return st;
         if (dq_status st = counter(ps, where_slot, o.ctr_a)) return st;
         if (where_slot >= 0)
@@ -777,7 +824,8 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
     prog.n_instr = (int32_t)code.size();
     std::copy(code.begin(), code.end(), prog.instr);
     for (int32_t i = 0; i < prog.n_instr; ++i)
-      if (prog.instr[i].op == PO_ATOM_CMP || prog.instr[i].op == PO_ATOM_ISNULL || prog.instr[i].op == PO_ATOM_NOTNULL)
+      if (prog.instr[i].op == PO_ATOM_CMP || prog.instr[i].op == PO_ATOM_ISNULL || prog.instr[i].op == PO_ATOM_NOTNULL ||
+          prog.instr[i].op == PO_ATOM_REGEX)
         prog.load_instr[prog.n_loads++] = (int16_t)i;
     prog.n_counters = (int32_t)counter_of.size();
     for (auto& kv : counter_of) prog.counters[kv.second] = PredCounter{kv.first.first, kv.first.second};
@@ -799,7 +847,7 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
     const PredInstr& ins = prog.instr[i];
     if (ins.col_a >= 0) {
       need_validity[ins.col_a] = 1;
-      if (ins.op == PO_ATOM_CMP) need_values[ins.col_a] = 1;
+      if (ins.op == PO_ATOM_CMP || ins.op == PO_ATOM_REGEX) need_values[ins.col_a] = 1;  // regex: offsets
     }
     if (ins.col_b >= 0) { need_validity[ins.col_b] = 1; need_values[ins.col_b] = 1; }
   }
@@ -831,6 +879,16 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
   if (!p->pair_groups.empty())
     HIP_TRY(hipMemcpyAsync(p->d_pair_groups, p->pair_groups.data(), p->pair_groups.size() * sizeof(PairGroup),
                            hipMemcpyHostToDevice, p->stream));
+  if (p->regex_blob.size() > (size_t)kMaxRegexWords)
+    return set_error(DQ_E_UNSUPPORTED, "compiled patterns need %zu KB (LDS budget %d KB)",
+                     p->regex_blob.size() * 2 / 1024, kMaxRegexWords * 2 / 1024);
+  if (!p->regex_blob.empty()) {
+    if (dq_status s = dmalloc(&p->d_regex, p->regex_blob.size() * sizeof(uint16_t))) return s;
+    HIP_TRY(hipMemcpyAsync(p->d_regex, p->regex_blob.data(), p->regex_blob.size() * sizeof(uint16_t),
+                           hipMemcpyHostToDevice, p->stream));
+  }
+  p->prog.regex = p->d_regex;
+  p->prog.regex_words = (int32_t)p->regex_blob.size();
   HIP_TRY(hipMemcpyAsync(p->d_prog, &p->prog, sizeof(PredProgram), hipMemcpyHostToDevice, p->stream));
   if (dq_status s = reset_acc(p)) return s;
   HIP_TRY(hipStreamSynchronize(p->stream));
@@ -858,7 +916,16 @@ const char* dq_last_error(void) { return g_err; }
 
 dq_status dq_plan_create(const dq_analyzer_spec* specs, int32_t n_specs, const dq_column_desc* schema, int32_t n_cols,
                          const dq_pred_node* pred_pool, int32_t n_pred, int32_t device, dq_plan** out) {
+  return dq_plan_create_ex(specs, n_specs, schema, n_cols, pred_pool, n_pred, nullptr, 0, device, out);
+}
+
+dq_status dq_plan_create_ex(const dq_analyzer_spec* specs, int32_t n_specs, const dq_column_desc* schema,
+                            int32_t n_cols, const dq_pred_node* pred_pool, int32_t n_pred,
+                            const char* const* patterns, int32_t n_patterns, int32_t device, dq_plan** out) {
   if (!out) return set_error(DQ_E_INVALID, "dq_plan_create: out is NULL");
+  if (n_patterns < 0 || (n_patterns > 0 && !patterns)) return set_error(DQ_E_INVALID, "dq_plan_create: bad patterns");
+  for (int32_t k = 0; k < n_patterns; ++k)
+    if (!patterns[k]) return set_error(DQ_E_INVALID, "dq_plan_create: pattern %d is NULL", k);
   *out = nullptr;
   if (n_specs < 0 || (n_specs > 0 && !specs)) return set_error(DQ_E_INVALID, "dq_plan_create: bad specs");
   if (n_cols < 0 || n_cols > kMaxCols || (n_cols > 0 && !schema))
@@ -875,6 +942,7 @@ dq_status dq_plan_create(const dq_analyzer_spec* specs, int32_t n_specs, const d
   p->device = device;
   p->schema.assign(schema, schema + n_cols);
   p->specs.assign(specs, specs + n_specs);
+  for (int32_t k = 0; k < n_patterns; ++k) p->patterns.emplace_back(patterns[k]);
   hipError_t e = hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking);
   if (e != hipSuccess) {
     delete p;
@@ -969,7 +1037,8 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
 
   if (p->has_pred)
     if (dq_status s = timed(p, 0, p->stream, [&] {
-          const int32_t lds = kWaves * 128 * (p->prog.stack_depth + p->prog.n_roots + p->prog.n_counters);
+          const int32_t lds = kWaves * 128 * (p->prog.stack_depth + p->prog.n_roots + p->prog.n_counters) +
+                              ((p->prog.regex_words * 2 + 15) & ~15);
           return launch_pred_scan(p->d_prog, sc, bm, n_rows, rpr_pred, nr_pred, p->d_pred_acc, lds, p->stream);
         }))
       return s;
@@ -1066,6 +1135,7 @@ dq_status dq_finish(dq_plan* p, dq_state* out) {
         }
         break;
       case DQ_OP_COMPLIANCE:
+      case DQ_OP_PATTERN_MATCH:
         s.u.ratio.num_matches = pred.t[o.ctr_a];
         s.has_value[0] = pred.nn[o.ctr_a] > 0;
         if (o.has_where) { s.u.ratio.count = pred.t[o.ctr_b]; s.has_value[1] = pred.nn[o.ctr_b] > 0; }

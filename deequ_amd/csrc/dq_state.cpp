@@ -201,6 +201,7 @@ static void state_sum_defined(const dq_state& a, const dq_state& b, dq_state& o)
     case DQ_OP_SIZE: o.u.size.num_matches = wrap_add(a.u.size.num_matches, b.u.size.num_matches); break;
     case DQ_OP_COMPLETENESS:
     case DQ_OP_COMPLIANCE:
+    case DQ_OP_PATTERN_MATCH:
       o.u.ratio.num_matches = wrap_add(a.u.ratio.num_matches, b.u.ratio.num_matches);
       o.u.ratio.count = wrap_add(a.u.ratio.count, b.u.ratio.count);
       break;
@@ -244,6 +245,7 @@ dq_status state_combine(const dq_state& a, const dq_state& b, dq_state& o) {
       break;
     case DQ_OP_COMPLETENESS:
     case DQ_OP_COMPLIANCE:
+    case DQ_OP_PATTERN_MATCH:
       pick(0, [] {}, [&] { o.u.ratio.num_matches = b.u.ratio.num_matches; },
            [&] { o.u.ratio.num_matches = wrap_add(a.u.ratio.num_matches, b.u.ratio.num_matches); });
       pick(1, [] {}, [&] { o.u.ratio.count = b.u.ratio.count; },
@@ -293,6 +295,7 @@ dq_status state_metric(const dq_state& s, double& out) {
     case DQ_OP_SIZE: out = (double)s.u.size.num_matches; break;
     case DQ_OP_COMPLETENESS:
     case DQ_OP_COMPLIANCE:
+    case DQ_OP_PATTERN_MATCH:
       out = s.u.ratio.count == 0 ? std::numeric_limits<double>::quiet_NaN()
                                  : jdiv((double)s.u.ratio.num_matches, (double)s.u.ratio.count);
       break;
@@ -335,7 +338,8 @@ int64_t state_to_bytes(const dq_state& s, uint8_t* buf, int64_t cap) {
   switch (s.op) {
     case DQ_OP_SIZE: w64((uint64_t)s.u.size.num_matches); break;                  // persistLongState
     case DQ_OP_COMPLETENESS:
-    case DQ_OP_COMPLIANCE: w64((uint64_t)s.u.ratio.num_matches); w64((uint64_t)s.u.ratio.count); break;
+    case DQ_OP_COMPLIANCE:
+    case DQ_OP_PATTERN_MATCH: w64((uint64_t)s.u.ratio.num_matches); w64((uint64_t)s.u.ratio.count); break;
     case DQ_OP_SUM: w64(dbits(s.u.sum.sum)); break;                               // persistDoubleState
     case DQ_OP_MEAN: w64(dbits(s.u.mean.sum)); w64((uint64_t)s.u.mean.count); break;
     case DQ_OP_MIN:
@@ -376,6 +380,7 @@ dq_status state_from_bytes(int32_t op, const uint8_t* buf, int64_t len, dq_state
       o.u.size.num_matches = (int64_t)r64(); return DQ_OK;
     case DQ_OP_COMPLETENESS:
     case DQ_OP_COMPLIANCE:
+    case DQ_OP_PATTERN_MATCH:
       if (!need(16)) break;
       o.u.ratio.num_matches = (int64_t)r64(); o.u.ratio.count = (int64_t)r64(); return DQ_OK;
     case DQ_OP_SUM:

@@ -87,10 +87,29 @@ class PredicatePool:
     def __init__(self, column_index: Dict[str, int]):
         self.column_index = column_index
         self.nodes: List[Tuple[int, int, int, int, int, float]] = []
+        self.patterns: List[str] = []  # DQ_PRED_REGEX patterns (dq_plan_create_ex)
 
     def _add(self, kind, a=-1, b=-1, cmp=0, i64=0, f64=0.0) -> int:
         self.nodes.append((kind, a, b, cmp, i64, f64))
         return len(self.nodes) - 1
+
+    def add_regex(self, column: int, pattern: str, mode: int) -> int:
+        """A DQ_PRED_REGEX node on plan column `column`; raises UnsupportedPredicate when the pattern
+        is outside the GPU regex subset (dq_regex_info), so the analyzer is routed to the fallback."""
+        import ctypes
+
+        if L.lib.dq_regex_info(pattern.encode("utf-8"), mode, None, None) != L.DQ_OK:
+            raise UnsupportedPredicate(L.lib.dq_last_error().decode("utf-8", "replace"))
+        if pattern not in self.patterns:
+            self.patterns.append(pattern)
+        col = self._add(L.PRED_COLUMN, column)
+        return self._add(L.PRED_REGEX, col, -1, mode, self.patterns.index(pattern))
+
+    def patterns_ctypes(self):
+        import ctypes
+
+        arr = (ctypes.c_char_p * max(1, len(self.patterns)))(*[p.encode("utf-8") for p in self.patterns])
+        return arr, len(self.patterns)
 
     def add(self, text: str) -> int:
         """Parse `text`; returns the root node index."""

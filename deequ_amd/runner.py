@@ -50,8 +50,10 @@ class ScanPlan:
         self.device = device
         self._specs, self._sch, self._pool = specs, sch, pool
         handle = ctypes.c_void_p()
-        L.check(L.lib.dq_plan_create(specs, len(self.analyzers), sch, len(self.columns), pool, npred, device,
-                                     ctypes.byref(handle)))
+        pats, npats = b.pool.patterns_ctypes()
+        self._pats = pats
+        L.check(L.lib.dq_plan_create_ex(specs, len(self.analyzers), sch, len(self.columns), pool, npred, pats, npats,
+                                        device, ctypes.byref(handle)))
         self.handle = handle
         self.chunk = 0
         with torch.cuda.device(device):

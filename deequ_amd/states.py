@@ -170,7 +170,7 @@ class DataTypeHistogram(State):  # DataType.scala:40-52
         raise TypeError("DataTypeHistogram yields a Distribution (DataTypeHistogram.toDistribution), not a double")
 
 
-_COMPLIANCE_LIKE = (L.OP_COMPLETENESS, L.OP_COMPLIANCE)
+_COMPLIANCE_LIKE = (L.OP_COMPLETENESS, L.OP_COMPLIANCE, L.OP_PATTERN_MATCH)
 
 
 def state_from_c(s: L.State) -> Optional[State]:

@@ -63,7 +63,9 @@ enum dq_op {
   DQ_OP_MAX = 8,                  /* analyzers/Maximum.scala:36-53 */
   DQ_OP_CORRELATION = 9,          /* analyzers/Correlation.scala:65-105 */
   DQ_OP_APPROX_COUNT_DISTINCT = 10,/* analyzers/ApproxCountDistinct.scala:47-64 */
-  DQ_OP_DATATYPE = 11             /* analyzers/DataType.scala:152-183, catalyst/StatefulDataType.scala:26-83 */
+  DQ_OP_DATATYPE = 11,            /* analyzers/DataType.scala:152-183, catalyst/StatefulDataType.scala:26-83 */
+  DQ_OP_PATTERN_MATCH = 12        /* analyzers/PatternMatch.scala:37-56: pred_root = a DQ_PRED_REGEX node
+                                     (mode DQ_REGEX_EXTRACT_NONEMPTY); state NumMatchesAndCount */
 };
 
 typedef struct dq_column_desc {
@@ -97,8 +99,16 @@ enum dq_pred_kind {
   DQ_PRED_NOT = 10,        /* NOT a */
   DQ_PRED_IS_NULL = 11,    /* a IS NULL */
   DQ_PRED_IS_NOT_NULL = 12,/* a IS NOT NULL */
-  DQ_PRED_COALESCE = 13    /* COALESCE(a, b): a = COLUMN node, b = literal node */
+  DQ_PRED_COALESCE = 13,   /* COALESCE(a, b): a = COLUMN node, b = literal node */
+  DQ_PRED_REGEX = 14       /* regex over a UTF8 column: a = COLUMN node, i64 = index into the plan's
+                              patterns (dq_plan_create_ex), cmp = enum dq_regex_mode */
 };
+/* DQ_PRED_REGEX semantics (java.util.regex Matcher.find on the value's code points):
+ *   DQ_REGEX_RLIKE            `col RLIKE p`: NULL on a NULL value, else TRUE iff find() succeeds;
+ *   DQ_REGEX_EXTRACT_NONEMPTY `CASE WHEN regexp_extract(col, p, 0) != '' THEN 1 ELSE 0` as PatternMatch
+ *                             builds it (PatternMatch.scala:48-49): FALSE on NULL, never NULL; patterns
+ *                             that can match the empty string are DQ_E_UNSUPPORTED (fallback). */
+enum dq_regex_mode { DQ_REGEX_RLIKE = 0, DQ_REGEX_EXTRACT_NONEMPTY = 1 };
 enum dq_cmp { DQ_CMP_LT = 1, DQ_CMP_LE = 2, DQ_CMP_GT = 3, DQ_CMP_GE = 4, DQ_CMP_EQ = 5, DQ_CMP_NE = 6 };
 
 typedef struct dq_pred_node {
@@ -131,7 +141,7 @@ typedef struct dq_state {
   uint8_t reserved[2];
   union {
     struct { int64_t num_matches; } size;                     /* NumMatches */
-    struct { int64_t num_matches; int64_t count; } ratio;     /* NumMatchesAndCount */
+    struct { int64_t num_matches; int64_t count; } ratio;     /* NumMatchesAndCount (Completeness, Compliance, PatternMatch) */
     struct { double sum; } sum;                               /* SumState */
     struct { double sum; int64_t count; } mean;               /* MeanState */
     struct { double n, avg, m2; } stddev;                     /* StandardDeviationState */
@@ -152,6 +162,19 @@ const char* dq_last_error(void);
 dq_status dq_plan_create(const dq_analyzer_spec* specs, int32_t n_specs, const dq_column_desc* schema,
                          int32_t n_cols, const dq_pred_node* pred_pool, int32_t n_pred, int32_t device,
                          dq_plan** out);
+/* As dq_plan_create, plus the UTF-8 regex patterns DQ_PRED_REGEX nodes refer to (i64 = index).
+ * Each pattern is compiled on the host into a byte-level search DFA (java.util.regex subset:
+ * literals, `.`, classes, \d \s \w, groups, alternation, greedy / lazy quantifiers, leading `^`,
+ * trailing `$`); backreferences, look-around, \b and inline flags are DQ_E_UNSUPPORTED. */
+dq_status dq_plan_create_ex(const dq_analyzer_spec* specs, int32_t n_specs, const dq_column_desc* schema,
+                            int32_t n_cols, const dq_pred_node* pred_pool, int32_t n_pred,
+                            const char* const* patterns, int32_t n_patterns, int32_t device, dq_plan** out);
+/* Compile a pattern without a GPU: DFA size (or the DQ_E_UNSUPPORTED reason in dq_last_error), and
+ * the host walk of the same DFA over n values (UTF-8 bytes data[offsets[r] .. offsets[r + 1]))
+ * for tests of the compiler; out[r] = 1 iff the value matches under `mode` (NULLs are the caller's). */
+dq_status dq_regex_info(const char* pattern, int32_t mode, int32_t* n_states, int32_t* n_classes);
+dq_status dq_regex_match_host(const char* pattern, int32_t mode, const uint8_t* data, const int64_t* offsets,
+                              int64_t n, uint8_t* out);
 /* Launch on this hipStream_t from now on (NULL = the device null stream).  A new plan launches on its
    own non-blocking stream, which does not order against other streams: set the producer's stream. */
 dq_status dq_plan_set_stream(dq_plan* plan, void* hip_stream);

@@ -1131,6 +1131,77 @@ def datatype_histogram(c: "OColumn", sel: np.ndarray) -> DataTypeHistogram:
     return DataTypeHistogram(*counts)
 
 
+# PatternMatch (analyzers/PatternMatch.scala:46-55): sum(CASE WHEN where THEN
+# (regexp_extract(col, pattern, 0) != "" ? 1 : 0) END) / conditionalCount(where).  Spark's RegExpExtract
+# runs java.util.regex Matcher.find() on the value (UTF8String -> java String) and returns group 0, or ""
+# without a match.  Python's `re` is the same leftmost-first backtracking engine for the constructs
+# PatternMatch patterns use; the Java defaults that differ are restated here: ASCII \d \s \w (re.ASCII),
+# `.` excludes \n \r \u0085 \u2028 \u2029, a trailing `$` also matches before a final line
+# terminator (but not between \r and \n), named groups are (?<name>...), \e is ESC, \x{h..} a code point.
+_JAVA_DOT = "[^\n\r\x85\u2028\u2029]"
+_JAVA_END = "(?:\\Z|(?=\r\n\\Z)|(?<!\r)(?=\n\\Z)|(?=[\r\x85\u2028\u2029]\\Z))"
+
+
+def java_regex_to_python(p: str) -> str:
+    out, i, in_class = [], 0, False
+    while i < len(p):
+        c = p[i]
+        if c == "\\" and i + 1 < len(p):
+            d = p[i + 1]
+            if d == "x" and i + 2 < len(p) and p[i + 2] == "{":
+                j = p.index("}", i + 3)
+                out.append("\\U%08x" % int(p[i + 3:j], 16))
+                i = j + 1
+                continue
+            if d == "e":
+                out.append("\\x1b")
+            elif d == "0":  # \0n, \0nn, \0mnn
+                j = i + 2
+                while j < len(p) and j < i + 5 and p[j] in "01234567" and int(p[i + 2:j + 1], 8) <= 0o377:
+                    j += 1
+                out.append("\\x%02x" % int(p[i + 2:j], 8))
+                i = j
+                continue
+            else:
+                out.append(p[i:i + 2])
+            i += 2
+            continue
+        if in_class:
+            if c == "]":
+                in_class = False
+            out.append(c)
+        elif c == "[":
+            in_class = True
+            out.append(c)
+            if i + 1 < len(p) and p[i + 1] == "^":
+                out.append("^")
+                i += 1
+        elif c == ".":
+            out.append(_JAVA_DOT)
+        elif c == "$" and i == len(p) - 1:
+            out.append(_JAVA_END)
+        elif p.startswith("(?<", i) and not p.startswith(("(?<=", "(?<!"), i):
+            out.append("(?P<")
+            i += 3
+            continue
+        else:
+            out.append(c)
+        i += 1
+    return "".join(out)
+
+
+_REGEX_CACHE: dict = {}
+
+
+def regexp_extract_nonempty(value: bytes, pattern: str) -> bool:
+    """regexp_extract(value, pattern, 0) != "" (Spark RegExpExtract: Matcher.find(), group 0)."""
+    rx = _REGEX_CACHE.get(pattern)
+    if rx is None:
+        rx = _REGEX_CACHE[pattern] = re.compile(java_regex_to_python(pattern), re.ASCII)
+    m = rx.search(value.decode("utf-8", "replace"))  # invalid UTF-8 -> U+FFFD, as UTF8String.toString
+    return m is not None and m.group(0) != ""
+
+
 def _where(cols, n, where: Optional[str]):
     """(where_true, where_notnull) masks; no where -> all true."""
     if where is None:
@@ -1192,6 +1263,17 @@ def compute_state(spec: tuple, cols: dict, n: int, n_partitions: int = 1):
                 return None
             return MinState(v) if op == "Minimum" else MaxState(v)
         return ApproxCountDistinctState(hll_words_for(c, sel))
+    if op == "PatternMatch":
+        col, pattern, where = spec[1], spec[2], spec[3]
+        c = cols[col]
+        wt, _ = _where(cols, n, where)
+        matches = sum(1 for i in range(n)
+                      if wt[i] and c.valid[i] and regexp_extract_nonempty(_value_string(c, i), pattern))
+        count = _conditional_count(cols, n, where)
+        # the CASE term is never NULL when `where` holds: the sum is NULL iff no row passes `where`
+        if not wt.any() or count is None:
+            return None
+        return NumMatchesAndCount(matches, count)
     if op == "DataType":  # stateful_datatype(conditionalSelection(column, where)); never NULL
         col, where = spec[1], spec[2]
         wt, _ = _where(cols, n, where)

@@ -113,9 +113,39 @@ datasets = {
             "marketplace": ["utf8", ["EU", "NA", "IN", "EU", "NA", "NA", "NA", "NA"]],
         },
     },
+    # PatternMatch (AnalyzerTests.scala:626-721, checks/CheckTest.scala:352-476)
+    "patternDoubles": {  # AnalyzerTests.scala:628-630 (DoubleType column: Spark casts it to string)
+        "columns": {"some": ["f64", [1.1, N, 3.2, 4.4]]}
+    },
+    "patternIntegers": {"columns": {"some": ["utf8", ["1", "a"]]}},  # :635
+    "patternEmails": {"columns": {"some": ["utf8", ["someone@somewhere.org", "someone@else"]]}},  # :641-642
+    "patternCreditCards": {"columns": {"some": ["utf8", [  # :648-664
+        "378282246310005", "6011111111111117", "6011 1111 1111 1117", "6011-1111-1111-1117",
+        "5555555555554444", "5555 5555 5555 4444", "5555-5555-5555-4444", "4111111111111111",
+        "4111 1111 1111 1111", "4111-1111-1111-1111", "0000111122223333", "000011112222333", "00001111222233"]]}},
+    "patternUrls": {"columns": {"some": ["utf8", [  # :674-693 (incl. non-ASCII hosts / paths)
+        "http://foo.com/blah_blah", "http://foo.com/blah_blah_(wikipedia)",
+        "http://foo.bar/?q=Test%20URL-encoded%20stuff", "http://\u27a1.ws/\u4a39", "http://\u2318.ws/",
+        "http://\u263a.damowmow.com/", "http://\u4f8b\u5b50.\u6d4b\u8bd5", "https://foo_bar.example.com/",
+        "http://userid@example.com:8080", "http://foo.com/blah_(wikipedia)#cite-1", "http://../", "h://test",
+        "http://.www.foo.bar/"]]}},
+    "patternSsns": {"columns": {"some": ["utf8", [  # :703-712
+        "111-05-1130", "111051130", "111-05-000", "111-00-000", "000-05-1130", "666-05-1130", "900-05-1130",
+        "999-05-1130"]]}},
+    "checkUrls": {"columns": {"some": ["utf8", [  # checks/CheckTest.scala:383-386
+        "https://www.example.com/foo/?bar=baz&inga=42&quux", "http:// shouldfail.com"]]}},
+    "checkEmails": {"columns": {"some": ["utf8", ["someone@somewhere.org", "someone@else.com"]]}},  # :354-355
 }
 
 S = "analyzers/AnalyzerTests.scala"
+EMAIL = (r"""(?:[a-z0-9!#$%&'*+/=?^_`{|}~-]+(?:\.[a-z0-9!#$%&'*+/=?^_`{|}~-]+)*|"(?:[\x01-\x08\x0b\x0c\x0e-\x1f\x21\x23-\x5b\x5d-\x7f]|\\[\x01-\x09\x0b\x0c\x0e-\x7f])*")"""
+         r"""@(?:(?:[a-z0-9](?:[a-z0-9-]*[a-z0-9])?\.)+[a-z0-9](?:[a-z0-9-]*[a-z0-9])?|\[(?:(?:25[0-5]|2[0-4][0-9]|[01]?[0-9][0-9]?)\.){3}"""
+         r"""(?:25[0-5]|2[0-4][0-9]|[01]?[0-9][0-9]?|[a-z0-9-]*[a-z0-9]:(?:[\x01-\x08\x0b\x0c\x0e-\x1f\x21-\x5a\x53-\x7f]|\\[\x01-\x09\x0b\x0c\x0e-\x7f])+)\])""")
+URL = r"""(https?|ftp)://[^\s/$.?#].[^\s]*"""
+SSN = (r"""((?!219-09-9999|078-05-1120)(?!666|000|9\d{2})\d{3}-(?!00)\d{2}-(?!0{4})\d{4})|"""
+       r"""((?!219 09 9999|078 05 1120)(?!666|000|9\d{2})\d{3} (?!00)\d{2} (?!0{4})\d{4})|"""
+       r"""((?!219099999|078051120)(?!666|000|9\d{2})\d{3}(?!00)\d{2}(?!0{4})\d{4})""")
+CREDITCARD = r"""\b(?:3[47]\d{2}([\ \-]?)\d{6}\1\d|(?:(?:4\d|5[1-5]|65)\d{2}|6011)([\ \-]?)\d{4}\2\d{4}\2)\d{4}\b"""
 cases = [
     # Size / Completeness
     ("dfMissing", ["Size", N], 12.0, S + ":39-42", []),
@@ -188,6 +218,15 @@ cases = [
     ("incrementalInitial", ["Size", N], 3.0, "analyzers/IncrementalAnalyzerTest.scala:58", []),
     ("incrementalInitial", ["Completeness", "att1", N], 0.6666666666666666, "analyzers/IncrementalAnalyzerTest.scala:96", []),
     ("incrementalInitial", ["Compliance", "att1", "att1 = 'b'", N], 0.3333333333333333, "analyzers/IncrementalAnalyzerTest.scala:77", ["string_predicate"]),
+    # PatternMatch: "regex_fallback" = outside the GPU regex subset / a non-string column (Spark path)
+    ("patternDoubles", ["PatternMatch", "some", r"\d\.\d", N], 0.75, S + ":628-631", ["regex_fallback"]),
+    ("patternIntegers", ["PatternMatch", "some", r"\d", N], 0.5, S + ":634-637", []),
+    ("patternEmails", ["PatternMatch", "some", EMAIL, N], 0.5, S + ":640-643", []),
+    ("patternCreditCards", ["PatternMatch", "some", CREDITCARD, N], 10.0 / 13.0, S + ":646-671", ["regex_fallback"]),
+    ("patternUrls", ["PatternMatch", "some", URL, N], 10.0 / 13.0, S + ":673-699", []),
+    ("patternSsns", ["PatternMatch", "some", SSN, N], 2.0 / 8.0, S + ":701-718", ["regex_fallback"]),
+    ("checkUrls", ["PatternMatch", "some", URL, N], 0.5, "checks/CheckTest.scala:381-389 (hasPattern default assertion fails)", []),
+    ("checkEmails", ["PatternMatch", "some", EMAIL, N], 1.0, "checks/CheckTest.scala:352-360 (hasPattern default assertion holds)", []),
     # partition merge (analyzers/StateAggregationIntegrationTest.scala:56-104)
     ("stateAggregation", ["Completeness", "origin", N], 0.625, "analyzers/StateAggregationIntegrationTest.scala:77", []),
 ]

@@ -99,7 +99,7 @@ def test_reference_kats_fused_and_single(dq, kats):
         for c, a in zip(cases, analyzers):
             for metric in (ctx.metric(a), a.calculate(table)):
                 exp = c["expected"]
-                if "string_predicate" in c["needs"]:
+                if c["needs"]:  # string predicate / regex outside the GPU subset: Spark fallback set
                     assert metric.value.isFailure
                     assert isinstance(metric.value.failed, UnsupportedOnGpuPathException), metric
                     continue
@@ -637,3 +637,66 @@ def test_datatype_vs_oracle(dq, n, large):
         else:  # +-inf / NaN in the column: Spark's sum is +-inf or NaN
             g = got[an]
             assert g.count == ref.count and ((math.isnan(g.sum_) and math.isnan(ref.sum_)) or g.sum_ == ref.sum_)
+
+
+# ---------------------------------------------------------------------------------------------
+# PatternMatch (PatternMatch.scala:37-56): the search-DFA atom of the predicate pass
+# ---------------------------------------------------------------------------------------------
+def _pm_strings(rng, n):
+    alphabet = list("abcdxyzq@.-_:/ \t0123456789é€𝄞☺") + ["someone@somewhere.org", "http://foo.com/x", "https://",
+                                                           "1.5", "ftp://a.b", "x@y.io", "colour"]
+    out = []
+    for i in range(n):
+        if rng.random() < 0.1:
+            out.append(None)
+            continue
+        k = int(rng.integers(0, 9)) if i % 97 else int(rng.integers(20, 60))  # a few long values
+        out.append("".join(alphabet[int(j)] for j in rng.integers(0, len(alphabet), k)).encode("utf-8"))
+    return out
+
+
+@pytest.mark.parametrize("large", [False, True])
+@pytest.mark.parametrize("n", [0, 1, 513, 4099, 70_001])
+def test_pattern_match_vs_oracle(dq, n, large):
+    """PatternMatch on the GPU (alone, with `where`, fused with HLL / Completeness / Compliance) vs the
+    oracle's regexp_extract restatement: NumMatchesAndCount bit-exact, incl. non-ASCII values, NULLs,
+    empty values and values longer than a dword-loop's worth; int32 and int64 offsets."""
+    from deequ_amd.runner import scan_states
+    from deequ_amd.table import column_from_numpy, utf8_column
+
+    rng = np.random.default_rng(1234 + n + int(large))
+    strs = _pm_strings(rng, n)
+    a = rng.integers(-3, 3, n).astype(np.int64)
+    t = dq.Table([utf8_column("s", strs, large=large), column_from_numpy("a", "i64", a, rng.random(n) >= 0.2)])
+    pats = [dq.Patterns.EMAIL, dq.Patterns.URL, r"\d\.\d", r"^\d+$", "é.", r"[^\s]{6,}", r"(?:ab|cd){2}"]
+    analyzers = [dq.PatternMatch("s", p) for p in pats] + [
+        dq.PatternMatch("s", dq.Patterns.EMAIL, "a > 0"), dq.PatternMatch("s", r"\d", "a >= 1"),
+        dq.ApproxCountDistinct("s"), dq.Completeness("s"), dq.Compliance("c", "a < 2"), dq.Size()]
+    got = scan_states(t, analyzers)
+    host = {name: host_column(c, n) for name, c in t.columns.items()}
+    ocols = {name: O.OColumn(t.columns[name].dtype.replace("large_", ""), host[name][0], host[name][1])
+             for name in t.columns}
+    for an in analyzers:
+        kind = type(an).__name__
+        if kind == "PatternMatch":
+            spec = ("PatternMatch", an.column, an.pattern, an.where)
+        elif kind == "Compliance":
+            spec = ("Compliance", an.instance, an.predicate, an.where)
+        elif kind == "Size":
+            spec = ("Size", an.where)
+        else:
+            spec = (kind, an.column, an.where)
+        ref = O.compute_state(spec, ocols, n)
+        assert_state_close(got[an], ref)
+
+
+def test_pattern_match_fallback_in_fused_run(dq):
+    """A pattern outside the GPU subset fails only its own metric (routed to the fallback set); the
+    rest of the fused pass is unaffected."""
+    from deequ_amd.metrics import UnsupportedOnGpuPathException
+
+    t = dq.Table.from_pydict({"s": ("utf8", ["111-05-1130", "x", None, "4111 1111 1111 1111"])})
+    ssn, url = dq.PatternMatch("s", dq.Patterns.SOCIAL_SECURITY_NUMBER_US), dq.PatternMatch("s", dq.Patterns.URL)
+    ctx = dq.AnalysisRunner.onData(t).addAnalyzers([ssn, url, dq.Size()]).run()
+    assert isinstance(ctx.metric(ssn).value.failed, UnsupportedOnGpuPathException)
+    assert ctx.metric(url).value.get() == 0.0 and ctx.metric(dq.Size()).value.get() == 4.0
