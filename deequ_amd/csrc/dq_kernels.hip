@@ -1188,6 +1188,81 @@ __device__ __forceinline__ void pred_atom_regex(const PredInstr& ins, const uint
   wn = ins.null_res == NR_NULL ? ~va : 0u;
 }
 
+// ATOM_REGEX over int32 offsets: the lane's 8 row offsets are loaded together, and each row's first
+// 32 bytes come in as two 16-byte buffer loads (bounds-checked over the chunk's bytes) issued while the
+// previous row is walked; the first 28 bytes are realigned in registers and walked branch-free
+// (select on `p < len && live`), in 4-byte groups skipped as soon as no lane of the wave needs them.
+// The rare value longer than 28 bytes continues with dword loads, as does a value whose 32-byte window
+// would reach past the last whole dword of the chunk's bytes (a buffer load zeroes such dwords).
+__device__ __forceinline__ void pred_atom_regex_utf8(const PredInstr& ins, const uint16_t* __restrict__ dfa,
+                                                     const uint8_t* __restrict__ bytes,
+                                                     const int32_t* __restrict__ offs, int64_t n_rows, int64_t row1,
+                                                     int64_t base, int lane, uint32_t va, uint32_t& wt, uint32_t& wn) {
+  const int ns = dfa[0], nc = dfa[1];
+  const uint32_t start = dfa[2];
+  const uint16_t* cls = dfa + 4;
+  const uint16_t* acc = cls + 256;
+  const uint16_t* tr = acc + ns;
+  const int32_t total = offs[n_rows];
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t*>(bytes), (short)0, total, 0x00020000);
+  const int32_t win = (total & ~3) - 32;  // window of a value at o0 is whole iff (o0 & ~3) <= win
+  int32_t o0[8], ln[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int64_t r = base + 64 * j + lane;
+    o0[j] = r < row1 ? offs[r] : 0;
+    ln[j] = r < row1 ? offs[r + 1] - o0[j] : 0;
+  }
+  u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rsrc, o0[0] & ~3, 0, 0);
+  u32x4 c = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (o0[0] & ~3) + 16, 0, 0);
+  uint32_t wc = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    u32x4 an = a, cn = c;
+    if (j < 7) {
+      an = __builtin_amdgcn_raw_buffer_load_b128(rsrc, o0[j + 1] & ~3, 0, 0);
+      cn = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (o0[j + 1] & ~3) + 16, 0, 0);
+    }
+    const uint32_t d[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+    const uint32_t sh = (uint32_t)o0[j] << 3;
+    uint32_t wv[7];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) wv[k] = alignbit32(d[k + 1], d[k], sh);
+    const int32_t L = ln[j];
+    const int32_t Lw = (o0[j] & ~3) <= win ? L : 0;  // bytes walked from the window
+    uint32_t st = start;
+#pragma unroll
+    for (int g = 0; g < 7; ++g) {
+      if (!__builtin_amdgcn_ballot_w64(Lw > 4 * g && st >= 2u)) break;  // wave-uniform
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const uint32_t nx = tr[st * nc + cls[(wv[g] >> (8 * b)) & 0xFFu]];
+        st = (4 * g + b < Lw && st >= 2u) ? nx : st;
+      }
+    }
+    const int32_t done = Lw < 28 ? Lw : 28;
+    if (L > done && st >= 2u) {  // long value / window past the end: the rest with dword loads
+      int64_t i = (int64_t)o0[j] + done;
+      const int64_t e = (int64_t)o0[j] + L;
+      while (i < e && st >= 2u) {
+        const uint32_t w = *reinterpret_cast<const uint32_t*>(bytes + (i & ~(int64_t)3));
+        const int64_t end = (i | 3) + 1 < e ? (i | 3) + 1 : e;
+        do {
+          st = tr[st * nc + cls[(w >> (8 * (i & 3))) & 0xFFu]];
+          ++i;
+        } while (i < end && st >= 2u);
+      }
+    }
+    const uint64_t cm = __builtin_amdgcn_ballot_w64(acc[st] != 0);
+    if ((lane >> 1) == j) wc = (lane & 1) ? (uint32_t)(cm >> 32) : (uint32_t)cm;
+    a = an;
+    c = cn;
+  }
+  wt = va & wc;
+  wn = ins.null_res == NR_NULL ? ~va : 0u;
+}
+
 __global__ __launch_bounds__(kBlock) void dq_pred_scan(const PredProgram* __restrict__ prog_g, ScanCols cols,
                                                        ScanBitmaps bm, int64_t n_rows, int64_t rows_per_range,
                                                        PredPartial* __restrict__ acc) {
@@ -1251,8 +1326,13 @@ __global__ __launch_bounds__(kBlock) void dq_pred_scan(const PredProgram* __rest
           else pred_atom_cmp(ins, B1, lane, wt, wn);
         } else if (op == PO_ATOM_REGEX) {
           const uint32_t va = (g & 1u) ? B1.va : B0.va;
-          pred_atom_regex(ins, dfa_lds + ins.lit_i, reinterpret_cast<const uint8_t*>(cols.values[ins.col_a]),
-                          cols.offsets[ins.col_a], row1, base, lane, va, wt, wn);
+          if (ins.kind_a == CK_UTF8)
+            pred_atom_regex_utf8(ins, dfa_lds + ins.lit_i, reinterpret_cast<const uint8_t*>(cols.values[ins.col_a]),
+                                 reinterpret_cast<const int32_t*>(cols.offsets[ins.col_a]), n_rows, row1, base, lane,
+                                 va, wt, wn);
+          else
+            pred_atom_regex(ins, dfa_lds + ins.lit_i, reinterpret_cast<const uint8_t*>(cols.values[ins.col_a]),
+                            cols.offsets[ins.col_a], row1, base, lane, va, wt, wn);
         } else {
           const uint32_t va = (g & 1u) ? B1.va : B0.va;
           wt = op == PO_ATOM_ISNULL ? ~va : va;

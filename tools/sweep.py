@@ -39,7 +39,7 @@ def measure(name, table, analyzers, reps=5):
             if hasattr(a, f):
                 cols.add(getattr(a, f))
     strb = sum(table.columns[c].data_bytes for c in cols if table.columns[c].dtype == "utf8" and
-               any(type(a).__name__ == "ApproxCountDistinct" and a.column == c for a in analyzers))
+               any(type(a).__name__ in ("ApproxCountDistinct", "PatternMatch") and a.column == c for a in analyzers))
     nbytes = plan.bytes_per_row() * table.num_rows + strb
     main = res.get("column") or res.get("pair") or res.get("pred")
     out = {"case": name, "rows": table.num_rows, "GB": nbytes / 1e9, "kernel_ms": res, "wall_ms": wall * 1e3,
@@ -69,6 +69,10 @@ def main():
         measure("profile16", t, synth.profile_analyzers(t))
         measure("compliance4", t, [dq.Compliance("p0", "i0 >= 0"), dq.Compliance("p1", "`i1` IS NULL OR (`i1` >= 10.0 AND `i1` <= 1000.0)"),
                                    dq.Compliance("p2", "i2 < i3"), dq.Compliance("p3", "COALESCE(i3, 0.0) >= 0")])
+        measure("pattern_email_utf8x1", t, [dq.PatternMatch(s[0], dq.Patterns.EMAIL)])
+        measure("pattern_url_utf8x1", t, [dq.PatternMatch(s[0], dq.Patterns.URL)])
+        measure("pattern_email_utf8x4", t, [dq.PatternMatch(c, dq.Patterns.EMAIL) for c in s])
+        measure("pattern_digit_utf8x4", t, [dq.PatternMatch(c, r"\d") for c in s])
     c4 = synth.c4_table(n // 2, seed=42)
     names = list(c4.columns)
     measure("corr28_half", c4, [dq.Correlation(names[a], names[b]) for a in range(8) for b in range(a + 1, 8)])
