@@ -57,6 +57,7 @@ PRED_REGEX = 14
 
 REGEX_RLIKE = 0             # col RLIKE p: NULL on NULL, find()
 REGEX_EXTRACT_NONEMPTY = 1  # regexp_extract(col, p, 0) != '' as PatternMatch builds it: FALSE on NULL
+REGEX_FULL = 2              # whole value in L(p): string = / IN lists; NULL on NULL
 
 CMP_LT, CMP_LE, CMP_GT, CMP_GE, CMP_EQ, CMP_NE = 1, 2, 3, 4, 5, 6
 

@@ -297,7 +297,7 @@ struct Lowering {
         const int32_t t = (*schema)[c.a].type;
         if (t != DQ_TYPE_UTF8 && t != DQ_TYPE_LARGE_UTF8)
           return set_error(DQ_E_UNSUPPORTED, "regex on a non-string column (%d)", c.a);
-        if (n.cmp != DQ_REGEX_RLIKE && n.cmp != DQ_REGEX_EXTRACT_NONEMPTY)
+        if (n.cmp != DQ_REGEX_RLIKE && n.cmp != DQ_REGEX_EXTRACT_NONEMPTY && n.cmp != DQ_REGEX_FULL)
           return set_error(DQ_E_INVALID, "regex mode %d", n.cmp);
         if (!patterns || n.i64 < 0 || n.i64 >= (int64_t)patterns->size())
           return set_error(DQ_E_INVALID, "regex pattern index %lld out of range", (long long)n.i64);
@@ -316,7 +316,7 @@ struct Lowering {
         PredInstr p{};
         p.op = PO_ATOM_REGEX; p.col_a = c.a; p.col_b = -1; p.kind_a = kind_of(t);
         p.lit_i = off;
-        p.null_res = n.cmp == DQ_REGEX_RLIKE ? NR_NULL : NR_FALSE;
+        p.null_res = n.cmp == DQ_REGEX_EXTRACT_NONEMPTY ? NR_FALSE : NR_NULL;
         out.push_back(p);
         return DQ_OK;
       }

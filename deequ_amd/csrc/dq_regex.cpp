@@ -509,13 +509,18 @@ dq_status regex_compile(const char* pattern, int32_t mode, RegexDfa& out) {
   if (!pattern) return set_error(DQ_E_INVALID, "NULL pattern");
   Parser P;
   if (!decode_utf8(pattern, P.cp)) return set_error(DQ_E_INVALID, "pattern is not valid UTF-8");
-  if (!P.cp.empty() && P.cp[0] == '^') { P.anchored_start = true; P.i = 1; }
+  const bool full = mode == DQ_REGEX_FULL;  // whole-value match: string = / IN
+  if (full) P.anchored_start = true;
+  else if (!P.cp.empty() && P.cp[0] == '^') { P.anchored_start = true; P.i = 1; }
   int root = -1;
   if (!P.parse_alt(root, 0) || !P.at_end()) {
     if (P.err.empty()) P.err = "unbalanced ')'";
     return set_error(DQ_E_UNSUPPORTED, "pattern /%s/: %s", pattern, P.err.c_str());
   }
-  if ((P.anchored_start || P.anchored_end) && P.nodes[root].k == Node::ALT)
+  if (full) {
+    if (P.anchored_end) return set_error(DQ_E_UNSUPPORTED, "pattern /%s/: `$` in a whole-value match", pattern);
+    P.anchored_end = true;  // accepted at end of input only, no line-terminator allowance
+  } else if ((P.anchored_start || P.anchored_end) && P.nodes[root].k == Node::ALT)
     return set_error(DQ_E_UNSUPPORTED, "pattern /%s/: anchor with top-level alternation", pattern);
   const bool can_be_empty = P.nullable(root);
   // regexp_extract(...) != "": an empty leftmost match counts as no match; which match Java's
@@ -530,7 +535,9 @@ dq_status regex_compile(const char* pattern, int32_t mode, RegexDfa& out) {
   auto f = B.build(root);
   N.eps[s0].push_back(f.first);
   const int accept = N.add();
-  if (P.anchored_end) {  // R then an optional final line terminator, accepted at end of input only
+  if (full) {
+    N.eps[f.second].push_back(accept);
+  } else if (P.anchored_end) {  // R then an optional final line terminator, accepted at end of input only
     N.eps[f.second].push_back(accept);
     static const char* kTerm[] = {"\r\n", "\n", "\r", "\xC2\x85", "\xE2\x80\xA8", "\xE2\x80\xA9"};
     for (const char* t : kTerm) {

@@ -11,10 +11,14 @@ accepted grammar is the numeric subset the GPU evaluates with SQL three-valued l
     cmp      := operand ( (< | <= | > | >= | = | == | != | <>) operand | IS [NOT] NULL )?
     operand  := column | `column` | number | NULL | TRUE | FALSE | COALESCE(operand, operand)
               | ( expr ) | - number
+    strcmp   := column (= | == | != | <>) 'string' | 'string' (= | ...) column
+              | column [NOT] IN ('string', ...)
 
-Literal typing follows Spark 2.2: `3` integer, `3.0` exact decimal, `3e0` double.  Anything
-else (string literals, IN lists, LIKE, functions) raises UnsupportedPredicate: such an analyzer is
-routed to the fallback set, exactly like a type the GPU plan does not cover.
+Literal typing follows Spark 2.2: `3` integer, `3.0` exact decimal, `3e0` double.  String
+(in)equality and IN lists on a string column are byte-wise equality of the UTF-8 values; they lower to
+a whole-value DFA (DQ_PRED_REGEX, mode DQ_REGEX_FULL) over the escaped literals.  Anything else
+(string ordering, LIKE, RLIKE, functions, literals with backslash escapes) raises UnsupportedPredicate:
+such an analyzer is routed to the fallback set, exactly like a type the GPU plan does not cover.
 """
 from __future__ import annotations
 
@@ -44,7 +48,13 @@ def _tokenize(s: str) -> List[Tuple[str, str]]:
             toks.append(("id", s[i + 1:j]))
             i = j + 1
         elif c in "'\"":
-            raise UnsupportedPredicate(f"string literal in {s!r}")
+            j = s.find(c, i + 1)
+            if j < 0:
+                raise UnsupportedPredicate(f"unterminated string literal in {s!r}")
+            if "\\" in s[i + 1:j]:  # Spark unescapes backslash sequences: not restated here
+                raise UnsupportedPredicate(f"string literal with a backslash escape in {s!r}")
+            toks.append(("str", s[i + 1:j]))
+            i = j + 1
         elif c.isdigit() or (c == "." and i + 1 < len(s) and s[i + 1].isdigit()):
             j = i
             while j < len(s) and (s[j].isdigit() or s[j] == "."):
@@ -104,6 +114,12 @@ class PredicatePool:
             self.patterns.append(pattern)
         col = self._add(L.PRED_COLUMN, column)
         return self._add(L.PRED_REGEX, col, -1, mode, self.patterns.index(pattern))
+
+    def is_string_column(self, plan_col: int) -> bool:
+        b = getattr(self.column_index, "b", None)
+        if b is None:
+            return False
+        return b.by_name[b.columns[plan_col]][1] in ("utf8", "large_utf8")
 
     def patterns_ctypes(self):
         import ctypes
@@ -169,7 +185,34 @@ class _Parser:
         if k == "op" and v in _CMP:
             self.take()
             b = self.parse_operand()
+            if isinstance(a, str) or isinstance(b, str):  # string (in)equality
+                if v not in ("=", "==", "!=", "<>"):
+                    raise UnsupportedPredicate(f"string ordering comparison in {self.text!r}")
+                col, lit = (b, a) if isinstance(a, str) else (a, b)
+                if isinstance(col, str):
+                    raise UnsupportedPredicate(f"comparison of two string literals in {self.text!r}")
+                e = self._string_in(col, [lit])
+                return self.pool._add(L.PRED_NOT, e) if v in ("!=", "<>") else e
             return self.pool._add(L.PRED_CMP, a, b, _CMP[v])
+        if (k, v) in (("kw", "IN"), ("kw", "NOT")) and not isinstance(a, str):
+            neg = v == "NOT"
+            save = self.pos
+            self.take()
+            if neg and self.peek() != ("kw", "IN"):
+                self.pos = save
+                return a
+            if neg:
+                self.take()
+            self.expect(("op", "("))
+            items = [self.take()]
+            while self.peek() == ("op", ","):
+                self.take()
+                items.append(self.take())
+            self.expect(("op", ")"))
+            if any(t[0] != "str" for t in items):
+                raise UnsupportedPredicate(f"IN list of non-string literals in {self.text!r}")
+            e = self._string_in(a, [t[1] for t in items])
+            return self.pool._add(L.PRED_NOT, e) if neg else e
         if (k, v) == ("kw", "IS"):
             self.take()
             neg = False
@@ -178,9 +221,26 @@ class _Parser:
                 neg = True
             self.expect(("kw", "NULL"))
             return self.pool._add(L.PRED_IS_NOT_NULL if neg else L.PRED_IS_NULL, a)
-        if k == "kw" and v in ("IN", "LIKE", "RLIKE", "BETWEEN"):
+        if k == "kw" and v in ("LIKE", "RLIKE", "BETWEEN"):
             raise UnsupportedPredicate(f"{v} is not in the GPU predicate grammar: {self.text!r}")
+        if isinstance(a, str):
+            raise UnsupportedPredicate(f"bare string literal in {self.text!r}")
         return a
+
+    def _string_in(self, col_node: int, literals):
+        """col IN (literals) as one whole-value DFA: (?:l1|l2|...) with every non-alphanumeric
+        ASCII character escaped (the DFA compiler reads `\\` + such a character as the literal)."""
+        k, c = self.pool.nodes[col_node][0], self.pool.nodes[col_node][1]
+        if k != L.PRED_COLUMN:
+            raise UnsupportedPredicate(f"string comparison on a non-column expression in {self.text!r}")
+        if not self.pool.is_string_column(c):
+            raise UnsupportedPredicate(f"string literal compared with a non-string column in {self.text!r}")
+        esc = ["".join(ch if (ch.isalnum() and ord(ch) < 128) or ord(ch) >= 128 else "\\" + ch for ch in lit)
+               for lit in literals]
+        pattern = "(?:" + "|".join(esc) + ")"
+        if col_node == len(self.pool.nodes) - 1:
+            self.pool.nodes.pop()  # the column node is re-added by add_regex
+        return self.pool.add_regex(c, pattern, L.REGEX_FULL)
 
     def parse_operand(self):
         k, v = self.take()
@@ -195,6 +255,8 @@ class _Parser:
             return self._number("-" + v2)
         if k == "num":
             return self._number(v)
+        if k == "str":
+            return v  # a python str: only valid as one side of a string (in)equality / IN
         if (k, v) == ("kw", "NULL"):
             return self.pool._add(L.PRED_LIT_NULL)
         if k == "kw" and v in ("TRUE", "FALSE"):

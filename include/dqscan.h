@@ -101,14 +101,18 @@ enum dq_pred_kind {
   DQ_PRED_IS_NOT_NULL = 12,/* a IS NOT NULL */
   DQ_PRED_COALESCE = 13,   /* COALESCE(a, b): a = COLUMN node, b = literal node */
   DQ_PRED_REGEX = 14       /* regex over a UTF8 column: a = COLUMN node, i64 = index into the plan's
-                              patterns (dq_plan_create_ex), cmp = enum dq_regex_mode */
+                              patterns (dq_plan_create_ex), cmp = enum dq_regex_mode;
+                              string equality / IN lists lower to mode DQ_REGEX_FULL */
 };
 /* DQ_PRED_REGEX semantics (java.util.regex Matcher.find on the value's code points):
  *   DQ_REGEX_RLIKE            `col RLIKE p`: NULL on a NULL value, else TRUE iff find() succeeds;
  *   DQ_REGEX_EXTRACT_NONEMPTY `CASE WHEN regexp_extract(col, p, 0) != '' THEN 1 ELSE 0` as PatternMatch
  *                             builds it (PatternMatch.scala:48-49): FALSE on NULL, never NULL; patterns
  *                             that can match the empty string are DQ_E_UNSUPPORTED (fallback). */
-enum dq_regex_mode { DQ_REGEX_RLIKE = 0, DQ_REGEX_EXTRACT_NONEMPTY = 1 };
+enum dq_regex_mode { DQ_REGEX_RLIKE = 0, DQ_REGEX_EXTRACT_NONEMPTY = 1, DQ_REGEX_FULL = 2 };
+/*   DQ_REGEX_FULL             the whole value is in L(p) (no search, no `^` / `$` handling): string
+ *                             equality `col = 'v'` / `col IN ('a', 'b')` lowered to p = (?:a|b) with
+ *                             escaped literals; NULL on a NULL value. */
 enum dq_cmp { DQ_CMP_LT = 1, DQ_CMP_LE = 2, DQ_CMP_GT = 3, DQ_CMP_GE = 4, DQ_CMP_EQ = 5, DQ_CMP_NE = 6 };
 
 typedef struct dq_pred_node {

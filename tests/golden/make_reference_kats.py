@@ -6,8 +6,8 @@ src/test/scala/com/amazon/deequ/).  This is data only: tables + expected metrics
 `expected` is a float, "NaN", "EmptyState" (metric fails with EmptyStateException,
 Analyzer.scala:420-431), or {"DataTypeHistogram": [numNull, numFractional, numIntegral,
 numBoolean, numString]} for DataType (its HistogramMetric is DataTypeHistogram.toDistribution of
-that state, DataType.scala:98-114).  `needs` lists GPU-path capabilities a case depends on beyond
-numeric columns (e.g. a string predicate), so tests can route/skip with a reason.
+that state, DataType.scala:98-114).  `needs` lists GPU-path capabilities a case depends on that the GPU path does not
+have (e.g. a regex outside the GPU subset), so tests expect the fallback route for it.
 """
 import json
 import os
@@ -152,18 +152,18 @@ cases = [
     ("dfFull", ["Size", N], 4.0, S + ":39-42", []),
     ("dfMissing", ["Completeness", "att1", N], 0.5, S + ":52-53", []),
     ("dfMissing", ["Completeness", "att2", N], 0.75, S + ":54-55", []),
-    ("dfMissing", ["Completeness", "att1", "item IN ('1', '2')"], 1.0, S + ":73-74", ["string_predicate"]),
+    ("dfMissing", ["Completeness", "att1", "item IN ('1', '2')"], 1.0, S + ":73-74", []),
     # Compliance
     ("dfWithNumericValues", ["Compliance", "rule1", "att1 > 3", N], 3.0 / 6, S + ":175-176", []),
     ("dfWithNumericValues", ["Compliance", "rule2", "att1 > 2", N], 4.0 / 6, S + ":177-178", []),
     ("dfWithNumericValues", ["Compliance", "rule1", "att2 = 0", "att1 < 4"], 1.0, S + ":184-185", []),
     # basic statistics
     ("dfWithNumericValues", ["Mean", "att1", N], 3.5, S + ":427-428", []),
-    ("dfWithNumericValues", ["Mean", "att1", "item != '6'"], 3.0, S + ":437-438", ["string_predicate"]),
+    ("dfWithNumericValues", ["Mean", "att1", "item != '6'"], 3.0, S + ":437-438", []),
     ("dfWithNumericValues", ["StandardDeviation", "att1", N], 1.707825127659933, S + ":443-444", []),
     ("dfWithNumericValues", ["Minimum", "att1", N], 1.0, S + ":453-454", []),
     ("dfWithNumericValues", ["Maximum", "att1", N], 6.0, S + ":463-464", []),
-    ("dfWithNumericValues", ["Maximum", "att1", "item != '6'"], 5.0, S + ":470-471", ["string_predicate"]),
+    ("dfWithNumericValues", ["Maximum", "att1", "item != '6'"], 5.0, S + ":470-471", []),
     ("dfWithNumericValues", ["Sum", "att1", N], 21.0, S + ":481", []),
     # HLL
     ("dfWithUniqueColumns", ["ApproxCountDistinct", "uniqueWithNulls", N], 5.0, S + ":509-513", []),
@@ -217,7 +217,7 @@ cases = [
     # incremental (analyzers/IncrementalAnalyzerTest.scala:49-99)
     ("incrementalInitial", ["Size", N], 3.0, "analyzers/IncrementalAnalyzerTest.scala:58", []),
     ("incrementalInitial", ["Completeness", "att1", N], 0.6666666666666666, "analyzers/IncrementalAnalyzerTest.scala:96", []),
-    ("incrementalInitial", ["Compliance", "att1", "att1 = 'b'", N], 0.3333333333333333, "analyzers/IncrementalAnalyzerTest.scala:77", ["string_predicate"]),
+    ("incrementalInitial", ["Compliance", "att1", "att1 = 'b'", N], 0.3333333333333333, "analyzers/IncrementalAnalyzerTest.scala:77", []),
     # PatternMatch: "regex_fallback" = outside the GPU regex subset / a non-string column (Spark path)
     ("patternDoubles", ["PatternMatch", "some", r"\d\.\d", N], 0.75, S + ":628-631", ["regex_fallback"]),
     ("patternIntegers", ["PatternMatch", "some", r"\d", N], 0.5, S + ":634-637", []),

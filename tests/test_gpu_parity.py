@@ -700,3 +700,37 @@ def test_pattern_match_fallback_in_fused_run(dq):
     ctx = dq.AnalysisRunner.onData(t).addAnalyzers([ssn, url, dq.Size()]).run()
     assert isinstance(ctx.metric(ssn).value.failed, UnsupportedOnGpuPathException)
     assert ctx.metric(url).value.get() == 0.0 and ctx.metric(dq.Size()).value.get() == 4.0
+
+
+@pytest.mark.parametrize("n", [1, 513, 70_001])
+def test_string_predicates_vs_oracle(dq, n):
+    """String (in)equality / IN / NOT IN on UTF8 columns (whole-value DFAs in the predicate pass) as
+    Compliance predicates and as `where` filters of value analyzers, three-valued, vs the oracle."""
+    from deequ_amd.runner import scan_states
+    from deequ_amd.table import column_from_numpy, utf8_column
+
+    rng = np.random.default_rng(99 + n)
+    pool = ["a", "b", "ab", "", "é€", "a b", "a\n", "US", "DE"]
+    strs = [None if rng.random() < 0.15 else pool[int(rng.integers(0, len(pool)))].encode() for _ in range(n)]
+    x = rng.normal(10, 3, n)
+    t = dq.Table([utf8_column("s", strs), utf8_column("t", strs[::-1], large=True),
+                  column_from_numpy("x", "f64", x, rng.random(n) >= 0.1)])
+    analyzers = [dq.Compliance("eq", "s = 'a'"), dq.Compliance("ne", "s != 'ab'"),
+                 dq.Compliance("in", "s IN ('a', 'é€', '')"), dq.Compliance("nin", "t NOT IN ('US', 'DE')"),
+                 dq.Compliance("mix", "x > 10 OR s = 'a b'"), dq.Mean("x", "s IN ('a', 'b')"),
+                 dq.Maximum("x", "t != 'a'"), dq.Completeness("t", "s = 'DE'"), dq.Size("s <> 'US'"),
+                 dq.ApproxCountDistinct("s", "t = 'b'")]
+    got = scan_states(t, analyzers)
+    host = {name: host_column(c, n) for name, c in t.columns.items()}
+    ocols = {name: O.OColumn(t.columns[name].dtype.replace("large_", ""), host[name][0], host[name][1])
+             for name in t.columns}
+    for an in analyzers:
+        kind = type(an).__name__
+        if kind == "Compliance":
+            spec = ("Compliance", an.instance, an.predicate, an.where)
+        elif kind == "Size":
+            spec = ("Size", an.where)
+        else:
+            spec = (kind, an.column, an.where)
+        ref = O.compute_state(spec, ocols, n)
+        assert_state_close(got[an], ref, scale=float(np.abs(x).sum()))

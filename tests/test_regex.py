@@ -144,3 +144,34 @@ def test_fallback_routing(lib):
             a._lower(b)
     op, ca, cb, root, where = lib.PatternMatch("s", lib.Patterns.EMAIL, "f > 0")._lower(b)
     assert root >= 0 and where >= 0 and b.pool.patterns == [lib.Patterns.EMAIL]
+
+
+@pytest.mark.parametrize("lits", [["a"], ["1", "2"], [""], ["a.b", "c d", "é€", "x|y", "(z)", "q*"], ["ab", "abc", "a"]])
+def test_string_in_full_match(lib, lits):
+    """`col IN (...)` / `col = '...'` lower to a whole-value DFA over the escaped literals: byte
+    equality with any literal, nothing else (no search, no trailing-terminator allowance)."""
+    from deequ_amd import _lib as L
+    from deequ_amd.analyzers import PlanBuilder
+
+    b = PlanBuilder([("s", "utf8", True)])
+    b.pred("s IN (" + ", ".join("'" + x + "'" for x in lits) + ")")
+    pattern = b.pool.patterns[-1]
+    values = [x.encode() for x in lits] + [x.encode() + b"\n" for x in lits] + [b"x" + x.encode() for x in lits] + \
+        _strings(11, 200) + [b"", b"a", b"ab\n", b"c d", b"x|y"]
+    st, got = _host_match(lib, pattern, L.REGEX_FULL, values)
+    assert st == 0, L.lib.dq_last_error()
+    want = [v in {x.encode() for x in lits} for v in values]
+    assert list(got) == want
+
+
+def test_string_predicate_grammar(lib):
+    from deequ_amd.analyzers import PlanBuilder
+    from deequ_amd.predicates import UnsupportedPredicate
+
+    b = PlanBuilder([("s", "utf8", True), ("n", "i64", True)])
+    for ok in ("s = 'x'", "'x' = s", "s != 'x'", "s <> 'x'", "s IN ('a', 'b')", "s NOT IN ('a')",
+               "n > 0 AND s = 'q'", "NOT s IN ('a', \"b\")"):
+        b.pred(ok)
+    for bad in ("n = 'x'", "s < 'x'", "s LIKE 'a%'", "'a' = 'b'", "s = 'a\\\\b'", "s IN (1, 2)", "s RLIKE 'x'"):
+        with pytest.raises(UnsupportedPredicate):
+            b.pred(bad)
