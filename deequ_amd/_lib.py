@@ -124,6 +124,11 @@ class _StateUnion(ctypes.Union):
                 ("minmax", _MinMax), ("corr", _Corr), ("hll", _Hll), ("dtype", _DType)]
 
 
+class FreqSummary(ctypes.Structure):
+    _fields_ = [("num_groups", ctypes.c_int64), ("num_unique", ctypes.c_int64), ("num_values", ctypes.c_int64),
+                ("entropy", ctypes.c_double)]
+
+
 class State(ctypes.Structure):
     _fields_ = [("op", ctypes.c_int32), ("has_value", ctypes.c_uint8 * 2), ("reserved", ctypes.c_uint8 * 2),
                 ("u", _StateUnion)]
@@ -159,6 +164,19 @@ def _load():
     L.dq_regex_info.argtypes = [c.c_char_p, c.c_int32, P(c.c_int32), P(c.c_int32)]
     L.dq_regex_match_host.restype = c.c_int32
     L.dq_regex_match_host.argtypes = [c.c_char_p, c.c_int32, c.c_void_p, c.c_void_p, c.c_int64, c.c_void_p]
+    L.dq_freq_build.restype = c.c_int32
+    L.dq_freq_build.argtypes = [P(c.c_int32), c.c_int32, P(ColumnView), P(c.c_int64), c.c_int32, c.c_int32,
+                                c.c_void_p, P(c.c_void_p)]
+    L.dq_freq_merge.restype = c.c_int32
+    L.dq_freq_merge.argtypes = [c.c_void_p, c.c_void_p, P(c.c_void_p)]
+    L.dq_freq_summarize.restype = c.c_int32
+    L.dq_freq_summarize.argtypes = [c.c_void_p, c.c_int64, P(FreqSummary)]
+    L.dq_freq_num_groups.restype = c.c_int64
+    L.dq_freq_num_groups.argtypes = [c.c_void_p]
+    L.dq_freq_export.restype = c.c_int32
+    L.dq_freq_export.argtypes = [c.c_void_p, c.c_void_p, c.c_void_p, c.c_int64]
+    L.dq_freq_destroy.restype = None
+    L.dq_freq_destroy.argtypes = [c.c_void_p]
     L.dq_plan_set_stream.restype = c.c_int32
     L.dq_plan_set_stream.argtypes = [c.c_void_p, c.c_void_p]
     L.dq_scan.restype = c.c_int32
@@ -205,7 +223,8 @@ lib = _load()
 # every symbol include/dqscan.h declares (checked by tests/test_boundary.py)
 EXPORTED = [
     "dq_abi_version", "dq_last_error", "dq_plan_create", "dq_plan_create_ex", "dq_regex_info", "dq_regex_match_host",
-    "dq_plan_set_stream", "dq_scan", "dq_finish",
+    "dq_plan_set_stream", "dq_freq_build", "dq_freq_merge", "dq_freq_summarize", "dq_freq_num_groups",
+    "dq_freq_export", "dq_freq_destroy", "dq_scan", "dq_finish",
     "dq_plan_reset", "dq_plan_destroy", "dq_plan_bytes_per_row_x1000", "dq_plan_num_launches",
     "dq_plan_enable_timing", "dq_plan_kernel_time", "dq_plan_variant_bytes_per_row_x1000",
     "dq_state_merge", "dq_state_combine", "dq_state_is_defined", "dq_state_metric", "dq_hll_estimate",

@@ -1,0 +1,432 @@
+// dq_group.hip -- frequencies of the grouping analyzers on the GPU (sort-based group-by count).
+//
+// Reference: FrequencyBasedAnalyzer.computeFrequencies (analyzers/GroupingAnalyzers.scala:44-82):
+//   SELECT cols, COUNT(*) FROM data WHERE col_1 IS NOT NULL AND ... GROUP BY cols
+// plus numRows = data.count(), and the metrics of Uniqueness / Distinctness / CountDistinct /
+// Entropy / UniqueValueRatio, which only need the multiset of group counts (Uniqueness.scala:27-29,
+// Distinctness.scala:29-31, CountDistinct.scala:25-31, Entropy.scala:29-41, UniqueValueRatio.scala:25-36).
+// FrequenciesAndNumRows.sum (GroupingAnalyzers.scala:118-138) = outer join adding counts.
+//
+// Layout: every row whose grouping columns are all non-null yields one 64-bit key.  A single 8-byte /
+// 4-byte numeric column is its own exact key (f64: NaN canonicalised as Spark's UnsafeRow.setDouble
+// does; -0.0 and 0.0 stay distinct groups in Spark 2.2).  Otherwise (strings, several columns) the key
+// is a 64-bit hash of the tuple, the rows ride along the sort, and every pair of neighbours with equal
+// keys is compared exactly: a collision between distinct tuples is reported (DQ_E_UNSUPPORTED), never
+// merged silently.  Keys are radix-sorted (hipCUB) and run-length encoded into (key, count) groups;
+// the summary is a fixed-order two-level reduction, so results are deterministic.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <cstring>
+#include <memory>
+#include <vector>
+
+#include "dq_device.h"
+#include "dq_hash.h"
+#include "dq_internal.h"
+
+namespace dq {
+namespace {
+
+constexpr int kMaxGroupCols = 8;
+constexpr int kMaxGroupChunks = 4096;
+constexpr int kRowBits = 40;  // row id = chunk << 40 | row
+
+struct GroupCols {
+  const void* values[kMaxGroupCols];
+  const uint32_t* validity[kMaxGroupCols];
+  const void* offsets[kMaxGroupCols];
+  int32_t type[kMaxGroupCols];
+  int32_t n_cols;
+};
+
+__device__ __forceinline__ bool row_valid(const GroupCols& g, int64_t r) {
+  for (int c = 0; c < g.n_cols; ++c)
+    if (g.validity[c] && !((g.validity[c][r >> 5] >> (r & 31)) & 1u)) return false;
+  return true;
+}
+
+__device__ __forceinline__ uint64_t canon_f64(uint64_t bits) {
+  const uint64_t mag = bits & 0x7FFFFFFFFFFFFFFFull;
+  return mag > 0x7FF0000000000000ull ? 0x7FF8000000000000ull : bits;  // any NaN -> Double.NaN
+}
+
+__device__ __forceinline__ uint64_t value_bits(const GroupCols& g, int c, int64_t r) {
+  switch (g.type[c]) {
+    case DQ_TYPE_F64: return canon_f64(reinterpret_cast<const uint64_t*>(g.values[c])[r]);
+    case DQ_TYPE_I64: return reinterpret_cast<const uint64_t*>(g.values[c])[r];
+    default: return (uint64_t)(int64_t)reinterpret_cast<const int32_t*>(g.values[c])[r];
+  }
+}
+
+__device__ __forceinline__ void str_of(const GroupCols& g, int c, int64_t r, const uint8_t*& p, int64_t& len) {
+  int64_t o0, o1;
+  if (g.type[c] == DQ_TYPE_LARGE_UTF8) {
+    o0 = reinterpret_cast<const int64_t*>(g.offsets[c])[r];
+    o1 = reinterpret_cast<const int64_t*>(g.offsets[c])[r + 1];
+  } else {
+    o0 = reinterpret_cast<const int32_t*>(g.offsets[c])[r];
+    o1 = reinterpret_cast<const int32_t*>(g.offsets[c])[r + 1];
+  }
+  p = reinterpret_cast<const uint8_t*>(g.values[c]) + o0;
+  len = o1 - o0;
+}
+
+__device__ __forceinline__ uint64_t mix8(uint64_t h, uint64_t k) {
+  return mul_add_c(rotl64(h ^ mul_add_c(k, XP2, 0), 27), XP1, XP4);
+}
+
+// 64-bit hash of the row's tuple (columns in order; strings by bytes and length)
+__device__ uint64_t tuple_hash(const GroupCols& g, int64_t r) {
+  uint64_t h = kSeed + XP5;
+  for (int c = 0; c < g.n_cols; ++c) {
+    if (g.type[c] == DQ_TYPE_UTF8 || g.type[c] == DQ_TYPE_LARGE_UTF8) {
+      const uint8_t* p;
+      int64_t len;
+      str_of(g, c, r, p, len);
+      int64_t i = 0;
+      for (; i + 8 <= len; i += 8) {
+        uint64_t k = 0;
+        for (int b = 0; b < 8; ++b) k |= (uint64_t)p[i + b] << (8 * b);
+        h = mix8(h, k);
+      }
+      uint64_t k = 0;
+      for (int b = 0; i + b < len; ++b) k |= (uint64_t)p[i + b] << (8 * b);
+      h = mix8(h, k ^ ((uint64_t)len << 56) ^ 0xA5);
+    } else {
+      h = mix8(h, value_bits(g, c, r));
+    }
+  }
+  return fmix64(h);
+}
+
+__device__ bool tuple_equal(const GroupCols* chunks, uint64_t ra, uint64_t rb) {
+  const GroupCols& ga = chunks[ra >> kRowBits];
+  const GroupCols& gb = chunks[rb >> kRowBits];
+  const int64_t a = (int64_t)(ra & ((1ull << kRowBits) - 1)), b = (int64_t)(rb & ((1ull << kRowBits) - 1));
+  for (int c = 0; c < ga.n_cols; ++c) {
+    if (ga.type[c] == DQ_TYPE_UTF8 || ga.type[c] == DQ_TYPE_LARGE_UTF8) {
+      const uint8_t *pa, *pb;
+      int64_t la, lb;
+      str_of(ga, c, a, pa, la);
+      str_of(gb, c, b, pb, lb);
+      if (la != lb) return false;
+      for (int64_t i = 0; i < la; ++i)
+        if (pa[i] != pb[i]) return false;
+    } else if (value_bits(ga, c, a) != value_bits(gb, c, b)) {
+      return false;
+    }
+  }
+  return true;
+}
+
+// one key (+ flag) per row of a chunk
+__global__ void group_keys(GroupCols g, int64_t n, int32_t hashed, uint64_t* __restrict__ keys,
+                           uint8_t* __restrict__ flags) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+    const bool v = row_valid(g, r);
+    flags[r] = v ? 1 : 0;
+    keys[r] = !v ? 0 : (hashed ? tuple_hash(g, r) : value_bits(g, 0, r));
+  }
+}
+
+__global__ void row_ids(int64_t chunk, int64_t n, uint64_t* __restrict__ out) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x)
+    out[r] = ((uint64_t)chunk << kRowBits) | (uint64_t)r;
+}
+
+// neighbours with equal hash keys must hold equal tuples
+__global__ void verify_runs(const uint64_t* __restrict__ keys, const uint64_t* __restrict__ rows, int64_t n,
+                            const GroupCols* __restrict__ chunks, int32_t* __restrict__ collision) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x + 1; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    if (keys[i] == keys[i - 1] && !tuple_equal(chunks, rows[i], rows[i - 1])) atomicOr(collision, 1);
+}
+
+constexpr int kSumBlocks = 1024;
+struct SumPart { int64_t unique; double ent; };
+
+// fixed-order partials: block b sums groups b, b + kSumBlocks, ... in a fixed tree
+__global__ __launch_bounds__(256) void summary_part(const int64_t* __restrict__ counts, int64_t n, double num_rows,
+                                                    SumPart* __restrict__ part) {
+  __shared__ int64_t su[256];
+  __shared__ double se[256];
+  int64_t u = 0;
+  double e = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const double c = (double)counts[i];
+    u += counts[i] == 1 ? 1 : 0;
+    // Entropy.scala:31-37: -(count / numRows) * ln(count / numRows), 0 for a zero count
+    if (c != 0.0) e += -(c / num_rows) * log(c / num_rows);
+  }
+  su[threadIdx.x] = u;
+  se[threadIdx.x] = e;
+  __syncthreads();
+  for (int s = 128; s >= 1; s >>= 1) {
+    if ((int)threadIdx.x < s) { su[threadIdx.x] += su[threadIdx.x + s]; se[threadIdx.x] += se[threadIdx.x + s]; }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = SumPart{su[0], se[0]};
+}
+
+__global__ void summary_final(const SumPart* __restrict__ part, int32_t nparts, SumPart* __restrict__ out) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    SumPart t{0, 0.0};
+    for (int i = 0; i < nparts; ++i) { t.unique += part[i].unique; t.ent += part[i].ent; }
+    *out = t;
+  }
+}
+
+#define GHIP(x)                                                                                  \
+  do {                                                                                           \
+    hipError_t e_ = (x);                                                                         \
+    if (e_ != hipSuccess) return set_error(DQ_E_HIP, "%s: %s", #x, hipGetErrorString(e_));      \
+  } while (0)
+
+struct DevBuf {  // hipMalloc'd scratch, freed on scope exit
+  void* p = nullptr;
+  ~DevBuf() { if (p) (void)hipFree(p); }
+  dq_status alloc(size_t bytes) {
+    if (p) { (void)hipFree(p); p = nullptr; }
+    if (hipMalloc(&p, bytes ? bytes : 16) != hipSuccess) return set_error(DQ_E_OOM, "hipMalloc(%zu) failed", bytes);
+    return DQ_OK;
+  }
+  template <typename T> T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+int grid_for(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>(8192, (n + 255) / 256)); }
+
+}  // namespace
+}  // namespace dq
+
+using namespace dq;
+
+struct dq_freq_table {
+  int32_t device = 0;
+  hipStream_t stream = nullptr;
+  int32_t hashed = 0;
+  std::vector<int32_t> types;
+  int64_t n_groups = 0;
+  int64_t n_values = 0;  // rows with all grouping columns non-null
+  uint64_t* d_keys = nullptr;
+  int64_t* d_counts = nullptr;
+  ~dq_freq_table() {
+    if (d_keys) (void)hipFree(d_keys);
+    if (d_counts) (void)hipFree(d_counts);
+  }
+};
+
+static dq_status rle_into(dq_freq_table* t, const uint64_t* sorted, int64_t n) {
+  DevBuf nruns, tmp;
+  if (dq_status s = nruns.alloc(sizeof(int64_t))) return s;
+  GHIP(hipMalloc(&t->d_keys, std::max<int64_t>(1, n) * sizeof(uint64_t)));
+  GHIP(hipMalloc(&t->d_counts, std::max<int64_t>(1, n) * sizeof(int64_t)));
+  if (n == 0) { t->n_groups = 0; return DQ_OK; }
+  size_t tb = 0;
+  GHIP(hipcub::DeviceRunLengthEncode::Encode(nullptr, tb, sorted, t->d_keys, t->d_counts, nruns.as<int64_t>(),
+                                             (int)n, t->stream));
+  if (dq_status s = tmp.alloc(tb)) return s;
+  GHIP(hipcub::DeviceRunLengthEncode::Encode(tmp.p, tb, sorted, t->d_keys, t->d_counts, nruns.as<int64_t>(),
+                                             (int)n, t->stream));
+  GHIP(hipMemcpyAsync(&t->n_groups, nruns.p, sizeof(int64_t), hipMemcpyDeviceToHost, t->stream));
+  GHIP(hipStreamSynchronize(t->stream));
+  return DQ_OK;
+}
+
+extern "C" {
+
+dq_status dq_freq_build(const int32_t* types, int32_t n_cols, const dq_column_view* cols, const int64_t* chunk_rows,
+                        int32_t n_chunks, int32_t device, void* hip_stream, dq_freq_table** out) {
+  if (!out) return set_error(DQ_E_INVALID, "dq_freq_build: out is NULL");
+  *out = nullptr;
+  if (n_cols < 1 || n_cols > kMaxGroupCols || !types)
+    return set_error(DQ_E_INVALID, "dq_freq_build: 1..%d grouping columns", kMaxGroupCols);
+  if (n_chunks < 0 || n_chunks > kMaxGroupChunks || (n_chunks > 0 && (!cols || !chunk_rows)))
+    return set_error(DQ_E_INVALID, "dq_freq_build: bad chunks (at most %d)", kMaxGroupChunks);
+  for (int c = 0; c < n_cols; ++c)
+    if (types[c] < DQ_TYPE_F64 || types[c] > DQ_TYPE_LARGE_UTF8)
+      return set_error(DQ_E_TYPE, "dq_freq_build: column %d has unknown type %d", c, types[c]);
+  int64_t total = 0;
+  for (int k = 0; k < n_chunks; ++k) {
+    if (chunk_rows[k] < 0 || chunk_rows[k] >= (1ll << kRowBits)) return set_error(DQ_E_INVALID, "chunk rows");
+    total += chunk_rows[k];
+  }
+  if (total >= (1ll << 31)) return set_error(DQ_E_UNSUPPORTED, "dq_freq_build: at most 2^31 - 1 rows per table");
+  GHIP(hipSetDevice(device));
+  auto* t = new dq_freq_table();
+  std::unique_ptr<dq_freq_table> guard(t);
+  t->device = device;
+  t->stream = reinterpret_cast<hipStream_t>(hip_stream);
+  t->types.assign(types, types + n_cols);
+  const bool numeric1 = n_cols == 1 && (types[0] == DQ_TYPE_F64 || types[0] == DQ_TYPE_I64 || types[0] == DQ_TYPE_I32);
+  t->hashed = numeric1 ? 0 : 1;
+
+  std::vector<GroupCols> gcs(std::max(1, n_chunks));
+  for (int k = 0; k < n_chunks; ++k) {
+    GroupCols& g = gcs[k];
+    std::memset(&g, 0, sizeof(g));
+    g.n_cols = n_cols;
+    for (int c = 0; c < n_cols; ++c) {
+      const dq_column_view& v = cols[(size_t)k * n_cols + c];
+      g.values[c] = v.values;
+      g.validity[c] = reinterpret_cast<const uint32_t*>(v.validity);
+      g.offsets[c] = v.offsets;
+      g.type[c] = types[c];
+    }
+  }
+  DevBuf keys, flags, sel_keys, rows_all, sel_rows, nsel, tmp, sorted_keys, sorted_rows, d_chunks;
+  int64_t maxn = 1;
+  for (int k = 0; k < n_chunks; ++k) maxn = std::max<int64_t>(maxn, chunk_rows[k]);
+  if (dq_status s = keys.alloc(maxn * 8)) return s;
+  if (dq_status s = flags.alloc(maxn)) return s;
+  if (dq_status s = nsel.alloc(8)) return s;
+  if (dq_status s = sel_keys.alloc(std::max<int64_t>(1, total) * 8)) return s;
+  if (t->hashed) {
+    if (dq_status s = rows_all.alloc(maxn * 8)) return s;
+    if (dq_status s = sel_rows.alloc(std::max<int64_t>(1, total) * 8)) return s;
+  }
+  int64_t nv = 0;
+  for (int k = 0; k < n_chunks; ++k) {
+    const int64_t n = chunk_rows[k];
+    if (n == 0) continue;
+    hipLaunchKernelGGL(group_keys, dim3(grid_for(n)), dim3(256), 0, t->stream, gcs[k], n, t->hashed,
+                       keys.as<uint64_t>(), flags.as<uint8_t>());
+    GHIP(hipGetLastError());
+    size_t tb = 0;
+    GHIP(hipcub::DeviceSelect::Flagged(nullptr, tb, keys.as<uint64_t>(), flags.as<uint8_t>(),
+                                       sel_keys.as<uint64_t>() + nv, nsel.as<int64_t>(), (int)n, t->stream));
+    if (dq_status s = tmp.alloc(tb)) return s;
+    GHIP(hipcub::DeviceSelect::Flagged(tmp.p, tb, keys.as<uint64_t>(), flags.as<uint8_t>(),
+                                       sel_keys.as<uint64_t>() + nv, nsel.as<int64_t>(), (int)n, t->stream));
+    if (t->hashed) {
+      hipLaunchKernelGGL(row_ids, dim3(grid_for(n)), dim3(256), 0, t->stream, (int64_t)k, n, rows_all.as<uint64_t>());
+      GHIP(hipGetLastError());
+      GHIP(hipcub::DeviceSelect::Flagged(tmp.p, tb, rows_all.as<uint64_t>(), flags.as<uint8_t>(),
+                                         sel_rows.as<uint64_t>() + nv, nsel.as<int64_t>(), (int)n, t->stream));
+    }
+    int64_t got = 0;
+    GHIP(hipMemcpyAsync(&got, nsel.p, 8, hipMemcpyDeviceToHost, t->stream));
+    GHIP(hipStreamSynchronize(t->stream));
+    nv += got;
+  }
+  t->n_values = nv;
+  if (dq_status s = sorted_keys.alloc(std::max<int64_t>(1, nv) * 8)) return s;
+  if (nv > 0) {
+    size_t tb = 0;
+    if (t->hashed) {
+      if (dq_status s = sorted_rows.alloc(nv * 8)) return s;
+      GHIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, sel_keys.as<uint64_t>(), sorted_keys.as<uint64_t>(),
+                                              sel_rows.as<uint64_t>(), sorted_rows.as<uint64_t>(), (int)nv, 0, 64,
+                                              t->stream));
+      if (dq_status s = tmp.alloc(tb)) return s;
+      GHIP(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, sel_keys.as<uint64_t>(), sorted_keys.as<uint64_t>(),
+                                              sel_rows.as<uint64_t>(), sorted_rows.as<uint64_t>(), (int)nv, 0, 64,
+                                              t->stream));
+      // exact check of equal-hash neighbours
+      if (dq_status s = d_chunks.alloc(gcs.size() * sizeof(GroupCols))) return s;
+      GHIP(hipMemcpyAsync(d_chunks.p, gcs.data(), gcs.size() * sizeof(GroupCols), hipMemcpyHostToDevice, t->stream));
+      GHIP(hipMemsetAsync(nsel.p, 0, 8, t->stream));
+      hipLaunchKernelGGL(verify_runs, dim3(grid_for(nv)), dim3(256), 0, t->stream, sorted_keys.as<uint64_t>(),
+                         sorted_rows.as<uint64_t>(), nv, d_chunks.as<GroupCols>(), nsel.as<int32_t>());
+      GHIP(hipGetLastError());
+      int32_t coll = 0;
+      GHIP(hipMemcpyAsync(&coll, nsel.p, 4, hipMemcpyDeviceToHost, t->stream));
+      GHIP(hipStreamSynchronize(t->stream));
+      if (coll) return set_error(DQ_E_UNSUPPORTED, "dq_freq_build: 64-bit tuple-hash collision between distinct values");
+    } else {
+      GHIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, sel_keys.as<uint64_t>(), sorted_keys.as<uint64_t>(),
+                                             (int)nv, 0, 64, t->stream));
+      if (dq_status s = tmp.alloc(tb)) return s;
+      GHIP(hipcub::DeviceRadixSort::SortKeys(tmp.p, tb, sel_keys.as<uint64_t>(), sorted_keys.as<uint64_t>(), (int)nv,
+                                             0, 64, t->stream));
+    }
+  }
+  if (dq_status s = rle_into(t, sorted_keys.as<uint64_t>(), nv)) return s;
+  *out = guard.release();
+  return DQ_OK;
+}
+
+dq_status dq_freq_merge(const dq_freq_table* a, const dq_freq_table* b, dq_freq_table** out) {
+  if (!a || !b || !out) return set_error(DQ_E_INVALID, "dq_freq_merge: NULL argument");
+  *out = nullptr;
+  if (a->types != b->types || a->hashed != b->hashed)
+    return set_error(DQ_E_STATE, "dq_freq_merge: frequency tables over different column types");
+  GHIP(hipSetDevice(a->device));
+  auto* t = new dq_freq_table();
+  std::unique_ptr<dq_freq_table> guard(t);
+  t->device = a->device;
+  t->stream = a->stream;
+  t->types = a->types;
+  t->hashed = a->hashed;
+  t->n_values = a->n_values + b->n_values;
+  const int64_t n = a->n_groups + b->n_groups;
+  DevBuf k_in, c_in, k_s, c_s, nruns, tmp;
+  for (DevBuf* d : {&k_in, &c_in, &k_s, &c_s})
+    if (dq_status s = d->alloc(std::max<int64_t>(1, n) * 8)) return s;
+  if (dq_status s = nruns.alloc(8)) return s;
+  GHIP(hipMemcpyAsync(k_in.p, a->d_keys, a->n_groups * 8, hipMemcpyDeviceToDevice, t->stream));
+  GHIP(hipMemcpyAsync(k_in.as<uint64_t>() + a->n_groups, b->d_keys, b->n_groups * 8, hipMemcpyDeviceToDevice, t->stream));
+  GHIP(hipMemcpyAsync(c_in.p, a->d_counts, a->n_groups * 8, hipMemcpyDeviceToDevice, t->stream));
+  GHIP(hipMemcpyAsync(c_in.as<int64_t>() + a->n_groups, b->d_counts, b->n_groups * 8, hipMemcpyDeviceToDevice, t->stream));
+  GHIP(hipMalloc(&t->d_keys, std::max<int64_t>(1, n) * 8));
+  GHIP(hipMalloc(&t->d_counts, std::max<int64_t>(1, n) * 8));
+  if (n > 0) {
+    size_t tb = 0;
+    GHIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k_in.as<uint64_t>(), k_s.as<uint64_t>(), c_in.as<int64_t>(),
+                                            c_s.as<int64_t>(), (int)n, 0, 64, t->stream));
+    if (dq_status s = tmp.alloc(tb)) return s;
+    GHIP(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, k_in.as<uint64_t>(), k_s.as<uint64_t>(), c_in.as<int64_t>(),
+                                            c_s.as<int64_t>(), (int)n, 0, 64, t->stream));
+    tb = 0;
+    GHIP(hipcub::DeviceReduce::ReduceByKey(nullptr, tb, k_s.as<uint64_t>(), t->d_keys, c_s.as<int64_t>(), t->d_counts,
+                                           nruns.as<int64_t>(), hipcub::Sum(), (int)n, t->stream));
+    if (dq_status s = tmp.alloc(tb)) return s;
+    GHIP(hipcub::DeviceReduce::ReduceByKey(tmp.p, tb, k_s.as<uint64_t>(), t->d_keys, c_s.as<int64_t>(), t->d_counts,
+                                           nruns.as<int64_t>(), hipcub::Sum(), (int)n, t->stream));
+    GHIP(hipMemcpyAsync(&t->n_groups, nruns.p, 8, hipMemcpyDeviceToHost, t->stream));
+  }
+  GHIP(hipStreamSynchronize(t->stream));
+  *out = guard.release();
+  return DQ_OK;
+}
+
+dq_status dq_freq_summarize(const dq_freq_table* t, int64_t num_rows, dq_freq_summary* out) {
+  if (!t || !out) return set_error(DQ_E_INVALID, "dq_freq_summarize: NULL argument");
+  GHIP(hipSetDevice(t->device));
+  std::memset(out, 0, sizeof(*out));
+  out->num_groups = t->n_groups;
+  out->num_values = t->n_values;
+  if (t->n_groups == 0) return DQ_OK;
+  DevBuf part, res;
+  if (dq_status s = part.alloc(kSumBlocks * sizeof(SumPart))) return s;
+  if (dq_status s = res.alloc(sizeof(SumPart))) return s;
+  const int nb = (int)std::min<int64_t>(kSumBlocks, (t->n_groups + 255) / 256);
+  hipLaunchKernelGGL(summary_part, dim3(nb), dim3(256), 0, t->stream, t->d_counts, t->n_groups, (double)num_rows,
+                     part.as<SumPart>());
+  GHIP(hipGetLastError());
+  hipLaunchKernelGGL(summary_final, dim3(1), dim3(64), 0, t->stream, part.as<SumPart>(), nb, res.as<SumPart>());
+  GHIP(hipGetLastError());
+  SumPart h{};
+  GHIP(hipMemcpyAsync(&h, res.p, sizeof(h), hipMemcpyDeviceToHost, t->stream));
+  GHIP(hipStreamSynchronize(t->stream));
+  out->num_unique = h.unique;
+  out->entropy = h.ent;
+  return DQ_OK;
+}
+
+int64_t dq_freq_num_groups(const dq_freq_table* t) { return t ? t->n_groups : -1; }
+
+dq_status dq_freq_export(const dq_freq_table* t, uint64_t* keys, int64_t* counts, int64_t cap) {
+  if (!t || cap < t->n_groups || (t->n_groups > 0 && (!keys || !counts)))
+    return set_error(DQ_E_INVALID, "dq_freq_export: bad arguments");
+  GHIP(hipSetDevice(t->device));
+  if (t->n_groups > 0) {
+    GHIP(hipMemcpyAsync(keys, t->d_keys, t->n_groups * 8, hipMemcpyDeviceToHost, t->stream));
+    GHIP(hipMemcpyAsync(counts, t->d_counts, t->n_groups * 8, hipMemcpyDeviceToHost, t->stream));
+  }
+  GHIP(hipStreamSynchronize(t->stream));
+  return DQ_OK;
+}
+
+void dq_freq_destroy(dq_freq_table* t) { delete t; }
+
+}  // extern "C"

@@ -201,8 +201,39 @@ class AnalysisRunner:
                 passed.append(a)
             else:
                 failures[a] = a.toFailureMetric(err)
-        ctx = AnalysisRunner.runScanningAnalyzers(data, passed, aggregateWith, saveStatesWith)
+        grouping = [a for a in passed if getattr(a, "grouping", False)]
+        scanning = [a for a in passed if not getattr(a, "grouping", False)]
+        ctx = AnalysisRunner.runScanningAnalyzers(data, scanning, aggregateWith, saveStatesWith)
+        by_cols: Dict[tuple, List[Analyzer]] = {}
+        for a in grouping:  # AnalysisRunner.scala:160-180: one frequency computation per column set
+            by_cols.setdefault(tuple(a.groupingColumns()), []).append(a)
+        for cols, group in by_cols.items():
+            ctx = ctx + AnalysisRunner.runGroupingAnalyzers(data, list(cols), group, aggregateWith, saveStatesWith)
         return AnalyzerContext(failures) + ctx
+
+    @staticmethod
+    def runGroupingAnalyzers(data, columns, analyzers, aggregateWith=None, saveStatesWith=None) -> AnalyzerContext:
+        """AnalysisRunner.scala:249-277 and runAnalyzersForParticularGrouping: frequencies once (GPU),
+        the state of the first analyzer merged with a loaded one, persisted for every analyzer."""
+        from .grouping import build_frequencies
+
+        try:
+            state = build_frequencies(data, columns)
+            if aggregateWith is not None:
+                prev = aggregateWith.load(analyzers[0])
+                if prev is not None:
+                    state = state.sum(prev)
+        except Exception as e:
+            return AnalyzerContext({a: a.toFailureMetric(e) for a in analyzers})
+        metrics = {}
+        for a in analyzers:
+            try:
+                if saveStatesWith is not None:
+                    saveStatesWith.persist(a, state)
+                metrics[a] = a.computeMetricFrom(state)
+            except Exception as e:
+                metrics[a] = a.toFailureMetric(e)
+        return AnalyzerContext(metrics)
 
     @staticmethod
     def runScanningAnalyzers(data, analyzers: Sequence[Analyzer], aggregateWith=None,

@@ -205,6 +205,29 @@ dq_status dq_plan_kernel_time(dq_plan* plan, int32_t kernel, double* total_ms, i
 /* Algorithmic bytes per row (x1000) the column-pass launch of variant v reads (excl. UTF8 data). */
 int64_t dq_plan_variant_bytes_per_row_x1000(const dq_plan* plan, int32_t variant);
 
+/* Grouping analyzers (analyzers/GroupingAnalyzers.scala:44-82, 118-138): the frequencies
+ * SELECT cols, COUNT(*) FROM data WHERE cols IS NOT NULL GROUP BY cols on the GPU (sort-based), and
+ * the summary Uniqueness / Distinctness / CountDistinct / Entropy / UniqueValueRatio compute from.
+ * cols: n_chunks x n_cols views, chunk-major (device pointers).  A single numeric column groups by
+ * its exact value (NaN canonical, -0.0 != 0.0 as Spark 2.2); strings / several columns group by a
+ * 64-bit tuple hash whose equal-hash neighbours are compared exactly (a collision between distinct
+ * tuples is DQ_E_UNSUPPORTED, never a silent merge).  dq_freq_merge is FrequenciesAndNumRows.sum
+ * (outer join adding counts; for hashed keys across two tables the exact check is not repeated). */
+typedef struct dq_freq_table dq_freq_table;
+typedef struct dq_freq_summary {
+  int64_t num_groups;  /* rows of the frequencies table (CountDistinct) */
+  int64_t num_unique;  /* groups with count == 1 */
+  int64_t num_values;  /* rows with every grouping column non-null */
+  double entropy;      /* sum over groups of -(c / num_rows) * ln(c / num_rows) (Entropy.scala:31-37) */
+} dq_freq_summary;
+dq_status dq_freq_build(const int32_t* types, int32_t n_cols, const dq_column_view* cols, const int64_t* chunk_rows,
+                        int32_t n_chunks, int32_t device, void* hip_stream, dq_freq_table** out);
+dq_status dq_freq_merge(const dq_freq_table* a, const dq_freq_table* b, dq_freq_table** out);
+dq_status dq_freq_summarize(const dq_freq_table* t, int64_t num_rows, dq_freq_summary* out);
+int64_t dq_freq_num_groups(const dq_freq_table* t);
+dq_status dq_freq_export(const dq_freq_table* t, uint64_t* keys, int64_t* counts, int64_t cap);
+void dq_freq_destroy(dq_freq_table* t);
+
 /* State algebra.
  * dq_state_merge:   Analyzers.merge / State.sum on Option[State] (Analyzer.scala:343-362):
  *                   None + x = x; Min/Max merge with java.lang.Math.min/max.

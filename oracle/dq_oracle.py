@@ -1202,6 +1202,51 @@ def regexp_extract_nonempty(value: bytes, pattern: str) -> bool:
     return m is not None and m.group(0) != ""
 
 
+# Grouping analyzers: FrequencyBasedAnalyzer.computeFrequencies (GroupingAnalyzers.scala:44-82) --
+# count(*) per distinct tuple of the grouping columns over rows where all of them are non-null; numRows
+# = data.count().  Grouping keys follow Spark 2.2's UnsafeRow: NaN canonical (setDouble), -0.0 and 0.0
+# distinct (binary comparison), strings by bytes.
+def _group_key(c: "OColumn", i: int):
+    if c.dtype == "f64":
+        v = float(c.values[i])
+        return ("f", b"nan" if math.isnan(v) else struct.pack("<d", v))
+    if c.dtype in ("utf8", "large_utf8"):
+        return ("s", c.values[i])
+    return ("i", int(c.values[i]))
+
+
+def frequencies(cols: dict, columns, n: int) -> dict:
+    freq: dict = {}
+    for i in range(n):
+        if all(cols[c].valid[i] for c in columns):
+            k = tuple(_group_key(cols[c], i) for c in columns)
+            freq[k] = freq.get(k, 0) + 1
+    return freq
+
+
+@dataclass
+class GroupingMetricState:
+    """FrequenciesAndNumRows + the analyzer that reads it (its aggregationFunctions)."""
+    op: str
+    freq: dict
+    numRows: int
+
+    def metricValue(self):
+        counts = list(self.freq.values())
+        unique = sum(1 for c in counts if c == 1)
+        if self.op == "Uniqueness":  # Uniqueness.scala:27-29
+            return unique / self.numRows
+        if self.op == "Distinctness":  # Distinctness.scala:29-31
+            return len(counts) / self.numRows
+        if self.op == "CountDistinct":  # CountDistinct.scala:25-31
+            return float(len(counts))
+        if self.op == "UniqueValueRatio":  # UniqueValueRatio.scala:25-36 (NULL sum unboxes to 0.0)
+            return unique / len(counts) if counts else float("nan")
+        if self.op == "Entropy":  # Entropy.scala:29-41
+            return sum(0.0 if c == 0 else -(c / self.numRows) * math.log(c / self.numRows) for c in counts)
+        raise ValueError(self.op)
+
+
 def _where(cols, n, where: Optional[str]):
     """(where_true, where_notnull) masks; no where -> all true."""
     if where is None:
@@ -1263,6 +1308,13 @@ def compute_state(spec: tuple, cols: dict, n: int, n_partitions: int = 1):
                 return None
             return MinState(v) if op == "Minimum" else MaxState(v)
         return ApproxCountDistinctState(hll_words_for(c, sel))
+    if op in ("Uniqueness", "Distinctness", "CountDistinct", "UniqueValueRatio", "Entropy"):
+        columns = [spec[1]] if isinstance(spec[1], str) else list(spec[1])
+        st = GroupingMetricState(op, frequencies(cols, columns, n), n)
+        # the SQL sum over an empty frequencies table is NULL -> EmptyStateException (metricFromEmpty)
+        if not st.freq and op in ("Uniqueness", "Distinctness", "Entropy"):
+            return None
+        return st
     if op == "PatternMatch":
         col, pattern, where = spec[1], spec[2], spec[3]
         c = cols[col]

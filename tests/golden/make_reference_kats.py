@@ -10,6 +10,7 @@ that state, DataType.scala:98-114).  `needs` lists GPU-path capabilities a case 
 have (e.g. a regex outside the GPU subset), so tests expect the fallback route for it.
 """
 import json
+import math
 import os
 
 N = None
@@ -227,6 +228,24 @@ cases = [
     ("patternSsns", ["PatternMatch", "some", SSN, N], 2.0 / 8.0, S + ":701-718", ["regex_fallback"]),
     ("checkUrls", ["PatternMatch", "some", URL, N], 0.5, "checks/CheckTest.scala:381-389 (hasPattern default assertion fails)", []),
     ("checkEmails", ["PatternMatch", "some", EMAIL, N], 1.0, "checks/CheckTest.scala:352-360 (hasPattern default assertion holds)", []),
+    # grouping analyzers (AnalyzerTests.scala:79-146, AnalysisTest.scala:30-93, NullHandlingTests.scala:112-115)
+    ("dfMissing", ["Uniqueness", ["att1"]], 0.0, S + ":84-85", []),
+    ("dfMissing", ["Uniqueness", ["att2"]], 0.0, S + ":86-87", []),
+    ("dfFull", ["Uniqueness", ["att1"]], 0.25, S + ":90-91", []),
+    ("dfFull", ["Uniqueness", ["att2"]], 0.25, S + ":92-93", []),
+    ("dfWithUniqueColumns", ["Uniqueness", ["unique"]], 1.0, S + ":99-100", []),
+    ("dfWithUniqueColumns", ["Uniqueness", ["uniqueWithNulls"]], 5 / 6.0, S + ":101-102", []),
+    ("dfWithUniqueColumns", ["Uniqueness", ["unique", "nonUnique"]], 1.0, S + ":103-104", []),
+    ("dfWithUniqueColumns", ["Uniqueness", ["unique", "nonUniqueWithNulls"]], 3 / 6.0, S + ":105-107", []),
+    ("dfWithUniqueColumns", ["Uniqueness", ["nonUnique", "onlyUniqueWithOtherNonUnique"]], 1.0, S + ":108-110", []),
+    ("dfFull", ["Entropy", "att1"], -(0.75 * math.log(0.75) + 0.25 * math.log(0.25)), S + ":138-140", []),
+    ("dfFull", ["Entropy", "att2"], -(0.75 * math.log(0.75) + 0.25 * math.log(0.25)), S + ":141-143", []),
+    ("dfFull", ["Distinctness", ["item"]], 1.0, "analyzers/AnalysisTest.scala:38,49", []),
+    ("dfFull", ["Uniqueness", ["att1", "att2"]], 0.25, "analyzers/AnalysisTest.scala:40,51", []),
+    ("dfWithNumericValues", ["CountDistinct", ["att1"]], 6.0, "analyzers/AnalysisTest.scala:80,93", []),
+    ("dfWithUniqueColumns", ["CountDistinct", ["uniqueWithNulls"]], 5.0, S + ":526-529", []),
+    ("dataWithNullColumns", ["CountDistinct", ["stringCol"]], 0.0, "analyzers/NullHandlingTests.scala:112", []),
+    ("dataWithNullColumns", ["Entropy", "stringCol"], "EmptyState", "analyzers/NullHandlingTests.scala:115", []),
     # partition merge (analyzers/StateAggregationIntegrationTest.scala:56-104)
     ("stateAggregation", ["Completeness", "origin", N], 0.625, "analyzers/StateAggregationIntegrationTest.scala:77", []),
 ]

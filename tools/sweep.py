@@ -73,6 +73,24 @@ def main():
         measure("pattern_url_utf8x1", t, [dq.PatternMatch(s[0], dq.Patterns.URL)])
         measure("pattern_email_utf8x4", t, [dq.PatternMatch(c, dq.Patterns.EMAIL) for c in s])
         measure("pattern_digit_utf8x4", t, [dq.PatternMatch(c, r"\d") for c in s])
+    if ONLY and ONLY.startswith("group"):
+        t = synth.c5_table(n, seed=42)
+        from deequ_amd.grouping import build_frequencies
+        for name, cols in (("group_i64_1e6", ["i1"]), ("group_i64_unique", ["i3"]), ("group_f64", ["c0"]),
+                           ("group_utf8_1e6", ["s1"]), ("group_i64_utf8", ["i0", "s0"])):
+            for _ in range(2):
+                build_frequencies(t, cols)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            reps = 3
+            for _ in range(reps):
+                st = build_frequencies(t, cols)
+                st.frequencies.summary(st.numRows)
+            ms = (time.perf_counter() - t0) / reps * 1e3
+            s = st.frequencies.summary(st.numRows)
+            print(json.dumps({"case": name, "rows": n, "wall_ms": ms, "groups": s.num_groups,
+                              "rows_per_s": n / ms * 1e3}), flush=True)
+        return
     c4 = synth.c4_table(n // 2, seed=42)
     names = list(c4.columns)
     measure("corr28_half", c4, [dq.Correlation(names[a], names[b]) for a in range(8) for b in range(a + 1, 8)])
