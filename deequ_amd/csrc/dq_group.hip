@@ -18,7 +18,9 @@
 #include <hipcub/hipcub.hpp>
 
 #include <cstring>
+#include <map>
 #include <memory>
+#include <mutex>
 #include <vector>
 
 #include "dq_device.h"
@@ -182,12 +184,29 @@ __global__ void summary_final(const SumPart* __restrict__ part, int32_t nparts, 
     if (e_ != hipSuccess) return set_error(DQ_E_HIP, "%s: %s", #x, hipGetErrorString(e_));      \
   } while (0)
 
-struct DevBuf {  // hipMalloc'd scratch, freed on scope exit
+// Scratch buffers come from a per-device arena of named slots that only grows: a GROUP BY over a
+// 62.5 M-row chunk needs ~2 GB of temporaries, and hipMalloc / hipFree of that much per call costs more
+// than the sort itself.  Calls are serialised by g_arena_mu (the arena is shared by all plans).
+std::mutex g_arena_mu;
+struct Slot { void* p = nullptr; size_t cap = 0; };
+std::map<std::pair<int, int>, Slot> g_arena;  // (device, slot) -> buffer
+
+struct DevBuf {
+  int dev = 0, slot = 0;
   void* p = nullptr;
-  ~DevBuf() { if (p) (void)hipFree(p); }
+  DevBuf(int device, int s) : dev(device), slot(s) {}
   dq_status alloc(size_t bytes) {
-    if (p) { (void)hipFree(p); p = nullptr; }
-    if (hipMalloc(&p, bytes ? bytes : 16) != hipSuccess) return set_error(DQ_E_OOM, "hipMalloc(%zu) failed", bytes);
+    bytes = std::max<size_t>(bytes, 256);
+    Slot& sl = g_arena[{dev, slot}];
+    if (sl.cap < bytes) {
+      if (sl.p) (void)hipFree(sl.p);
+      sl.p = nullptr;
+      sl.cap = 0;
+      const size_t want = bytes + bytes / 8;  // headroom for the next, slightly larger call
+      if (hipMalloc(&sl.p, want) != hipSuccess) return set_error(DQ_E_OOM, "hipMalloc(%zu) failed", want);
+      sl.cap = want;
+    }
+    p = sl.p;
     return DQ_OK;
   }
   template <typename T> T* as() const { return reinterpret_cast<T*>(p); }
@@ -216,7 +235,7 @@ struct dq_freq_table {
 };
 
 static dq_status rle_into(dq_freq_table* t, const uint64_t* sorted, int64_t n) {
-  DevBuf nruns, tmp;
+  DevBuf nruns(t->device, 20), tmp(t->device, 21);
   if (dq_status s = nruns.alloc(sizeof(int64_t))) return s;
   GHIP(hipMalloc(&t->d_keys, std::max<int64_t>(1, n) * sizeof(uint64_t)));
   GHIP(hipMalloc(&t->d_counts, std::max<int64_t>(1, n) * sizeof(int64_t)));
@@ -273,7 +292,10 @@ dq_status dq_freq_build(const int32_t* types, int32_t n_cols, const dq_column_vi
       g.type[c] = types[c];
     }
   }
-  DevBuf keys, flags, sel_keys, rows_all, sel_rows, nsel, tmp, sorted_keys, sorted_rows, d_chunks;
+  std::lock_guard<std::mutex> lock(g_arena_mu);
+  const int D = device;
+  DevBuf keys(D, 0), flags(D, 1), sel_keys(D, 2), rows_all(D, 3), sel_rows(D, 4), nsel(D, 5), tmp(D, 6),
+      sorted_keys(D, 7), sorted_rows(D, 8), d_chunks(D, 9);
   int64_t maxn = 1;
   for (int k = 0; k < n_chunks; ++k) maxn = std::max<int64_t>(maxn, chunk_rows[k]);
   if (dq_status s = keys.alloc(maxn * 8)) return s;
@@ -359,7 +381,9 @@ dq_status dq_freq_merge(const dq_freq_table* a, const dq_freq_table* b, dq_freq_
   t->hashed = a->hashed;
   t->n_values = a->n_values + b->n_values;
   const int64_t n = a->n_groups + b->n_groups;
-  DevBuf k_in, c_in, k_s, c_s, nruns, tmp;
+  std::lock_guard<std::mutex> lock(g_arena_mu);
+  const int D = a->device;
+  DevBuf k_in(D, 10), c_in(D, 11), k_s(D, 12), c_s(D, 13), nruns(D, 14), tmp(D, 15);
   for (DevBuf* d : {&k_in, &c_in, &k_s, &c_s})
     if (dq_status s = d->alloc(std::max<int64_t>(1, n) * 8)) return s;
   if (dq_status s = nruns.alloc(8)) return s;
@@ -396,7 +420,8 @@ dq_status dq_freq_summarize(const dq_freq_table* t, int64_t num_rows, dq_freq_su
   out->num_groups = t->n_groups;
   out->num_values = t->n_values;
   if (t->n_groups == 0) return DQ_OK;
-  DevBuf part, res;
+  std::lock_guard<std::mutex> lock(g_arena_mu);
+  DevBuf part(t->device, 16), res(t->device, 17);
   if (dq_status s = part.alloc(kSumBlocks * sizeof(SumPart))) return s;
   if (dq_status s = res.alloc(sizeof(SumPart))) return s;
   const int nb = (int)std::min<int64_t>(kSumBlocks, (t->n_groups + 255) / 256);
