@@ -463,8 +463,9 @@ __device__ void numeric_range(const void* values, const uint32_t* validity, cons
   // per row.  dq_scan bounds a chunk to < 2^31 rows, so a range is < 2^31 bytes.
   const __amdgpu_buffer_rsrc_t vr = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<T*>(v + row0), (short)0, (int)((row1 - row0) * (int64_t)sizeof(T)), 0x00020000);
-  int64_t nan_w = 0;  // wave-uniform count of selected NaN values
-  int64_t pinf_w = 0, ninf_w = 0;  // ... of selected +inf / -inf values
+  // counts of selected NaN / +inf / -inf values, kept by lane 0 in VGPRs (as wave-uniform SGPR
+  // counters they pushed the loop's SGPR pressure into spills)
+  int64_t nan_v = 0, pinf_v = 0, ninf_v = 0;
   int64_t cnt_w = 0;  // wave-uniform count of selected rows (HLL-only variant)
   LaneMoments a{0.0, 0.0, 0.0, 0, 0};
   int32_t qmin = 0;
@@ -472,7 +473,7 @@ __device__ void numeric_range(const void* values, const uint32_t* validity, cons
   for (int64_t blk = row0; blk < row1; blk += kRowsPerIter, ++nb) {
     const int64_t base = blk + (int64_t)wave * 512;
     const bool full = blk + kRowsPerIter <= row1;
-    uint64_t bits[8], m[8], nanm[8];
+    uint64_t bits[8], m[8];
     double x[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -489,28 +490,33 @@ __device__ void numeric_range(const void* values, const uint32_t* validity, cons
       }
     }
     block_masks(validity, mask, base, row1, full, m);
+    // one v_cmp_class per value (NaN or +-inf); only their OR stays live on the common path (keeping
+    // the 8 masks for the rare path spilled SGPRs into v_writelane / v_readlane on every block)
     uint64_t nf_any = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      // one v_cmp_class per value: NaN or +-inf
-      nanm[j] = KIND == CK_F64 ? __builtin_amdgcn_ballot_w64(!__builtin_isfinite(x[j])) & m[j] : 0ull;
-      nf_any |= nanm[j];
+      if (KIND == CK_F64) nf_any |= __builtin_amdgcn_ballot_w64(!__builtin_isfinite(x[j])) & m[j];
       if (!STATS) cnt_w += __builtin_popcountll(m[j]);
     }
+    uint64_t nanm[8];
     if (KIND == CK_F64 && nf_any != 0) {
       uint64_t mm[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const uint64_t nf = nanm[j];
+        const uint64_t nf = __builtin_amdgcn_ballot_w64(!__builtin_isfinite(x[j])) & m[j];
         nanm[j] = __builtin_amdgcn_ballot_w64(x[j] != x[j]) & m[j];
         const uint64_t inf = nf & ~nanm[j], pinf = __builtin_amdgcn_ballot_w64(x[j] > 0.0) & inf;
-        nan_w += __builtin_popcountll(nanm[j]);
-        pinf_w += __builtin_popcountll(pinf);
-        ninf_w += __builtin_popcountll(inf & ~pinf);
+        if (lane == 0) {
+          nan_v += __builtin_popcountll(nanm[j]);
+          pinf_v += __builtin_popcountll(pinf);
+          ninf_v += __builtin_popcountll(inf & ~pinf);
+        }
         mm[j] = STATS ? m[j] & ~inf : m[j];
       }
       numeric_block<KIND, STATS, HLL, true>(x, bits, m, mm, nanm, s, a, regs, qmin);
     } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) nanm[j] = 0;
       numeric_block<KIND, STATS, HLL, false>(x, bits, m, m, nanm, s, a, regs, qmin);
     }
     if (STATS && (nb % kChunkBlocks) == kChunkBlocks - 1) moments_flush<KIND>(s, a);
@@ -518,10 +524,10 @@ __device__ void numeric_range(const void* values, const uint32_t* validity, cons
   if (STATS) moments_flush<KIND>(s, a);
   if (!STATS && lane == 0) s.count += cnt_w;
   if (KIND == CK_F64 && lane == 0) {
-    s.nan_count += nan_w;
-    s.pinf += pinf_w;
-    s.ninf += ninf_w;
-    if (STATS) s.count += pinf_w + ninf_w;  // the moments' k counted only the finite / NaN rows
+    s.nan_count += nan_v;
+    s.pinf += pinf_v;
+    s.ninf += ninf_v;
+    if (STATS) s.count += pinf_v + ninf_v;  // the moments' k counted only the finite / NaN rows
   }
 }
 
