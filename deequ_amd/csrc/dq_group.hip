@@ -178,6 +178,94 @@ __global__ void summary_final(const SumPart* __restrict__ part, int32_t nparts, 
   }
 }
 
+// key of one column of a row (exact value for numeric columns, 64-bit hash of the bytes for strings)
+__device__ uint64_t col_key(const GroupCols& g, int c, int64_t r) {
+  if (g.type[c] != DQ_TYPE_UTF8 && g.type[c] != DQ_TYPE_LARGE_UTF8) return value_bits(g, c, r);
+  GroupCols one = g;
+  one.n_cols = 1;
+  one.values[0] = g.values[c];
+  one.offsets[0] = g.offsets[c];
+  one.type[0] = g.type[c];
+  return tuple_hash(one, r);
+}
+
+__device__ bool col_equal(const GroupCols* chunks, int c, uint64_t ra, uint64_t rb) {
+  const GroupCols& ga = chunks[ra >> kRowBits];
+  const GroupCols& gb = chunks[rb >> kRowBits];
+  const int64_t a = (int64_t)(ra & ((1ull << kRowBits) - 1)), b = (int64_t)(rb & ((1ull << kRowBits) - 1));
+  if (ga.type[c] != DQ_TYPE_UTF8 && ga.type[c] != DQ_TYPE_LARGE_UTF8) return value_bits(ga, c, a) == value_bits(gb, c, b);
+  const uint8_t *pa, *pb;
+  int64_t la, lb;
+  str_of(ga, c, a, pa, la);
+  str_of(gb, c, b, pb, lb);
+  if (la != lb) return false;
+  for (int64_t i = 0; i < la; ++i)
+    if (pa[i] != pb[i]) return false;
+  return true;
+}
+
+// MutualInformation: per joint group g its representative row and the keys of both columns
+__global__ void mi_group_keys(const uint64_t* __restrict__ sorted_rows, const int64_t* __restrict__ starts, int64_t G,
+                              const GroupCols* __restrict__ chunks, uint64_t* __restrict__ rep, uint64_t* __restrict__ xk,
+                              uint64_t* __restrict__ yk, uint64_t* __restrict__ idx) {
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < G; g += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t r = sorted_rows[starts[g]];
+    const GroupCols& gc = chunks[r >> kRowBits];
+    const int64_t lr = (int64_t)(r & ((1ull << kRowBits) - 1));
+    rep[g] = r;
+    xk[g] = col_key(gc, 0, lr);
+    yk[g] = col_key(gc, 1, lr);
+    idx[g] = (uint64_t)g;
+  }
+}
+
+// marginal of column c over the joint groups sorted by that column's key: segment heads, an exact
+// check of equal-hash neighbours (strings), then segment sums of the joint counts (integer atomics)
+__global__ void mi_heads(const uint64_t* __restrict__ sk, const uint64_t* __restrict__ sidx, const uint64_t* __restrict__ rep,
+                         int64_t G, const GroupCols* __restrict__ chunks, int c, uint32_t* __restrict__ head,
+                         int32_t* __restrict__ collision) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < G; i += (int64_t)gridDim.x * blockDim.x) {
+    const bool h = i == 0 || sk[i] != sk[i - 1];
+    head[i] = h ? 1u : 0u;
+    if (!h && !col_equal(chunks, c, rep[sidx[i]], rep[sidx[i - 1]])) atomicOr(collision, 1);
+  }
+}
+__global__ void mi_segsum(const uint64_t* __restrict__ sidx, const uint32_t* __restrict__ seg, const int64_t* __restrict__ gc,
+                          int64_t G, unsigned long long* __restrict__ segsum) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < G; i += (int64_t)gridDim.x * blockDim.x)
+    atomicAdd(&segsum[seg[i] - 1], (unsigned long long)gc[sidx[i]]);
+}
+__global__ void mi_scatter(const uint64_t* __restrict__ sidx, const uint32_t* __restrict__ seg,
+                           const unsigned long long* __restrict__ segsum, int64_t G, int64_t* __restrict__ pm) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < G; i += (int64_t)gridDim.x * blockDim.x)
+    pm[sidx[i]] = (int64_t)segsum[seg[i] - 1];
+}
+// fixed-order partial sums of (pxy / N) * ln((pxy / N) / ((px / N) * (py / N)))  (MutualInformation.scala:53-56)
+__global__ __launch_bounds__(256) void mi_part(const int64_t* __restrict__ gc, const int64_t* __restrict__ px,
+                                               const int64_t* __restrict__ py, int64_t G, double total,
+                                               double* __restrict__ part) {
+  __shared__ double se[256];
+  double e = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < G; i += (int64_t)gridDim.x * 256) {
+    const double pxy = (double)gc[i], a = (double)px[i], b = (double)py[i];
+    e += (pxy / total) * log((pxy / total) / ((a / total) * (b / total)));
+  }
+  se[threadIdx.x] = e;
+  __syncthreads();
+  for (int s = 128; s >= 1; s >>= 1) {
+    if ((int)threadIdx.x < s) se[threadIdx.x] += se[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = se[0];
+}
+__global__ void mi_final(const double* __restrict__ part, int32_t nparts, double* __restrict__ out) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    double t = 0.0;
+    for (int i = 0; i < nparts; ++i) t += part[i];
+    *out = t;
+  }
+}
+
 #define GHIP(x)                                                                                  \
   do {                                                                                           \
     hipError_t e_ = (x);                                                                         \
@@ -253,8 +341,13 @@ static dq_status rle_into(dq_freq_table* t, const uint64_t* sorted, int64_t n) {
 
 extern "C" {
 
-dq_status dq_freq_build(const int32_t* types, int32_t n_cols, const dq_column_view* cols, const int64_t* chunk_rows,
-                        int32_t n_chunks, int32_t device, void* hip_stream, dq_freq_table** out) {
+struct MiRequest { double total; double* value; int32_t* defined; };
+static dq_status mi_from_joint(dq_freq_table* t, const uint64_t* sorted_keys, const uint64_t* sorted_rows, int64_t nv,
+                               const GroupCols* d_chunks, const MiRequest& mi);
+
+static dq_status freq_build_impl(const int32_t* types, int32_t n_cols, const dq_column_view* cols,
+                                 const int64_t* chunk_rows, int32_t n_chunks, int32_t device, void* hip_stream,
+                                 dq_freq_table** out, const MiRequest* mi) {
   if (!out) return set_error(DQ_E_INVALID, "dq_freq_build: out is NULL");
   *out = nullptr;
   if (n_cols < 1 || n_cols > kMaxGroupCols || !types)
@@ -277,7 +370,7 @@ dq_status dq_freq_build(const int32_t* types, int32_t n_cols, const dq_column_vi
   t->stream = reinterpret_cast<hipStream_t>(hip_stream);
   t->types.assign(types, types + n_cols);
   const bool numeric1 = n_cols == 1 && (types[0] == DQ_TYPE_F64 || types[0] == DQ_TYPE_I64 || types[0] == DQ_TYPE_I32);
-  t->hashed = numeric1 ? 0 : 1;
+  t->hashed = numeric1 && !mi ? 0 : 1;
 
   std::vector<GroupCols> gcs(std::max(1, n_chunks));
   for (int k = 0; k < n_chunks; ++k) {
@@ -362,9 +455,99 @@ dq_status dq_freq_build(const int32_t* types, int32_t n_cols, const dq_column_vi
                                              0, 64, t->stream));
     }
   }
+  if (mi) return mi_from_joint(t, sorted_keys.as<uint64_t>(), sorted_rows.as<uint64_t>(), nv, d_chunks.as<GroupCols>(), *mi);
   if (dq_status s = rle_into(t, sorted_keys.as<uint64_t>(), nv)) return s;
   *out = guard.release();
   return DQ_OK;
+}
+
+static dq_status mi_from_joint(dq_freq_table* t, const uint64_t* sorted_keys, const uint64_t* sorted_rows, int64_t nv,
+                               const GroupCols* d_chunks, const MiRequest& mi) {
+  *mi.defined = 0;
+  *mi.value = 0.0;
+  if (nv == 0) return DQ_OK;  // sum over an empty join is NULL -> metricFromEmpty
+  const int D = t->device;
+  const hipStream_t S = t->stream;
+  DevBuf gk(D, 30), gc(D, 31), nruns(D, 32), starts(D, 33), rep(D, 34), xk(D, 35), yk(D, 36), idx(D, 37), sk(D, 38),
+      sidx(D, 39), head(D, 40), seg(D, 41), segsum(D, 42), px(D, 43), py(D, 44), tmp(D, 45), part(D, 46), res(D, 47),
+      coll(D, 48);
+  for (DevBuf* b : {&gk, &gc, &starts, &rep, &xk, &yk, &idx, &sk, &sidx, &segsum, &px, &py})
+    if (dq_status s = b->alloc(nv * 8)) return s;
+  for (DevBuf* b : {&head, &seg})
+    if (dq_status s = b->alloc(nv * 4)) return s;
+  for (DevBuf* b : {&nruns, &res, &coll})
+    if (dq_status s = b->alloc(8)) return s;
+  if (dq_status s = part.alloc(kSumBlocks * sizeof(double))) return s;
+  size_t tb = 0, need = 0;
+  GHIP(hipcub::DeviceRunLengthEncode::Encode(nullptr, tb, sorted_keys, gk.as<uint64_t>(), gc.as<int64_t>(),
+                                             nruns.as<int64_t>(), (int)nv, S));
+  need = std::max(need, tb);
+  GHIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, gc.as<int64_t>(), starts.as<int64_t>(), (int)nv, S));
+  need = std::max(need, tb);
+  GHIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, xk.as<uint64_t>(), sk.as<uint64_t>(), idx.as<uint64_t>(),
+                                          sidx.as<uint64_t>(), (int)nv, 0, 64, S));
+  need = std::max(need, tb);
+  GHIP(hipcub::DeviceScan::InclusiveSum(nullptr, tb, head.as<uint32_t>(), seg.as<uint32_t>(), (int)nv, S));
+  need = std::max(need, tb);
+  if (dq_status s = tmp.alloc(need)) return s;
+  tb = need;
+  GHIP(hipcub::DeviceRunLengthEncode::Encode(tmp.p, tb, sorted_keys, gk.as<uint64_t>(), gc.as<int64_t>(),
+                                             nruns.as<int64_t>(), (int)nv, S));
+  int64_t G = 0;
+  GHIP(hipMemcpyAsync(&G, nruns.p, 8, hipMemcpyDeviceToHost, S));
+  GHIP(hipStreamSynchronize(S));
+  tb = need;
+  GHIP(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, gc.as<int64_t>(), starts.as<int64_t>(), (int)G, S));
+  hipLaunchKernelGGL(mi_group_keys, dim3(grid_for(G)), dim3(256), 0, S, sorted_rows, starts.as<int64_t>(), G, d_chunks,
+                     rep.as<uint64_t>(), xk.as<uint64_t>(), yk.as<uint64_t>(), idx.as<uint64_t>());
+  GHIP(hipGetLastError());
+  GHIP(hipMemsetAsync(coll.p, 0, 8, S));
+  for (int c = 0; c < 2; ++c) {
+    tb = need;
+    GHIP(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, (c == 0 ? xk : yk).as<uint64_t>(), sk.as<uint64_t>(),
+                                            idx.as<uint64_t>(), sidx.as<uint64_t>(), (int)G, 0, 64, S));
+    hipLaunchKernelGGL(mi_heads, dim3(grid_for(G)), dim3(256), 0, S, sk.as<uint64_t>(), sidx.as<uint64_t>(),
+                       rep.as<uint64_t>(), G, d_chunks, c, head.as<uint32_t>(), coll.as<int32_t>());
+    GHIP(hipGetLastError());
+    tb = need;
+    GHIP(hipcub::DeviceScan::InclusiveSum(tmp.p, tb, head.as<uint32_t>(), seg.as<uint32_t>(), (int)G, S));
+    GHIP(hipMemsetAsync(segsum.p, 0, G * 8, S));
+    hipLaunchKernelGGL(mi_segsum, dim3(grid_for(G)), dim3(256), 0, S, sidx.as<uint64_t>(), seg.as<uint32_t>(),
+                       gc.as<int64_t>(), G, segsum.as<unsigned long long>());
+    GHIP(hipGetLastError());
+    hipLaunchKernelGGL(mi_scatter, dim3(grid_for(G)), dim3(256), 0, S, sidx.as<uint64_t>(), seg.as<uint32_t>(),
+                       segsum.as<unsigned long long>(), G, (c == 0 ? px : py).as<int64_t>());
+    GHIP(hipGetLastError());
+  }
+  const int nb = (int)std::min<int64_t>(kSumBlocks, (G + 255) / 256);
+  hipLaunchKernelGGL(mi_part, dim3(nb), dim3(256), 0, S, gc.as<int64_t>(), px.as<int64_t>(), py.as<int64_t>(), G,
+                     mi.total, part.as<double>());
+  GHIP(hipGetLastError());
+  hipLaunchKernelGGL(mi_final, dim3(1), dim3(64), 0, S, part.as<double>(), nb, res.as<double>());
+  GHIP(hipGetLastError());
+  int32_t collided = 0;
+  GHIP(hipMemcpyAsync(&collided, coll.p, 4, hipMemcpyDeviceToHost, S));
+  GHIP(hipMemcpyAsync(mi.value, res.p, 8, hipMemcpyDeviceToHost, S));
+  GHIP(hipStreamSynchronize(S));
+  if (collided) return set_error(DQ_E_UNSUPPORTED, "dq_mutual_information: 64-bit key collision between distinct values");
+  *mi.defined = 1;
+  return DQ_OK;
+}
+
+dq_status dq_freq_build(const int32_t* types, int32_t n_cols, const dq_column_view* cols, const int64_t* chunk_rows,
+                        int32_t n_chunks, int32_t device, void* hip_stream, dq_freq_table** out) {
+  return freq_build_impl(types, n_cols, cols, chunk_rows, n_chunks, device, hip_stream, out, nullptr);
+}
+
+dq_status dq_mutual_information(const int32_t* types, const dq_column_view* cols, const int64_t* chunk_rows,
+                                int32_t n_chunks, int64_t num_rows, int32_t device, void* hip_stream, double* value,
+                                int32_t* defined) {
+  if (!value || !defined) return set_error(DQ_E_INVALID, "dq_mutual_information: NULL output");
+  MiRequest mi{(double)num_rows, value, defined};
+  dq_freq_table* unused = nullptr;
+  dq_status s = freq_build_impl(types, 2, cols, chunk_rows, n_chunks, device, hip_stream, &unused, &mi);
+  if (unused) dq_freq_destroy(unused);
+  return s;
 }
 
 dq_status dq_freq_merge(const dq_freq_table* a, const dq_freq_table* b, dq_freq_table** out) {

@@ -211,4 +211,58 @@ class Entropy(FrequencyBasedAnalyzer):  # Entropy.scala:26-44 (single column)
         return None if s.num_groups == 0 else s.entropy
 
 
-GROUPING_ANALYZERS = (Uniqueness, Distinctness, CountDistinct, UniqueValueRatio, Entropy)
+
+
+class MutualInformation(FrequencyBasedAnalyzer):  # MutualInformation.scala:32-80
+    """sum over the joint groups of (pxy/N) ln((pxy/N) / ((px/N)(py/N))), marginals summed from the joint
+    counts (rows with both values), N = numRows -- computed in one device pass (dq_mutual_information).
+    The joint frequencies are not materialised as a state here: aggregateWith / saveStatesWith of a
+    MutualInformation are reported as failures of that metric."""
+    name = "MutualInformation"
+    direct = True
+
+    def __init__(self, columnA, columnB: Optional[str] = None):
+        super().__init__(list(columnA) if columnB is None else [columnA, columnB])
+
+    @property
+    def entity(self):
+        return Entity.Mutlicolumn
+
+    def preconditions(self):
+        def exactly_two(schema):  # Preconditions.exactlyNColumns(columns, 2)
+            if len(self.columns) != 2:
+                raise ValueError(f"{self.columns} has {len(self.columns)} columns, but exactly 2 are required")
+        return [exactly_two] + [Preconditions.hasColumn(c) for c in self.columns]
+
+    def compute(self, data) -> DoubleMetric:
+        import torch
+
+        from .runner import _chunks
+
+        chunks = _chunks(data)
+        schema = {name: dt for name, dt, _ in chunks[0].schema}
+        types = (ctypes.c_int32 * 2)(*[_TYPES[schema[c]] for c in self.columns])
+        views = (L.ColumnView * max(1, 2 * len(chunks)))()
+        rows = (ctypes.c_int64 * max(1, len(chunks)))()
+        for k, t in enumerate(chunks):
+            rows[k] = t.num_rows
+            for c, name in enumerate(self.columns):
+                views[2 * k + c] = t.columns[name].view()
+        value, defined = ctypes.c_double(), ctypes.c_int32()
+        stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        L.check(L.lib.dq_mutual_information(types, views, rows, len(chunks), sum(t.num_rows for t in chunks),
+                                            torch.cuda.current_device(), stream, ctypes.byref(value),
+                                            ctypes.byref(defined)))
+        if not defined.value:
+            return self._empty()
+        return DoubleMetric(self.entity, self.name, self.instance, Success(value.value))
+
+    def calculate(self, data, aggregateWith=None, saveStatesWith=None) -> DoubleMetric:
+        try:
+            for cond in self.preconditions():
+                cond(data_schema(data))
+            if aggregateWith is not None or saveStatesWith is not None:
+                raise NotImplementedError("incremental MutualInformation needs the joint frequencies as a state")
+            return self.compute(data)
+        except Exception as e:
+            return self.toFailureMetric(e)

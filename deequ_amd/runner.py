@@ -206,6 +206,9 @@ class AnalysisRunner:
         ctx = AnalysisRunner.runScanningAnalyzers(data, scanning, aggregateWith, saveStatesWith)
         by_cols: Dict[tuple, List[Analyzer]] = {}
         for a in grouping:  # AnalysisRunner.scala:160-180: one frequency computation per column set
+            if getattr(a, "direct", False):  # MutualInformation: its own device pass
+                ctx = ctx + AnalyzerContext({a: a.calculate(data, aggregateWith, saveStatesWith)})
+                continue
             by_cols.setdefault(tuple(a.groupingColumns()), []).append(a)
         for cols, group in by_cols.items():
             ctx = ctx + AnalysisRunner.runGroupingAnalyzers(data, list(cols), group, aggregateWith, saveStatesWith)

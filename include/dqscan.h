@@ -227,6 +227,13 @@ dq_status dq_freq_summarize(const dq_freq_table* t, int64_t num_rows, dq_freq_su
 int64_t dq_freq_num_groups(const dq_freq_table* t);
 dq_status dq_freq_export(const dq_freq_table* t, uint64_t* keys, int64_t* counts, int64_t cap);
 void dq_freq_destroy(dq_freq_table* t);
+/* MutualInformation(a, b) (analyzers/MutualInformation.scala:32-72): joint frequencies of the two
+ * columns, their marginals summed from the joint counts, and
+ * sum (pxy / N) * ln((pxy / N) / ((px / N) * (py / N))) with N = num_rows.  cols: n_chunks x 2 views.
+ * *defined = 0 when no row has both values (the SQL sum is NULL -> EmptyStateException). */
+dq_status dq_mutual_information(const int32_t* types, const dq_column_view* cols, const int64_t* chunk_rows,
+                                int32_t n_chunks, int64_t num_rows, int32_t device, void* hip_stream, double* value,
+                                int32_t* defined);
 
 /* State algebra.
  * dq_state_merge:   Analyzers.merge / State.sum on Option[State] (Analyzer.scala:343-362):

@@ -1242,6 +1242,13 @@ class GroupingMetricState:
             return float(len(counts))
         if self.op == "UniqueValueRatio":  # UniqueValueRatio.scala:25-36 (NULL sum unboxes to 0.0)
             return unique / len(counts) if counts else float("nan")
+        if self.op == "MutualInformation":  # MutualInformation.scala:37-66: marginals from the joint counts
+            px, py = {}, {}
+            for (x, y), c in self.freq.items():
+                px[x] = px.get(x, 0) + c
+                py[y] = py.get(y, 0) + c
+            n = self.numRows
+            return sum((c / n) * math.log((c / n) / ((px[x] / n) * (py[y] / n))) for (x, y), c in self.freq.items())
         if self.op == "Entropy":  # Entropy.scala:29-41
             return sum(0.0 if c == 0 else -(c / self.numRows) * math.log(c / self.numRows) for c in counts)
         raise ValueError(self.op)
@@ -1308,11 +1315,11 @@ def compute_state(spec: tuple, cols: dict, n: int, n_partitions: int = 1):
                 return None
             return MinState(v) if op == "Minimum" else MaxState(v)
         return ApproxCountDistinctState(hll_words_for(c, sel))
-    if op in ("Uniqueness", "Distinctness", "CountDistinct", "UniqueValueRatio", "Entropy"):
+    if op in ("Uniqueness", "Distinctness", "CountDistinct", "UniqueValueRatio", "Entropy", "MutualInformation"):
         columns = [spec[1]] if isinstance(spec[1], str) else list(spec[1])
         st = GroupingMetricState(op, frequencies(cols, columns, n), n)
         # the SQL sum over an empty frequencies table is NULL -> EmptyStateException (metricFromEmpty)
-        if not st.freq and op in ("Uniqueness", "Distinctness", "Entropy"):
+        if not st.freq and op in ("Uniqueness", "Distinctness", "Entropy", "MutualInformation"):
             return None
         return st
     if op == "PatternMatch":

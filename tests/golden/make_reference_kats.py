@@ -246,6 +246,11 @@ cases = [
     ("dfWithUniqueColumns", ["CountDistinct", ["uniqueWithNulls"]], 5.0, S + ":526-529", []),
     ("dataWithNullColumns", ["CountDistinct", ["stringCol"]], 0.0, "analyzers/NullHandlingTests.scala:112", []),
     ("dataWithNullColumns", ["Entropy", "stringCol"], "EmptyState", "analyzers/NullHandlingTests.scala:115", []),
+    ("dfFull", ["MutualInformation", ["att1", "att2"]], -(0.75 * math.log(0.75) + 0.25 * math.log(0.25)), S + ":148-152", []),
+    ("dfWithConditionallyUninformativeColumns", ["MutualInformation", ["att1", "att2"]], 0.0, S + ":153-156", []),
+    ("dfFull", ["MutualInformation", ["att1", "att1"]], -(0.75 * math.log(0.75) + 0.25 * math.log(0.25)), S + ":157-167 (equals Entropy(att1))", []),
+    ("dataWithNullColumns", ["MutualInformation", ["numericCol", "numericCol2"]], "EmptyState", "analyzers/NullHandlingTests.scala:116", []),
+    ("dataWithNullColumns", ["MutualInformation", ["numericCol", "numericCol3"]], "EmptyState", "analyzers/NullHandlingTests.scala:117", []),
     # partition merge (analyzers/StateAggregationIntegrationTest.scala:56-104)
     ("stateAggregation", ["Completeness", "origin", N], 0.625, "analyzers/StateAggregationIntegrationTest.scala:77", []),
 ]

@@ -18,7 +18,7 @@ from tests.helpers import close, host_column, oracle_columns
 pytestmark = pytest.mark.gpu
 
 REL = 1e-12
-GROUPING = ("Uniqueness", "Distinctness", "CountDistinct", "UniqueValueRatio", "Entropy")
+GROUPING = ("Uniqueness", "Distinctness", "CountDistinct", "UniqueValueRatio", "Entropy", "MutualInformation")
 
 
 @pytest.fixture(scope="module")
@@ -113,7 +113,7 @@ def test_reference_kats_fused_and_single(dq, kats):
                     assert metric.value.isFailure and isinstance(metric.value.failed, EmptyStateException), (c, metric)
                 elif exp == "NaN":
                     assert math.isnan(metric.value.get()), (c, metric)
-                elif c["analyzer"][0] == "Entropy":  # device log vs the JVM's: fp64 tolerance
+                elif c["analyzer"][0] in ("Entropy", "MutualInformation"):  # device log vs the JVM's: fp64 tolerance
                     assert close(metric.value.get(), exp, REL), (c["source"], a, metric, exp)
                 else:
                     assert metric.value.get() == exp, (c["source"], a, metric, exp)
@@ -776,7 +776,8 @@ def test_grouping_vs_oracle(dq, n, chunked):
     data = _group_table(dq, n, 5 + n, chunked)
     analyzers = [dq.Uniqueness("f"), dq.Distinctness("l"), dq.CountDistinct("i"), dq.UniqueValueRatio("s"),
                  dq.Entropy("t"), dq.Entropy("f"), dq.Uniqueness(["s", "i"]), dq.CountDistinct(["l", "f", "t"]),
-                 dq.Distinctness(["i"]), dq.Size()]
+                 dq.Distinctness(["i"]), dq.MutualInformation("s", "i"), dq.MutualInformation("f", "l"),
+                 dq.MutualInformation(["t", "t"]), dq.Size()]
     ctx = dq.AnalysisRunner.onData(data).addAnalyzers(analyzers).run()
     parts = _chunks(data)
     ocols, total = {}, 0
@@ -799,7 +800,7 @@ def test_grouping_vs_oracle(dq, n, chunked):
             continue
         want = ref.metricValue()
         got = m.value.get()
-        assert close(got, want, REL) if type(a).__name__ == "Entropy" else (got == want or (math.isnan(got) and math.isnan(want))), (a, got, want)
+        assert close(got, want, REL, 1e-15) if type(a).__name__ in ("Entropy", "MutualInformation") else (got == want or (math.isnan(got) and math.isnan(want))), (a, got, want)
 
 
 def test_grouping_state_merge_and_incremental(dq):
