@@ -108,7 +108,9 @@ DQ_HD uint64_t xxh64_int(uint32_t v) { return fmix_tail(xxh64_int_head(v)); }
 
 // Predicated 64-bit move dst = cond ? src : dst.  On the device it is one exec-masked v_mov_b64
 // (s_and_saveexec / s_mov exec around it) instead of two v_cndmask_b32.
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && defined(DQ_SEL64_CNDMASK)
+__device__ __forceinline__ void sel64(uint64_t& dst, uint64_t src, bool cond) { dst = cond ? src : dst; }
+#elif defined(__HIP_DEVICE_COMPILE__)
 __device__ __forceinline__ void sel64(uint64_t& dst, uint64_t src, bool cond) {
   uint64_t save;
   asm("s_and_saveexec_b64 %[s], %[m]\n\t"
