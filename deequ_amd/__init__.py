@@ -8,8 +8,8 @@ from ._lib import DQError, lib  # noqa: F401  (fails loudly if libdqscan.so is m
 from .analyzers import (ApproxCountDistinct, Completeness, Compliance, Correlation, DataType,  # noqa: F401
                         DataTypeInstances, Maximum, Mean, Minimum, PatternMatch, Patterns, Size, StandardDeviation,
                         Sum)
-from .grouping import (CountDistinct, Distinctness, Entropy, FrequenciesAndNumRows, MutualInformation,  # noqa: F401
-                       Uniqueness, UniqueValueRatio)
+from .grouping import (CountDistinct, Distinctness, Entropy, FrequenciesAndNumRows, Histogram,  # noqa: F401
+                       MutualInformation, Uniqueness, UniqueValueRatio)
 from .metrics import DoubleMetric, Distribution, DistributionValue, Entity, HistogramMetric  # noqa: F401
 from .runner import AnalysisRunner, AnalyzerContext  # noqa: F401
 from .state_provider import HdfsStateProvider, InMemoryStateProvider  # noqa: F401

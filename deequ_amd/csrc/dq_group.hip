@@ -316,13 +316,40 @@ struct dq_freq_table {
   int64_t n_values = 0;  // rows with all grouping columns non-null
   uint64_t* d_keys = nullptr;
   int64_t* d_counts = nullptr;
+  uint64_t* d_rep = nullptr;  // hashed tables built from data: one row id (chunk << 40 | row) per group
   ~dq_freq_table() {
     if (d_keys) (void)hipFree(d_keys);
     if (d_counts) (void)hipFree(d_counts);
+    if (d_rep) (void)hipFree(d_rep);
   }
 };
 
-static dq_status rle_into(dq_freq_table* t, const uint64_t* sorted, int64_t n) {
+namespace dq {
+namespace {
+__global__ void gather_rep(const uint64_t* __restrict__ sorted_rows, const int64_t* __restrict__ starts, int64_t G,
+                           uint64_t* __restrict__ rep) {
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < G; g += (int64_t)gridDim.x * blockDim.x)
+    rep[g] = sorted_rows[starts[g]];
+}
+__global__ void iota_u32(uint32_t* __restrict__ out, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = (uint32_t)i;
+}
+__global__ void gather_top(const uint32_t* __restrict__ idx, int32_t n, const uint64_t* __restrict__ keys,
+                           const int64_t* __restrict__ counts, const uint64_t* __restrict__ rep,
+                           uint64_t* __restrict__ ok, int64_t* __restrict__ oc, uint64_t* __restrict__ orp) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    const uint32_t g = idx[i];
+    ok[i] = keys[g];
+    oc[i] = counts[g];
+    orp[i] = rep ? rep[g] : ~0ull;
+  }
+}
+}  // namespace
+}  // namespace dq
+
+static dq_status rle_into(dq_freq_table* t, const uint64_t* sorted, int64_t n, const uint64_t* sorted_rows = nullptr) {
   DevBuf nruns(t->device, 20), tmp(t->device, 21);
   if (dq_status s = nruns.alloc(sizeof(int64_t))) return s;
   GHIP(hipMalloc(&t->d_keys, std::max<int64_t>(1, n) * sizeof(uint64_t)));
@@ -336,6 +363,19 @@ static dq_status rle_into(dq_freq_table* t, const uint64_t* sorted, int64_t n) {
                                              (int)n, t->stream));
   GHIP(hipMemcpyAsync(&t->n_groups, nruns.p, sizeof(int64_t), hipMemcpyDeviceToHost, t->stream));
   GHIP(hipStreamSynchronize(t->stream));
+  if (sorted_rows && t->n_groups > 0) {  // representative row of every group (Histogram renders its value)
+    DevBuf starts(t->device, 22);
+    if (dq_status s = starts.alloc(t->n_groups * 8)) return s;
+    size_t tb2 = 0;
+    GHIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, t->d_counts, starts.as<int64_t>(), (int)t->n_groups, t->stream));
+    if (dq_status s = tmp.alloc(tb2)) return s;
+    GHIP(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb2, t->d_counts, starts.as<int64_t>(), (int)t->n_groups, t->stream));
+    GHIP(hipMalloc(&t->d_rep, t->n_groups * 8));
+    hipLaunchKernelGGL(gather_rep, dim3(grid_for(t->n_groups)), dim3(256), 0, t->stream, sorted_rows,
+                       starts.as<int64_t>(), t->n_groups, t->d_rep);
+    GHIP(hipGetLastError());
+    GHIP(hipStreamSynchronize(t->stream));
+  }
   return DQ_OK;
 }
 
@@ -456,7 +496,8 @@ static dq_status freq_build_impl(const int32_t* types, int32_t n_cols, const dq_
     }
   }
   if (mi) return mi_from_joint(t, sorted_keys.as<uint64_t>(), sorted_rows.as<uint64_t>(), nv, d_chunks.as<GroupCols>(), *mi);
-  if (dq_status s = rle_into(t, sorted_keys.as<uint64_t>(), nv)) return s;
+  if (dq_status s = rle_into(t, sorted_keys.as<uint64_t>(), nv, t->hashed ? sorted_rows.as<uint64_t>() : nullptr))
+    return s;
   *out = guard.release();
   return DQ_OK;
 }
@@ -636,5 +677,41 @@ dq_status dq_freq_export(const dq_freq_table* t, uint64_t* keys, int64_t* counts
 }
 
 void dq_freq_destroy(dq_freq_table* t) { delete t; }
+
+dq_status dq_freq_top(const dq_freq_table* t, int32_t n, uint64_t* keys, int64_t* counts, uint64_t* rep_rows,
+                      int32_t* n_out) {
+  if (!t || n < 0 || !n_out || (n > 0 && (!keys || !counts || !rep_rows)))
+    return set_error(DQ_E_INVALID, "dq_freq_top: bad arguments");
+  const int32_t m = (int32_t)std::min<int64_t>(n, t->n_groups);
+  *n_out = m;
+  if (m == 0) return DQ_OK;
+  GHIP(hipSetDevice(t->device));
+  std::lock_guard<std::mutex> lock(g_arena_mu);
+  const int D = t->device;
+  const int64_t G = t->n_groups;
+  DevBuf idx(D, 50), sidx(D, 51), sc(D, 52), tmp(D, 53), ok(D, 54), oc(D, 55), orp(D, 56);
+  if (dq_status s = idx.alloc(G * 4)) return s;
+  if (dq_status s = sidx.alloc(G * 4)) return s;
+  if (dq_status s = sc.alloc(G * 8)) return s;
+  for (DevBuf* b : {&ok, &oc, &orp})
+    if (dq_status s = b->alloc((size_t)m * 8)) return s;
+  hipLaunchKernelGGL(iota_u32, dim3(grid_for(G)), dim3(256), 0, t->stream, idx.as<uint32_t>(), G);
+  GHIP(hipGetLastError());
+  // counts descending, ties in key order (stable radix sort over groups already in key order)
+  size_t tb = 0;
+  GHIP(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tb, t->d_counts, sc.as<int64_t>(), idx.as<uint32_t>(),
+                                                    sidx.as<uint32_t>(), (int)G, 0, 64, t->stream));
+  if (dq_status s = tmp.alloc(tb)) return s;
+  GHIP(hipcub::DeviceRadixSort::SortPairsDescending(tmp.p, tb, t->d_counts, sc.as<int64_t>(), idx.as<uint32_t>(),
+                                                    sidx.as<uint32_t>(), (int)G, 0, 64, t->stream));
+  hipLaunchKernelGGL(gather_top, dim3((m + 255) / 256), dim3(256), 0, t->stream, sidx.as<uint32_t>(), m, t->d_keys,
+                     t->d_counts, t->d_rep, ok.as<uint64_t>(), oc.as<int64_t>(), orp.as<uint64_t>());
+  GHIP(hipGetLastError());
+  GHIP(hipMemcpyAsync(keys, ok.p, (size_t)m * 8, hipMemcpyDeviceToHost, t->stream));
+  GHIP(hipMemcpyAsync(counts, oc.p, (size_t)m * 8, hipMemcpyDeviceToHost, t->stream));
+  GHIP(hipMemcpyAsync(rep_rows, orp.p, (size_t)m * 8, hipMemcpyDeviceToHost, t->stream));
+  GHIP(hipStreamSynchronize(t->stream));
+  return DQ_OK;
+}
 
 }  // extern "C"

@@ -266,3 +266,138 @@ class MutualInformation(FrequencyBasedAnalyzer):  # MutualInformation.scala:32-8
             return self.compute(data)
         except Exception as e:
             return self.toFailureMetric(e)
+
+
+def _java_double_to_string(d: float) -> str:
+    """java.lang.Double.toString (Spark's CAST(double AS STRING)): plain decimal for 1e-3 <= |d| < 1e7,
+    computerized scientific notation otherwise; digits from the shortest round-trip repr (Java 8 can
+    print one more digit in rare cases)."""
+    import math
+
+    if math.isnan(d):
+        return "NaN"
+    if math.isinf(d):
+        return "Infinity" if d > 0 else "-Infinity"
+    if d == 0.0:
+        return "-0.0" if math.copysign(1.0, d) < 0 else "0.0"
+    if 1e-3 <= abs(d) < 1e7:
+        r = repr(d)
+        return r if "." in r else r + ".0"
+    from decimal import Decimal
+
+    t = Decimal(repr(abs(d))).as_tuple()  # the shortest round-trip digits
+    digits = "".join(map(str, t.digits)).lstrip("0")
+    exp10 = t.exponent + len(t.digits) - 1 - (len(t.digits) - len("".join(map(str, t.digits)).lstrip("0")))
+    digits = digits.rstrip("0") or "0"
+    mant = digits[0] + "." + (digits[1:] or "0")
+    return f"{'-' if d < 0 else ''}{mant}E{exp10}"
+
+
+class Histogram(Analyzer):  # Histogram.scala:33-99
+    """Counts of the column's values cast to string (NULL -> "NullValue"): the maxDetailBins largest
+    groups (ties in key order; Spark's rdd.top leaves them unspecified) with ratio count / numRows, and
+    the number of bins.  The frequencies are the device table of build_frequencies; values are
+    rendered on the host only for the returned bins."""
+    name = "Histogram"
+    grouping = True
+    direct = True
+    NullFieldReplacement = "NullValue"
+    MaximumAllowedDetailBins = 1000
+
+    def __init__(self, column: str, binningUdf=None, maxDetailBins: int = 1000):
+        self.column = column
+        self.binningUdf = binningUdf
+        self.maxDetailBins = maxDetailBins
+
+    def _fields(self):
+        return (self.column, id(self.binningUdf) if self.binningUdf is not None else None, self.maxDetailBins)
+
+    def __str__(self):
+        return f"Histogram({self.column},{'None' if self.binningUdf is None else 'Some(udf)'},{self.maxDetailBins})"
+
+    __repr__ = __str__
+
+    @property
+    def instance(self):
+        return self.column
+
+    def groupingColumns(self):
+        return [self.column]
+
+    def preconditions(self):
+        from .metrics import IllegalAnalyzerParameterException
+
+        def param_check(schema):
+            if self.maxDetailBins > Histogram.MaximumAllowedDetailBins:
+                raise IllegalAnalyzerParameterException(
+                    f"Cannot return histogram values for more than {Histogram.MaximumAllowedDetailBins} values")
+        return [param_check, Preconditions.hasColumn(self.column)]
+
+    def toFailureMetric(self, e: BaseException):
+        from .metrics import HistogramMetric
+
+        return HistogramMetric(self.column, Failure(wrap_if_necessary(e)))
+
+    def _render(self, data, dtype: str, key: int, rep: int) -> str:
+        import numpy as np
+
+        if dtype in ("i64", "i32"):
+            return str(int(np.uint64(key).astype(np.int64)))
+        if dtype == "f64":
+            return _java_double_to_string(float(np.uint64(key).view(np.float64)))
+        if rep == (1 << 64) - 1:
+            raise NotImplementedError("Histogram of a merged string frequency table (no representative rows)")
+        from .runner import _chunks
+
+        col = _chunks(data)[rep >> 40].columns[self.column]
+        r = rep & ((1 << 40) - 1)
+        width = 8 if col.dtype == "large_utf8" else 4
+        o = col.offsets[r * width:(r + 2) * width].cpu().numpy().view(np.int64 if width == 8 else np.int32)
+        return bytes(col.values[int(o[0]):int(o[1])].cpu().numpy()).decode("utf-8", "replace")
+
+    def computeMetricFromState(self, state: "FrequenciesAndNumRows", data):
+        from .metrics import Distribution, DistributionValue, HistogramMetric
+
+        n = self.maxDetailBins
+        keys = (ctypes.c_uint64 * max(1, n))()
+        counts = (ctypes.c_int64 * max(1, n))()
+        reps = (ctypes.c_uint64 * max(1, n))()
+        got = ctypes.c_int32()
+        L.check(L.lib.dq_freq_top(state.frequencies.handle, n, keys, counts, reps, ctypes.byref(got)))
+        dtype = {v: k for k, v in _TYPES.items()}[state.frequencies.types[0]]
+        bins = [(self._render(data, dtype, keys[i], reps[i]), int(counts[i])) for i in range(got.value)]
+        summary = state.frequencies.summary(state.numRows)
+        nulls = state.numRows - summary.num_values
+        bin_count = summary.num_groups
+        if nulls > 0:  # .na.fill("NullValue"): the NULLs are one more group
+            merged = False
+            for i, (k, c) in enumerate(bins):
+                if k == Histogram.NullFieldReplacement:  # a literal "NullValue" string joins them
+                    bins[i] = (k, c + nulls)
+                    merged = True
+            if not merged:
+                bins.append((Histogram.NullFieldReplacement, nulls))
+                bin_count += 1
+            bins.sort(key=lambda kc: -kc[1])
+            bins = bins[:n]
+        values = {k: DistributionValue(c, c / state.numRows) for k, c in bins}
+        return HistogramMetric(self.column, Success(Distribution(values, numberOfBins=bin_count)))
+
+    def calculate(self, data, aggregateWith=None, saveStatesWith=None):
+        try:
+            for cond in self.preconditions():
+                cond(data_schema(data))
+            if self.binningUdf is not None:
+                from .metrics import UnsupportedOnGpuPathException
+
+                raise UnsupportedOnGpuPathException(f"{self}: a binning UDF runs in Spark, not on the GPU path")
+            state = build_frequencies(data, [self.column])
+            if aggregateWith is not None:
+                prev = aggregateWith.load(self)
+                if prev is not None:
+                    state = state.sum(prev)
+            if saveStatesWith is not None:
+                saveStatesWith.persist(self, state)
+            return self.computeMetricFromState(state, data)
+        except Exception as e:
+            return self.toFailureMetric(e)

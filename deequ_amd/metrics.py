@@ -51,6 +51,10 @@ class NumberOfSpecifiedColumnsException(MetricCalculationPreconditionException):
     pass
 
 
+class IllegalAnalyzerParameterException(MetricCalculationException):  # analyzers/Analyzer.scala (Histogram PARAM_CHECK)
+    pass
+
+
 class UnsupportedOnGpuPathException(MetricCalculationRuntimeException):
     """The analyzer (or its predicate) is outside the GPU-eligible set; a Spark shim keeps such
     analyzers on data.agg (fallback set).  This host has no Spark, so it surfaces as a

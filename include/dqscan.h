@@ -227,6 +227,11 @@ dq_status dq_freq_summarize(const dq_freq_table* t, int64_t num_rows, dq_freq_su
 int64_t dq_freq_num_groups(const dq_freq_table* t);
 dq_status dq_freq_export(const dq_freq_table* t, uint64_t* keys, int64_t* counts, int64_t cap);
 void dq_freq_destroy(dq_freq_table* t);
+/* Histogram (analyzers/Histogram.scala:33-99): the n largest groups by count (ties in key order):
+ * key, count and -- for a table built from data with hashed keys (strings) -- one representative row
+ * id (chunk << 40 | row) whose value the caller renders; ~0 when not available (merged tables). */
+dq_status dq_freq_top(const dq_freq_table* t, int32_t n, uint64_t* keys, int64_t* counts, uint64_t* rep_rows,
+                      int32_t* n_out);
 /* MutualInformation(a, b) (analyzers/MutualInformation.scala:32-72): joint frequencies of the two
  * columns, their marginals summed from the joint counts, and
  * sum (pxy / N) * ln((pxy / N) / ((px / N) * (py / N))) with N = num_rows.  cols: n_chunks x 2 views.

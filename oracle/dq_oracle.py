@@ -1254,6 +1254,17 @@ class GroupingMetricState:
         raise ValueError(self.op)
 
 
+def histogram(cols: dict, column: str, n: int):
+    """Histogram.computeStateFrom (Histogram.scala:51-66): CAST(col AS STRING), NULL -> "NullValue",
+    count per string -> {value: count}; numberOfBins = number of groups."""
+    freq: dict = {}
+    c = cols[column]
+    for i in range(n):
+        k = _value_string(c, i).decode("utf-8", "replace") if c.valid[i] else "NullValue"
+        freq[k] = freq.get(k, 0) + 1
+    return freq
+
+
 def _where(cols, n, where: Optional[str]):
     """(where_true, where_notnull) masks; no where -> all true."""
     if where is None:

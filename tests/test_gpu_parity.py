@@ -818,3 +818,44 @@ def test_grouping_state_merge_and_incremental(dq):
     dq.AnalysisRunner.onData(a).addAnalyzer(u).saveStatesWith(prov).run()
     inc = dq.AnalysisRunner.onData(b).addAnalyzer(u).aggregateWith(prov).run().metric(u).value.get()
     assert inc == dq.AnalysisRunner.onData([a, b]).addAnalyzer(u).run().metric(u).value.get()
+
+
+def test_histogram_reference_cases(dq, kats):
+    """AnalyzerTests.scala:200-272: bins of a string column with NULLs, of a numeric column, top-N
+    truncation, the maxDetailBins precondition, and a binning UDF (Spark-side, not on the GPU path)."""
+    from deequ_amd.metrics import UnsupportedOnGpuPathException
+
+    missing = _device_table(dq, kats["datasets"]["dfMissing"])
+    h = dq.Histogram("att1").calculate(missing).value.get()
+    assert h.numberOfBins == 3 and set(h.values) == {"a", "b", "NullValue"}
+    assert h.values["a"].absolute == 4 and h.values["NullValue"].ratio == 6 / 12
+    numeric = _device_table(dq, kats["datasets"]["dfWithNumericValues"])
+    h = dq.Histogram("att2").calculate(numeric).value.get()
+    assert h.numberOfBins == 4 and len(h.values) == 4 and h.values["0"].absolute == 3
+    h = dq.Histogram("att1", None, 2).calculate(missing).value.get()
+    assert h.numberOfBins == 3 and set(h.values) == {"a", "NullValue"}
+    m = dq.Histogram("att1", None, 1001).calculate(_device_table(dq, kats["datasets"]["dfFull"]))
+    assert str(m.value.failed) == "Cannot return histogram values for more than 1000 values"
+    m = dq.Histogram("att1", lambda v: v).calculate(missing)
+    assert isinstance(m.value.failed, UnsupportedOnGpuPathException)
+
+
+@pytest.mark.parametrize("n", [1, 4099, 70_001])
+def test_histogram_vs_oracle(dq, n):
+    """Histogram of f64 (NaN, -0.0, scientific notation), i64, i32, UTF8 and LARGE_UTF8 columns with
+    NULLs vs the oracle's CAST-to-string frequencies; with maxDetailBins below the number of bins the
+    returned counts are the largest ones."""
+    data = _group_table(dq, n, 11 + n)
+    host = {name: host_column(c, n) for name, c in data.columns.items()}
+    ocols = {name: O.OColumn(data.columns[name].dtype.replace("large_", ""), host[name][0], host[name][1])
+             for name in data.columns}
+    for col in ("f", "l", "i", "s", "t"):
+        want = O.histogram(ocols, col, n)
+        h = dq.Histogram(col).calculate(data).value.get()
+        assert h.numberOfBins == len(want), (col, h.numberOfBins, len(want))
+        top = sorted(want.values(), reverse=True)[:1000]
+        assert sorted((v.absolute for v in h.values.values()), reverse=True) == top, col
+        for k, v in h.values.items():
+            assert want[k] == v.absolute and v.ratio == v.absolute / n, (col, k)
+        h5 = dq.Histogram(col, None, 5).calculate(data).value.get()
+        assert sorted((v.absolute for v in h5.values.values()), reverse=True) == top[:5], col
