@@ -1,6 +1,6 @@
 #!/bin/bash
 # profile_round.sh <tag> -- rocprofv3 evidence for bench.py on the GPU box (run via gpurun):
-#   1. kernel trace + stats of the default bench workload (C5, 1e9 rows, 16 chunks)
+#   1. kernel trace + stats of the default bench workload (C5, 1e9 rows, 8 chunks of 125 M rows)
 #   2. FETCH_SIZE pass (its own run, no tracing domains besides the counters), 4 chunks
 #   3. SQ instruction-count pass (VALU / VMEM / LDS instructions per kernel), 4 chunks
 # then tools/summarize_prof.py writes profiles/<tag>_*.  Stops at the first failing step.
