@@ -1269,6 +1269,9 @@ __device__ __forceinline__ void pred_atom_regex_utf8(const PredInstr& ins, const
   wn = ins.null_res == NR_NULL ? ~va : 0u;
 }
 
+// RX: the program holds regex atoms.  Instantiated separately so that the DFA walk's registers (142
+// VGPRs with it, 119 without: 3 vs 4 waves per SIMD) do not cost the plain numeric programs occupancy.
+template <bool RX>
 __global__ __launch_bounds__(kBlock) void dq_pred_scan(const PredProgram* __restrict__ prog_g, ScanCols cols,
                                                        ScanBitmaps bm, int64_t n_rows, int64_t rows_per_range,
                                                        PredPartial* __restrict__ acc) {
@@ -1285,7 +1288,7 @@ __global__ __launch_bounds__(kBlock) void dq_pred_scan(const PredProgram* __rest
   }
   // compiled regex DFAs -> LDS after the waves' scratch
   uint16_t* dfa_lds = reinterpret_cast<uint16_t*>(pred_lds + kWaves * wave_words);
-  if (prog.regex_words > 0) {
+  if (RX && prog.regex_words > 0) {
     for (int k = threadIdx.x; k < prog.regex_words; k += kBlock) dfa_lds[k] = prog.regex[k];
     __syncthreads();
   }
@@ -1330,7 +1333,7 @@ __global__ __launch_bounds__(kBlock) void dq_pred_scan(const PredProgram* __rest
         if (op == PO_ATOM_CMP) {
           if ((g & 1u) == 0) pred_atom_cmp(ins, B0, lane, wt, wn);
           else pred_atom_cmp(ins, B1, lane, wt, wn);
-        } else if (op == PO_ATOM_REGEX) {
+        } else if (RX && op == PO_ATOM_REGEX) {
           const uint32_t va = (g & 1u) ? B1.va : B0.va;
           if (ins.kind_a == CK_UTF8)
             pred_atom_regex_utf8(ins, dfa_lds + ins.lit_i, reinterpret_cast<const uint8_t*>(cols.values[ins.col_a]),
@@ -1488,9 +1491,14 @@ __global__ void dq_init_acc(ColPartial* col_acc, int32_t ncol, CorrPartial* pair
 // host-side launchers (called from dq_plan.cpp)
 // ------------------------------------------------------------------------------------------
 hipError_t launch_pred_scan(const PredProgram* prog, const ScanCols& cols, const ScanBitmaps& bm, int64_t n_rows,
-                            int64_t rows_per_range, int32_t nranges, PredPartial* acc, int32_t lds_bytes, hipStream_t st) {
-  hipLaunchKernelGGL(dq_pred_scan, dim3(nranges), dim3(kBlock), (size_t)lds_bytes, st, prog, cols, bm, n_rows,
-                     rows_per_range, acc);
+                            int64_t rows_per_range, int32_t nranges, PredPartial* acc, int32_t lds_bytes, hipStream_t st,
+                            bool has_regex) {
+  if (has_regex)
+    hipLaunchKernelGGL(dq_pred_scan<true>, dim3(nranges), dim3(kBlock), (size_t)lds_bytes, st, prog, cols, bm, n_rows,
+                       rows_per_range, acc);
+  else
+    hipLaunchKernelGGL(dq_pred_scan<false>, dim3(nranges), dim3(kBlock), (size_t)lds_bytes, st, prog, cols, bm, n_rows,
+                       rows_per_range, acc);
   return hipGetLastError();
 }
 

@@ -28,7 +28,8 @@
 namespace dq {
 
 hipError_t launch_pred_scan(const PredProgram* prog, const ScanCols& cols, const ScanBitmaps& bm, int64_t n_rows,
-                            int64_t rows_per_range, int32_t nranges, PredPartial* acc, int32_t lds_bytes, hipStream_t st);
+                            int64_t rows_per_range, int32_t nranges, PredPartial* acc, int32_t lds_bytes, hipStream_t st,
+                            bool has_regex);
 hipError_t launch_column_scan(int32_t variant, const ColTask* tasks, int32_t ntasks, int32_t part_base,
                               const ScanCols& cols, const ScanBitmaps& bm, int64_t n_rows, int64_t rows_per_range,
                               int32_t nranges, ColPartial* partials, uint32_t* hll_acc, hipStream_t st);
@@ -1039,7 +1040,8 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
     if (dq_status s = timed(p, 0, p->stream, [&] {
           const int32_t lds = kWaves * 128 * (p->prog.stack_depth + p->prog.n_roots + p->prog.n_counters) +
                               ((p->prog.regex_words * 2 + 15) & ~15);
-          return launch_pred_scan(p->d_prog, sc, bm, n_rows, rpr_pred, nr_pred, p->d_pred_acc, lds, p->stream);
+          return launch_pred_scan(p->d_prog, sc, bm, n_rows, rpr_pred, nr_pred, p->d_pred_acc, lds, p->stream,
+                                  p->prog.regex_words > 0);
         }))
       return s;
   // fork: variant launches (and the pair pass) round-robin over the plan stream + side streams
