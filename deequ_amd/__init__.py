@@ -10,7 +10,9 @@ from .analyzers import (ApproxCountDistinct, Completeness, Compliance, Correlati
                         Sum)
 from .grouping import (CountDistinct, Distinctness, Entropy, FrequenciesAndNumRows, Histogram,  # noqa: F401
                        MutualInformation, Uniqueness, UniqueValueRatio)
-from .metrics import DoubleMetric, Distribution, DistributionValue, Entity, HistogramMetric  # noqa: F401
+from .metrics import (DoubleMetric, Distribution, DistributionValue, Entity, HistogramMetric,  # noqa: F401
+                      KeyedDoubleMetric)
+from .quantiles import ApproxQuantile, ApproxQuantiles  # noqa: F401
 from .runner import AnalysisRunner, AnalyzerContext  # noqa: F401
 from .state_provider import HdfsStateProvider, InMemoryStateProvider  # noqa: F401
 from .states import (ApproxCountDistinctState, CorrelationState, DataTypeHistogram, MaxState, MeanState,  # noqa: F401

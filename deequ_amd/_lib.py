@@ -149,6 +149,9 @@ def _load():
         raise ImportError(
             f"{LIB_PATH} is missing: build it with `make -C deequ_amd` or __graft_entry__.build(); "
             "the MI355X scan has no CPU fallback")
+    # torch first: its HIP runtime is then the one libdqscan.so binds to, so device pointers, streams and
+    # the device list are shared (loaded the other way round, a second runtime instance can see no device)
+    import torch  # noqa: F401
     L = ctypes.CDLL(LIB_PATH)
     c = ctypes
     P = c.POINTER
@@ -178,6 +181,9 @@ def _load():
     L.dq_mutual_information.restype = c.c_int32
     L.dq_mutual_information.argtypes = [P(c.c_int32), P(ColumnView), P(c.c_int64), c.c_int32, c.c_int64, c.c_int32,
                                         c.c_void_p, P(c.c_double), P(c.c_int32)]
+    L.dq_approx_quantiles.restype = c.c_int32
+    L.dq_approx_quantiles.argtypes = [c.c_int32, P(ColumnView), P(c.c_int64), c.c_int32, P(c.c_double), c.c_int32,
+                                      c.c_double, c.c_int32, c.c_void_p, P(c.c_double), P(c.c_int64)]
     L.dq_freq_top.restype = c.c_int32
     L.dq_freq_top.argtypes = [c.c_void_p, c.c_int32, P(c.c_uint64), P(c.c_int64), P(c.c_uint64), P(c.c_int32)]
     L.dq_freq_destroy.restype = None
@@ -229,7 +235,7 @@ lib = _load()
 EXPORTED = [
     "dq_abi_version", "dq_last_error", "dq_plan_create", "dq_plan_create_ex", "dq_regex_info", "dq_regex_match_host",
     "dq_plan_set_stream", "dq_freq_build", "dq_freq_merge", "dq_freq_summarize", "dq_freq_num_groups",
-    "dq_freq_export", "dq_freq_destroy", "dq_mutual_information", "dq_freq_top", "dq_scan", "dq_finish",
+    "dq_freq_export", "dq_freq_destroy", "dq_mutual_information", "dq_approx_quantiles", "dq_freq_top", "dq_scan", "dq_finish",
     "dq_plan_reset", "dq_plan_destroy", "dq_plan_bytes_per_row_x1000", "dq_plan_num_launches",
     "dq_plan_enable_timing", "dq_plan_kernel_time", "dq_plan_variant_bytes_per_row_x1000",
     "dq_state_merge", "dq_state_combine", "dq_state_is_defined", "dq_state_metric", "dq_hll_estimate",

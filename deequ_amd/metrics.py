@@ -171,3 +171,17 @@ class HistogramMetric:  # HistogramMetric.scala:37-61
             out.append(DoubleMetric(self.entity, f"{self.name}.abs.{key}", self.instance, Success(float(v.absolute))))
             out.append(DoubleMetric(self.entity, f"{self.name}.ratio.{key}", self.instance, Success(v.ratio)))
         return out
+
+
+@dataclass(eq=True)
+class KeyedDoubleMetric:  # Metric.scala:51-63 (ApproxQuantiles: quantile.toString -> value)
+    entity: Entity
+    name: str
+    instance: str
+    value: Try
+
+    def flatten(self):
+        if self.value.isSuccess:
+            return [DoubleMetric(self.entity, f"name-{k}", self.instance, Success(v))  # the reference's literal s"name-$key"
+                    for k, v in self.value.get().items()]
+        return [DoubleMetric(self.entity, "name", self.instance, self.value)]

@@ -227,6 +227,18 @@ dq_status dq_freq_summarize(const dq_freq_table* t, int64_t num_rows, dq_freq_su
 int64_t dq_freq_num_groups(const dq_freq_table* t);
 dq_status dq_freq_export(const dq_freq_table* t, uint64_t* keys, int64_t* counts, int64_t cap);
 void dq_freq_destroy(dq_freq_table* t);
+/* ApproxQuantile / ApproxQuantiles (analyzers/ApproxQuantile.scala:49-103, ApproxQuantiles.scala:30-105;
+ * replaces their DeequFunctions.stateful_approx_quantile aggregation + PercentileDigest.getPercentiles).
+ * One numeric column (DQ_TYPE_F64 / I64 / I32) over n_chunks chunk views; per quantile the exact order
+ * statistic of rank ceil(q * n) over the non-null values (rank 1 if q <= relative_error, n if
+ * q >= 1 - relative_error, as Spark 2.2's QuantileSummaries.query), which is inside the GK error bound
+ * the reference guarantees.  NaN sorts last (java.lang.Double.compare), -0.0 before 0.0.  *count = the
+ * number of non-null values (0: no digest, out untouched).  Parameters outside [0, 1] are DQ_E_INVALID
+ * with the reference's MetricCalculationException message in dq_last_error(). */
+#define DQ_MAX_QUANTILES 8
+dq_status dq_approx_quantiles(int32_t type, const dq_column_view* cols, const int64_t* chunk_rows, int32_t n_chunks,
+                              const double* quantiles, int32_t n_q, double relative_error, int32_t device,
+                              void* hip_stream, double* out, int64_t* count);
 /* Histogram (analyzers/Histogram.scala:33-99): the n largest groups by count (ties in key order):
  * key, count and -- for a table built from data with hashed keys (strings) -- one representative row
  * id (chunk << 40 | row) whose value the caller renders; ~0 when not available (merged tables). */

@@ -1431,3 +1431,41 @@ def state_to_bytes(state) -> bytes:
                         state.numString)
         return struct.pack(">i", len(b)) + b
     raise TypeError(type(state))
+
+
+# --------------------------------------------------------------------------------------
+# ApproxQuantile(s): the GPU path's contract (analyzers/ApproxQuantile.scala:49-103,
+# ApproxQuantiles.scala:30-105).  Spark 2.2.2's QuantileSummaries.query answers min for
+# q <= relativeError, max for q >= 1 - relativeError, otherwise a value whose rank is within
+# ceil(relativeError * n) of ceil(q * n); the path returns the exact order statistic of that target
+# rank (NaN last as java.lang.Double.compare, -0.0 < 0.0).  Pinned by the reference's band tests
+# (AnalyzerTests.scala:533-565); GK's own order-dependent pick is not restated (parity vs GK
+# unpinned -- any value inside its bound is a correct ApproxQuantile).
+# --------------------------------------------------------------------------------------
+def approx_quantiles_exact(values: np.ndarray, valid: np.ndarray, quantiles: Sequence[float],
+                           relative_error: float = 0.01) -> Optional[List[float]]:
+    v = np.asarray(values)[np.asarray(valid, bool)]
+    n = len(v)
+    if n == 0:
+        return None
+    if v.dtype == np.float64:
+        bits = v.view(np.uint64).copy()
+        bits[np.isnan(v)] = np.uint64(0x7FF8000000000000)
+        sign = (bits >> np.uint64(63)) == 1
+        keys = np.where(sign, ~bits, bits | np.uint64(1 << 63))
+        order = np.sort(keys)
+        back = np.where((order >> np.uint64(63)) == 1, order & np.uint64(MASK64 >> 1), ~order)
+        srt = back.view(np.float64)
+    else:
+        srt = np.sort(v.astype(np.int64)).astype(np.float64)
+    out = []
+    for q in quantiles:
+        if q <= relative_error:
+            r = 1
+        elif q >= 1.0 - relative_error:
+            r = n
+        else:
+            r = int(math.ceil(q * n))
+        r = min(n, max(1, r))
+        out.append(float(srt[r - 1]))
+    return out

@@ -1,0 +1,145 @@
+"""ApproxQuantile / ApproxQuantiles (ApproxQuantile.scala:49-103, ApproxQuantiles.scala:30-105).
+
+CPU: the oracle against the reference's own band tests (AnalyzerTests.scala:533-565) and the
+parameter checks' messages (:567-600).  GPU (`-m gpu`): dq_approx_quantiles through the C ABI
+against the oracle's exact order statistic, bit-exact (it is a selection, no arithmetic), over f64
+with NaN / +-inf / -0.0 / nulls, i64, i32, several chunks, all-null and ragged sizes.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import pytest
+
+from oracle import dq_oracle as O
+
+
+def test_oracle_reference_bands():
+    v = np.arange(-1000, 1000, dtype=np.int64)  # sparkContext.range(-1000L, 1000L)
+    med, q1, q3 = O.approx_quantiles_exact(v, np.ones(len(v), bool), [0.5, 0.25, 0.75])
+    assert -20 < med < 20 and -520 < q1 < -480 and 480 < q3 < 520
+
+
+def test_oracle_order_and_ends():
+    f = np.array([np.nan, -0.0, 0.0, -np.inf, np.inf, 1.5, -2.5])
+    got = O.approx_quantiles_exact(f, np.ones(7, bool), [0.0, 0.3, 0.45, 0.6, 0.75, 1.0], 0.0)
+    assert got[0] == -np.inf and math.copysign(1, got[1]) < 0 and got[1] == 0 and math.copysign(1, got[2]) > 0
+    assert got[3] == 1.5 and got[4] == np.inf and math.isnan(got[5])
+    # q <= relativeError -> min, q >= 1 - relativeError -> max (QuantileSummaries.query)
+    assert O.approx_quantiles_exact(np.arange(100.0), np.ones(100, bool), [0.01, 0.995], 0.01) == [0.0, 99.0]
+    assert O.approx_quantiles_exact(np.arange(3.0), np.zeros(3, bool), [0.5]) is None
+
+
+@pytest.mark.parametrize("q,err,msg", [
+    (0.5, 1.1, "Relative error parameter must be in the closed interval [0, 1]. Currently, the value is: 1.1!"),
+    (0.5, -0.1, "Relative error parameter must be in the closed interval [0, 1]. Currently, the value is: -0.1!"),
+    (-0.1, 0.01, "Quantile parameter must be in the closed interval [0, 1]. Currently, the value is: -0.1!"),
+    (1.1, 0.01, "Quantile parameter must be in the closed interval [0, 1]. Currently, the value is: 1.1!"),
+])
+def test_param_checks(q, err, msg):
+    from deequ_amd import ApproxQuantile, ApproxQuantiles
+    from deequ_amd.analyzers import Preconditions
+
+    schema = [("att1", "f64", True), ("s", "utf8", True)]
+    for a in (ApproxQuantile("att1", q, err), ApproxQuantiles("att1", [0.5, q], err)):
+        e = Preconditions.findFirstFailing(schema, a.preconditions())
+        assert e is not None and str(e) == msg, (a, e)
+    assert Preconditions.findFirstFailing(schema, ApproxQuantile("att1", 0.5).preconditions()) is None
+    assert "Expected type of column s" in str(Preconditions.findFirstFailing(schema, ApproxQuantile("s", 0.5).preconditions()))
+    assert str(ApproxQuantile("att1", 0.5)) == "ApproxQuantile(att1,0.5,0.01)"
+
+
+# ---------------------------------------------------------------------------------------------
+# GPU parity
+# ---------------------------------------------------------------------------------------------
+def _f64_data(rng, n):
+    x = rng.normal(0, 1e3, n)
+    x[rng.random(n) < 0.01] = np.nan
+    x[rng.random(n) < 0.01] = np.inf
+    x[rng.random(n) < 0.01] = -np.inf
+    x[rng.random(n) < 0.02] = -0.0
+    x[rng.random(n) < 0.02] = 0.0
+    x[rng.random(n) < 0.05] = 12.5  # ties
+    return x
+
+
+QS = [0.0, 0.001, 0.01, 0.1, 0.25, 0.5, 0.75, 0.9, 0.99, 0.999, 1.0]
+
+
+def _same(a, b):
+    return (math.isnan(a) and math.isnan(b)) or (a == b and math.copysign(1, a) == math.copysign(1, b))
+
+
+@pytest.fixture(scope="module")
+def dq():
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    import deequ_amd
+
+    return deequ_amd
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 2, 63, 1000, 70_001, 1_000_003])
+@pytest.mark.parametrize("dtype", ["f64", "i64", "i32"])
+def test_gpu_quantiles_vs_oracle(dq, n, dtype):
+    from deequ_amd.table import column_from_numpy
+
+    rng = np.random.default_rng(n * 7 + len(dtype))
+    if dtype == "f64":
+        v = _f64_data(rng, n)
+    elif dtype == "i64":
+        v = rng.integers(-(1 << 62), 1 << 62, n, dtype=np.int64)
+        v[rng.random(n) < 0.1] = rng.integers(-5, 5)
+    else:
+        v = rng.integers(-(1 << 31), (1 << 31) - 1, n, dtype=np.int64).astype(np.int32)
+    valid = rng.random(n) >= 0.1
+    t = dq.Table([column_from_numpy("x", dtype, v, valid)])
+    for err in (0.01, 0.0, 0.25):
+        want = O.approx_quantiles_exact(v, valid, QS, err)
+        m = dq.ApproxQuantiles("x", QS, err).calculate(t)
+        if want is None:
+            assert m.value.isFailure
+            continue
+        got = m.value.get()
+        for q, w in zip(QS, want):
+            key = O_str(q)
+            assert _same(got[key], w), (dtype, n, err, q, got[key], w)
+        single = dq.ApproxQuantile("x", 0.5, err).calculate(t).value.get()
+        assert _same(single, want[QS.index(0.5)])
+
+
+def O_str(q):
+    from deequ_amd.grouping import _java_double_to_string
+
+    return _java_double_to_string(q)
+
+
+@pytest.mark.gpu
+def test_gpu_quantiles_chunks_nulls_and_reference_bands(dq):
+    from deequ_amd.table import column_from_numpy
+
+    # AnalyzerTests.scala:533-565 on the device, through the runner
+    v = np.arange(-1000, 1000, dtype=np.int64)
+    t = dq.Table([column_from_numpy("att1", "i64", v, None)])
+    ctx = dq.AnalysisRunner.onData(t).addAnalyzers(
+        [dq.ApproxQuantile("att1", 0.5), dq.ApproxQuantile("att1", 0.25), dq.ApproxQuantile("att1", 0.75),
+         dq.ApproxQuantile("att1", 1.1), dq.Size()]).run()
+    assert -20 < ctx.metric(dq.ApproxQuantile("att1", 0.5)).value.get() < 20
+    assert -520 < ctx.metric(dq.ApproxQuantile("att1", 0.25)).value.get() < -480
+    assert 480 < ctx.metric(dq.ApproxQuantile("att1", 0.75)).value.get() < 520
+    assert ctx.metric(dq.ApproxQuantile("att1", 1.1)).value.isFailure
+    # several chunks == one table
+    rng = np.random.default_rng(3)
+    x = _f64_data(rng, 300_001)
+    ok = rng.random(len(x)) >= 0.2
+    cuts = [0, 1, 100_000, 100_000, 250_017, len(x)]
+    parts = [dq.Table([column_from_numpy("x", "f64", x[a:b], ok[a:b])]) for a, b in zip(cuts, cuts[1:])]
+    want = O.approx_quantiles_exact(x, ok, QS, 0.01)
+    got = dq.ApproxQuantiles("x", QS).calculate(parts).value.get()
+    assert all(_same(got[O_str(q)], w) for q, w in zip(QS, want))
+    # all NULL -> empty state failure
+    t0 = dq.Table([column_from_numpy("x", "f64", x[:100], np.zeros(100, bool))])
+    assert dq.ApproxQuantile("x", 0.5).calculate(t0).value.isFailure

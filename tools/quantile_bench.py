@@ -1,0 +1,49 @@
+"""ApproxQuantile(s) on the device: rows/s and HBM rate of dq_approx_quantiles (diagnostic).
+
+Algorithmic bytes per row = 6 passes x (8 B value + 1/8 B validity) for f64 / i64.
+    python tools/quantile_bench.py [--rows 1e9] [--reps 5]
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    import torch
+
+    assert torch.cuda.is_available()
+    import deequ_amd as dq
+    from deequ_amd.quantiles import device_quantiles
+    from deequ_amd.table import Column
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=float, default=1e9)
+    ap.add_argument("--reps", type=int, default=5)
+    a = ap.parse_args()
+    n = int(a.rows)
+    g = torch.Generator(device="cuda").manual_seed(7)
+    vals = torch.randn(n, device="cuda", dtype=torch.float64, generator=g) * 1e3
+    valid = torch.randint(0, 256, ((n + 31) // 32 * 4,), device="cuda", dtype=torch.uint8, generator=g)
+    valid |= 0xEF  # ~1/8 nulls
+    col = Column("x", "f64", n, vals.view(torch.uint8), valid, None, nullable=True)
+    t = dq.Table([col])
+    for qs in ([0.5], [0.25, 0.5, 0.75], [0.01, 0.1, 0.25, 0.5, 0.75, 0.9, 0.99, 0.999]):
+        device_quantiles(t, "x", qs, 0.01)  # warm-up
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.reps):
+            r = device_quantiles(t, "x", qs, 0.01)
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) / a.reps * 1e3
+        gbs = 6 * (8 + 1 / 8) * n / (ms * 1e-3) / 1e9
+        print(f"quantiles={len(qs)} rows={n:.3g} ms={ms:.3f} rows/s={n / (ms * 1e-3):.4g} "
+              f"algorithmic GB/s={gbs:.0f} ({gbs / 8000:.2f} of 8 TB/s) first={r[0]:.6g}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
