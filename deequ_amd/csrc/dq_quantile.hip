@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "dq_internal.h"
@@ -33,7 +34,7 @@ namespace {
 
 constexpr int kQBlock = 256;
 constexpr int kQBins = 2048;  // 11-bit digits
-constexpr int kQRowsPerThread = 8;
+constexpr int kQUnroll = 4;   // 16-byte vectors in flight per thread
 constexpr int kQPasses = 6;
 constexpr int kQShift[kQPasses] = {53, 42, 31, 20, 9, 0};
 constexpr int kQWidth[kQPasses] = {11, 11, 11, 11, 11, 9};
@@ -41,6 +42,8 @@ constexpr int kQWidth[kQPasses] = {11, 11, 11, 11, 11, 9};
 struct QSelect {
   uint64_t prefix[DQ_MAX_QUANTILES];
   uint64_t pmask[DQ_MAX_QUANTILES];
+  unsigned long long* cand[DQ_MAX_QUANTILES];  // APPEND: keys matching prefix[q] go to cand[q][...]
+  unsigned long long* cand_cnt;                // APPEND: nq append cursors
 };
 
 __device__ __forceinline__ uint64_t order_key_f64(uint64_t b) {
@@ -49,44 +52,111 @@ __device__ __forceinline__ uint64_t order_key_f64(uint64_t b) {
 }
 
 template <int TYPE>
+__device__ __forceinline__ uint64_t order_key(uint64_t raw) {
+  if constexpr (TYPE == DQ_TYPE_F64) return order_key_f64(raw);
+  else if constexpr (TYPE == DQ_TYPE_I64) return raw ^ 0x8000000000000000ull;
+  else return (uint64_t)(int64_t)(int32_t)(uint32_t)raw ^ 0x8000000000000000ull;
+}
+
+// One key into the digit histograms of every quantile whose prefix it matches; with APPEND the
+// matching keys are also appended to that quantile's candidate list (one global atomic per wave).
+template <bool APPEND>
+__device__ __forceinline__ void q_count(uint64_t key, bool ok, int32_t shift, uint32_t dmask, int32_t nq,
+                                        const QSelect& sel, uint32_t* lds_hist) {
+  const uint32_t d = (uint32_t)(key >> shift) & dmask;
+  for (int q = 0; q < nq; ++q) {
+    const bool m = ok && (key & sel.pmask[q]) == sel.prefix[q];
+    if (m) atomicAdd(&lds_hist[q * kQBins + d], 1u);
+    if constexpr (APPEND) {
+      const uint64_t b = __builtin_amdgcn_ballot_w64(m);
+      if (b) {
+        const int lane = threadIdx.x & 63, first = __builtin_ctzll(b);
+        unsigned long long base = 0;
+        if (lane == first) base = atomicAdd(&sel.cand_cnt[q], (unsigned long long)__builtin_popcountll(b));
+        base = __shfl(base, first);
+        if (m) sel.cand[q][base + __builtin_popcountll(b & ((1ull << lane) - 1ull))] = key;
+      }
+    }
+  }
+}
+
+// Pass over a column chunk: each thread reads 16-byte vectors (V rows; V = 1 when the values are not
+// 16-byte aligned), kQUnroll of them in flight, grid-stride; one validity word per vector.
+template <int TYPE, int V, bool APPEND>
 __global__ __launch_bounds__(kQBlock) void dq_quantile_hist(const void* __restrict__ values,
                                                             const uint32_t* __restrict__ validity, int64_t n,
                                                             int32_t shift, uint32_t dmask, int32_t nq, QSelect sel,
                                                             unsigned long long* __restrict__ hist) {
+  using T = typename std::conditional<TYPE == DQ_TYPE_I32, uint32_t, uint64_t>::type;
   extern __shared__ uint32_t lds_hist[];  // nq x kQBins
   for (int i = threadIdx.x; i < nq * kQBins; i += kQBlock) lds_hist[i] = 0;
   __syncthreads();
+  const T* v = reinterpret_cast<const T*>(values);
+  const int64_t nvec = (n + V - 1) / V;
   const int64_t stride = (int64_t)gridDim.x * kQBlock;
-  for (int64_t r0 = (int64_t)blockIdx.x * kQBlock + threadIdx.x; r0 < n; r0 += stride * kQRowsPerThread) {
-    uint64_t key[kQRowsPerThread];
-    bool ok[kQRowsPerThread];
+  for (int64_t v0 = (int64_t)blockIdx.x * kQBlock + threadIdx.x; v0 - threadIdx.x < nvec; v0 += stride * kQUnroll) {
+    T raw[kQUnroll][V];
+    uint32_t vw[kQUnroll];
 #pragma unroll
-    for (int j = 0; j < kQRowsPerThread; ++j) {
-      const int64_t r = r0 + j * stride;
-      ok[j] = r < n;
-      uint64_t k = 0;
-      if (ok[j]) {
-        if constexpr (TYPE == DQ_TYPE_F64)
-          k = order_key_f64(__builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(values) + r));
-        else if constexpr (TYPE == DQ_TYPE_I64)
-          k = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(values) + r) ^ 0x8000000000000000ull;
-        else
-          k = (uint64_t)(int64_t)__builtin_nontemporal_load(reinterpret_cast<const int32_t*>(values) + r) ^
-              0x8000000000000000ull;
-        if (validity) ok[j] = (validity[r >> 5] >> (r & 31)) & 1u;
+    for (int u = 0; u < kQUnroll; ++u) {
+      const int64_t vi = v0 + u * stride;
+      const int64_t r = vi * V;
+      vw[u] = 0;
+      if (r + V <= n) {
+        if constexpr (V > 1) {
+          typedef T vec_t __attribute__((ext_vector_type(V)));
+          const vec_t x = __builtin_nontemporal_load(reinterpret_cast<const vec_t*>(v + r));
+#pragma unroll
+          for (int e = 0; e < V; ++e) raw[u][e] = x[e];
+        } else {
+          raw[u][0] = __builtin_nontemporal_load(v + r);
+        }
+        vw[u] = validity ? (validity[r >> 5] >> (r & 31)) : 0xFFFFFFFFu;
+      } else {
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+          raw[u][e] = r + e < n ? v[r + e] : 0;
+          if (r + e < n) vw[u] |= (validity ? (validity[(r + e) >> 5] >> ((r + e) & 31)) & 1u : 1u) << e;
+        }
       }
-      key[j] = k;
     }
 #pragma unroll
-    for (int j = 0; j < kQRowsPerThread; ++j) {
-      const uint32_t d = (uint32_t)(key[j] >> shift) & dmask;
-      for (int q = 0; q < nq; ++q)
-        if (ok[j] && (key[j] & sel.pmask[q]) == sel.prefix[q]) atomicAdd(&lds_hist[q * kQBins + d], 1u);
-    }
+    for (int u = 0; u < kQUnroll; ++u)
+#pragma unroll
+      for (int e = 0; e < V; ++e)
+        q_count<APPEND>(order_key<TYPE>(raw[u][e]), (vw[u] >> e) & 1u, shift, dmask, nq, sel, lds_hist);
   }
   __syncthreads();
   for (int i = threadIdx.x; i < nq * kQBins; i += kQBlock)
     if (lds_hist[i]) atomicAdd(&hist[i], (unsigned long long)lds_hist[i]);
+}
+
+// Later passes over one quantile's candidate keys (already order keys, all non-null).
+__global__ __launch_bounds__(kQBlock) void dq_quantile_cand_hist(const unsigned long long* __restrict__ keys,
+                                                                 int64_t n, int32_t shift, uint32_t dmask,
+                                                                 uint64_t prefix, uint64_t pmask,
+                                                                 unsigned long long* __restrict__ hist) {
+  __shared__ uint32_t lds_hist[kQBins];
+  for (int i = threadIdx.x; i < kQBins; i += kQBlock) lds_hist[i] = 0;
+  __syncthreads();
+  for (int64_t r = (int64_t)blockIdx.x * kQBlock + threadIdx.x; r < n; r += (int64_t)gridDim.x * kQBlock) {
+    const uint64_t key = keys[r];
+    if ((key & pmask) == prefix) atomicAdd(&lds_hist[(uint32_t)(key >> shift) & dmask], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kQBins; i += kQBlock)
+    if (lds_hist[i]) atomicAdd(&hist[i], (unsigned long long)lds_hist[i]);
+}
+
+template <int TYPE, int V>
+void launch_hist(bool append, int grid, size_t lds, hipStream_t st, const void* values, const uint32_t* val,
+                 int64_t rows, int shift, uint32_t dmask, int nq, const QSelect& sel, unsigned long long* hist) {
+  if (append)
+    hipLaunchKernelGGL((dq_quantile_hist<TYPE, V, true>), dim3(grid), dim3(kQBlock), lds, st, values, val, rows, shift,
+                       dmask, nq, sel, hist);
+  else
+    hipLaunchKernelGGL((dq_quantile_hist<TYPE, V, false>), dim3(grid), dim3(kQBlock), lds, st, values, val, rows,
+                       shift, dmask, nq, sel, hist);
 }
 
 #define QHIP(x)                                                                             \
@@ -97,6 +167,8 @@ __global__ __launch_bounds__(kQBlock) void dq_quantile_hist(const void* __restri
 
 struct DevHist {
   unsigned long long* p = nullptr;
+  DevHist() = default;
+  DevHist(const DevHist&) = delete;
   ~DevHist() {
     if (p) (void)hipFree(p);
   }
@@ -154,31 +226,103 @@ dq_status dq_approx_quantiles(int32_t type, const dq_column_view* cols, const in
   QSelect sel{};
   std::vector<int64_t> rank(n_q, 0);  // 1-based rank still to find inside the selected prefix
   int64_t n = 0;
+  // candidate lists: once every quantile's remaining candidates (the rows matching its selected
+  // prefix) fit in n / 16 keys in total, the next column pass appends them, and the passes after it
+  // read only those keys instead of the column
+  DevHist cand, cand_cnt;
+  bool compacted = false;
+  std::vector<int64_t> remaining(n_q, 0), cand_off(n_q, 0), cand_len(n_q, 0);
+  std::vector<int> hrow(n_q);  // histogram row of quantile q in this pass
   for (int pass = 0; pass < kQPasses; ++pass) {
     QHIP(hipMemsetAsync(dh.p, 0, hist_bytes, stream));
-    for (int c = 0; c < n_chunks; ++c) {
-      const int64_t rows = chunk_rows[c];
-      if (rows == 0) continue;
-      const int64_t per_block = (int64_t)kQBlock * kQRowsPerThread;
-      const int grid = (int)std::min<int64_t>(8192, (rows + per_block - 1) / per_block);
-      const auto* val = reinterpret_cast<const uint32_t*>(cols[c].validity);
-      const uint32_t dmask = (1u << kQWidth[pass]) - 1u;
-      const size_t lds = (size_t)n_q * kQBins * sizeof(uint32_t);
-      if (type == DQ_TYPE_F64)
-        hipLaunchKernelGGL(dq_quantile_hist<DQ_TYPE_F64>, dim3(grid), dim3(kQBlock), lds, stream, cols[c].values, val,
-                           rows, kQShift[pass], dmask, n_q, sel, dh.p);
-      else if (type == DQ_TYPE_I64)
-        hipLaunchKernelGGL(dq_quantile_hist<DQ_TYPE_I64>, dim3(grid), dim3(kQBlock), lds, stream, cols[c].values, val,
-                           rows, kQShift[pass], dmask, n_q, sel, dh.p);
-      else
-        hipLaunchKernelGGL(dq_quantile_hist<DQ_TYPE_I32>, dim3(grid), dim3(kQBlock), lds, stream, cols[c].values, val,
-                           rows, kQShift[pass], dmask, n_q, sel, dh.p);
-      QHIP(hipGetLastError());
+    for (int q = 0; q < n_q; ++q) hrow[q] = q;
+    const uint32_t dmask32 = (1u << kQWidth[pass]) - 1u;
+    if (compacted) {
+      for (int q = 0; q < n_q; ++q) {
+        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(1024, (cand_len[q] + kQBlock * 8 - 1) / (kQBlock * 8)));
+        hipLaunchKernelGGL(dq_quantile_cand_hist, dim3(grid), dim3(kQBlock), 0, stream, cand.p + cand_off[q],
+                           (int64_t)cand_len[q], kQShift[pass], dmask32, sel.prefix[q], sel.pmask[q],
+                           dh.p + (size_t)q * kQBins);
+        QHIP(hipGetLastError());
+      }
+    } else {
+      // quantiles that share a selected prefix (all of them in pass 0) share one histogram row and one
+      // candidate list: the column pass does each distinct (prefix, digit) count once
+      QSelect usel{};
+      int nu = 0;
+      std::vector<int64_t> uremaining;
+      for (int q = 0; q < n_q; ++q) {
+        int u = 0;
+        while (u < nu && !(usel.prefix[u] == sel.prefix[q] && usel.pmask[u] == sel.pmask[q])) ++u;
+        if (u == nu) {
+          usel.prefix[nu] = sel.prefix[q];
+          usel.pmask[nu] = sel.pmask[q];
+          uremaining.push_back(remaining[q]);
+          ++nu;
+        }
+        hrow[q] = u;
+      }
+      bool append = false;
+      if (pass > 0 && pass < kQPasses - 1) {
+        int64_t total = 0;
+        for (int u = 0; u < nu; ++u) total += uremaining[u];
+        if (total <= std::max<int64_t>(n / 16, 1 << 16)) {
+          QHIP(hipMalloc(&cand.p, (size_t)std::max<int64_t>(total, 1) * 8));
+          QHIP(hipMalloc(&cand_cnt.p, DQ_MAX_QUANTILES * 8));
+          QHIP(hipMemsetAsync(cand_cnt.p, 0, DQ_MAX_QUANTILES * 8, stream));
+          std::vector<int64_t> uoff(nu, 0);
+          int64_t off = 0;
+          for (int u = 0; u < nu; ++u) {
+            uoff[u] = off;
+            usel.cand[u] = cand.p + off;
+            off += uremaining[u];
+          }
+          for (int q = 0; q < n_q; ++q) {
+            cand_off[q] = uoff[hrow[q]];
+            cand_len[q] = uremaining[hrow[q]];
+          }
+          usel.cand_cnt = cand_cnt.p;
+          append = true;
+        }
+      }
+      for (int c = 0; c < n_chunks; ++c) {
+        const int64_t rows = chunk_rows[c];
+        if (rows == 0) continue;
+        const auto* val = reinterpret_cast<const uint32_t*>(cols[c].validity);
+        const size_t lds = (size_t)nu * kQBins * sizeof(uint32_t);
+        const bool aligned = (reinterpret_cast<uintptr_t>(cols[c].values) & 15u) == 0;
+        const int64_t rows_per_vec = aligned ? (type == DQ_TYPE_I32 ? 4 : 2) : 1;
+        const int64_t per_block = (int64_t)kQBlock * kQUnroll * rows_per_vec;
+        const int grid = (int)std::min<int64_t>(4096, (rows + per_block - 1) / per_block);
+        const void* vals = cols[c].values;
+        const int sh = kQShift[pass];
+        if (type == DQ_TYPE_F64) {
+          if (aligned) launch_hist<DQ_TYPE_F64, 2>(append, grid, lds, stream, vals, val, rows, sh, dmask32, nu, usel, dh.p);
+          else launch_hist<DQ_TYPE_F64, 1>(append, grid, lds, stream, vals, val, rows, sh, dmask32, nu, usel, dh.p);
+        } else if (type == DQ_TYPE_I64) {
+          if (aligned) launch_hist<DQ_TYPE_I64, 2>(append, grid, lds, stream, vals, val, rows, sh, dmask32, nu, usel, dh.p);
+          else launch_hist<DQ_TYPE_I64, 1>(append, grid, lds, stream, vals, val, rows, sh, dmask32, nu, usel, dh.p);
+        } else {
+          if (aligned) launch_hist<DQ_TYPE_I32, 4>(append, grid, lds, stream, vals, val, rows, sh, dmask32, nu, usel, dh.p);
+          else launch_hist<DQ_TYPE_I32, 1>(append, grid, lds, stream, vals, val, rows, sh, dmask32, nu, usel, dh.p);
+        }
+        QHIP(hipGetLastError());
+      }
+      if (append) {
+        std::vector<unsigned long long> got(DQ_MAX_QUANTILES);
+        QHIP(hipMemcpyAsync(got.data(), cand_cnt.p, DQ_MAX_QUANTILES * 8, hipMemcpyDeviceToHost, stream));
+        QHIP(hipStreamSynchronize(stream));
+        for (int u = 0; u < nu; ++u)
+          if ((int64_t)got[u] != uremaining[u])
+            return set_error(DQ_E_HIP, "dq_approx_quantiles: %llu candidates for prefix %d, expected %lld (data changed?)",
+                             got[u], u, (long long)uremaining[u]);
+        compacted = true;
+      }
     }
     QHIP(hipMemcpyAsync(h.data(), dh.p, hist_bytes, hipMemcpyDeviceToHost, stream));
     QHIP(hipStreamSynchronize(stream));
     if (pass == 0) {
-      for (int b = 0; b < kQBins; ++b) n += (int64_t)h[b];  // every non-null row matches the empty prefix
+      for (int b = 0; b < kQBins; ++b) n += (int64_t)h[b];  // every non-null row matches the empty prefix (row 0)
       *count = n;
       if (n == 0) return DQ_OK;  // all values NULL: no digest (fromAggregationResult -> None)
       for (int q = 0; q < n_q; ++q) {
@@ -193,7 +337,7 @@ dq_status dq_approx_quantiles(int32_t type, const dq_column_view* cols, const in
     }
     const uint64_t dmask = (1ull << kQWidth[pass]) - 1ull;
     for (int q = 0; q < n_q; ++q) {
-      const unsigned long long* hq = h.data() + (size_t)q * kQBins;
+      const unsigned long long* hq = h.data() + (size_t)hrow[q] * kQBins;
       int64_t cum = 0;
       int b = 0;
       for (; b < (int)dmask; ++b) {
@@ -203,6 +347,7 @@ dq_status dq_approx_quantiles(int32_t type, const dq_column_view* cols, const in
       if (cum + (int64_t)hq[b] < rank[q])
         return set_error(DQ_E_HIP, "dq_approx_quantiles: histogram of pass %d lost rows (data changed?)", pass);
       rank[q] -= cum;
+      remaining[q] = (int64_t)hq[b];
       sel.prefix[q] |= (uint64_t)b << kQShift[pass];
       sel.pmask[q] |= dmask << kQShift[pass];
     }
