@@ -141,40 +141,52 @@ __global__ __launch_bounds__(kQBlock) void dq_quantile_hist(const void* __restri
             if (((vw[u] >> e) & 1u) && (key[u * V + e] & pm) == pf) atomicAdd(&hq[dig[u * V + e]], 1u);
       }
     } else {
-      // histogram as above, and per quantile one append reservation per wave for all kQUnroll x V rows
-      // of its lanes (a wave-wide exclusive scan of the lanes' match counts)
-      const int lane = threadIdx.x & 63;
+      // histogram as above (the common path: no lane of the wave matches), then, only in waves with a
+      // match, per quantile one append reservation per wave for all kQUnroll x V rows of its lanes (a
+      // wave-wide exclusive scan of the lanes' match counts)
+      bool any = false;
       for (int q = 0; q < nq; ++q) {
         const uint64_t pm = sel.pmask[q], pf = sel.prefix[q];
         uint32_t* hq = lds_hist + q * kQBins;
-        uint32_t mbits = 0;
-#pragma unroll
-        for (int u = 0; u < kQUnroll; ++u)
-#pragma unroll
-          for (int e = 0; e < V; ++e) {
-            const bool m = ((vw[u] >> e) & 1u) && (key[u * V + e] & pm) == pf;
-            if (m) atomicAdd(&hq[dig[u * V + e]], 1u);
-            mbits |= (uint32_t)m << (u * V + e);
-          }
-        if (__builtin_amdgcn_ballot_w64(mbits != 0) == 0) continue;
-        const uint32_t cnt = __builtin_popcount(mbits);
-        uint32_t incl = cnt;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-          const uint32_t y = __shfl_up(incl, d);
-          if (lane >= d) incl += y;
-        }
-        const uint32_t total = __shfl(incl, 63);
-        unsigned long long base = 0;
-        if (lane == 0) base = atomicAdd(&sel.cand_cnt[q], (unsigned long long)total);
-        base = __shfl(base, 0);
-        unsigned long long* const cq = sel.cand[q];
-        unsigned long long pos = base + (incl - cnt);
 #pragma unroll
         for (int u = 0; u < kQUnroll; ++u)
 #pragma unroll
           for (int e = 0; e < V; ++e)
-            if ((mbits >> (u * V + e)) & 1u) cq[pos++] = key[u * V + e];
+            if (((vw[u] >> e) & 1u) && (key[u * V + e] & pm) == pf) {
+              atomicAdd(&hq[dig[u * V + e]], 1u);
+              any = true;
+            }
+      }
+      if (__builtin_amdgcn_ballot_w64(any) != 0) {
+        const int lane = threadIdx.x & 63;
+        for (int q = 0; q < nq; ++q) {
+          const uint64_t pm = sel.pmask[q], pf = sel.prefix[q];
+          uint32_t mbits = 0;
+#pragma unroll
+          for (int u = 0; u < kQUnroll; ++u)
+#pragma unroll
+            for (int e = 0; e < V; ++e)
+              mbits |= (uint32_t)(((vw[u] >> e) & 1u) && (key[u * V + e] & pm) == pf) << (u * V + e);
+          if (__builtin_amdgcn_ballot_w64(mbits != 0) == 0) continue;
+          const uint32_t cnt = __builtin_popcount(mbits);
+          uint32_t incl = cnt;
+#pragma unroll
+          for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(incl, d);
+            if (lane >= d) incl += y;
+          }
+          const uint32_t total = __shfl(incl, 63);
+          unsigned long long base = 0;
+          if (lane == 0) base = atomicAdd(&sel.cand_cnt[q], (unsigned long long)total);
+          base = __shfl(base, 0);
+          unsigned long long* const cq = sel.cand[q];
+          unsigned long long pos = base + (incl - cnt);
+#pragma unroll
+          for (int u = 0; u < kQUnroll; ++u)
+#pragma unroll
+            for (int e = 0; e < V; ++e)
+              if ((mbits >> (u * V + e)) & 1u) cq[pos++] = key[u * V + e];
+        }
       }
     }
   }
