@@ -36,6 +36,7 @@ constexpr int kQBlock = 256;
 constexpr int kQBins = 2048;  // 11-bit digits
 constexpr int kQUnroll = 4;   // 16-byte vectors in flight per thread
 constexpr int kQPasses = 6;
+constexpr int kQStage = 256;  // APPEND: candidate keys staged in LDS per quantile and workgroup
 constexpr int kQShift[kQPasses] = {53, 42, 31, 20, 9, 0};
 constexpr int kQWidth[kQPasses] = {11, 11, 11, 11, 11, 9};
 
@@ -88,8 +89,13 @@ __global__ __launch_bounds__(kQBlock) void dq_quantile_hist(const void* __restri
                                                             int32_t shift, uint32_t dmask, int32_t nq, QSelect sel,
                                                             unsigned long long* __restrict__ hist) {
   using T = typename std::conditional<TYPE == DQ_TYPE_I32, uint32_t, uint64_t>::type;
-  extern __shared__ uint32_t lds_hist[];  // nq x kQBins
+  // LDS: nq x kQBins digit counts; APPEND: + nq x kQStage staged keys + nq reserved / nq staged counts
+  extern __shared__ uint32_t lds_hist[];
+  unsigned long long* stage = reinterpret_cast<unsigned long long*>(lds_hist + nq * kQBins);
+  uint32_t* st_res = reinterpret_cast<uint32_t*>(stage + (APPEND ? nq * kQStage : 0));
+  uint32_t* st_ok = st_res + nq;
   for (int i = threadIdx.x; i < nq * kQBins; i += kQBlock) lds_hist[i] = 0;
+  if (APPEND && threadIdx.x < 2 * nq) st_res[threadIdx.x] = 0;
   __syncthreads();
   const T* v = reinterpret_cast<const T*>(values);
   const int64_t nvec = (n + V - 1) / V;
@@ -176,11 +182,25 @@ __global__ __launch_bounds__(kQBlock) void dq_quantile_hist(const void* __restri
             if (lane >= d) incl += y;
           }
           const uint32_t total = __shfl(incl, 63);
-          unsigned long long base = 0;
-          if (lane == 0) base = atomicAdd(&sel.cand_cnt[q], (unsigned long long)total);
-          base = __shfl(base, 0);
-          unsigned long long* const cq = sel.cand[q];
-          unsigned long long pos = base + (incl - cnt);
+          // reserve in the workgroup's LDS stage (flushed with one global atomic per workgroup); a wave
+          // whose keys do not fit goes to the global list directly.  Reservations are ordered, so the
+          // staged keys are exactly [0, st_ok[q]): every wave before the first misfit fitted.
+          uint32_t spos = 0;
+          if (lane == 0) spos = atomicAdd(&st_res[q], total);
+          spos = __shfl(spos, 0);
+          unsigned long long* cq;
+          unsigned long long pos;
+          if (spos + total <= (uint32_t)kQStage) {
+            if (lane == 0) atomicAdd(&st_ok[q], total);
+            cq = stage + q * kQStage;
+            pos = spos + (incl - cnt);
+          } else {
+            unsigned long long base = 0;
+            if (lane == 0) base = atomicAdd(&sel.cand_cnt[q], (unsigned long long)total);
+            base = __shfl(base, 0);
+            cq = sel.cand[q];
+            pos = base + (incl - cnt);
+          }
 #pragma unroll
           for (int u = 0; u < kQUnroll; ++u)
 #pragma unroll
@@ -193,6 +213,16 @@ __global__ __launch_bounds__(kQBlock) void dq_quantile_hist(const void* __restri
   __syncthreads();
   for (int i = threadIdx.x; i < nq * kQBins; i += kQBlock)
     if (lds_hist[i]) atomicAdd(&hist[i], (unsigned long long)lds_hist[i]);
+  if constexpr (APPEND) {
+    __shared__ unsigned long long flush_base[DQ_MAX_QUANTILES];
+    if (threadIdx.x < nq && st_ok[threadIdx.x] > 0)
+      flush_base[threadIdx.x] = atomicAdd(&sel.cand_cnt[threadIdx.x], (unsigned long long)st_ok[threadIdx.x]);
+    __syncthreads();
+    for (int q = 0; q < nq; ++q) {
+      const uint32_t k = st_ok[q];
+      for (uint32_t i = threadIdx.x; i < k; i += kQBlock) sel.cand[q][flush_base[q] + i] = stage[q * kQStage + i];
+    }
+  }
 }
 
 // Later passes over one quantile's candidate keys (already order keys, all non-null).
@@ -353,7 +383,8 @@ dq_status dq_approx_quantiles(int32_t type, const dq_column_view* cols, const in
         const int64_t rows = chunk_rows[c];
         if (rows == 0) continue;
         const auto* val = reinterpret_cast<const uint32_t*>(cols[c].validity);
-        const size_t lds = (size_t)nu * kQBins * sizeof(uint32_t);
+        const size_t lds = (size_t)nu * kQBins * sizeof(uint32_t) +
+                           (append ? (size_t)nu * kQStage * 8 + (size_t)2 * nu * sizeof(uint32_t) : 0);
         const bool aligned = (reinterpret_cast<uintptr_t>(cols[c].values) & 15u) == 0;
         const int64_t rows_per_vec = aligned ? (type == DQ_TYPE_I32 ? 4 : 2) : 1;
         const int64_t per_block = (int64_t)kQBlock * kQUnroll * rows_per_vec;
