@@ -3,16 +3,25 @@
 Per GPU: ROWS rows (default 1e9) x 16 columns (8 fp64 + 4 int64 + 4 UTF8, 10 % nulls, synthetic,
 generated on the device), held in HBM as CHUNK-row chunks (UTF8 int32 offsets < 2 GiB per chunk).
 One step = one fused scan of every chunk with the ColumnProfiler pass-1/2 analyzer set
-(Size, Completeness x16, ApproxCountDistinct x16, Min/Max/Mean/StdDev/Sum x12), dq_finish, and for
-N > 1 the RCCL allgather of the per-rank state blobs + fixed-order merge.  Rows shard across ranks
-(weak scaling).  Prints ONE JSON line on rank 0.
+(Size, Completeness x16, ApproxCountDistinct x16, Min/Max/Mean/StdDev/Sum x12), dq_finish, for N > 1 the
+RCCL all-gather of the per-rank state slot sets + fixed rank-order merge, and the incremental StateLoader
+append of C5 (the previous run's states merged in and persisted, Analyzer.scala:107-128).  Rows shard
+across ranks (weak scaling).  Prints ONE JSON line on rank 0.
+
+`--gpus N` with N > 1 and no RANK in the environment re-launches this script as N ranks
+(torch.distributed.run, one process per GPU) before anything touches the GPU.
+
+At N = 1 the line also carries the other BASELINE configs measured on this GPU ("configs": C1 Item table,
+C2 moments, C3 HLL + Compliance, C4 correlations + moments, each at its BASELINE size) and the CPU
+baselines (the oracle's C restatement on this host's CPU share).
 """
 from __future__ import annotations
 
 import argparse
-import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -35,23 +44,62 @@ def parse():
     p.add_argument("--chunk", type=int, default=DEFAULT_CHUNK, help="rows per chunk")
     p.add_argument("--cpu-sample", type=int, default=62_500_000, help="rows timed on the CPU baseline (0 = skip)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="repeat the CPU sample for at least this long")
-    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--cpu-threads", type=int, default=0, help="0 = this host's CPU share (see host_cpu_share)")
+    p.add_argument("--configs", default="c1,c2,c3,c4", help="other BASELINE configs to measure at N=1 ('' = none)")
+    p.add_argument("--config-steps", type=int, default=3)
     return p.parse_args()
+
+
+def launch_ranks(args) -> int:
+    """N fresh processes (one per GPU) through torch.distributed.run; the parent never touches the GPU."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def host_cpu_share() -> tuple:
+    """(threads, description): the CPUs this process may use -- affinity, the cgroup CPU quota and the
+    pool's OMP_NUM_THREADS (the per-GPU CPU share on the GPU boxes) -- whichever is smallest."""
+    aff = len(os.sched_getaffinity(0))
+    n = aff
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+            n = min(n, quota)
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return n, f"affinity {aff} CPUs (os.cpu_count() {os.cpu_count()}), cgroup quota {quota}, OMP_NUM_THREADS {omp}"
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "RANK" not in os.environ:
+        sys.exit(launch_ranks(args))
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_env != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} disagrees with WORLD_SIZE={world_env}")
     import torch
     import torch.distributed as dist
 
     rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world = world_env
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local % max(1, torch.cuda.device_count())))
 
-    import deequ_amd as dq
+    from deequ_amd import _lib as L
     from deequ_amd import distributed, synth
     from deequ_amd.runner import ScanPlan
 
@@ -69,6 +117,8 @@ def main():
     plan = ScanPlan(analyzers, chunks[0].schema)
     str_bytes = sum(c.data_bytes for t in chunks for c in t.columns.values() if c.dtype in ("utf8", "large_utf8"))
     algo_bytes_per_step = plan.bytes_per_row() * n_total + str_bytes  # each needed buffer once
+    persisted = [None]  # the StateLoader / StatePersister of C5's incremental append (in memory)
+    host_ms = {"merge": 0.0, "append": 0.0}
 
     def step():
         plan.reset()
@@ -76,38 +126,32 @@ def main():
             plan.scan(t)
         states = plan.finish()
         if world > 1:
+            a = time.perf_counter()
             states = distributed.allgather_combine(states)
+            host_ms["merge"] += (time.perf_counter() - a) * 1e3
+        a = time.perf_counter()
+        if persisted[0] is not None:  # load -> Analyzers.merge(state, loaded) -> persist
+            states = distributed.merge_loaded(states, persisted[0])
+        persisted[0] = states
+        host_ms["append"] += (time.perf_counter() - a) * 1e3
         return states
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
     plan.enable_timing(True)
+    host_ms.update(merge=0.0, append=0.0)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        states = step()
+        step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    from deequ_amd import _lib as L
-
-    per_variant = {}
-    for v, name in L.VARIANT_NAMES.items():
-        ms, nl = plan.kernel_time(16 + v)
-        if nl:
-            bpr = plan.variant_bytes_per_row(v)
-            data = sum(c.data_bytes for t in chunks for c in t.columns.values()
-                       if (v == 10 and c.dtype == "utf8") or (v == 11 and c.dtype == "large_utf8"))
-            per_variant[name] = {"launches": nl, "ms_total": ms, "avg_ms": ms / nl,
-                                 "bytes_per_launch": (bpr * n_total + data) / len(chunks)}
-    for rec in per_variant.values():
-        rec["GBps"] = rec["bytes_per_launch"] / (rec["avg_ms"] / 1e3) / 1e9
-    col_ms, col_launches = plan.kernel_time(1)
-    fin_ms, _ = plan.kernel_time(3)
+    kernels = kernel_report(plan, chunks, n_total)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -115,11 +159,9 @@ def main():
 
     rows_all = n_total * world * args.steps
     value = rows_all / elapsed
-    # roofline of the dominant kernel (largest total time): algorithmic bytes per launch / avg duration
-    dom_name, dom = max(per_variant.items(), key=lambda kv: kv[1]["ms_total"])
-    dom_v = {name: v for v, name in L.VARIANT_NAMES.items()}[dom_name]
-    achieved = dom["GBps"]
-    traffic = pmc_traffic(f"dq::dq_column_scan<{dom_v}>") if chunk == DEFAULT_CHUNK else None
+    dom_name, dom = max(((k, v) for k, v in kernels.items() if k.startswith("dq_column_scan")),
+                        key=lambda kv: kv[1]["ms_total"])
+    traffic = pmc_traffic(dom["pmc_name"]) if chunk == DEFAULT_CHUNK else None
     out = {
         "metric": "rows/sec (whole node) for fused 16-col profile scan; % of HBM peak BW",
         "value": value,
@@ -133,27 +175,142 @@ def main():
         "vs_baseline": None,
         "dtype": "f64+int64+utf8",
         "data": "synthetic (device-generated, seeded; SURVEY 8d C5 distributions)",
-        "config": {"workload": "C5 fused 16-col profile scan (8 f64 + 4 i64 + 4 utf8, 10% nulls)",
+        "config": {"workload": "C5 fused 16-col profile scan (8 f64 + 4 i64 + 4 utf8, 10% nulls) + state merge "
+                               "+ incremental StateLoader append",
                    "rows_per_gpu": n_total, "chunk_rows": chunk, "analyzers": len(analyzers),
                    "parallelism": f"row-shard x{world}"},
         "hbm_frac_of_step": (algo_bytes_per_step / (elapsed / args.steps)) / 1e9 / HBM_PEAK_GBS,
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+        "rank_merge_ms_per_step": host_ms["merge"] / args.steps if world > 1 else 0.0,
+        "append_ms_per_step": host_ms["append"] / args.steps,
+        "roofline": {"bound": "hbm", "achieved": dom["GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": dom["GBps"] / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": os.path.relpath(PMC_FILE, ROOT) if traffic is not None else None,
-                     "kernel": f"dq_column_scan<{dom_name}>", "bytes_per_launch": dom["bytes_per_launch"],
-                     "avg_launch_ms": dom["avg_ms"], "launches": dom["launches"],
-                     "column_pass_ms_per_step": col_ms / args.steps,
-                     "finalize_ms_per_step": fin_ms / args.steps, "per_variant": per_variant},
+                     "kernel": dom_name, "bytes_per_launch": dom["bytes_per_launch"],
+                     "avg_launch_ms": dom["avg_ms"], "launches": dom["launches"], "kernels": kernels},
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and args.cpu_sample > 0:
-        out["cpu_baseline"] = cpu_baseline(chunks[0], min(args.cpu_sample, chunks[0].num_rows), args.cpu_threads,
-                                           args.cpu_seconds)
+    if rank == 0 and world == 1:
+        out["state_io"] = state_io_timing(analyzers, persisted[0])
+        if args.cpu_sample > 0:
+            out["cpu_baseline"] = cpu_baseline(chunks[0], min(args.cpu_sample, chunks[0].num_rows), args.cpu_threads,
+                                               args.cpu_seconds)
+    plan.close()
+    del chunks
+    torch.cuda.empty_cache()
+    if world == 1 and args.configs:
+        out["configs"] = {}
+        for cfg in [c for c in args.configs.split(",") if c]:
+            out["configs"][cfg] = run_config(cfg, args)
+            torch.cuda.empty_cache()
     if rank == 0:
         print(json.dumps(out), flush=True)
-    plan.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def kernel_report(plan, chunks, n_total) -> dict:
+    """Per-kernel launches, average hipEvent duration and algorithmic bytes per launch (plan timing)."""
+    from deequ_amd import _lib as L
+
+    nch = len(chunks)
+    out = {}
+    ids = [(0, "dq_pred_scan"), (2, "dq_pair_scan")] + [(16 + v, f"dq_column_scan<{nm}>") for v, nm in L.VARIANT_NAMES.items()]
+    for kid, name in ids:
+        ms, nl = plan.kernel_time(kid)
+        if not nl:
+            continue
+        bpr = plan.kernel_bytes_per_row(kid)
+        data = 0
+        if kid >= 16:
+            v = kid - 16
+            data = sum(c.data_bytes for t in chunks for c in t.columns.values()
+                       if (v in (10, 13) and c.dtype == "utf8") or (v in (11, 15) and c.dtype == "large_utf8"))
+        per_launch = (bpr * n_total + data) / nch
+        rec = {"launches": nl, "ms_total": ms, "avg_ms": ms / nl, "bytes_per_launch": per_launch,
+               "GBps": per_launch / (ms / nl / 1e3) / 1e9,
+               "pmc_name": f"dq::dq_column_scan<{kid - 16}>" if kid >= 16 else name}
+        out[name] = rec
+    fin_ms, fin_n = plan.kernel_time(3)
+    if fin_n:
+        out["dq_finalize"] = {"launches": fin_n, "ms_total": fin_ms, "avg_ms": fin_ms / fin_n, "bytes_per_launch": 0,
+                              "GBps": 0.0, "pmc_name": "dq::dq_finalize"}
+    return out
+
+
+def config_setup(cfg, n, chunk):
+    """(chunk tables, analyzers, description) of a BASELINE config."""
+    import deequ_amd as dq
+    from deequ_amd import synth
+
+    gen = {"c1": synth.item_table, "c2": synth.c2_table, "c3": synth.c3_table, "c4": synth.c4_table}[cfg]
+    tables = []
+    r = 0
+    while r < n:
+        m = min(chunk, n - r)
+        tables.append(gen(m, r, 42))
+        r += m
+    names = list(tables[0].columns)
+    if cfg == "c1":
+        analyzers = synth.item_checks().requiredAnalyzers()
+        desc = "C1 Item table (examples/entities.scala:19-25): Size, isComplete x5, Mean/StdDev/Min/Max on id, numViews"
+    elif cfg == "c2":
+        analyzers = [dq.Size()] + [a for c in names for a in (dq.Completeness(c), dq.Mean(c), dq.StandardDeviation(c),
+                                                              dq.Minimum(c), dq.Maximum(c))]
+        desc = "C2 8 x f64 (10% nulls): Size + Completeness/Mean/StdDev/Min/Max per column"
+    elif cfg == "c3":
+        analyzers = [dq.Size()] + [dq.ApproxCountDistinct(c) for c in names]
+        analyzers += [dq.Compliance("p0", "i0 >= 0"),
+                      dq.Compliance("p1", "`i1` IS NULL OR (`i1` >= 10.0 AND `i1` <= 1000.0)"),
+                      dq.Compliance("p2", "i2 < i3"), dq.Compliance("p3", "COALESCE(i3, 0.0) >= 0")]
+        desc = "C3 4 x i64 + 4 x utf8 (10% nulls): Size + ApproxCountDistinct x8 + Compliance x4"
+    else:
+        analyzers = [dq.Correlation(names[i], names[j]) for i in range(8) for j in range(i + 1, 8)]
+        analyzers += [dq.Mean(c) for c in names] + [dq.StandardDeviation(c) for c in names]
+        desc = "C4 8 x f64 correlated (10% nulls): 28 Correlations + Mean/StdDev per column"
+    return tables, analyzers, desc
+
+
+def run_config(cfg, args) -> dict:
+    """One BASELINE config at its size on this GPU: rows/s, per-kernel roofline, HBM fraction of the step."""
+    import torch
+
+    from deequ_amd.runner import ScanPlan
+
+    n = 10_000_000 if cfg == "c1" else 1_000_000_000
+    tables, analyzers, desc = config_setup(cfg, n, DEFAULT_CHUNK)
+    torch.cuda.synchronize()
+    plan = ScanPlan(analyzers, tables[0].schema)
+    str_bytes = sum(c.data_bytes for t in tables for c in t.columns.values() if c.dtype in ("utf8", "large_utf8"))
+
+    def step():
+        plan.reset()
+        for t in tables:
+            plan.scan(t)
+        return plan.finish()
+
+    step()
+    torch.cuda.synchronize()
+    plan.enable_timing(True)
+    k = max(1, args.config_steps)
+    t0 = time.perf_counter()
+    for _ in range(k):
+        step()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / k
+    kernels = kernel_report(plan, tables, n)
+    # C1's string columns are read for Completeness only (validity bytes): exclude their payload
+    algo = plan.bytes_per_row() * n + (str_bytes if cfg == "c3" else 0)
+    dom_name, dom = max(kernels.items(), key=lambda kv: kv[1]["ms_total"])
+    rec = {"workload": desc, "rows": n, "analyzers": len(analyzers), "ms_per_step": dt * 1e3, "rows_per_s": n / dt,
+           "hbm_frac_of_step": algo / dt / 1e9 / HBM_PEAK_GBS,
+           "roofline": {"kernel": dom_name, "achieved": dom["GBps"], "frac": dom["GBps"] / HBM_PEAK_GBS,
+                        "avg_launch_ms": dom["avg_ms"], "bytes_per_launch": dom["bytes_per_launch"]},
+           "kernels": {k_: {kk: v[kk] for kk in ("launches", "avg_ms", "GBps")} for k_, v in kernels.items()}}
+    if cfg == "c1" and args.cpu_sample > 0:
+        rec["cpu_baseline"] = cpu_baseline_c1(tables[0], args.cpu_threads, min(args.cpu_seconds, 5.0))
+    plan.close()
+    del tables
+    return rec
 
 
 def pmc_traffic(kernel):
@@ -169,11 +326,28 @@ def pmc_traffic(kernel):
     return None
 
 
-def cpu_baseline(table, n, threads, min_seconds=10.0):
-    """The C restatement (oracle/, "port") of the same profile scan on the host cores."""
-    import numpy as np
+def state_io_timing(analyzers, states) -> dict:
+    """HdfsStateProvider round trip of the C5 state set (binary big-endian files): persist + load ms."""
+    import tempfile
 
-    from oracle import dq_oracle_c as C
+    from deequ_amd import HdfsStateProvider
+
+    with tempfile.TemporaryDirectory() as d:
+        prov = HdfsStateProvider(os.path.join(d, "c5"), allowOverwrite=True)
+        objs = [(a, a._from_result(s)) for a, s in zip(analyzers, states)]
+        t0 = time.perf_counter()
+        for a, s in objs:
+            if s is not None:
+                prov.persist(a, s)
+        t1 = time.perf_counter()
+        for a, _ in objs:
+            prov.load(a)
+        t2 = time.perf_counter()
+    return {"persist_ms": (t1 - t0) * 1e3, "load_ms": (t2 - t1) * 1e3, "states": len(objs)}
+
+
+def _host_cols(table, n):
+    import numpy as np
 
     cols = []
     for c in table.columns.values():
@@ -186,8 +360,17 @@ def cpu_baseline(table, n, threads, min_seconds=10.0):
         else:
             w = 4 if c.dtype == "i32" else 8
             cols.append((c.dtype, c.values[: n * w].cpu().numpy().view({"f64": np.float64, "i64": np.int64,
-                                                                       "i32": np.int32}[c.dtype]), None, bm))
-    threads = max(1, min(threads, os.cpu_count() or 1))
+                                                                        "i32": np.int32}[c.dtype]), None, bm))
+    return cols
+
+
+def cpu_baseline(table, n, threads, min_seconds=10.0):
+    """The C restatement (oracle/, "port") of the same profile scan on the host's CPU share."""
+    from oracle import dq_oracle_c as C
+
+    cols = _host_cols(table, n)
+    share, how = host_cpu_share()
+    threads = threads or share
     reps = 0
     t0 = time.perf_counter()
     while True:
@@ -197,9 +380,39 @@ def cpu_baseline(table, n, threads, min_seconds=10.0):
         if dt >= min_seconds:
             break
     return {"value": reps * n / dt, "unit": "rows/s", "cores": threads, "kind": "port",
+            "per_core_rows_per_s": reps * n / dt / threads,
             "sample": f"{reps} x {n} rows x 16 cols of the same C5 data (first chunk), profile scan in oracle/c "
                       f"(Spark partial/final aggregation order, per-row Welford + XXH64 HLL), {threads} OpenMP "
-                      f"threads, {dt:.1f} s"}
+                      f"threads = this host's CPU share ({how}), {dt:.1f} s"}
+
+
+def cpu_baseline_c1(table, threads, min_seconds):
+    """C1's CPU path: the oracle's C restatement of the Item-table analyzers (count / moments / min / max of
+    id and numViews, validity counts of the strings) on the host's CPU share."""
+    from oracle import dq_oracle_c as C
+
+    n = table.num_rows
+    share, how = host_cpu_share()
+    threads = threads or share
+    import numpy as np
+
+    cols = [c for c in _host_cols(table, n) if c[0] == "i64"]
+    bitmaps = [c.validity[: (n + 7) // 8].cpu().numpy() for c in table.columns.values() if c.validity is not None]
+    reps = 0
+    t0 = time.perf_counter()
+    while True:
+        for kind, vals, _, bm in cols:
+            parts = C.column_stats_partials(kind, vals, bm, threads * 4, threads)
+            C.stats_fold(kind, parts)
+        for bm in bitmaps:  # Completeness of the string columns: popcount of their validity
+            int(np.unpackbits(bm, bitorder="little")[:n].sum())
+        reps += 1
+        dt = time.perf_counter() - t0
+        if dt >= min_seconds:
+            break
+    return {"value": reps * n / dt, "unit": "rows/s", "cores": threads, "kind": "port",
+            "sample": f"{reps} x {n} Item rows: Spark-order moments / min / max of id and numViews in oracle/c, "
+                      f"{threads} OpenMP threads ({how}), {dt:.1f} s"}
 
 
 if __name__ == "__main__":

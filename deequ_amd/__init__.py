@@ -5,6 +5,8 @@ libdqscan.so: hand-written gfx950 HIP kernels behind the C ABI in include/dqscan
 is the host-side mirror of the reference's analyzer / state / runner API over that ABI.
 """
 from ._lib import DQError, lib  # noqa: F401  (fails loudly if libdqscan.so is missing)
+from .checks import (Check, CheckLevel, CheckStatus, ConstraintStatus, VerificationResult,  # noqa: F401
+                     VerificationSuite)
 from .analyzers import (ApproxCountDistinct, Completeness, Compliance, Correlation, DataType,  # noqa: F401
                         DataTypeInstances, Maximum, Mean, Minimum, PatternMatch, Patterns, Size, StandardDeviation,
                         Sum)

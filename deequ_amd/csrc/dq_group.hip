@@ -13,10 +13,14 @@
 // is a 64-bit hash of the tuple, the rows ride along the sort, and every pair of neighbours with equal
 // keys is compared exactly: a collision between distinct tuples is reported (DQ_E_UNSUPPORTED), never
 // merged silently.  Keys are radix-sorted (hipCUB) and run-length encoded into (key, count) groups;
-// the summary is a fixed-order two-level reduction, so results are deterministic.
+// the summary is a fixed-order two-level reduction, so results are deterministic.  A hashed table also
+// keeps a second, independently seeded 64-bit hash per group (its representative row's tuple), so that
+// dq_freq_merge -- which no longer has the rows -- detects two distinct tuples whose first hashes collide
+// (equal first hash, different second hash: DQ_E_UNSUPPORTED) instead of adding their counts.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -40,7 +44,10 @@ struct GroupCols {
   const void* offsets[kMaxGroupCols];
   int32_t type[kMaxGroupCols];
   int32_t n_cols;
+  uint64_t key_mask;  // applied to the primary tuple hash: ~0, or fewer bits from DQ_TEST_GROUP_HASH_MASK (tests)
 };
+
+constexpr uint64_t kSeed2 = 0x9E3779B97F4A7C15ull;  // seed of the second (verification) tuple hash
 
 __device__ __forceinline__ bool row_valid(const GroupCols& g, int64_t r) {
   for (int c = 0; c < g.n_cols; ++c)
@@ -79,8 +86,8 @@ __device__ __forceinline__ uint64_t mix8(uint64_t h, uint64_t k) {
 }
 
 // 64-bit hash of the row's tuple (columns in order; strings by bytes and length)
-__device__ uint64_t tuple_hash(const GroupCols& g, int64_t r) {
-  uint64_t h = kSeed + XP5;
+__device__ uint64_t tuple_hash(const GroupCols& g, int64_t r, uint64_t seed = kSeed) {
+  uint64_t h = seed + XP5;
   for (int c = 0; c < g.n_cols; ++c) {
     if (g.type[c] == DQ_TYPE_UTF8 || g.type[c] == DQ_TYPE_LARGE_UTF8) {
       const uint8_t* p;
@@ -101,6 +108,7 @@ __device__ uint64_t tuple_hash(const GroupCols& g, int64_t r) {
   }
   return fmix64(h);
 }
+__device__ uint64_t tuple_key(const GroupCols& g, int64_t r) { return tuple_hash(g, r) & g.key_mask; }
 
 __device__ bool tuple_equal(const GroupCols* chunks, uint64_t ra, uint64_t rb) {
   const GroupCols& ga = chunks[ra >> kRowBits];
@@ -128,7 +136,7 @@ __global__ void group_keys(GroupCols g, int64_t n, int32_t hashed, uint64_t* __r
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
     const bool v = row_valid(g, r);
     flags[r] = v ? 1 : 0;
-    keys[r] = !v ? 0 : (hashed ? tuple_hash(g, r) : value_bits(g, 0, r));
+    keys[r] = !v ? 0 : (hashed ? tuple_key(g, r) : value_bits(g, 0, r));
   }
 }
 
@@ -186,7 +194,7 @@ __device__ uint64_t col_key(const GroupCols& g, int c, int64_t r) {
   one.values[0] = g.values[c];
   one.offsets[0] = g.offsets[c];
   one.type[0] = g.type[c];
-  return tuple_hash(one, r);
+  return tuple_key(one, r);
 }
 
 __device__ bool col_equal(const GroupCols* chunks, int c, uint64_t ra, uint64_t rb) {
@@ -317,8 +325,10 @@ struct dq_freq_table {
   uint64_t* d_keys = nullptr;
   int64_t* d_counts = nullptr;
   uint64_t* d_rep = nullptr;  // hashed tables built from data: one row id (chunk << 40 | row) per group
+  uint64_t* d_keys2 = nullptr;  // hashed tables: second tuple hash per group (merge collision check)
   ~dq_freq_table() {
     if (d_keys) (void)hipFree(d_keys);
+    if (d_keys2) (void)hipFree(d_keys2);
     if (d_counts) (void)hipFree(d_counts);
     if (d_rep) (void)hipFree(d_rep);
   }
@@ -331,6 +341,33 @@ __global__ void gather_rep(const uint64_t* __restrict__ sorted_rows, const int64
   for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < G; g += (int64_t)gridDim.x * blockDim.x)
     rep[g] = sorted_rows[starts[g]];
 }
+// second hash of every group's representative row (hashed tables built from data)
+__global__ void group_keys2(const uint64_t* __restrict__ rep, int64_t G, const GroupCols* __restrict__ chunks,
+                            uint64_t* __restrict__ keys2) {
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < G; g += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t r = rep[g];
+    keys2[g] = tuple_hash(chunks[r >> kRowBits], (int64_t)(r & ((1ull << kRowBits) - 1)), kSeed2);
+  }
+}
+__global__ void iota_u64(uint64_t* __restrict__ out, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = (uint64_t)i;
+}
+// merge of hashed tables: (second hash, count) in first-hash order; equal first hashes with different
+// second hashes are distinct tuples
+__global__ void merge_gather_check(const uint64_t* __restrict__ k1s, const uint64_t* __restrict__ pos,
+                                   const uint64_t* __restrict__ k2, const int64_t* __restrict__ c, int64_t n,
+                                   uint64_t* __restrict__ k2s, int64_t* __restrict__ cs, int32_t* __restrict__ collision) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t p = pos[i];
+    k2s[i] = k2[p];
+    cs[i] = c[p];
+    if (i > 0 && k1s[i] == k1s[i - 1] && k2[p] != k2[pos[i - 1]]) atomicOr(collision, 1);
+  }
+}
+struct TakeFirst {
+  __host__ __device__ uint64_t operator()(const uint64_t& a, const uint64_t&) const { return a; }
+};
 __global__ void iota_u32(uint32_t* __restrict__ out, int64_t n) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     out[i] = (uint32_t)i;
@@ -412,11 +449,15 @@ static dq_status freq_build_impl(const int32_t* types, int32_t n_cols, const dq_
   const bool numeric1 = n_cols == 1 && (types[0] == DQ_TYPE_F64 || types[0] == DQ_TYPE_I64 || types[0] == DQ_TYPE_I32);
   t->hashed = numeric1 && !mi ? 0 : 1;
 
+  // test hook: keep only some bits of the primary tuple hash, to force collisions between distinct tuples
+  uint64_t key_mask = ~0ull;
+  if (const char* e = std::getenv("DQ_TEST_GROUP_HASH_MASK")) key_mask = std::strtoull(e, nullptr, 16);
   std::vector<GroupCols> gcs(std::max(1, n_chunks));
   for (int k = 0; k < n_chunks; ++k) {
     GroupCols& g = gcs[k];
     std::memset(&g, 0, sizeof(g));
     g.n_cols = n_cols;
+    g.key_mask = key_mask;
     for (int c = 0; c < n_cols; ++c) {
       const dq_column_view& v = cols[(size_t)k * n_cols + c];
       g.values[c] = v.values;
@@ -498,6 +539,15 @@ static dq_status freq_build_impl(const int32_t* types, int32_t n_cols, const dq_
   if (mi) return mi_from_joint(t, sorted_keys.as<uint64_t>(), sorted_rows.as<uint64_t>(), nv, d_chunks.as<GroupCols>(), *mi);
   if (dq_status s = rle_into(t, sorted_keys.as<uint64_t>(), nv, t->hashed ? sorted_rows.as<uint64_t>() : nullptr))
     return s;
+  if (t->hashed) {
+    GHIP(hipMalloc(&t->d_keys2, std::max<int64_t>(1, t->n_groups) * 8));
+    if (t->n_groups > 0) {
+      hipLaunchKernelGGL(group_keys2, dim3(grid_for(t->n_groups)), dim3(256), 0, t->stream, t->d_rep, t->n_groups,
+                         d_chunks.as<GroupCols>(), t->d_keys2);
+      GHIP(hipGetLastError());
+      GHIP(hipStreamSynchronize(t->stream));
+    }
+  }
   *out = guard.release();
   return DQ_OK;
 }
@@ -596,6 +646,11 @@ dq_status dq_freq_merge(const dq_freq_table* a, const dq_freq_table* b, dq_freq_
   *out = nullptr;
   if (a->types != b->types || a->hashed != b->hashed)
     return set_error(DQ_E_STATE, "dq_freq_merge: frequency tables over different column types");
+  const int64_t n = a->n_groups + b->n_groups;
+  if (n >= (int64_t(1) << 31))  // hipCUB sorts take an int item count
+    return set_error(DQ_E_UNSUPPORTED, "dq_freq_merge: %lld groups in the two tables (at most 2^31 - 1)", (long long)n);
+  if (a->hashed && ((a->n_groups > 0 && !a->d_keys2) || (b->n_groups > 0 && !b->d_keys2)))
+    return set_error(DQ_E_STATE, "dq_freq_merge: hashed table without its verification hashes");
   GHIP(hipSetDevice(a->device));
   auto* t = new dq_freq_table();
   std::unique_ptr<dq_freq_table> guard(t);
@@ -604,10 +659,10 @@ dq_status dq_freq_merge(const dq_freq_table* a, const dq_freq_table* b, dq_freq_
   t->types = a->types;
   t->hashed = a->hashed;
   t->n_values = a->n_values + b->n_values;
-  const int64_t n = a->n_groups + b->n_groups;
   std::lock_guard<std::mutex> lock(g_arena_mu);
   const int D = a->device;
-  DevBuf k_in(D, 10), c_in(D, 11), k_s(D, 12), c_s(D, 13), nruns(D, 14), tmp(D, 15);
+  DevBuf k_in(D, 10), c_in(D, 11), k_s(D, 12), c_s(D, 13), nruns(D, 14), tmp(D, 15), k2_in(D, 16), pos(D, 17),
+      pos_s(D, 18), k2_s(D, 19), coll(D, 23), kdrop(D, 24);
   for (DevBuf* d : {&k_in, &c_in, &k_s, &c_s})
     if (dq_status s = d->alloc(std::max<int64_t>(1, n) * 8)) return s;
   if (dq_status s = nruns.alloc(8)) return s;
@@ -617,7 +672,8 @@ dq_status dq_freq_merge(const dq_freq_table* a, const dq_freq_table* b, dq_freq_
   GHIP(hipMemcpyAsync(c_in.as<int64_t>() + a->n_groups, b->d_counts, b->n_groups * 8, hipMemcpyDeviceToDevice, t->stream));
   GHIP(hipMalloc(&t->d_keys, std::max<int64_t>(1, n) * 8));
   GHIP(hipMalloc(&t->d_counts, std::max<int64_t>(1, n) * 8));
-  if (n > 0) {
+  if (t->hashed) GHIP(hipMalloc(&t->d_keys2, std::max<int64_t>(1, n) * 8));
+  if (n > 0 && !t->hashed) {
     size_t tb = 0;
     GHIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k_in.as<uint64_t>(), k_s.as<uint64_t>(), c_in.as<int64_t>(),
                                             c_s.as<int64_t>(), (int)n, 0, 64, t->stream));
@@ -631,6 +687,48 @@ dq_status dq_freq_merge(const dq_freq_table* a, const dq_freq_table* b, dq_freq_
     GHIP(hipcub::DeviceReduce::ReduceByKey(tmp.p, tb, k_s.as<uint64_t>(), t->d_keys, c_s.as<int64_t>(), t->d_counts,
                                            nruns.as<int64_t>(), hipcub::Sum(), (int)n, t->stream));
     GHIP(hipMemcpyAsync(&t->n_groups, nruns.p, 8, hipMemcpyDeviceToHost, t->stream));
+  } else if (n > 0) {
+    // hashed keys: sort by the first hash carrying positions, gather (second hash, count), refuse equal first
+    // hashes with different second hashes, then reduce counts and keep each group's second hash
+    for (DevBuf* d : {&k2_in, &pos, &pos_s, &k2_s, &kdrop})
+      if (dq_status s = d->alloc(n * 8)) return s;
+    if (dq_status s = coll.alloc(8)) return s;
+    GHIP(hipMemcpyAsync(k2_in.p, a->d_keys2, a->n_groups * 8, hipMemcpyDeviceToDevice, t->stream));
+    GHIP(hipMemcpyAsync(k2_in.as<uint64_t>() + a->n_groups, b->d_keys2, b->n_groups * 8, hipMemcpyDeviceToDevice,
+                        t->stream));
+    hipLaunchKernelGGL(iota_u64, dim3(grid_for(n)), dim3(256), 0, t->stream, pos.as<uint64_t>(), n);
+    GHIP(hipGetLastError());
+    size_t tb = 0, need = 0;
+    GHIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k_in.as<uint64_t>(), k_s.as<uint64_t>(), pos.as<uint64_t>(),
+                                            pos_s.as<uint64_t>(), (int)n, 0, 64, t->stream));
+    need = tb;
+    GHIP(hipcub::DeviceReduce::ReduceByKey(nullptr, tb, k_s.as<uint64_t>(), t->d_keys, c_s.as<int64_t>(), t->d_counts,
+                                           nruns.as<int64_t>(), hipcub::Sum(), (int)n, t->stream));
+    need = std::max(need, tb);
+    GHIP(hipcub::DeviceReduce::ReduceByKey(nullptr, tb, k_s.as<uint64_t>(), kdrop.as<uint64_t>(), k2_s.as<uint64_t>(),
+                                           t->d_keys2, nruns.as<int64_t>(), TakeFirst(), (int)n, t->stream));
+    need = std::max(need, tb);
+    if (dq_status s = tmp.alloc(need)) return s;
+    tb = need;
+    GHIP(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, k_in.as<uint64_t>(), k_s.as<uint64_t>(), pos.as<uint64_t>(),
+                                            pos_s.as<uint64_t>(), (int)n, 0, 64, t->stream));
+    GHIP(hipMemsetAsync(coll.p, 0, 8, t->stream));
+    hipLaunchKernelGGL(merge_gather_check, dim3(grid_for(n)), dim3(256), 0, t->stream, k_s.as<uint64_t>(),
+                       pos_s.as<uint64_t>(), k2_in.as<uint64_t>(), c_in.as<int64_t>(), n, k2_s.as<uint64_t>(),
+                       c_s.as<int64_t>(), coll.as<int32_t>());
+    GHIP(hipGetLastError());
+    tb = need;
+    GHIP(hipcub::DeviceReduce::ReduceByKey(tmp.p, tb, k_s.as<uint64_t>(), t->d_keys, c_s.as<int64_t>(), t->d_counts,
+                                           nruns.as<int64_t>(), hipcub::Sum(), (int)n, t->stream));
+    tb = need;
+    GHIP(hipcub::DeviceReduce::ReduceByKey(tmp.p, tb, k_s.as<uint64_t>(), kdrop.as<uint64_t>(), k2_s.as<uint64_t>(),
+                                           t->d_keys2, nruns.as<int64_t>(), TakeFirst(), (int)n, t->stream));
+    int32_t collided = 0;
+    GHIP(hipMemcpyAsync(&collided, coll.p, 4, hipMemcpyDeviceToHost, t->stream));
+    GHIP(hipMemcpyAsync(&t->n_groups, nruns.p, 8, hipMemcpyDeviceToHost, t->stream));
+    GHIP(hipStreamSynchronize(t->stream));
+    if (collided)
+      return set_error(DQ_E_UNSUPPORTED, "dq_freq_merge: 64-bit tuple-hash collision between distinct values of the two tables");
   }
   GHIP(hipStreamSynchronize(t->stream));
   *out = guard.release();

@@ -463,6 +463,7 @@ struct dq_plan {
   double kernel_ms[kTimers] = {0};       // 0 pred, 2 pair, 3 finalize, 16 + v column variant v
   int64_t kernel_launches[kTimers] = {0};
   int64_t bytes_per_row_x1000 = 0;
+  int64_t pred_bytes_x1000 = 0, pair_bytes_x1000 = 0;
   int32_t launches_per_scan = 0;
 };
 
@@ -859,6 +860,27 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
     if (need_validity[c] && p->schema[c].nullable) b1000 += 125;
   }
   p->bytes_per_row_x1000 = b1000;
+  // per-kernel algorithmic bytes: the predicate pass (its atoms' columns) and the pair pass (its columns)
+  {
+    auto bytes_of = [&](const std::vector<int>& vals, const std::vector<int>& valid) {
+      int64_t b = 0;
+      for (int c = 0; c < ncols; ++c) {
+        int32_t t = p->schema[c].type;
+        if (vals[c]) b += (t == DQ_TYPE_I32 || t == DQ_TYPE_UTF8) ? 4000 : 8000;
+        if (valid[c] && p->schema[c].nullable) b += 125;
+      }
+      return b;
+    };
+    std::vector<int> pv(ncols, 0), pn(ncols, 0), qv(ncols, 0), qn(ncols, 0);
+    for (int i = 0; i < prog.n_instr; ++i) {
+      const PredInstr& ins = prog.instr[i];
+      if (ins.col_a >= 0) { pn[ins.col_a] = 1; if (ins.op == PO_ATOM_CMP || ins.op == PO_ATOM_REGEX) pv[ins.col_a] = 1; }
+      if (ins.col_b >= 0) { pn[ins.col_b] = 1; pv[ins.col_b] = 1; }
+    }
+    for (const PairTask& pt : p->pair_tasks) { qv[pt.col_x] = qv[pt.col_y] = qn[pt.col_x] = qn[pt.col_y] = 1; }
+    p->pred_bytes_x1000 = bytes_of(pv, pn);
+    p->pair_bytes_x1000 = bytes_of(qv, qn);
+  }
   p->launches_per_scan = (p->has_pred ? 1 : 0) + (int32_t)p->groups.size() + (p->pair_tasks.empty() ? 0 : 1) +
                          ((p->col_tasks.size() + p->pair_tasks.size()) ? 1 : 0);
 
@@ -1273,5 +1295,13 @@ int64_t dq_plan_variant_bytes_per_row_x1000(const dq_plan* p, int32_t variant) {
   return b;
 }
 int32_t dq_plan_num_launches(const dq_plan* p) { return p ? p->launches_per_scan : 0; }
+
+int64_t dq_plan_kernel_bytes_per_row_x1000(const dq_plan* p, int32_t kernel) {
+  if (!p) return 0;
+  if (kernel == 0) return p->pred_bytes_x1000;
+  if (kernel == 2) return p->pair_bytes_x1000;
+  if (kernel >= 16 && kernel < dq_plan::kTimers) return dq_plan_variant_bytes_per_row_x1000(p, kernel - 16);
+  return 0;
+}
 
 }  // extern "C"

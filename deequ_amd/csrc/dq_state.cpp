@@ -489,6 +489,20 @@ dq_status dq_state_combine(const dq_state* a, const dq_state* b, dq_state* out) 
   return st;
 }
 
+dq_status dq_state_merge_n(const dq_state* a, const dq_state* b, int32_t n, dq_state* out) {
+  if (n < 0 || (n > 0 && (!a || !b || !out))) return dq::set_error(DQ_E_INVALID, "dq_state_merge_n: bad arguments");
+  for (int32_t i = 0; i < n; ++i)
+    if (dq_status st = dq_state_merge(a + i, b + i, out + i)) return st;
+  return DQ_OK;
+}
+
+dq_status dq_state_combine_n(const dq_state* a, const dq_state* b, int32_t n, dq_state* out) {
+  if (n < 0 || (n > 0 && (!a || !b || !out))) return dq::set_error(DQ_E_INVALID, "dq_state_combine_n: bad arguments");
+  for (int32_t i = 0; i < n; ++i)
+    if (dq_status st = dq_state_combine(a + i, b + i, out + i)) return st;
+  return DQ_OK;
+}
+
 int32_t dq_state_is_defined(const dq_state* s) { return s ? dq::state_is_defined(*s) : 0; }
 
 dq_status dq_state_metric(const dq_state* s, double* out) {

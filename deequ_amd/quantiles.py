@@ -139,7 +139,10 @@ class ApproxQuantiles(_QuantileBase):  # ApproxQuantiles.scala:30-105
             return KeyedDoubleMetric(Entity.Column, self.name, self.column, Success({}))
         r = device_quantiles(data, self.column, self.quantiles, self.relativeError)
         if r is None:
-            return self.toFailureMetric(self._empty_exc())
+            # all values NULL: the digest is still Some (ApproxQuantiles.scala:64-72, no isEmpty check as in
+            # ApproxQuantile.scala:72-77) and Spark 2.2's PercentileDigest.getPercentiles returns an empty
+            # array for count == 0, so quantiles.zip(...) is an empty map
+            return KeyedDoubleMetric(Entity.Column, self.name, self.column, Success({}))
         vals: Dict[str, float] = {_java_double_to_string(q): v for q, v in zip(self.quantiles, r)}
         return KeyedDoubleMetric(Entity.Column, self.name, self.column, Success(vals))
 

@@ -71,6 +71,10 @@ class ScanPlan:
     def variant_bytes_per_row(self, variant: int) -> float:
         return L.lib.dq_plan_variant_bytes_per_row_x1000(self.handle, variant) / 1000.0
 
+    def kernel_bytes_per_row(self, kernel: int) -> float:
+        """Algorithmic bytes per row of timing kernel `kernel` (0 pred, 2 pair, 16+v variant v; no UTF8 data)."""
+        return L.lib.dq_plan_kernel_bytes_per_row_x1000(self.handle, kernel) / 1000.0
+
     def kernel_time(self, kernel: int):
         """(total ms, launches) of kernel 0 pred / 1 column (all) / 2 pair / 3 finalize / 16+v column
         variant v, since enable_timing."""

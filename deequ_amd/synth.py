@@ -161,3 +161,71 @@ def profile_analyzers(table: Table):
         if dtype in ("f64", "i64", "i32"):
             out += [Minimum(name), Maximum(name), Mean(name), StandardDeviation(name), Sum(name)]
     return out
+
+
+def _device_i64_column(name, values, nullable=False) -> Column:
+    """An int64 device column from a torch int64 tensor (padded as dqscan.h requires, no nulls)."""
+    n = values.numel()
+    buf = _alloc(n * 8)
+    buf[: n * 8].copy_(values.view(__import__("torch").uint8))
+    return Column(name, "i64", n, buf, None, None, nullable=nullable)
+
+
+def _enum_utf8_column(name, n, seed, words, null_frac, row0=0) -> Column:
+    """UTF8 column whose values are words[k] with k uniform (a counter hash of the row), on the device."""
+    import torch
+
+    k = torch.empty(n, dtype=torch.int64, device="cuda")
+    _check(lib().dqs_i64(k.data_ptr(), row0, n, seed, len(words), 0, _stream()))
+    wl = torch.tensor([len(w) for w in words], dtype=torch.int64, device="cuda")
+    lens = wl[k]
+    offs = torch.zeros(n + 1, dtype=torch.int64, device="cuda")
+    torch.cumsum(lens, 0, out=offs[1:])
+    total = int(offs[-1].item())
+    width = max(len(w) for w in words)
+    table = torch.zeros((len(words), width), dtype=torch.uint8)
+    for i, w in enumerate(words):
+        table[i, : len(w)] = torch.tensor(list(w), dtype=torch.uint8)
+    table = table.cuda()
+    row = torch.repeat_interleave(torch.arange(n, device="cuda"), lens)
+    pos = torch.arange(total, device="cuda") - offs[row]
+    data = _alloc(total)
+    data[:total] = table[k[row], pos]
+    o = _alloc((n + 1) * 4)
+    _check(lib().dqs_i64_to_i32(o.data_ptr(), offs.data_ptr(), n + 1, _stream()))
+    bm = validity(n, seed ^ 0xABCDEF, null_frac, row0)
+    return Column(name, "utf8", n, data, bm, o, nullable=bm is not None, data_bytes=total)
+
+
+def item_table(n, row0=0, seed=42) -> Table:
+    """Config C1: the Item entity of examples/entities.scala:19-25 (id: Long, name, description, priority:
+    String, numViews: Long).  id = row index and numViews uniform over [0, 10000] are non-nullable Scala
+    Longs; name / description / priority have 10 % / 30 % / 10 % NULLs, priority in {high, low}
+    (SURVEY §8d C1)."""
+    import torch
+
+    assert row0 % 32 == 0
+    ids = torch.arange(row0, row0 + n, dtype=torch.int64, device="cuda")
+    id_col = _device_i64_column("id", ids)
+    views = i64_column("numViews", n, seed + 401, 10001, 0, 0.0, row0)
+    views.nullable = False
+    return Table([id_col,
+                  utf8_column("name", n, seed + 402, 0, 8, 24, 0.10, row0),
+                  utf8_column("description", n, seed + 403, 1_000_000, 16, 48, 0.30, row0),
+                  _enum_utf8_column("priority", n, seed + 404, [b"high", b"low"], 0.10, row0),
+                  views])
+
+
+def item_checks():
+    """The C1 verification: hasSize, isComplete x 5, hasMean / hasStandardDeviation / hasMin / hasMax on
+    id and numViews, as one Check of the reference's DSL (checks/Check.scala)."""
+    from .checks import Check, CheckLevel
+
+    c = Check(CheckLevel.Error, "item table")
+    c = c.hasSize(lambda n: n > 0)
+    for col in ("id", "name", "description", "priority", "numViews"):
+        c = c.isComplete(col)
+    for col in ("id", "numViews"):
+        c = (c.hasMean(col, lambda v: v >= 0).hasStandardDeviation(col, lambda v: v >= 0)
+              .hasMin(col, lambda v: v >= 0).hasMax(col, lambda v: v >= 0))
+    return c

@@ -204,6 +204,9 @@ dq_status dq_plan_enable_timing(dq_plan* plan, int32_t on);
 dq_status dq_plan_kernel_time(dq_plan* plan, int32_t kernel, double* total_ms, int64_t* launches);
 /* Algorithmic bytes per row (x1000) the column-pass launch of variant v reads (excl. UTF8 data). */
 int64_t dq_plan_variant_bytes_per_row_x1000(const dq_plan* plan, int32_t variant);
+/* The same per timing kernel id (0 = predicate pass: its atoms' columns, 2 = pair pass: its columns,
+ * 16 + v = variant v); UTF8 data bytes excluded. */
+int64_t dq_plan_kernel_bytes_per_row_x1000(const dq_plan* plan, int32_t kernel);
 
 /* Grouping analyzers (analyzers/GroupingAnalyzers.scala:44-82, 118-138): the frequencies
  * SELECT cols, COUNT(*) FROM data WHERE cols IS NOT NULL GROUP BY cols on the GPU (sort-based), and
@@ -212,7 +215,9 @@ int64_t dq_plan_variant_bytes_per_row_x1000(const dq_plan* plan, int32_t variant
  * its exact value (NaN canonical, -0.0 != 0.0 as Spark 2.2); strings / several columns group by a
  * 64-bit tuple hash whose equal-hash neighbours are compared exactly (a collision between distinct
  * tuples is DQ_E_UNSUPPORTED, never a silent merge).  dq_freq_merge is FrequenciesAndNumRows.sum
- * (outer join adding counts; for hashed keys across two tables the exact check is not repeated). */
+ * (outer join adding counts).  Hashed tables carry a second, independently seeded hash per group, so a
+ * merge of two tables whose distinct tuples share a first hash is DQ_E_UNSUPPORTED, not a silent
+ * merge; more than 2^31 - 1 groups in the two tables together is DQ_E_UNSUPPORTED. */
 typedef struct dq_freq_table dq_freq_table;
 typedef struct dq_freq_summary {
   int64_t num_groups;  /* rows of the frequencies table (CountDistinct) */
@@ -260,6 +265,10 @@ dq_status dq_mutual_information(const int32_t* types, const dq_column_view* cols
  *                   min/max ordering.  Used for the multi-GPU allgather merge. */
 dq_status dq_state_merge(const dq_state* a, const dq_state* b, dq_state* out);
 dq_status dq_state_combine(const dq_state* a, const dq_state* b, dq_state* out);
+/* Element-wise over n slot sets (a whole run's analyzers in one call: the fixed rank-order merge of the
+ * multi-GPU all-gather, the incremental StateLoader append).  out may alias a or b. */
+dq_status dq_state_merge_n(const dq_state* a, const dq_state* b, int32_t n, dq_state* out);
+dq_status dq_state_combine_n(const dq_state* a, const dq_state* b, int32_t n, dq_state* out);
 /* 1 if fromAggregationResult would produce Some(state). */
 int32_t dq_state_is_defined(const dq_state* s);
 /* metricValue() of a defined state (DoubleMetric analyzers; DATATYPE has a histogram, not a double:

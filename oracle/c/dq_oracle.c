@@ -338,3 +338,148 @@ void dqo_profile_scan(int ncols, const int* kinds, const void* const* values, co
   free(parts);
   free(pregs);
 }
+
+/*
+ * Spark-order partials in parallel (full-scale parity checks): partition p of [0, n) folds its rows
+ * sequentially (Spark's partial aggregate); the caller merges the partials in partition order from the
+ * zero buffer (the final aggregate), so the result is bitwise that of dqo_column_stats / dqo_corr with
+ * the same partition count -- only the partitions run on several threads.
+ */
+void dqo_column_stats_partials(int kind, const void* values, const uint8_t* validity, const uint8_t* mask,
+                               int64_t n, int nparts, int nthreads, dqo_col_stats* out /* [nparts] */) {
+  if (nparts < 1) nparts = 1;
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 1)
+#endif
+  for (int p = 0; p < nparts; ++p)
+    stats_partial(kind, values, validity, mask, part_bound(n, p, nparts), part_bound(n, p + 1, nparts), &out[p]);
+}
+
+/* acc <- acc (+) part  (CentralMomentAgg / sum / min / max merge of the final aggregate), and the cast
+   of integral sums / min / max to double at the end (dqo_stats_finish) */
+void dqo_stats_merge(int kind, dqo_col_stats* acc, const dqo_col_stats* part) { stats_merge(kind, acc, part); }
+void dqo_stats_finish(int kind, dqo_col_stats* s) { stats_finish(kind, s); }
+
+void dqo_corr_partials(int kx, const void* x, const uint8_t* vx, int ky, const void* y, const uint8_t* vy,
+                       const uint8_t* mask, int64_t n, int nparts, int nthreads, double* out /* [nparts][6] */) {
+  if (nparts < 1) nparts = 1;
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 1)
+#endif
+  for (int p = 0; p < nparts; ++p)
+    corr_partial(kx, x, vx, ky, y, vy, mask, part_bound(n, p, nparts), part_bound(n, p + 1, nparts), out + 6 * p);
+}
+
+/*
+ * Near-exact references (SURVEY §7 "hard parts": which side carries the fp64 error at 1e9 rows).
+ * Sums of (x - pivot) and (x - pivot)^2 -- and, for a pair, of the cross products -- accumulated in
+ * double-double arithmetic (error-free TwoSum / TwoProd with fma, ~106-bit significand), so the
+ * accumulated rounding error over 1e9 terms is ~1e-22 relative: far below the 1e-12 parity bar.  The
+ * caller combines the per-chunk (hi, lo) pairs exactly (Python Fraction) and forms
+ * mean = pivot + S1 / n, m2 = S2 - S1^2 / n, ck = Sxy - Sx Sy / n.
+ */
+typedef struct { double hi, lo; } dd_t;
+
+static inline dd_t dd_two_sum(double a, double b) {
+  double s = a + b, bb = s - a;
+  dd_t r = {s, (a - (s - bb)) + (b - bb)};
+  return r;
+}
+static inline dd_t dd_add_dd(dd_t a, dd_t b) {
+  dd_t s = dd_two_sum(a.hi, b.hi);
+  double lo = s.lo + a.lo + b.lo;
+  return dd_two_sum(s.hi, lo);
+}
+static inline __attribute__((unused)) dd_t dd_add_d(dd_t a, double b) {
+  dd_t s = dd_two_sum(a.hi, b);
+  return dd_two_sum(s.hi, s.lo + a.lo);
+}
+static inline dd_t dd_prod(double a, double b) { /* exact product a * b = hi + lo */
+  double p = a * b;
+  dd_t r = {p, fma(a, b, -p)};
+  return r;
+}
+static inline dd_t dd_mul(dd_t a, dd_t b) { /* (a.hi + a.lo)(b.hi + b.lo), dropping lo*lo */
+  dd_t p = dd_prod(a.hi, b.hi);
+  return dd_two_sum(p.hi, p.lo + (a.hi * b.lo + a.lo * b.hi));
+}
+static inline dd_t dd_diff(double x, double p) { return dd_two_sum(x, -p); } /* x - p exactly */
+
+/* out = {count, S1.hi, S1.lo, S2.hi, S2.lo}: selected rows (valid & mask), finite values only */
+void dqo_exact_moments(int kind, const void* values, const uint8_t* validity, const uint8_t* mask, int64_t n,
+                       double pivot, int nthreads, double* out) {
+  int nb = 1024;
+  double* acc = (double*)calloc((size_t)nb * 5, sizeof(double));
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 1)
+#endif
+  for (int b = 0; b < nb; ++b) {
+    int64_t lo = part_bound(n, b, nb), hi = part_bound(n, b + 1, nb);
+    dd_t s1 = {0, 0}, s2 = {0, 0};
+    double cnt = 0;
+    for (int64_t i = lo; i < hi; ++i) {
+      if (!bit(validity, i) || !bit(mask, i)) continue;
+      double x = as_double(kind, values, i);
+      if (!isfinite(x)) continue;
+      dd_t d = dd_diff(x, pivot);
+      s1 = dd_add_dd(s1, d);
+      s2 = dd_add_dd(s2, dd_mul(d, d));
+      cnt += 1.0;
+    }
+    double* a = acc + 5 * b;
+    a[0] = cnt; a[1] = s1.hi; a[2] = s1.lo; a[3] = s2.hi; a[4] = s2.lo;
+  }
+  dd_t s1 = {0, 0}, s2 = {0, 0};
+  double cnt = 0;
+  for (int b = 0; b < nb; ++b) {
+    double* a = acc + 5 * b;
+    cnt += a[0];
+    s1 = dd_add_dd(s1, (dd_t){a[1], a[2]});
+    s2 = dd_add_dd(s2, (dd_t){a[3], a[4]});
+  }
+  out[0] = cnt; out[1] = s1.hi; out[2] = s1.lo; out[3] = s2.hi; out[4] = s2.lo;
+  free(acc);
+}
+
+/* out = {count, Sx, Sy, Sxy, Sxx, Syy} as (hi, lo) pairs -> 11 doubles; rows valid in both columns */
+void dqo_exact_comoments(int kx, const void* x, const uint8_t* vx, int ky, const void* y, const uint8_t* vy,
+                         const uint8_t* mask, int64_t n, double px, double py, int nthreads, double* out) {
+  int nb = 1024;
+  double* acc = (double*)calloc((size_t)nb * 11, sizeof(double));
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 1)
+#endif
+  for (int b = 0; b < nb; ++b) {
+    int64_t lo = part_bound(n, b, nb), hi = part_bound(n, b + 1, nb);
+    dd_t sx = {0, 0}, sy = {0, 0}, sxy = {0, 0}, sxx = {0, 0}, syy = {0, 0};
+    double cnt = 0;
+    for (int64_t i = lo; i < hi; ++i) {
+      if (!bit(vx, i) || !bit(vy, i) || !bit(mask, i)) continue;
+      dd_t dx = dd_diff(as_double(kx, x, i), px), dy = dd_diff(as_double(ky, y, i), py);
+      sx = dd_add_dd(sx, dx);
+      sy = dd_add_dd(sy, dy);
+      sxy = dd_add_dd(sxy, dd_mul(dx, dy));
+      sxx = dd_add_dd(sxx, dd_mul(dx, dx));
+      syy = dd_add_dd(syy, dd_mul(dy, dy));
+      cnt += 1.0;
+    }
+    double* a = acc + 11 * b;
+    a[0] = cnt;
+    a[1] = sx.hi; a[2] = sx.lo; a[3] = sy.hi; a[4] = sy.lo; a[5] = sxy.hi; a[6] = sxy.lo;
+    a[7] = sxx.hi; a[8] = sxx.lo; a[9] = syy.hi; a[10] = syy.lo;
+  }
+  dd_t s[5] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}, {0, 0}};
+  double cnt = 0;
+  for (int b = 0; b < nb; ++b) {
+    double* a = acc + 11 * b;
+    cnt += a[0];
+    for (int k = 0; k < 5; ++k) s[k] = dd_add_dd(s[k], (dd_t){a[1 + 2 * k], a[2 + 2 * k]});
+  }
+  out[0] = cnt;
+  for (int k = 0; k < 5; ++k) { out[1 + 2 * k] = s[k].hi; out[2 + 2 * k] = s[k].lo; }
+  free(acc);
+}

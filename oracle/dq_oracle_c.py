@@ -48,6 +48,16 @@ def lib():
         L.dqo_count_bits.argtypes = [u8p, u8p, ctypes.c_int64]
         L.dqo_profile_scan.argtypes = [ctypes.c_int, vp, vp, vp, vp, ctypes.c_int64, ctypes.c_int,
                                        ctypes.c_int, ctypes.POINTER(ColStats), vp]
+        L.dqo_column_stats_partials.argtypes = [ctypes.c_int, vp, u8p, u8p, ctypes.c_int64, ctypes.c_int,
+                                                ctypes.c_int, ctypes.POINTER(ColStats)]
+        L.dqo_stats_merge.argtypes = [ctypes.c_int, ctypes.POINTER(ColStats), ctypes.POINTER(ColStats)]
+        L.dqo_stats_finish.argtypes = [ctypes.c_int, ctypes.POINTER(ColStats)]
+        L.dqo_corr_partials.argtypes = [ctypes.c_int, vp, u8p, ctypes.c_int, vp, u8p, u8p, ctypes.c_int64,
+                                        ctypes.c_int, ctypes.c_int, vp]
+        L.dqo_corr_merge.argtypes = [vp, vp]
+        L.dqo_exact_moments.argtypes = [ctypes.c_int, vp, u8p, u8p, ctypes.c_int64, ctypes.c_double, ctypes.c_int, vp]
+        L.dqo_exact_comoments.argtypes = [ctypes.c_int, vp, u8p, ctypes.c_int, vp, u8p, u8p, ctypes.c_int64,
+                                          ctypes.c_double, ctypes.c_double, ctypes.c_int, vp]
         _lib = L
     return _lib
 
@@ -87,3 +97,52 @@ def profile_scan(cols, n, nparts, nthreads):
     lib().dqo_profile_scan(nc, kinds.ctypes.data, ctypes.addressof(vals), ctypes.addressof(offs),
                            ctypes.addressof(vals_v), n, nparts, nthreads, stats, _p(regs))
     return list(stats), regs
+
+
+# ---- full-scale parity helpers (Spark partition order over many chunks; double-double references) ----
+def column_stats_partials(kind, values, validity, nparts, nthreads, mask=None):
+    """Spark partial aggregates of nparts row partitions of this array (one per partition, in order)."""
+    out = (ColStats * nparts)()
+    lib().dqo_column_stats_partials(KINDS[kind], _p(values), _p(validity), _p(mask), len(values), nparts, nthreads,
+                                    out)
+    return list(out)
+
+
+def stats_fold(kind, partials):
+    """The final aggregate: merge partition partials in order from the zero buffer, then cast."""
+    acc = ColStats()
+    for p in partials:
+        lib().dqo_stats_merge(KINDS[kind], ctypes.byref(acc), ctypes.byref(p))
+    lib().dqo_stats_finish(KINDS[kind], ctypes.byref(acc))
+    return acc
+
+
+def corr_partials(kx, x, vx, ky, y, vy, nparts, nthreads, mask=None):
+    out = np.zeros((nparts, 6), dtype=np.float64)
+    lib().dqo_corr_partials(KINDS[kx], _p(x), _p(vx), KINDS[ky], _p(y), _p(vy), _p(mask), len(x), nparts, nthreads,
+                            _p(out))
+    return [tuple(r) for r in out]
+
+
+def corr_fold(partials):
+    acc = np.zeros(6, dtype=np.float64)
+    for p in partials:
+        b = np.array(p, dtype=np.float64)
+        lib().dqo_corr_merge(_p(acc), _p(b))
+    return tuple(acc)
+
+
+def exact_moments(kind, values, validity, pivot, nthreads, mask=None):
+    """(count, S1, S2) of the finite selected values around `pivot`, each S as a double-double (hi, lo)."""
+    out = np.zeros(5, dtype=np.float64)
+    lib().dqo_exact_moments(KINDS[kind], _p(values), _p(validity), _p(mask), len(values), float(pivot), nthreads,
+                            _p(out))
+    return int(out[0]), (out[1], out[2]), (out[3], out[4])
+
+
+def exact_comoments(kx, x, vx, ky, y, vy, px, py, nthreads, mask=None):
+    """(count, Sx, Sy, Sxy, Sxx, Syy) around (px, py) over rows valid in both, as double-doubles."""
+    out = np.zeros(11, dtype=np.float64)
+    lib().dqo_exact_comoments(KINDS[kx], _p(x), _p(vx), KINDS[ky], _p(y), _p(vy), _p(mask), len(x), float(px),
+                              float(py), nthreads, _p(out))
+    return (int(out[0]),) + tuple((out[1 + 2 * k], out[2 + 2 * k]) for k in range(5))

@@ -169,3 +169,70 @@ def eval_state(text):
 
     nan = float("nan")  # noqa: F841 - used by eval of repr
     return eval(text, {k: getattr(S, k) for k in dir(S)} | {"nan": float("nan")})
+
+
+def _gpu_worker(rank, world, port, n_shard, q):
+    """One rank on the (single) GPU: scan its row shard of the C5 table with the profile analyzers, then
+    all-gather + merge the slot sets in rank order (gloo on this box; RCCL in bench.py)."""
+    import sys
+
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    from deequ_amd import distributed, synth
+    from deequ_amd.runner import scan_results
+    from deequ_amd.states import state_from_c
+
+    t = synth.c5_table(n_shard, row0=rank * n_shard, seed=13)
+    analyzers = synth.profile_analyzers(t) + _extra(__import__("deequ_amd"))
+    merged = distributed.allgather_combine(scan_results(t, analyzers))
+    q.put((rank, [repr(state_from_c(s)) for s in merged]))
+    dist.destroy_process_group()
+
+
+def _extra(dq):
+    return [dq.Correlation("c0", "c1"), dq.Compliance("p", "i0 >= 500"), dq.Sum("c2", "c3 > 3000")]
+
+
+@pytest.mark.gpu
+def test_two_rank_gpu_shards_equal_whole_table_scan():
+    """AnalysisRunner.scala:303's partial -> final contract across processes: two ranks each dq_scan a
+    different row shard on the GPU and merge through deequ_amd.distributed; the result equals ONE process
+    scanning both shards (as two chunks) -- counts / min / max / HLL bit-exact, fp64 within 1e-12."""
+    import torch.multiprocessing as mp
+
+    import deequ_amd as dq
+    from deequ_amd import synth
+    from deequ_amd.runner import scan_states
+    from tests.helpers import close
+
+    n_shard = 300_032
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gpu_worker, args=(r, 2, port, n_shard, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert res[0] == res[1]
+    parts = [synth.c5_table(n_shard, row0=r * n_shard, seed=13) for r in range(2)]
+    analyzers = synth.profile_analyzers(parts[0]) + _extra(dq)
+    whole = scan_states(parts, analyzers)
+    for a, got_txt in zip(analyzers, res[0]):
+        got, want = eval_state(got_txt), whole[a]
+        if want is None:
+            assert got is None, a
+            continue
+        gv, wv = got.metricValue(), want.metricValue()
+        if type(a).__name__ in ("Mean", "StandardDeviation", "Sum", "Correlation"):
+            assert close(gv, wv, 1e-12), (a, gv, wv)
+        else:
+            assert gv == wv or (math.isnan(gv) and math.isnan(wv)), (a, got, want)

@@ -461,7 +461,8 @@ def test_configs_vs_oracle(dq, cfg):
     from deequ_amd import synth
     from deequ_amd.runner import scan_states
 
-    n = 1_000_003
+    # c3: the fused Compliance states are checked against the (pure-Python) oracle evaluator over every row
+    n = 300_007 if cfg == "c3" else 1_000_003
     t = getattr(synth, f"{cfg}_table")(n, seed=5)
     if cfg == "c4":
         names = list(t.columns)
@@ -502,14 +503,10 @@ def _check_config_analyzer(dq, t, a, prod, host, n, nparts):
             regs = C.hll_registers(col.dtype, vals, None, bm, None, n)
         assert prod.words == tuple(O.registers_to_words(regs.tolist())), "HLL words differ"
     elif name == "Compliance":
+        # the state of the FUSED scan (HLL x 8 + 4 predicates in one plan) vs the oracle over all n rows
         cols = {k: O.OColumn(t.columns[k].dtype, host[k][0], host[k][1]) for k in ("i0", "i1", "i2", "i3")}
-        sub = 200_000  # python oracle evaluator on a prefix
-        ref = O.compute_state(("Compliance", a.instance, a.predicate, None),
-                              {k: O.OColumn(v.dtype, v.values[:sub], v.valid[:sub]) for k, v in cols.items()}, sub)
-        from deequ_amd.table import column_from_numpy
-        dev_sub = dq.Table([column_from_numpy(k, "i64", cols[k].values[:sub], cols[k].valid[:sub]) for k in cols])
-        got = dq.Compliance(a.instance, a.predicate).computeStateFrom(dev_sub)
-        assert got == dq.NumMatchesAndCount(ref.numMatches, ref.count), (got, ref)
+        ref = O.compute_state(("Compliance", a.instance, a.predicate, None), cols, n)
+        assert prod == dq.NumMatchesAndCount(ref.numMatches, ref.count), (prod, ref)
     elif name == "Correlation":
         x, vx, bx = host[a.firstColumn]
         y, vy, by = host[a.secondColumn]
@@ -818,6 +815,29 @@ def test_grouping_state_merge_and_incremental(dq):
     dq.AnalysisRunner.onData(a).addAnalyzer(u).saveStatesWith(prov).run()
     inc = dq.AnalysisRunner.onData(b).addAnalyzer(u).aggregateWith(prov).run().metric(u).value.get()
     assert inc == dq.AnalysisRunner.onData([a, b]).addAnalyzer(u).run().metric(u).value.get()
+
+
+def test_grouping_merge_refuses_hash_collisions(dq, monkeypatch):
+    """Two tables whose distinct string keys share the first tuple hash (forced by keeping none of its bits)
+    must not merge silently: the per-group second hash catches it (DQ_E_UNSUPPORTED); equal tuples still
+    merge; a merge of one table with itself adds counts."""
+    from deequ_amd import _lib as L
+    from deequ_amd.grouping import build_frequencies
+
+    monkeypatch.setenv("DQ_TEST_GROUP_HASH_MASK", "0")  # every tuple's first hash is 0
+    ta = dq.Table.from_pydict({"s": ("utf8", ["apple", "apple", None])})
+    tb = dq.Table.from_pydict({"s": ("utf8", ["pear", None, "pear", "pear"])})
+    tc = dq.Table.from_pydict({"s": ("utf8", ["apple"])})
+    fa, fb, fc = (build_frequencies(t, ["s"]) for t in (ta, tb, tc))
+    with pytest.raises(L.DQError) as e:
+        fa.sum(fb)
+    assert "collision" in str(e.value)
+    same = fa.sum(fc)  # one group "apple": 2 + 1
+    keys, counts = same.frequencies.export()
+    assert list(counts) == [3]
+    monkeypatch.delenv("DQ_TEST_GROUP_HASH_MASK")
+    ok = build_frequencies(ta, ["s"]).sum(build_frequencies(tb, ["s"]))
+    assert sorted(ok.frequencies.export()[1].tolist()) == [2, 3]
 
 
 def test_histogram_reference_cases(dq, kats):
