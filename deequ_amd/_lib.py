@@ -90,11 +90,11 @@ class _Ratio(ctypes.Structure):
 
 
 class _Sum(ctypes.Structure):
-    _fields_ = [("sum", ctypes.c_double)]
+    _fields_ = [("sum", ctypes.c_double), ("partial", ctypes.c_int64)]
 
 
 class _Mean(ctypes.Structure):
-    _fields_ = [("sum", ctypes.c_double), ("count", ctypes.c_int64)]
+    _fields_ = [("sum", ctypes.c_double), ("count", ctypes.c_int64), ("partial", ctypes.c_int64)]
 
 
 class _StdDev(ctypes.Structure):
@@ -130,8 +130,8 @@ class FreqSummary(ctypes.Structure):
 
 
 class State(ctypes.Structure):
-    _fields_ = [("op", ctypes.c_int32), ("has_value", ctypes.c_uint8 * 2), ("reserved", ctypes.c_uint8 * 2),
-                ("u", _StateUnion)]
+    _fields_ = [("op", ctypes.c_int32), ("has_value", ctypes.c_uint8 * 2), ("integral", ctypes.c_uint8),
+                ("reserved", ctypes.c_uint8), ("u", _StateUnion)]
 
 
 STATE_SIZE = ctypes.sizeof(State)

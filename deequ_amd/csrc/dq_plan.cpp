@@ -1167,10 +1167,14 @@ dq_status dq_finish(dq_plan* p, dq_state* out) {
         break;
       case DQ_OP_SUM:
         s.u.sum.sum = o.col_type == DQ_TYPE_F64 ? f64_sum(*c) : (double)c->isum;
+        s.integral = o.col_type != DQ_TYPE_F64;
+        s.u.sum.partial = s.integral ? c->isum : 0;
         set1(c->count > 0);
         break;
       case DQ_OP_MEAN:
         s.u.mean.sum = o.col_type == DQ_TYPE_F64 ? f64_sum(*c) : (double)c->isum;
+        s.integral = o.col_type != DQ_TYPE_F64;
+        s.u.mean.partial = s.integral ? c->isum : 0;
         s.u.mean.count = c->count;
         s.has_value[0] = c->count > 0;
         s.has_value[1] = 1;  // count(...) is never NULL

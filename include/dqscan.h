@@ -142,12 +142,15 @@ typedef struct dq_column_view {
 typedef struct dq_state {
   int32_t op;           /* enum dq_op */
   uint8_t has_value[2];
-  uint8_t reserved[2];
+  uint8_t integral;     /* SUM / MEAN of an integral column: `partial` holds Spark's int64 partial-aggregate
+                           sum (wraps like Spark's LongType sum); dq_state_combine adds the partials and
+                           casts, so row shards combine exactly as Spark's partial -> final merge */
+  uint8_t reserved;
   union {
     struct { int64_t num_matches; } size;                     /* NumMatches */
     struct { int64_t num_matches; int64_t count; } ratio;     /* NumMatchesAndCount (Completeness, Compliance, PatternMatch) */
-    struct { double sum; } sum;                               /* SumState */
-    struct { double sum; int64_t count; } mean;               /* MeanState */
+    struct { double sum; int64_t partial; } sum;              /* SumState (+ integral partial) */
+    struct { double sum; int64_t count; int64_t partial; } mean;  /* MeanState (+ integral partial) */
     struct { double n, avg, m2; } stddev;                     /* StandardDeviationState */
     struct { double value; } minmax;                          /* MinState / MaxState */
     struct { double n, x_avg, y_avg, ck, x_mk, y_mk; } corr;  /* CorrelationState */
