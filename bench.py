@@ -47,6 +47,8 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = this host's CPU share (see host_cpu_share)")
     p.add_argument("--configs", default="c1,c2,c3,c4", help="other BASELINE configs to measure at N=1 ('' = none)")
     p.add_argument("--config-steps", type=int, default=3)
+    p.add_argument("--config-rows", type=int, default=0, help="rows of C2-C4 (0 = BASELINE's 1e9; profiling runs)")
+    p.add_argument("--skip-headline", action="store_true", help="profiling runs: only the --configs")
     return p.parse_args()
 
 
@@ -103,6 +105,10 @@ def main():
     from deequ_amd import distributed, synth
     from deequ_amd.runner import ScanPlan
 
+    if args.skip_headline:
+        out = {"configs": {cfg: run_config(cfg, args) for cfg in args.configs.split(",") if cfg}}
+        print(json.dumps(out), flush=True)
+        return
     n_total = args.rows
     chunk = min(args.chunk, n_total)
     row0 = rank * n_total
@@ -276,7 +282,7 @@ def run_config(cfg, args) -> dict:
 
     from deequ_amd.runner import ScanPlan
 
-    n = 10_000_000 if cfg == "c1" else 1_000_000_000
+    n = 10_000_000 if cfg == "c1" else (args.config_rows or 1_000_000_000)
     tables, analyzers, desc = config_setup(cfg, n, DEFAULT_CHUNK)
     torch.cuda.synchronize()
     plan = ScanPlan(analyzers, tables[0].schema)

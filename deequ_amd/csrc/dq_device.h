@@ -73,6 +73,27 @@ struct PairGroup {
   int8_t pi[kTilePairs], pj[kTilePairs];  // local column index of x / y per pair
 };
 
+// Lane-per-row Correlation pass (dq_pair.hip): one wave task = up to kLaneCols columns of a pair group, the
+// active slots of the fixed pattern of all kLaneSlots pairs over those positions, and the column-moment
+// tasks (Mean / StandardDeviation / Sum / Min / Max of the same rows and `where`) of positions
+// 0 .. kLaneMoments-1, fused so each column is read from HBM once for its correlations AND its moments.
+constexpr int kLaneCols = 5;
+constexpr int kLaneSlots = 10;
+constexpr int kLaneMoments = 2;
+constexpr int kLaneSlotA[kLaneSlots] = {0, 0, 0, 0, 1, 1, 1, 2, 2, 3};
+constexpr int kLaneSlotB[kLaneSlots] = {1, 2, 3, 4, 2, 3, 4, 3, 4, 4};
+struct PairWaveTask {
+  int32_t ncols;                   // positions in use (0: an idle padding task)
+  int32_t where;                   // where-bitmap index or -1
+  uint32_t pair_mask;              // bit q: slot q (positions kLaneSlotA[q], kLaneSlotB[q]) is a pair task
+  uint32_t mom_mask;               // bit p: position p has a column-moments task
+  uint32_t swap_mask;              // bit q: the pair task's first column is position kLaneSlotB[q]
+  int32_t cols[kLaneCols];         // plan column indices
+  int32_t kinds[kLaneCols];        // CK_F64 / CK_I64 / CK_I32
+  int32_t pair_out[kLaneSlots];    // pair-task index of each active slot
+  int32_t mom_out[kLaneMoments];   // column-task index of each moments position
+};
+
 // Per-workgroup partial of one column task.  Moments are Chan-mergeable (n, mean, m2).
 struct alignas(16) ColPartial {
   double n, mean, m2;   // over selected rows, values converted to double

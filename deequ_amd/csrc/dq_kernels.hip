@@ -21,6 +21,7 @@
 
 #include "dq_device.h"
 #include "dq_hash.h"
+#include "dq_lane.h"
 
 namespace dq {
 
@@ -130,18 +131,6 @@ __device__ __forceinline__ HllKey hll_key_from_fmix(uint64_t b) {
 __device__ __forceinline__ HllKey hll_key_long(uint64_t v) { return hll_key_from_fmix(xxh64_long_head(v)); }
 __device__ __forceinline__ HllKey hll_key_int(uint32_t v) { return hll_key_from_fmix(xxh64_int_head(v)); }
 
-// Hardware v_min_f64 / v_max_f64 (IEEE mode: a NaN operand yields the other operand).  Inline asm
-// keeps the compiler from canonicalising both inputs first (two extra v_max_f64 per call).
-__device__ __forceinline__ double hw_min(double a, double b) {
-  double r;
-  asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
-__device__ __forceinline__ double hw_max(double a, double b) {
-  double r;
-  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
 
 // ------------------------------------------------------------------------------------------
 // Chan-mergeable column statistics
@@ -257,11 +246,6 @@ struct RangeBits {
 // loads into SGPRs and used directly as the lane mask of v_cndmask (inverse ballot) -- no VALU work
 // per row for validity, and counts come from s_bcnt1.
 // ------------------------------------------------------------------------------------------
-typedef const __attribute__((address_space(4))) uint32_t* const_u32s;
-
-__device__ __forceinline__ uint64_t load_word64(const uint32_t* p, int64_t w) {
-  return ((uint64_t)((const_u32s)p)[w + 1] << 32) | ((const_u32s)p)[w];
-}
 
 // selected-row masks of the 8 lane groups [base + 64 j, + 64) of a wave's block (base a multiple of
 // 64; `full`: the whole block lies below row1).  All branches are wave-uniform.
@@ -297,7 +281,6 @@ __device__ __forceinline__ void block_masks(const uint32_t* validity, const uint
   }
 }
 
-__device__ __forceinline__ bool lane_bit(uint64_t m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
 
 // Per-lane streaming moments of a numeric column (lane l of a wave owns rows base + 64 j + l).  Values
 // are accumulated as shifted sums sd = sum(x - shift), sdd = sum((x - shift)^2), k under the selection

@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <limits>
 #include <map>
 #include <string>
@@ -36,6 +37,10 @@ hipError_t launch_column_scan(int32_t variant, const ColTask* tasks, int32_t nta
 hipError_t launch_pair_tile_scan(const PairGroup* groups, int32_t ngroups, const ScanCols& cols,
                                  const ScanBitmaps& bm, int64_t n_rows, int64_t rows_per_range, int32_t nranges,
                                  CorrPartial* partials, hipStream_t st);
+hipError_t launch_pair_lane_scan(const PairWaveTask* tasks, int32_t ntasks, const ScanCols& cols,
+                                 const ScanBitmaps& bm, const uint32_t* ones, int64_t n_rows, int64_t rows_per_range,
+                                 int32_t nranges, CorrPartial* pair_part, ColPartial* col_part, bool all_f64,
+                                 hipStream_t st);
 hipError_t launch_finalize(int32_t ncol, int32_t nranges_col, const ColPartial* col_part, ColPartial* col_acc,
                            int32_t npair, int32_t nranges_pair, const CorrPartial* pair_part, CorrPartial* pair_acc,
                            int32_t has_pred, int32_t nranges_pred, const PredPartial* pred_part, PredPartial* pred_acc,
@@ -424,7 +429,10 @@ struct dq_plan {
   struct Group { int32_t variant, first, count; };
   std::vector<Group> groups;              // one column-scan launch per variant group
   std::vector<PairTask> pair_tasks;      // sorted by pair group
-  std::vector<PairGroup> pair_groups;     // <= 8 columns / <= 32 pairs / one where each
+  std::vector<PairGroup> pair_groups;     // <= 8 columns / <= 32 pairs / one where each (LDS-tile kernel)
+  std::vector<PairWaveTask> lane_tasks;   // pair groups planned for the lane-per-row kernel (dq_pair.hip)
+  int32_t n_fused = 0;                    // column tasks computed by the lane pair kernel (sorted last)
+  bool lane_all_f64 = true;               // every lane task column is fp64 (the conversion-free instantiation)
   int32_t concurrency = 1;                // HIP streams the variant launches are spread over
   std::vector<hipStream_t> side;          // concurrency - 1 extra streams
   std::vector<hipEvent_t> side_done;
@@ -440,6 +448,7 @@ struct dq_plan {
   ColTask* d_col_tasks = nullptr;
   PairTask* d_pair_tasks = nullptr;
   PairGroup* d_pair_groups = nullptr;
+  PairWaveTask* d_lane_tasks = nullptr;
   PredProgram* d_prog = nullptr;
   ColPartial* d_col_part = nullptr;
   CorrPartial* d_pair_part = nullptr;
@@ -450,6 +459,8 @@ struct dq_plan {
   PredPartial* d_pred_acc = nullptr;
   uint64_t* d_where_bits[kMaxWhere] = {nullptr};
   int64_t where_cap_words = 0;
+  uint32_t* d_ones = nullptr;  // all-ones bitmap (lane pair pass: columns without validity, tasks without where)
+  int64_t ones_cap_words = 0;
 
   int64_t total_rows = 0;
   int64_t next_chunk = 0;
@@ -515,12 +526,13 @@ static dq_status free_plan_mem(dq_plan* p) {
   p->pending.clear();
   for (hipEvent_t e : p->ev_pool) (void)hipEventDestroy(e);
   p->ev_pool.clear();
-  void* ptrs[] = {p->d_col_tasks, p->d_pair_tasks, p->d_pair_groups, p->d_prog, p->d_col_part, p->d_pair_part,
+  void* ptrs[] = {p->d_col_tasks, p->d_pair_tasks, p->d_pair_groups, p->d_lane_tasks, p->d_prog, p->d_col_part, p->d_pair_part,
                   p->d_pred_part, p->d_col_acc, p->d_hll_acc, p->d_pair_acc, p->d_pred_acc, p->d_regex};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   for (int i = 0; i < kMaxWhere; ++i)
     if (p->d_where_bits[i]) (void)hipFree(p->d_where_bits[i]);
+  if (p->d_ones) (void)hipFree(p->d_ones);
   return DQ_OK;
 }
 
@@ -539,6 +551,180 @@ static dq_status dmalloc(T** ptr, size_t bytes) {
   if (bytes == 0) bytes = 16;
   HIP_TRY(hipMalloc((void**)ptr, bytes));
   return DQ_OK;
+}
+
+// Plan one pair group for the lane-per-row kernel (dq_pair.hip): cover its pairs with the fewest column
+// subsets of kLaneCols local columns (one wave task each; every pair of 8 columns fits 4 subsets of 5), put
+// each fusable moments column -- a stats-only column task of the group's columns and `where` -- at position
+// 0 / 1 of a task holding it (extra moments-only tasks if the covers have no room), and hand every pair to
+// the least-loaded task covering it.  Returns false when the group cannot be planned this way.
+static bool plan_lane_tasks(const dq_plan* p, const PairGroup& g, std::vector<PairWaveTask>& out,
+                            std::vector<int>& fused) {
+  const int k = g.ncols;
+  if (k < 2 || k > kTileCols || g.npairs < 1) return false;
+  std::vector<int32_t> mom_task(k, -1);
+  for (int c = 0; c < k; ++c)
+    for (size_t t = 0; t < p->col_tasks.size(); ++t) {
+      const ColTask& ct = p->col_tasks[t];
+      if (ct.col == g.cols[c] && ct.where == g.where && !fused[t] &&
+          (ct.variant == CV_F64_S || ct.variant == CV_I64_S || ct.variant == CV_I32_S))
+        mom_task[c] = (int32_t)t;
+    }
+  auto pbit = [](int a, int b) { return a < b ? 1ull << (a * 8 + b) : 1ull << (b * 8 + a); };
+  uint64_t need = 0;
+  for (int q = 0; q < g.npairs; ++q) need |= pbit(g.pi[q], g.pj[q]);
+  const int sz = std::min(k, kLaneCols);
+  std::vector<uint32_t> subs;
+  std::vector<uint64_t> cov;
+  for (uint32_t m = 1; m < (1u << k); ++m) {
+    if (__builtin_popcount(m) != sz) continue;
+    uint64_t c = 0;
+    for (int a = 0; a < k; ++a)
+      for (int b = a + 1; b < k; ++b)
+        if (((m >> a) & 1u) && ((m >> b) & 1u)) c |= pbit(a, b);
+    if ((c & need) == 0) continue;
+    subs.push_back(m);
+    cov.push_back(c & need);
+  }
+  // moments matching: column -> one task holding it, at most kLaneMoments per task (augmenting paths)
+  auto match = [&](const std::vector<uint32_t>& tasks, std::vector<int>& col_of_slot) {
+    col_of_slot.assign(tasks.size() * kLaneMoments, -1);
+    int matched = 0;
+    for (int c = 0; c < k; ++c) {
+      if (mom_task[c] < 0) continue;
+      std::vector<char> seen(col_of_slot.size(), 0);
+      std::function<bool(int)> aug = [&](int col) {
+        for (size_t t = 0; t < tasks.size(); ++t) {
+          if (!((tasks[t] >> col) & 1u)) continue;
+          for (int sl = 0; sl < kLaneMoments; ++sl) {
+            const size_t i = t * kLaneMoments + sl;
+            if (seen[i]) continue;
+            seen[i] = 1;
+            if (col_of_slot[i] < 0 || aug(col_of_slot[i])) { col_of_slot[i] = col; return true; }
+          }
+        }
+        return false;
+      };
+      if (aug(c)) ++matched;
+    }
+    return matched;
+  };
+  const int n_mom = (int)std::count_if(mom_task.begin(), mom_task.end(), [](int32_t t) { return t >= 0; });
+  std::vector<uint32_t> best;
+  std::vector<int> best_slots;
+  int best_matched = -1;
+  const int ns = (int)subs.size();
+  for (int T = 1; T <= 4 && best.empty(); ++T) {
+    std::vector<int> idx(T);
+    for (int i = 0; i < T; ++i) idx[i] = i;
+    while (T <= ns) {
+      uint64_t c = 0;
+      for (int i : idx) c |= cov[i];
+      if ((c & need) == need) {
+        std::vector<uint32_t> tasks;
+        for (int i : idx) tasks.push_back(subs[i]);
+        std::vector<int> slots;
+        const int mt = match(tasks, slots);
+        if (mt > best_matched) { best = tasks; best_slots = slots; best_matched = mt; }
+        if (mt == n_mom) break;
+      }
+      int i = T - 1;  // next combination
+      while (i >= 0 && idx[i] == ns - T + i) --i;
+      if (i < 0) break;
+      ++idx[i];
+      for (int j = i + 1; j < T; ++j) idx[j] = idx[j - 1] + 1;
+    }
+  }
+  if (best.empty()) return false;
+  // position lists: matched moments columns first, then the rest of the subset
+  std::vector<std::vector<int>> pos(best.size());
+  std::vector<int> task_moms(best.size(), 0);
+  for (size_t t = 0; t < best.size(); ++t) {
+    for (int sl = 0; sl < kLaneMoments; ++sl)
+      if (best_slots[t * kLaneMoments + sl] >= 0) { pos[t].push_back(best_slots[t * kLaneMoments + sl]); task_moms[t]++; }
+    for (int c = 0; c < k; ++c)
+      if (((best[t] >> c) & 1u) && std::find(pos[t].begin(), pos[t].end(), c) == pos[t].end()) pos[t].push_back(c);
+  }
+  std::vector<char> mom_done(k, 0);
+  for (int v : best_slots)
+    if (v >= 0) mom_done[v] = 1;
+  for (int c = 0; c < k;) {  // unmatched moments columns: moments-only tasks
+    if (mom_task[c] < 0 || mom_done[c]) { ++c; continue; }
+    std::vector<int> ps{c};
+    mom_done[c] = 1;
+    for (int d = c + 1; d < k && (int)ps.size() < kLaneMoments; ++d)
+      if (mom_task[d] >= 0 && !mom_done[d]) { ps.push_back(d); mom_done[d] = 1; }
+    best.push_back(0);
+    pos.push_back(ps);
+    task_moms.push_back((int)ps.size());
+  }
+  std::vector<PairWaveTask> tasks(pos.size());
+  std::vector<int> load(pos.size(), 0);
+  for (size_t t = 0; t < pos.size(); ++t) {
+    PairWaveTask& w = tasks[t];
+    std::memset(&w, 0, sizeof(w));
+    w.ncols = (int32_t)pos[t].size();
+    w.where = g.where;
+    for (int i = 0; i < kLaneCols; ++i) {  // unused positions repeat position 0 (loaded, never used)
+      const int l = pos[t][i < w.ncols ? i : 0];
+      w.cols[i] = g.cols[l];
+      w.kinds[i] = g.kinds[l];
+    }
+    for (int i = 0; i < kLaneSlots; ++i) w.pair_out[i] = -1;
+    for (int i = 0; i < kLaneMoments; ++i) w.mom_out[i] = -1;
+    for (int i = 0; i < task_moms[t]; ++i) {
+      w.mom_mask |= 1u << i;
+      w.mom_out[i] = mom_task[pos[t][i]];
+    }
+    load[t] = 4 * task_moms[t] + w.ncols;
+  }
+  auto slot_of = [](int a, int b) {
+    for (int i = 0; i < kLaneSlots; ++i)
+      if (kLaneSlotA[i] == std::min(a, b) && kLaneSlotB[i] == std::max(a, b)) return i;
+    return -1;
+  };
+  for (int q = 0; q < g.npairs; ++q) {
+    int bt = -1, ba = -1, bb = -1;
+    for (size_t t = 0; t < pos.size(); ++t) {
+      auto ia = std::find(pos[t].begin(), pos[t].end(), (int)g.pi[q]);
+      auto ib = std::find(pos[t].begin(), pos[t].end(), (int)g.pj[q]);
+      if (ia == pos[t].end() || ib == pos[t].end()) continue;
+      const int sl = slot_of((int)(ia - pos[t].begin()), (int)(ib - pos[t].begin()));
+      if ((tasks[t].pair_mask >> sl) & 1u) continue;  // e.g. Correlation(a, b) and Correlation(b, a)
+      if (bt < 0 || load[t] < load[bt]) { bt = (int)t; ba = (int)(ia - pos[t].begin()); bb = (int)(ib - pos[t].begin()); }
+    }
+    if (bt < 0) {  // no covering task with the slot free: a two-column task of its own
+      PairWaveTask w;
+      std::memset(&w, 0, sizeof(w));
+      w.ncols = 2;
+      w.where = g.where;
+      for (int i = 0; i < kLaneCols; ++i) {
+        const int l = i == 1 ? g.pj[q] : g.pi[q];
+        w.cols[i] = g.cols[l];
+        w.kinds[i] = g.kinds[l];
+      }
+      for (int i = 0; i < kLaneSlots; ++i) w.pair_out[i] = -1;
+      for (int i = 0; i < kLaneMoments; ++i) w.mom_out[i] = -1;
+      tasks.push_back(w);
+      pos.push_back({(int)g.pi[q], (int)g.pj[q]});
+      load.push_back(2);
+      bt = (int)tasks.size() - 1;
+      ba = 0;
+      bb = 1;
+    }
+    const int slot = slot_of(ba, bb);
+    if (slot < 0) return false;
+    // the slot computes (position a, position b); a pair whose first column sits at b swaps x / y on output
+    if (ba > bb) tasks[bt].swap_mask |= 1u << slot;
+    tasks[bt].pair_mask |= 1u << slot;
+    tasks[bt].pair_out[slot] = g.first_pair + q;
+    load[bt] += 5;
+  }
+  for (size_t t = 0; t < pos.size(); ++t)
+    for (int i = 0; i < kLaneMoments; ++i)
+      if ((tasks[t].mom_mask >> i) & 1u) fused[tasks[t].mom_out[i]] = 1;
+  out = tasks;
+  return true;
 }
 
 static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred) {
@@ -735,28 +921,6 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
     }
   }
 
-  // sort column tasks by variant (stable), remap the analyzers' task indices, form launch groups
-  {
-    std::vector<int32_t> order(p->col_tasks.size());
-    for (size_t t = 0; t < order.size(); ++t) order[t] = (int32_t)t;
-    std::stable_sort(order.begin(), order.end(),
-                     [&](int32_t a, int32_t b) { return p->col_tasks[a].variant < p->col_tasks[b].variant; });
-    std::vector<int32_t> new_index(order.size());
-    std::vector<ColTask> sorted(order.size());
-    for (size_t k = 0; k < order.size(); ++k) {
-      sorted[k] = p->col_tasks[order[k]];
-      new_index[order[k]] = (int32_t)k;
-    }
-    p->col_tasks.swap(sorted);
-    for (SpecOut& o : p->outs)
-      if (o.col_task >= 0) o.col_task = new_index[o.col_task];
-    for (int32_t k = 0; k < (int32_t)p->col_tasks.size(); ++k) {
-      if (p->groups.empty() || p->groups.back().variant != p->col_tasks[k].variant)
-        p->groups.push_back({p->col_tasks[k].variant, k, 0});
-      p->groups.back().count++;
-    }
-  }
-
   // correlation pairs -> groups sharing one LDS row tile (greedy, per where bitmap)
   {
     std::vector<int32_t> order;
@@ -799,6 +963,57 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
     p->pair_groups.swap(groups);
     for (SpecOut& o : p->outs)
       if (o.pair_task >= 0) o.pair_task = new_index[o.pair_task];
+  }
+
+  // pair groups -> lane-per-row wave tasks (dq_pair.hip) with the groups' stats-only column tasks fused in;
+  // a group that cannot be planned that way keeps the LDS-tile pair kernel
+  std::vector<int> fused(p->col_tasks.size(), 0);
+  {
+    const bool tile_only = std::getenv("DQ_PAIR_TILE") != nullptr;  // diagnostic A/B override (tests)
+    std::vector<PairGroup> tile_groups;
+    for (const PairGroup& g : p->pair_groups) {
+      std::vector<PairWaveTask> w;
+      if (!tile_only && plan_lane_tasks(p, g, w, fused)) {
+        while (w.size() % kWaves) w.push_back(PairWaveTask{});  // idle padding: 4 tasks of one range per workgroup
+        p->lane_tasks.insert(p->lane_tasks.end(), w.begin(), w.end());
+      } else {
+        tile_groups.push_back(g);
+      }
+    }
+    p->pair_groups.swap(tile_groups);
+    for (const PairWaveTask& w : p->lane_tasks)
+      for (int c = 0; c < w.ncols; ++c) p->lane_all_f64 = p->lane_all_f64 && w.kinds[c] == CK_F64;
+    // idle padding tasks still need valid column indices for nothing: they return before any load
+  }
+
+  // sort column tasks by (fused into the pair pass, variant) (stable), remap the analyzers' and lane tasks'
+  // task indices, form one launch group per variant of the tasks the column pass still runs
+  {
+    std::vector<int32_t> order(p->col_tasks.size());
+    for (size_t t = 0; t < order.size(); ++t) order[t] = (int32_t)t;
+    std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
+      if (fused[a] != fused[b]) return fused[a] < fused[b];
+      return p->col_tasks[a].variant < p->col_tasks[b].variant;
+    });
+    std::vector<int32_t> new_index(order.size());
+    std::vector<ColTask> sorted(order.size());
+    for (size_t k = 0; k < order.size(); ++k) {
+      sorted[k] = p->col_tasks[order[k]];
+      new_index[order[k]] = (int32_t)k;
+    }
+    p->col_tasks.swap(sorted);
+    for (SpecOut& o : p->outs)
+      if (o.col_task >= 0) o.col_task = new_index[o.col_task];
+    for (PairWaveTask& w : p->lane_tasks)
+      for (int k = 0; k < kLaneMoments; ++k)
+        if ((w.mom_mask >> k) & 1u) w.mom_out[k] = new_index[w.mom_out[k]];
+    for (int32_t k = 0; k < (int32_t)p->col_tasks.size(); ++k) {
+      if (fused[order[k]]) break;  // fused tasks sort last: their partials come from the pair pass
+      if (p->groups.empty() || p->groups.back().variant != p->col_tasks[k].variant)
+        p->groups.push_back({p->col_tasks[k].variant, k, 0});
+      p->groups.back().count++;
+    }
+    p->n_fused = (int32_t)std::count(fused.begin(), fused.end(), 1);
   }
 
   // predicate program: roots in slot order, each followed by STORE
@@ -881,7 +1096,8 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
     p->pred_bytes_x1000 = bytes_of(pv, pn);
     p->pair_bytes_x1000 = bytes_of(qv, qn);
   }
-  p->launches_per_scan = (p->has_pred ? 1 : 0) + (int32_t)p->groups.size() + (p->pair_tasks.empty() ? 0 : 1) +
+  p->launches_per_scan = (p->has_pred ? 1 : 0) + (int32_t)p->groups.size() + (p->pair_groups.empty() ? 0 : 1) +
+                         (p->lane_tasks.empty() ? 0 : 1) +
                          ((p->col_tasks.size() + p->pair_tasks.size()) ? 1 : 0);
 
   // device allocations
@@ -889,6 +1105,10 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
   if (dq_status s = dmalloc(&p->d_col_tasks, nct * sizeof(ColTask))) return s;
   if (dq_status s = dmalloc(&p->d_pair_tasks, npt * sizeof(PairTask))) return s;
   if (dq_status s = dmalloc(&p->d_pair_groups, p->pair_groups.size() * sizeof(PairGroup))) return s;
+  if (dq_status s = dmalloc(&p->d_lane_tasks, p->lane_tasks.size() * sizeof(PairWaveTask))) return s;
+  if (!p->lane_tasks.empty())
+    HIP_TRY(hipMemcpyAsync(p->d_lane_tasks, p->lane_tasks.data(), p->lane_tasks.size() * sizeof(PairWaveTask),
+                           hipMemcpyHostToDevice, p->stream));
   if (dq_status s = dmalloc(&p->d_prog, sizeof(PredProgram))) return s;
   if (dq_status s = dmalloc(&p->d_col_part, nct * kMaxWG * sizeof(ColPartial))) return s;
   if (dq_status s = dmalloc(&p->d_pair_part, npt * kMaxWG * sizeof(CorrPartial))) return s;
@@ -917,7 +1137,9 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
   HIP_TRY(hipStreamSynchronize(p->stream));
   // concurrency: DQ_COLUMN_STREAMS (default 1) streams for the variant launches
   if (const char* e = std::getenv("DQ_COLUMN_STREAMS")) p->concurrency = std::max(1, std::min(8, std::atoi(e)));
-  p->concurrency = std::min<int32_t>(p->concurrency, std::max<int32_t>(1, (int32_t)p->groups.size() + (npt ? 1 : 0)));
+  p->concurrency = std::min<int32_t>(
+      p->concurrency, std::max<int32_t>(1, (int32_t)p->groups.size() + (p->pair_groups.empty() ? 0 : 1) +
+                                               (p->lane_tasks.empty() ? 0 : 1)));
   HIP_TRY(hipEventCreateWithFlags(&p->fork_ev, hipEventDisableTiming));
   for (int32_t k = 1; k < p->concurrency; ++k) {
     hipStream_t st;
@@ -1037,6 +1259,15 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
   }
   ScanBitmaps bm{};
   for (int b = 0; b < kMaxWhere; ++b) bm.where_bits[b] = p->d_where_bits[b];
+  // all-ones bitmap standing in for a missing validity / where bitmap in the lane pair pass
+  if (!p->lane_tasks.empty() && words + 1 > p->ones_cap_words) {
+    HIP_TRY(hipStreamSynchronize(p->stream));
+    if (p->d_ones) (void)hipFree(p->d_ones);
+    p->d_ones = nullptr;
+    if (dq_status s = dmalloc(&p->d_ones, (size_t)(words + 1) * 8)) return s;
+    HIP_TRY(hipMemsetAsync(p->d_ones, 0xFF, (size_t)(words + 1) * 8, p->stream));
+    p->ones_cap_words = words + 1;
+  }
 
   // row ranges: column / pair passes in multiples of 2048 rows, predicate pass in multiples of 256
   // each variant (and the pair pass) is its own launch of (tasks x ranges) workgroups: size the ranges
@@ -1045,6 +1276,10 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
   for (const auto& g : p->groups) min_launch = min_launch ? std::min<int64_t>(min_launch, g.count) : g.count;
   if (!p->pair_groups.empty())
     min_launch = min_launch ? std::min<int64_t>(min_launch, (int64_t)p->pair_groups.size()) : (int64_t)p->pair_groups.size();
+  if (!p->lane_tasks.empty()) {  // workgroups of the lane pair launch per row range
+    const int64_t wg = (int64_t)p->lane_tasks.size() / kWaves;
+    min_launch = min_launch ? std::min<int64_t>(min_launch, wg) : wg;
+  }
   static const int64_t target = [] {
     const char* e = std::getenv("DQ_TARGET_WGS");  // tuning override (diagnostic)
     return e ? std::max<int64_t>(256, std::atoll(e)) : (int64_t)kTargetWGs;
@@ -1082,7 +1317,15 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
         }))
       return s;
   }
-  if (!p->pair_tasks.empty()) {
+  if (!p->lane_tasks.empty()) {
+    hipStream_t st = stream_for(li++);
+    if (dq_status s = timed(p, 2, st, [&] {
+          return launch_pair_lane_scan(p->d_lane_tasks, (int32_t)p->lane_tasks.size(), sc, bm, p->d_ones, n_rows, rpr_col,
+                                       nr_col, p->d_pair_part, p->d_col_part, p->lane_all_f64, st);
+        }))
+      return s;
+  }
+  if (!p->pair_groups.empty()) {
     hipStream_t st = stream_for(li++);
     if (dq_status s = timed(p, 2, st, [&] {
           return launch_pair_tile_scan(p->d_pair_groups, (int32_t)p->pair_groups.size(), sc, bm, n_rows, rpr_col,
@@ -1289,7 +1532,9 @@ dq_status dq_plan_kernel_time(dq_plan* p, int32_t kernel, double* total_ms, int6
 int64_t dq_plan_variant_bytes_per_row_x1000(const dq_plan* p, int32_t variant) {
   if (!p) return 0;
   int64_t b = 0;
-  for (const ColTask& t : p->col_tasks) {
+  const size_t n_run = p->col_tasks.size() - (size_t)p->n_fused;  // fused tasks run in the pair pass
+  for (size_t i = 0; i < n_run; ++i) {
+    const ColTask& t = p->col_tasks[i];
     if (t.variant != variant) continue;
     const dq_column_desc& cd = p->schema[t.col];
     if (t.variant != CV_VALIDITY) b += (cd.type == DQ_TYPE_I32 || cd.type == DQ_TYPE_UTF8) ? 4000 : 8000;

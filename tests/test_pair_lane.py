@@ -1,0 +1,162 @@
+"""The lane-per-row Correlation pass fused with the column moments (deequ_amd/csrc/dq_pair.hip).
+
+Correlation co-moments (Correlation.scala:37-52) and the Mean / StandardDeviation / Sum / Minimum /
+Maximum states of the same columns are computed in ONE read of each column.  Checked against the C
+oracle (Spark partition order) and against the LDS-tile kernel (DQ_PAIR_TILE=1) on: nulls, `where`
+filters, f64 / i64 / i32 columns, NaN / +-inf values, pairs in both orientations, ragged sizes around
+the 64 / 128-row blocks, and a complete 8-column pair set (C4's 28 correlations) plus pairs on columns
+without moments.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import pytest
+
+from oracle import dq_oracle as O
+from oracle import dq_oracle_c as C
+from tests.helpers import close
+
+pytestmark = pytest.mark.gpu
+REL = 1e-12
+
+
+@pytest.fixture(scope="module")
+def dq():
+    import torch
+
+    assert torch.cuda.is_available()
+    import deequ_amd
+
+    return deequ_amd
+
+
+def _data(n, seed, special=False):
+    rng = np.random.default_rng(seed)
+    cols = {}
+    z0 = rng.normal(size=n)
+    for c in range(6):
+        x = 0.4 * z0 + rng.normal(size=n) + 100.0 * c
+        cols[f"f{c}"] = ("f64", x, rng.random(n) > 0.1 * (c % 3))
+    cols["l"] = ("i64", rng.integers(-(1 << 40), 1 << 40, n), rng.random(n) > 0.2)
+    cols["i"] = ("i32", rng.integers(-50000, 50000, n).astype(np.int32), np.ones(n, bool))
+    cols["w"] = ("i64", rng.integers(-3, 10, n), rng.random(n) > 0.05)
+    if special and n > 10:
+        f = cols["f1"][1]
+        f[rng.integers(0, n, 3)] = np.nan
+        f[rng.integers(0, n, 2)] = np.inf
+        f[rng.integers(0, n, 1)] = -np.inf
+    return cols
+
+
+def _table(dq, cols):
+    from deequ_amd.table import column_from_numpy
+
+    return dq.Table([column_from_numpy(k, t, v, m, nullable=not m.all() or k != "i") for k, (t, v, m) in cols.items()])
+
+
+def _bm(valid):
+    return np.packbits(valid, bitorder="little")
+
+
+def _analyzers(dq, where):
+    names = [f"f{c}" for c in range(6)] + ["l", "i"]
+    out = [dq.Correlation(names[i], names[j], where) for i in range(8) for j in range(i + 1, 8)]
+    out += [dq.Correlation("f3", "f0", where), dq.Correlation("i", "f5", where)]  # reversed orientations
+    for c in names:
+        out += [dq.Mean(c, where), dq.StandardDeviation(c, where), dq.Minimum(c, where), dq.Maximum(c, where),
+                dq.Sum(c, where)]
+    return out
+
+
+def _check(dq, cols, states, analyzers, n, where_mask):
+    mask = None if where_mask is None else _bm(where_mask)
+    for a in analyzers:
+        got = states[a]
+        name = type(a).__name__
+        if name == "Correlation":
+            (kx, x, vx), (ky, y, vy) = cols[a.firstColumn], cols[a.secondColumn]
+            r = C.corr(kx, x, _bm(vx), ky, y, _bm(vy), mask, 4)
+            if r[0] == 0:
+                assert got is None or got.n == 0, (a, got)
+                continue
+            ref = O.CorrelationState(*r)
+            assert got.n == ref.n, (a, got, ref)
+            g, w = got.metricValue(), ref.metricValue()
+            assert close(g, w, 0.0, 1e-12) or (math.isnan(g) and math.isnan(w)), (a, g, w)
+            if math.isnan(w):  # a NaN / inf in the pair: the other state fields depend on Spark's row order
+                continue
+            for k in ("xAvg", "yAvg"):
+                scale = abs(getattr(ref, k)) + math.sqrt(abs(ref.xMk) / ref.n + abs(ref.yMk) / ref.n)
+                assert close(getattr(got, k), getattr(ref, k), REL, REL * scale), (a, k, got, ref)
+            continue
+        kind, v, valid = cols[a.column]
+        s = C.column_stats(kind, v, _bm(valid), mask, 4)
+        if s.count == 0:
+            assert got is None, (a, got)
+            continue
+        fin = valid & (np.ones(len(v), bool) if where_mask is None else where_mask)
+        scale = float(np.abs(v.astype(np.float64)[fin & np.isfinite(v.astype(np.float64))]).sum())
+        if name == "Mean":
+            assert got.count == s.count and close(got.sum_, s.sum_f64, REL, REL * scale), (a, got, s.sum_f64)
+        elif name == "Sum":
+            assert close(got.sum_, s.sum_f64, REL, REL * scale), (a, got, s.sum_f64)
+        elif name == "StandardDeviation":
+            assert got.n == s.n, (a, got.n, s.n)
+            g, w = got.metricValue(), math.sqrt(s.m2 / s.n) if s.m2 == s.m2 else float("nan")
+            assert close(g, w, REL) or (math.isnan(g) and math.isnan(w)), (a, g, w)
+        elif name == "Minimum":
+            assert got.metricValue() == s.min or (math.isnan(got.metricValue()) and math.isnan(s.min)), (a, got, s.min)
+        elif name == "Maximum":
+            assert got.metricValue() == s.max or (math.isnan(got.metricValue()) and math.isnan(s.max)), (a, got, s.max)
+
+
+@pytest.mark.parametrize("n", [0, 1, 63, 64, 65, 127, 128, 129, 2047, 2049, 100_003])
+@pytest.mark.parametrize("where", [None, "w > 2"])
+def test_lane_pair_pass_vs_oracle(dq, n, where):
+    from deequ_amd.runner import scan_states
+
+    cols = _data(n, n * 3 + (where is not None), special=(n % 2 == 1))
+    t = _table(dq, cols)
+    an = _analyzers(dq, where)
+    states = scan_states(t, an)
+    wm = None
+    if where is not None:
+        wv, wvalid = cols["w"][1], cols["w"][2]
+        wm = wvalid & (wv > 2)
+    _check(dq, cols, states, an, n, wm)
+
+
+def test_lane_pass_equals_tile_pass_and_fuses_moments(dq, monkeypatch):
+    """The planner routes every pair group to the lane kernel (the column pass then runs no stats task of
+    those columns); results agree with the LDS-tile kernel within the fp64 tolerance."""
+    from deequ_amd.runner import ScanPlan, scan_states
+
+    n = 300_001
+    cols = _data(n, 7)
+    t = _table(dq, cols)
+    an = _analyzers(dq, None)
+    plan = ScanPlan(an, t.schema)
+    launches = plan.num_launches()
+    plan.close()
+    assert launches == 2, launches  # the lane pair pass + finalize: moments fused, no column pass
+    lane = scan_states(t, an)
+    monkeypatch.setenv("DQ_PAIR_TILE", "1")
+    tile = scan_states(t, an)
+    for a in an:
+        g, w = lane[a].metricValue(), tile[a].metricValue()
+        tol = (0.0, 1e-12) if type(a).__name__ == "Correlation" else (1e-12, 0.0)  # correlation: absolute
+        assert close(g, w, *tol) or (math.isnan(g) and math.isnan(w)), (a, g, w)
+
+
+def test_c4_complete_pair_set_deterministic(dq):
+    from deequ_amd import synth
+    from deequ_amd.runner import scan_results
+
+    t = synth.c4_table(1_000_003, seed=21)
+    names = list(t.columns)
+    an = [dq.Correlation(names[i], names[j]) for i in range(8) for j in range(i + 1, 8)]
+    an += [dq.Mean(c) for c in names] + [dq.StandardDeviation(c) for c in names]
+    runs = [[bytes(s) for s in scan_results(t, an)] for _ in range(2)]
+    assert runs[0] == runs[1]
