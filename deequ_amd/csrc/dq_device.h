@@ -71,6 +71,7 @@ struct PairGroup {
   int32_t cols[kTileCols];          // plan column indices
   int32_t kinds[kTileCols];         // CK_F64 / CK_I64 / CK_I32
   int8_t pi[kTilePairs], pj[kTilePairs];  // local column index of x / y per pair
+  int32_t mom_task[kTileCols];      // MFMA pass: column-moments task fused for local column c, or -1
 };
 
 // Lane-per-row Correlation pass (dq_pair.hip): one wave task = up to kLaneCols columns of a pair group, the

@@ -426,4 +426,352 @@ hipError_t launch_pair_lane_scan(const PairWaveTask* tasks, int32_t ntasks, cons
   return hipGetLastError();
 }
 
+
+
+// ================================================================================================
+// Gram-matrix form on the matrix cores (v_mfma_f64_16x16x4_f64).
+//
+// For the <= 8 columns of a pair group and a row k, let z_c = d_c (= x_c - shift_c) if the row is selected
+// in column c (valid, `where`, finite) and 0 otherwise, f_c = 1 if selected (incl. non-finite) else 0,
+// q_c = z_c^2.  With A = [z_0..z_7 | q_0..q_7] and B = [f_0..f_7 | z_0..z_7] (16 features per row),
+// C = sum_k A_k^T B_k is a 16 x 16 tile holding, for EVERY pair (a, b):
+//   Sx = C[a][b] = sum z_a f_b   Sy = C[b][a]   Sxy = C[a][8 + b]   Sxx = C[8 + a][b]   Syy = C[8 + b][a]
+// -- the co-moment sums over the rows selected in both columns (products with 0 / 1 are exact) -- and,
+// on its diagonal, each column's own moments: S = C[c][c], Q = C[8 + c][c].  One MFMA folds 4 rows of all
+// 28 pairs and 8 columns.  Lane l supplies feature (l & 15) of row (l >> 4) of each 4-row step: it loads
+// its own element straight from HBM (column l & 7), so no LDS staging; pair counts are SGPR popcounts of
+// the selection masks.  The 4 waves of a workgroup fold interleaved 64-row groups of its row range with
+// the same shifts, then add their tiles in wave order (LDS) into one partial per range.
+// ================================================================================================
+typedef double dq_d4 __attribute__((ext_vector_type(4)));
+
+// F64: every column of every group is fp64; MINMAX: a fused moments task feeds Minimum / Maximum
+template <bool F64, bool MINMAX>
+__global__ __launch_bounds__(kBlock) void dq_pair_mfma_scan(const PairGroup* __restrict__ groups, int32_t ngroups,
+                                                            ScanCols cols, ScanBitmaps bm, const uint32_t* ones,
+                                                            int64_t n_rows, int64_t rows_per_range, int32_t nranges,
+                                                            CorrPartial* __restrict__ pair_part,
+                                                            ColPartial* __restrict__ col_part) {
+  __shared__ double shift_s[kTileCols];
+  __shared__ double tile[kWaves][16][17];  // the waves' C tiles (+1: bank spread)
+  __shared__ uint32_t cnt_s[kWaves][kTileCols][kTileCols];
+  __shared__ int64_t nan_s[kWaves][kTileCols], pinf_s[kWaves][kTileCols], ninf_s[kWaves][kTileCols];
+  __shared__ int64_t isum_s[kWaves][kTileCols];
+  __shared__ double lo_s[kWaves][kTileCols], hi_s[kWaves][kTileCols];
+  __shared__ uint64_t poison_s[kWaves];
+  const int gi = blockIdx.x % ngroups, range = blockIdx.x / ngroups;
+  const PairGroup& g = groups[gi];
+  const int nc = g.ncols;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t row0 = (int64_t)range * rows_per_range;
+  const int64_t row1 = row0 + rows_per_range < n_rows ? row0 + rows_per_range : n_rows;
+  const uint32_t* where = g.where >= 0 ? reinterpret_cast<const uint32_t*>(bm.where_bits[g.where]) : ones;
+
+  // ---- shifts (workgroup-uniform): wave 0 computes the mean of each column's first finite selected group
+  if (wave == 0) {
+    for (int c = 0; c < nc; ++c) {
+      const int col = g.cols[c];
+      const uint32_t* vb = cols.validity[col] ? cols.validity[col] : ones;
+      double s = 0.0;
+      for (int64_t gr = row0; gr < row1; gr += 64) {
+        const int64_t r = gr + lane < row1 ? gr + lane : row1 - 1;
+        const int k = F64 ? CK_F64 : g.kinds[c];
+        const double x = load_row<F64>(reinterpret_cast<const char*>(cols.values[col]), k, r).x;
+        const uint64_t fm = __builtin_amdgcn_ballot_w64(__builtin_isfinite(x)) & bits64_tail(vb, gr, row1) &
+                            bits64_tail(where, gr, row1);
+        if (fm != 0) {
+          s = wave_sum(lane_bit(fm) ? x : 0.0) / (double)__builtin_popcountll(fm);
+          break;
+        }
+      }
+      if (lane == 0) shift_s[c] = s;
+    }
+  }
+  __syncthreads();
+
+  // ---- this lane's feature: column c = lane & 7 (lanes of columns >= ncols stay zero), A/B half hi,
+  // row slot rs.  Step j (0..15) of the 64-row group at `base` folds row base + 8 (j >> 1) + 2 rs + (j & 1):
+  // a lane's two rows of steps 2 t, 2 t + 1 are adjacent, so one 16-byte load brings both (fp64).
+  const int feat = lane & 15, c = feat & 7, rs = lane >> 4;
+  const bool hi = (feat >> 3) != 0;
+  const bool live = c < nc;
+  const int colc = live ? g.cols[c] : g.cols[0];
+  const int kind = F64 ? CK_F64 : g.kinds[live ? c : 0];
+  const char* colp = reinterpret_cast<const char*>(cols.values[colc]);
+  const double sh = live ? shift_s[c] : 0.0;
+  // 16-byte loads need 16-byte aligned columns (a table sliced at an odd row is not): wave-uniform choice
+  const bool vec16 = F64 && __builtin_amdgcn_ballot_w64((reinterpret_cast<uintptr_t>(colp) & 15u) != 0) == 0;
+  // selection words come through the vector path: lane l reads the validity word of column a = l & 7 (its
+  // own feature column) and of column b = (l >> 3) & 7, so lane l also owns the count and the poison flag
+  // of the ordered column pair (a, b) -- no SGPR arrays, no scalar loads of streamed bitmaps
+  const int pb = (lane >> 3) & 7;
+  const bool live_b = pb < nc;
+  const uint32_t* va;
+  const uint32_t* vb;
+  {
+    const int ca = g.cols[live ? c : 0], cb = g.cols[live_b ? pb : 0];
+    va = cols.validity[ca] ? cols.validity[ca] : ones;
+    vb = cols.validity[cb] ? cols.validity[cb] : ones;
+  }
+  // the `where` words come through the vector path too (a VGPR copy of the uniform pointer; global
+  // address space, so the loads stay out of the scalar / LDS counters and the prefetch is not waited for)
+  typedef const __attribute__((address_space(1))) uint32_t* gu32;
+  gu32 where_v = (gu32)where;
+  asm volatile("" : "+v"(where_v));
+
+  dq_d4 acc = {0.0, 0.0, 0.0, 0.0};
+  uint32_t cnt = 0;           // rows selected in both a and b (lane (a, b)); a == b: the column count
+  bool poison = false;        // pair (a, b) met a selected NaN / +-inf of column a in a row selected in b
+  int64_t nanv = 0, pinfv = 0, ninfv = 0, isum = 0;  // column c's rows of slot rs (lanes with hi == 0)
+  double lo = __builtin_bit_cast(double, 0x7FF0000000000000ull), hiv = __builtin_bit_cast(double, 0xFFF0000000000000ull);
+  const double qnan = __builtin_bit_cast(double, 0x7FF8000000000000ull);
+
+  struct Grp {
+    double x[16];
+    int64_t raw[F64 ? 1 : 16];
+    uint32_t wa[2], wb[2], wm[2];
+  };
+  // one 64-row group's values and selection words; TAIL: rows at or past row1 are clamped (masked later)
+  // VEC: the 16-byte loads of a full group of aligned fp64 columns; TAIL: rows at or past row1 are clamped
+  auto load = [&](int64_t base, Grp& gr, auto vec_tag, auto tail_tag) __attribute__((always_inline)) {
+    constexpr bool VEC = decltype(vec_tag)::value, TAIL = decltype(tail_tag)::value;
+    const int64_t w = base >> 5;
+    const bool two = !TAIL || base + 32 < row1;  // the second dword holds a row below row1
+    gr.wa[0] = va[w];
+    gr.wb[0] = vb[w];
+    gr.wm[0] = where_v[w];
+    gr.wa[1] = two ? va[w + 1] : 0u;
+    gr.wb[1] = two ? vb[w + 1] : 0u;
+    gr.wm[1] = two ? where_v[w + 1] : 0u;
+    if (VEC && !TAIL) {
+      typedef double d2 __attribute__((ext_vector_type(2)));
+      const d2* p = reinterpret_cast<const d2*>(colp) + ((base >> 1) + rs);
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const d2 v = p[4 * t];
+        gr.x[2 * t] = v.x;
+        gr.x[2 * t + 1] = v.y;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        int64_t r = base + 8 * (j >> 1) + 2 * rs + (j & 1);
+        if (TAIL) r = r < row1 ? r : row1 - 1;
+        const PosLoad pl = load_row<F64>(colp, kind, r);
+        gr.x[j] = pl.x;
+        if (!F64) gr.raw[j] = pl.raw;
+      }
+    }
+  };
+  // Fold one group.  Fast path: z = x - shift on a selected row (no finiteness tests).  A selected NaN / +-inf
+  // reaches at least the tile's diagonal term z_a f_a of its column, so a tile that is finite after the
+  // group proves there was none; otherwise (rare) the group is folded again from the saved tile with the
+  // non-finite values kept out, counted, and their pairs poisoned.  Min / max / integral sums are taken
+  // once, in the fast path (min / max see the same values either way; NaN is skipped by v_min / v_max).
+  auto fold = [&](int64_t base, const Grp& gr, auto tail_tag) __attribute__((always_inline)) {
+    constexpr bool TAIL = decltype(tail_tag)::value;
+    uint64_t wm = ((uint64_t)gr.wm[1] << 32) | gr.wm[0];
+    if (TAIL && base + 64 > row1) wm &= (1ull << (row1 - base)) - 1ull;
+    const uint64_t wa = live ? (((uint64_t)gr.wa[1] << 32) | gr.wa[0]) & wm : 0ull;
+    const uint64_t wb = live_b ? (((uint64_t)gr.wb[1] << 32) | gr.wb[0]) & wm : 0ull;
+    cnt += (uint32_t)__builtin_popcountll(wa & wb);
+    const uint64_t wr = wa >> (2 * rs);  // step j's bit: 8 (j >> 1) + (j & 1)
+    const uint32_t wlo = (uint32_t)wr, whi = (uint32_t)(wr >> 32);
+    const dq_d4 acc0 = acc;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int bit = 8 * (j >> 1) + (j & 1);
+      const bool sel = ((bit < 32 ? wlo : whi) >> (bit & 31)) & 1u;
+      const double x = gr.x[j];
+      const double z = sel ? x - sh : 0.0;
+      const double av = hi ? z * z : z;
+      const double bv = hi ? z : (sel ? 1.0 : 0.0);
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+      if (!F64 && kind != CK_F64) isum = (int64_t)((uint64_t)isum + (uint64_t)(sel ? gr.raw[j] : 0));
+      if (MINMAX) {
+        const double xm = sel ? x : qnan;  // v_min / v_max (IEEE mode) skip a NaN operand: unselected, NaN rows
+        lo = hw_min(lo, xm);
+        hiv = hw_max(hiv, xm);
+      }
+    }
+    const bool tile_fin = __builtin_isfinite(acc[0]) && __builtin_isfinite(acc[1]) && __builtin_isfinite(acc[2]) &&
+                          __builtin_isfinite(acc[3]);
+    if (__builtin_amdgcn_ballot_w64(!tile_fin) != 0) {  // rare (unrolled: no indexed register arrays)
+      acc = acc0;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int bit = 8 * (j >> 1) + (j & 1);
+        const bool sel = ((bit < 32 ? wlo : whi) >> (bit & 31)) & 1u;
+        const double x = gr.x[j];
+        const bool fin = __builtin_isfinite(x);
+        const double z = sel && fin ? x - sh : 0.0;
+        const double av = hi ? z * z : z;
+        const double bv = hi ? z : (sel ? 1.0 : 0.0);
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+        const bool nf = sel && !fin;
+        const uint64_t m = __builtin_amdgcn_ballot_w64(nf && !hi);  // lane a + 16 rs: column a, row slot rs
+        if (m == 0) continue;
+        const bool own = nf && !hi, isn = x != x;  // branch-free: keeps the counters in registers
+        nanv += own && isn;
+        pinfv += own && !isn && x > 0.0;
+        ninfv += own && !isn && x < 0.0;
+        const uint64_t t = m >> (lane & 7);  // column a's non-finite rows of slots 0..3
+        const uint32_t ma = (uint32_t)((t & 1ull) | ((t >> 15) & 2ull) | ((t >> 30) & 4ull) | ((t >> 45) & 8ull));
+        const uint64_t bs = wb >> bit;  // column b's selection of the same rows (slot k: bit 2 k)
+        const uint32_t mb = (uint32_t)((bs & 1ull) | ((bs >> 1) & 2ull) | ((bs >> 2) & 4ull) | ((bs >> 3) & 8ull));
+        if (ma & mb) poison = true;
+      }
+    }
+  };
+
+  // full groups, software-pipelined over two buffers: the next group's loads fly while this one folds.  The
+  // prefetch is unconditional (the last one re-reads the current group) so every path into a fold has the
+  // same loads in flight and the wait before it stays a partial vmcnt, not a drain.
+  const int64_t full_end = row0 + ((row1 - row0) >> 6 << 6);
+  constexpr int64_t kStride = 64 * kWaves;
+  int64_t base = row0 + 64 * (int64_t)wave;
+  auto run_full = [&](auto vec_tag) __attribute__((always_inline)) {
+    Grp b0, b1;
+    if (base >= full_end) return;
+    load(base, b0, vec_tag, std::false_type{});
+    while (true) {
+      load(base + kStride < full_end ? base + kStride : base, b1, vec_tag, std::false_type{});
+      fold(base, b0, std::false_type{});
+      base += kStride;
+      if (base >= full_end) break;
+      load(base + kStride < full_end ? base + kStride : base, b0, vec_tag, std::false_type{});
+      fold(base, b1, std::false_type{});
+      base += kStride;
+      if (base >= full_end) break;
+    }
+  };
+  if (vec16) run_full(std::true_type{});
+  else run_full(std::false_type{});
+  if (base < row1) {
+    Grp bt;
+    load(base, bt, std::false_type{}, std::true_type{});
+    fold(base, bt, std::true_type{});
+  }
+
+  // ---- workgroup merge (fixed order: waves 0..3) and the per-range partials
+#pragma unroll
+  for (int r = 0; r < 4; ++r) tile[wave][(lane >> 4) + 4 * r][lane & 15] = acc[r];
+  cnt_s[wave][lane >> 3][lane & 7] = cnt;  // [b][a]
+  {
+    const uint64_t pz = __builtin_amdgcn_ballot_w64(poison);
+    if (lane == 0) poison_s[wave] = pz;
+  }
+  // per-column lane values: lanes with hi == 0 of column c (4 row offsets) -> reduce within the wave
+  {
+    int64_t nv = nanv, pv = pinfv, mv = ninfv, iv = isum;
+    double l2 = lo, h2 = hiv;
+    // lanes c, c + 16, c + 32, c + 48 hold column c's hi == 0 partials
+    for (int off = 16; off <= 32; off <<= 1) {
+      nv += __shfl_xor(nv, off);
+      pv += __shfl_xor(pv, off);
+      mv += __shfl_xor(mv, off);
+      iv = (int64_t)((uint64_t)iv + (uint64_t)__shfl_xor(iv, off));
+      l2 = hw_min(l2, __shfl_xor(l2, off));
+      h2 = hw_max(h2, __shfl_xor(h2, off));
+    }
+    if (lane < kTileCols) {
+      nan_s[wave][lane] = nv;
+      pinf_s[wave][lane] = pv;
+      ninf_s[wave][lane] = mv;
+      isum_s[wave][lane] = iv;
+      lo_s[wave][lane] = l2;
+      hi_s[wave][lane] = h2;
+    }
+  }
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t < g.npairs) {
+    const int a = g.pi[t], b = g.pj[t];
+    double Sx = 0, Sy = 0, Sxy = 0, Sxx = 0, Syy = 0;
+    int64_t n = 0;
+    uint64_t pz = 0;
+    for (int wv = 0; wv < kWaves; ++wv) {
+      Sx += tile[wv][a][b];
+      Sy += tile[wv][b][a];
+      Sxy += tile[wv][a][8 + b];
+      Sxx += tile[wv][8 + a][b];
+      Syy += tile[wv][8 + b][a];
+      n += cnt_s[wv][b][a];
+      pz |= poison_s[wv];
+    }
+    CorrPartial r{0, 0, 0, 0, 0, 0, 0, 0};
+    if (n > 0) {
+      const double nd = (double)n;
+      if (((pz >> (a + 8 * b)) | (pz >> (b + 8 * a))) & 1ull) {
+        const double nan = __builtin_bit_cast(double, 0x7FF8000000000000ull);
+        r = CorrPartial{nd, nan, nan, nan, nan, nan, 0, 0};
+      } else {
+        const double qx = Sx / nd, qy = Sy / nd;
+        r.n = nd;
+        r.xa = shift_s[a] + qx;
+        r.ya = shift_s[b] + qy;
+        r.ck = Sxy - Sx * qy;
+        r.xm = Sxx - Sx * qx;
+        r.ym = Syy - Sy * qy;
+      }
+    }
+    pair_part[(size_t)(g.first_pair + t) * kMaxWG + range] = r;
+  } else if (t >= 64 && t < 64 + nc && g.mom_task[t - 64] >= 0) {
+    const int cc = t - 64;
+    double S = 0, Q = 0, fmin = __builtin_bit_cast(double, 0x7FF0000000000000ull),
+           fmax = __builtin_bit_cast(double, 0xFFF0000000000000ull);
+    int64_t count = 0, nan = 0, pinf = 0, ninf = 0, is = 0;
+    for (int wv = 0; wv < kWaves; ++wv) {
+      S += tile[wv][cc][cc];
+      Q += tile[wv][8 + cc][cc];
+      count += cnt_s[wv][cc][cc];
+      nan += nan_s[wv][cc];
+      pinf += pinf_s[wv][cc];
+      ninf += ninf_s[wv][cc];
+      is = (int64_t)((uint64_t)is + (uint64_t)isum_s[wv][cc]);
+      fmin = hw_min(fmin, lo_s[wv][cc]);
+      fmax = hw_max(fmax, hi_s[wv][cc]);
+    }
+    ColPartial r;
+    const int64_t nm = count - pinf - ninf;
+    r.n = (double)nm;
+    r.mean = r.m2 = r.sum = 0.0;
+    if (nm > 0) {
+      const double q1 = S / (double)nm;
+      r.mean = shift_s[cc] + q1;
+      r.m2 = Q - S * q1;
+      r.sum = __builtin_fma((double)nm, shift_s[cc], S);
+      if (nan > 0) r.mean = r.m2 = r.sum = __builtin_bit_cast(double, 0x7FF8000000000000ull);
+    }
+    r.isum = is;
+    r.count = count;
+    r.nan_count = nan;
+    r.fmin = fmin;
+    r.fmax = fmax;
+    r.pinf_count = pinf;
+    r.ninf_count = ninf;
+    r.pad = 0;
+    col_part[(size_t)g.mom_task[cc] * kMaxWG + range] = r;
+  }
+}
+
+hipError_t launch_pair_mfma_scan(const PairGroup* groups, int32_t ngroups, const ScanCols& cols,
+                                 const ScanBitmaps& bm, const uint32_t* ones, int64_t n_rows, int64_t rows_per_range,
+                                 int32_t nranges, CorrPartial* pair_part, ColPartial* col_part, bool all_f64,
+                                 bool minmax, hipStream_t st) {
+  const uint32_t blocks = (uint32_t)ngroups * (uint32_t)nranges;
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(kBlock), 0, st, groups, ngroups, cols, bm, ones, n_rows, rows_per_range,
+                       nranges, pair_part, col_part);
+  };
+  if (all_f64) {
+    if (minmax) go(dq_pair_mfma_scan<true, true>);
+    else go(dq_pair_mfma_scan<true, false>);
+  } else {
+    if (minmax) go(dq_pair_mfma_scan<false, true>);
+    else go(dq_pair_mfma_scan<false, false>);
+  }
+  return hipGetLastError();
+}
+
 }  // namespace dq

@@ -41,6 +41,10 @@ hipError_t launch_pair_lane_scan(const PairWaveTask* tasks, int32_t ntasks, cons
                                  const ScanBitmaps& bm, const uint32_t* ones, int64_t n_rows, int64_t rows_per_range,
                                  int32_t nranges, CorrPartial* pair_part, ColPartial* col_part, bool all_f64,
                                  hipStream_t st);
+hipError_t launch_pair_mfma_scan(const PairGroup* groups, int32_t ngroups, const ScanCols& cols,
+                                 const ScanBitmaps& bm, const uint32_t* ones, int64_t n_rows, int64_t rows_per_range,
+                                 int32_t nranges, CorrPartial* pair_part, ColPartial* col_part, bool all_f64,
+                                 bool minmax, hipStream_t st);
 hipError_t launch_finalize(int32_t ncol, int32_t nranges_col, const ColPartial* col_part, ColPartial* col_acc,
                            int32_t npair, int32_t nranges_pair, const CorrPartial* pair_part, CorrPartial* pair_acc,
                            int32_t has_pred, int32_t nranges_pred, const PredPartial* pred_part, PredPartial* pred_acc,
@@ -433,6 +437,9 @@ struct dq_plan {
   std::vector<PairWaveTask> lane_tasks;   // pair groups planned for the lane-per-row kernel (dq_pair.hip)
   int32_t n_fused = 0;                    // column tasks computed by the lane pair kernel (sorted last)
   bool lane_all_f64 = true;               // every lane task column is fp64 (the conversion-free instantiation)
+  std::vector<PairGroup> mfma_groups;     // pair groups of the matrix-core Gram kernel (dq_pair.hip), moments fused
+  bool mfma_all_f64 = true;
+  bool mfma_minmax = false;               // a fused moments task feeds Minimum / Maximum
   int32_t concurrency = 1;                // HIP streams the variant launches are spread over
   std::vector<hipStream_t> side;          // concurrency - 1 extra streams
   std::vector<hipEvent_t> side_done;
@@ -449,6 +456,7 @@ struct dq_plan {
   PairTask* d_pair_tasks = nullptr;
   PairGroup* d_pair_groups = nullptr;
   PairWaveTask* d_lane_tasks = nullptr;
+  PairGroup* d_mfma_groups = nullptr;
   PredProgram* d_prog = nullptr;
   ColPartial* d_col_part = nullptr;
   CorrPartial* d_pair_part = nullptr;
@@ -526,7 +534,7 @@ static dq_status free_plan_mem(dq_plan* p) {
   p->pending.clear();
   for (hipEvent_t e : p->ev_pool) (void)hipEventDestroy(e);
   p->ev_pool.clear();
-  void* ptrs[] = {p->d_col_tasks, p->d_pair_tasks, p->d_pair_groups, p->d_lane_tasks, p->d_prog, p->d_col_part, p->d_pair_part,
+  void* ptrs[] = {p->d_col_tasks, p->d_pair_tasks, p->d_pair_groups, p->d_lane_tasks, p->d_mfma_groups, p->d_prog, p->d_col_part, p->d_pair_part,
                   p->d_pred_part, p->d_col_acc, p->d_hll_acc, p->d_pair_acc, p->d_pred_acc, p->d_regex};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
@@ -965,15 +973,31 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
       if (o.pair_task >= 0) o.pair_task = new_index[o.pair_task];
   }
 
-  // pair groups -> lane-per-row wave tasks (dq_pair.hip) with the groups' stats-only column tasks fused in;
-  // a group that cannot be planned that way keeps the LDS-tile pair kernel
+  // pair groups -> the matrix-core Gram kernel (default) or lane-per-row wave tasks (dq_pair.hip), with the
+  // groups' stats-only column tasks fused in; DQ_PAIR_KERNEL=lane|tile selects the older kernels (A/B tests)
   std::vector<int> fused(p->col_tasks.size(), 0);
   {
-    const bool tile_only = std::getenv("DQ_PAIR_TILE") != nullptr;  // diagnostic A/B override (tests)
+    const char* kern = std::getenv("DQ_PAIR_KERNEL");
+    const bool tile_only = std::getenv("DQ_PAIR_TILE") != nullptr || (kern && std::strcmp(kern, "tile") == 0);
+    const bool lane = kern && std::strcmp(kern, "lane") == 0;
     std::vector<PairGroup> tile_groups;
-    for (const PairGroup& g : p->pair_groups) {
+    for (PairGroup g : p->pair_groups) {
       std::vector<PairWaveTask> w;
-      if (!tile_only && plan_lane_tasks(p, g, w, fused)) {
+      if (!tile_only && !lane && g.ncols >= 1) {
+        for (int c = 0; c < kTileCols; ++c) g.mom_task[c] = -1;
+        for (int c = 0; c < g.ncols; ++c)
+          for (size_t t = 0; t < p->col_tasks.size(); ++t) {
+            const ColTask& ct = p->col_tasks[t];
+            if (ct.col == g.cols[c] && ct.where == g.where && !fused[t] &&
+                (ct.variant == CV_F64_S || ct.variant == CV_I64_S || ct.variant == CV_I32_S)) {
+              g.mom_task[c] = (int32_t)t;
+              fused[t] = 1;
+              break;
+            }
+          }
+        for (int c = 0; c < g.ncols; ++c) p->mfma_all_f64 = p->mfma_all_f64 && g.kinds[c] == CK_F64;
+        p->mfma_groups.push_back(g);
+      } else if (!tile_only && plan_lane_tasks(p, g, w, fused)) {
         while (w.size() % kWaves) w.push_back(PairWaveTask{});  // idle padding: 4 tasks of one range per workgroup
         p->lane_tasks.insert(p->lane_tasks.end(), w.begin(), w.end());
       } else {
@@ -1007,6 +1031,13 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
     for (PairWaveTask& w : p->lane_tasks)
       for (int k = 0; k < kLaneMoments; ++k)
         if ((w.mom_mask >> k) & 1u) w.mom_out[k] = new_index[w.mom_out[k]];
+    for (PairGroup& g : p->mfma_groups)
+      for (int c = 0; c < g.ncols; ++c)
+        if (g.mom_task[c] >= 0) {
+          g.mom_task[c] = new_index[g.mom_task[c]];
+          for (const SpecOut& o : p->outs)
+            if (o.col_task == g.mom_task[c] && (o.op == DQ_OP_MIN || o.op == DQ_OP_MAX)) p->mfma_minmax = true;
+        }
     for (int32_t k = 0; k < (int32_t)p->col_tasks.size(); ++k) {
       if (fused[order[k]]) break;  // fused tasks sort last: their partials come from the pair pass
       if (p->groups.empty() || p->groups.back().variant != p->col_tasks[k].variant)
@@ -1097,7 +1128,7 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
     p->pair_bytes_x1000 = bytes_of(qv, qn);
   }
   p->launches_per_scan = (p->has_pred ? 1 : 0) + (int32_t)p->groups.size() + (p->pair_groups.empty() ? 0 : 1) +
-                         (p->lane_tasks.empty() ? 0 : 1) +
+                         (p->lane_tasks.empty() ? 0 : 1) + (p->mfma_groups.empty() ? 0 : 1) +
                          ((p->col_tasks.size() + p->pair_tasks.size()) ? 1 : 0);
 
   // device allocations
@@ -1106,6 +1137,10 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
   if (dq_status s = dmalloc(&p->d_pair_tasks, npt * sizeof(PairTask))) return s;
   if (dq_status s = dmalloc(&p->d_pair_groups, p->pair_groups.size() * sizeof(PairGroup))) return s;
   if (dq_status s = dmalloc(&p->d_lane_tasks, p->lane_tasks.size() * sizeof(PairWaveTask))) return s;
+  if (dq_status s = dmalloc(&p->d_mfma_groups, p->mfma_groups.size() * sizeof(PairGroup))) return s;
+  if (!p->mfma_groups.empty())
+    HIP_TRY(hipMemcpyAsync(p->d_mfma_groups, p->mfma_groups.data(), p->mfma_groups.size() * sizeof(PairGroup),
+                           hipMemcpyHostToDevice, p->stream));
   if (!p->lane_tasks.empty())
     HIP_TRY(hipMemcpyAsync(p->d_lane_tasks, p->lane_tasks.data(), p->lane_tasks.size() * sizeof(PairWaveTask),
                            hipMemcpyHostToDevice, p->stream));
@@ -1139,7 +1174,7 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
   if (const char* e = std::getenv("DQ_COLUMN_STREAMS")) p->concurrency = std::max(1, std::min(8, std::atoi(e)));
   p->concurrency = std::min<int32_t>(
       p->concurrency, std::max<int32_t>(1, (int32_t)p->groups.size() + (p->pair_groups.empty() ? 0 : 1) +
-                                               (p->lane_tasks.empty() ? 0 : 1)));
+                                               (p->lane_tasks.empty() ? 0 : 1) + (p->mfma_groups.empty() ? 0 : 1)));
   HIP_TRY(hipEventCreateWithFlags(&p->fork_ev, hipEventDisableTiming));
   for (int32_t k = 1; k < p->concurrency; ++k) {
     hipStream_t st;
@@ -1260,7 +1295,7 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
   ScanBitmaps bm{};
   for (int b = 0; b < kMaxWhere; ++b) bm.where_bits[b] = p->d_where_bits[b];
   // all-ones bitmap standing in for a missing validity / where bitmap in the lane pair pass
-  if (!p->lane_tasks.empty() && words + 1 > p->ones_cap_words) {
+  if ((!p->lane_tasks.empty() || !p->mfma_groups.empty()) && words + 1 > p->ones_cap_words) {
     HIP_TRY(hipStreamSynchronize(p->stream));
     if (p->d_ones) (void)hipFree(p->d_ones);
     p->d_ones = nullptr;
@@ -1278,6 +1313,10 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
     min_launch = min_launch ? std::min<int64_t>(min_launch, (int64_t)p->pair_groups.size()) : (int64_t)p->pair_groups.size();
   if (!p->lane_tasks.empty()) {  // workgroups of the lane pair launch per row range
     const int64_t wg = (int64_t)p->lane_tasks.size() / kWaves;
+    min_launch = min_launch ? std::min<int64_t>(min_launch, wg) : wg;
+  }
+  if (!p->mfma_groups.empty()) {
+    const int64_t wg = (int64_t)p->mfma_groups.size();
     min_launch = min_launch ? std::min<int64_t>(min_launch, wg) : wg;
   }
   static const int64_t target = [] {
@@ -1322,6 +1361,15 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
     if (dq_status s = timed(p, 2, st, [&] {
           return launch_pair_lane_scan(p->d_lane_tasks, (int32_t)p->lane_tasks.size(), sc, bm, p->d_ones, n_rows, rpr_col,
                                        nr_col, p->d_pair_part, p->d_col_part, p->lane_all_f64, st);
+        }))
+      return s;
+  }
+  if (!p->mfma_groups.empty()) {
+    hipStream_t st = stream_for(li++);
+    if (dq_status s = timed(p, 2, st, [&] {
+          return launch_pair_mfma_scan(p->d_mfma_groups, (int32_t)p->mfma_groups.size(), sc, bm, p->d_ones, n_rows,
+                                       rpr_col, nr_col, p->d_pair_part, p->d_col_part, p->mfma_all_f64,
+                                       p->mfma_minmax, st);
         }))
       return s;
   }

@@ -1,8 +1,9 @@
-"""The lane-per-row Correlation pass fused with the column moments (deequ_amd/csrc/dq_pair.hip).
+"""The Correlation pass fused with the column moments (deequ_amd/csrc/dq_pair.hip): the matrix-core Gram
+kernel (default) and the lane-per-row kernel (DQ_PAIR_KERNEL=lane).
 
 Correlation co-moments (Correlation.scala:37-52) and the Mean / StandardDeviation / Sum / Minimum /
 Maximum states of the same columns are computed in ONE read of each column.  Checked against the C
-oracle (Spark partition order) and against the LDS-tile kernel (DQ_PAIR_TILE=1) on: nulls, `where`
+oracle (Spark partition order) and against the LDS-tile kernel (DQ_PAIR_KERNEL=tile) on: nulls, `where`
 filters, f64 / i64 / i32 columns, NaN / +-inf values, pairs in both orientations, ragged sizes around
 the 64 / 128-row blocks, and a complete 8-column pair set (C4's 28 correlations) plus pairs on columns
 without moments.
@@ -112,10 +113,13 @@ def _check(dq, cols, states, analyzers, n, where_mask):
             assert got.metricValue() == s.max or (math.isnan(got.metricValue()) and math.isnan(s.max)), (a, got, s.max)
 
 
-@pytest.mark.parametrize("n", [0, 1, 63, 64, 65, 127, 128, 129, 2047, 2049, 100_003])
+@pytest.mark.parametrize("kernel", ["mfma", "lane"])
+@pytest.mark.parametrize("n", [0, 1, 63, 64, 65, 127, 128, 129, 255, 257, 2047, 2049, 100_003])
 @pytest.mark.parametrize("where", [None, "w > 2"])
-def test_lane_pair_pass_vs_oracle(dq, n, where):
+def test_pair_pass_vs_oracle(dq, n, where, kernel, monkeypatch):
     from deequ_amd.runner import scan_states
+
+    monkeypatch.setenv("DQ_PAIR_KERNEL", kernel)
 
     cols = _data(n, n * 3 + (where is not None), special=(n % 2 == 1))
     t = _table(dq, cols)
@@ -128,11 +132,13 @@ def test_lane_pair_pass_vs_oracle(dq, n, where):
     _check(dq, cols, states, an, n, wm)
 
 
-def test_lane_pass_equals_tile_pass_and_fuses_moments(dq, monkeypatch):
-    """The planner routes every pair group to the lane kernel (the column pass then runs no stats task of
+@pytest.mark.parametrize("kernel", ["mfma", "lane"])
+def test_fused_pass_equals_tile_pass_and_fuses_moments(dq, monkeypatch, kernel):
+    """The planner routes every pair group to the fused kernel (the column pass then runs no stats task of
     those columns); results agree with the LDS-tile kernel within the fp64 tolerance."""
     from deequ_amd.runner import ScanPlan, scan_states
 
+    monkeypatch.setenv("DQ_PAIR_KERNEL", kernel)
     n = 300_001
     cols = _data(n, 7)
     t = _table(dq, cols)
@@ -142,7 +148,7 @@ def test_lane_pass_equals_tile_pass_and_fuses_moments(dq, monkeypatch):
     plan.close()
     assert launches == 2, launches  # the lane pair pass + finalize: moments fused, no column pass
     lane = scan_states(t, an)
-    monkeypatch.setenv("DQ_PAIR_TILE", "1")
+    monkeypatch.setenv("DQ_PAIR_KERNEL", "tile")
     tile = scan_states(t, an)
     for a in an:
         g, w = lane[a].metricValue(), tile[a].metricValue()
