@@ -165,6 +165,22 @@ def _load():
                                     P(c.c_char_p), c.c_int32, c.c_int32, P(c.c_void_p)]
     L.dq_regex_info.restype = c.c_int32
     L.dq_regex_info.argtypes = [c.c_char_p, c.c_int32, P(c.c_int32), P(c.c_int32)]
+    L.dq_pred_pool_create.restype = c.c_int32
+    L.dq_pred_pool_create.argtypes = [P(c.c_char_p), P(c.c_int32), c.c_int32, P(c.c_void_p)]
+    L.dq_pred_pool_add.restype = c.c_int32
+    L.dq_pred_pool_add.argtypes = [c.c_void_p, c.c_char_p, P(c.c_int32)]
+    L.dq_pred_pool_add_regex.restype = c.c_int32
+    L.dq_pred_pool_add_regex.argtypes = [c.c_void_p, c.c_int32, c.c_char_p, c.c_int32, P(c.c_int32)]
+    L.dq_pred_pool_size.restype = c.c_int32
+    L.dq_pred_pool_size.argtypes = [c.c_void_p]
+    L.dq_pred_pool_nodes.restype = P(PredNode)
+    L.dq_pred_pool_nodes.argtypes = [c.c_void_p]
+    L.dq_pred_pool_num_patterns.restype = c.c_int32
+    L.dq_pred_pool_num_patterns.argtypes = [c.c_void_p]
+    L.dq_pred_pool_patterns.restype = P(c.c_char_p)
+    L.dq_pred_pool_patterns.argtypes = [c.c_void_p]
+    L.dq_pred_pool_destroy.restype = None
+    L.dq_pred_pool_destroy.argtypes = [c.c_void_p]
     L.dq_regex_match_host.restype = c.c_int32
     L.dq_regex_match_host.argtypes = [c.c_char_p, c.c_int32, c.c_void_p, c.c_void_p, c.c_int64, c.c_void_p]
     L.dq_freq_build.restype = c.c_int32
@@ -239,6 +255,8 @@ lib = _load()
 # every symbol include/dqscan.h declares (checked by tests/test_boundary.py)
 EXPORTED = [
     "dq_abi_version", "dq_last_error", "dq_plan_create", "dq_plan_create_ex", "dq_regex_info", "dq_regex_match_host",
+    "dq_pred_pool_create", "dq_pred_pool_add", "dq_pred_pool_add_regex", "dq_pred_pool_size", "dq_pred_pool_nodes",
+    "dq_pred_pool_num_patterns", "dq_pred_pool_patterns", "dq_pred_pool_destroy",
     "dq_plan_set_stream", "dq_freq_build", "dq_freq_merge", "dq_freq_summarize", "dq_freq_num_groups",
     "dq_freq_export", "dq_freq_destroy", "dq_mutual_information", "dq_approx_quantiles", "dq_freq_top", "dq_scan", "dq_finish",
     "dq_plan_reset", "dq_plan_destroy", "dq_plan_bytes_per_row_x1000", "dq_plan_num_launches",

@@ -66,8 +66,7 @@ class PlanBuilder:
         self.table_schema = list(table_schema)
         self.by_name = {c[0]: c for c in self.table_schema}
         self.columns: List[str] = []
-        self.col_index = _LazyIndex(self)
-        self.pool = PredicatePool(self.col_index)
+        self.pool = PredicatePool(self)
         self.specs: List[tuple] = []
 
     def col(self, name: str) -> int:
@@ -89,20 +88,6 @@ class PlanBuilder:
             arr[i].type = DTYPES[dt]
             arr[i].nullable = 1 if nullable else 0
         return arr
-
-
-class _LazyIndex(dict):
-    """Column-name -> plan column index, registering columns on first reference."""
-
-    def __init__(self, builder):
-        super().__init__()
-        self.b = builder
-
-    def __contains__(self, name):
-        return name in self.b.by_name
-
-    def __getitem__(self, name):
-        return self.b.col(name)
 
 
 class Analyzer:

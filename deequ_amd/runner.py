@@ -136,23 +136,7 @@ def gpu_eligible(analyzer: Analyzer, schema) -> Optional[Exception]:
         return e
     except Exception:
         return None  # a missing column etc. is an aggregation error, not a routing decision
-    # comparisons on string columns are outside the GPU grammar (IS [NOT] NULL on them is fine)
-    nodes = b.pool.nodes
-
-    def column_of(i):
-        k, a = nodes[i][0], nodes[i][1]
-        if k == L.PRED_COLUMN:
-            return b.columns[a]
-        if k == L.PRED_COALESCE and nodes[a][0] == L.PRED_COLUMN:
-            return b.columns[nodes[a][1]]
-        return None
-
-    for (kind, a, bb, cmp, i64, f64) in nodes:
-        if kind == L.PRED_CMP:
-            for child in (a, bb):
-                c = column_of(child)
-                if c is not None and b.by_name[c][1] not in ("f64", "i64", "i32"):
-                    return UnsupportedPredicate(f"predicate compares string column {c!r}")
+    # a comparison on a string column is rejected by the predicate compiler itself (UnsupportedPredicate)
     return None
 
 

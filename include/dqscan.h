@@ -182,6 +182,28 @@ dq_status dq_plan_create_ex(const dq_analyzer_spec* specs, int32_t n_specs, cons
 dq_status dq_regex_info(const char* pattern, int32_t mode, int32_t* n_states, int32_t* n_classes);
 dq_status dq_regex_match_host(const char* pattern, int32_t mode, const uint8_t* data, const int64_t* offsets,
                               int64_t n, uint8_t* out);
+/* Predicate compiler: Spark SQL predicate text -> the IR above, on the host (replaces Spark's expr(...)
+ * parse of the strings deequ builds: Analyzer.scala:385-408 `where`, Check.scala:538-548, 670-871).
+ * A pool holds the table's columns (name, enum dq_type; node column indices are positions in that list)
+ * and accumulates the nodes and regex patterns of every root of one plan, ready for dq_plan_create_ex.
+ * Grammar: OR / AND / NOT, comparisons < <= > >= = == != <>, IS [NOT] NULL, COALESCE(a, b), parentheses,
+ * numeric literals typed as Spark 2.2 (`3` int, `3.0` exact decimal, `3e0` double), NULL / TRUE / FALSE,
+ * string (in)equality and [NOT] IN ('a', ...) on a string column (lowered to a DQ_REGEX_FULL node).
+ * dq_pred_pool_add: DQ_E_UNSUPPORTED (reason in dq_last_error) for text outside that grammar -- string
+ * ordering, a numeric comparison of a string column, LIKE / RLIKE / BETWEEN, function calls, typed literal
+ * suffixes, escapes -- i.e. route the analyzer to the Spark fallback; DQ_E_INVALID "no such column: x" for
+ * an unknown column.  A failed add leaves the pool unchanged.  dq_pred_pool_add_regex appends a
+ * DQ_PRED_REGEX root over `column` (PatternMatch; DQ_E_UNSUPPORTED outside the DFA subset).  Node and
+ * pattern arrays stay valid until the next add or destroy. */
+typedef struct dq_pred_pool dq_pred_pool;
+dq_status dq_pred_pool_create(const char* const* names, const int32_t* types, int32_t n_cols, dq_pred_pool** out);
+dq_status dq_pred_pool_add(dq_pred_pool* pool, const char* sql, int32_t* root);
+dq_status dq_pred_pool_add_regex(dq_pred_pool* pool, int32_t column, const char* pattern, int32_t mode, int32_t* root);
+int32_t dq_pred_pool_size(const dq_pred_pool* pool);
+const dq_pred_node* dq_pred_pool_nodes(const dq_pred_pool* pool);
+int32_t dq_pred_pool_num_patterns(const dq_pred_pool* pool);
+const char* const* dq_pred_pool_patterns(const dq_pred_pool* pool);
+void dq_pred_pool_destroy(dq_pred_pool* pool);
 /* Launch on this hipStream_t from now on (NULL = the device null stream).  A new plan launches on its
    own non-blocking stream, which does not order against other streams: set the producer's stream. */
 dq_status dq_plan_set_stream(dq_plan* plan, void* hip_stream);

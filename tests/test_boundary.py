@@ -25,7 +25,8 @@ def test_header_symbols_exported(dq):
     from deequ_amd import _lib as L
 
     hdr = open(os.path.join(ROOT, "include", "dqscan.h")).read()
-    declared = set(re.findall(r"^\s*(?:dq_status|int32_t|int64_t|void|const char\*)\s+(dq_\w+)\s*\(", hdr, re.M))
+    declared = set(re.findall(r"^\s*(?:dq_status|int32_t|int64_t|void|const char\* const\*|const char\*|const dq_\w+\*)"
+                              r"\s+(dq_\w+)\s*\(", hdr, re.M))
     assert len(declared) >= 18
     for name in declared:
         assert hasattr(L.lib, name), name
@@ -157,24 +158,91 @@ def test_analyzer_tostring_and_equality(dq):
     assert dq.Size() == dq.Size() and len({dq.Size(), dq.Size(), dq.Size("x > 1")}) == 2
 
 
-def test_predicate_parser(dq):
-    from deequ_amd import _lib as L
-    from deequ_amd.predicates import PredicatePool, UnsupportedPredicate
+class _CPool:
+    """dq_pred_pool_* straight through ctypes (what a JNI / cgo shim binds)."""
 
-    cols = {"a": 0, "b": 1}
-    p = PredicatePool(cols)
-    r = p.add("`a` IS NULL OR (`a` >= 0.0 AND `a` <= 7.5)")
-    kinds = [n[0] for n in p.nodes]
-    assert kinds.count(L.PRED_LIT_DECIMAL) == 2 and p.nodes[r][0] == L.PRED_OR
-    dec = [n for n in p.nodes if n[0] == L.PRED_LIT_DECIMAL]
-    assert (dec[1][4], dec[1][3]) == (75, 1)  # 7.5 = 75 / 10^1
-    p.add("COALESCE(b, 1.0) > 0")
-    p.add("a > -1.5e2 AND NOT b <> 3")
-    for bad in ("a IN (1, 2)", "a = 'x'", "abs(a) > 1", "a LIKE 'x%'", "1.0D > a"):
-        with pytest.raises(UnsupportedPredicate):
-            PredicatePool(cols).add(bad)
+    def __init__(self, L, cols):
+        names = (ctypes.c_char_p * len(cols))(*[n.encode() for n, _ in cols])
+        types = (ctypes.c_int32 * len(cols))(*[t for _, t in cols])
+        self.L, self.h = L, ctypes.c_void_p()
+        assert L.lib.dq_pred_pool_create(names, types, len(cols), ctypes.byref(self.h)) == L.DQ_OK
+
+    def add(self, text):
+        r = ctypes.c_int32(-7)
+        st = self.L.lib.dq_pred_pool_add(self.h, text.encode(), ctypes.byref(r))
+        return st, r.value
+
+    def nodes(self):
+        n = self.L.lib.dq_pred_pool_size(self.h)
+        p = self.L.lib.dq_pred_pool_nodes(self.h)
+        return [(p[i].kind, p[i].a, p[i].b, p[i].cmp, p[i].i64, p[i].f64) for i in range(n)]
+
+    def patterns(self):
+        n = self.L.lib.dq_pred_pool_num_patterns(self.h)
+        p = self.L.lib.dq_pred_pool_patterns(self.h)
+        return [p[i].decode() for i in range(n)]
+
+    def close(self):
+        self.L.lib.dq_pred_pool_destroy(self.h)
+
+
+def test_predicate_compiler_c_abi(dq):
+    """dq_pred_pool_add: the Spark 2.2 literal typing and the grammar's routing decisions, via ctypes."""
+    from deequ_amd import _lib as L
+
+    P = _CPool(L, [("a", L.TYPE_F64), ("b", L.TYPE_I64), ("s", L.TYPE_UTF8)])
+    st, r = P.add("`a` IS NULL OR (`a` >= 0.0 AND `a` <= 7.5)")
+    nodes = P.nodes()
+    assert st == L.DQ_OK and nodes[r][0] == L.PRED_OR
+    dec = [n for n in nodes if n[0] == L.PRED_LIT_DECIMAL]
+    assert [(d[4], d[3]) for d in dec] == [(0, 1), (75, 1)]  # 0.0 = 0 / 10^1, 7.5 = 75 / 10^1
+    st, r = P.add("COALESCE(b, 1.0) > 0 AND a > -1.5e2 AND NOT b <> 3")
+    nodes = P.nodes()
+    assert st == L.DQ_OK
+    assert [n[5] for n in nodes if n[0] == L.PRED_LIT_DOUBLE] == [-150.0]
+    assert [n[4] for n in nodes if n[0] == L.PRED_LIT_INT] == [0, 3]
+    assert any(n[0] == L.PRED_COALESCE for n in nodes) and any(n[3] == L.CMP_NE for n in nodes if n[0] == L.PRED_CMP)
+    # 64-bit literal bounds (Spark: a literal beyond Long is a decimal / fails; the GPU takes int64 only)
+    for text, want in (("b > 9223372036854775807", (1 << 63) - 1), ("b > -9223372036854775808", -(1 << 63))):
+        st, r = P.add(text)
+        assert st == L.DQ_OK and P.nodes()[P.nodes()[r][2]][4] == want
+    # string equality / IN on the string column: one whole-value DFA node, literals escaped
+    st, r = P.add("s IN ('a.b', 'c') OR s = 'd' OR s NOT IN ('e')")
+    assert st == L.DQ_OK
+    assert P.patterns() == [r"(?:a\.b|c)", "(?:d)", "(?:e)"]
+    regex = [n for n in P.nodes() if n[0] == L.PRED_REGEX]
+    assert len(regex) == 3 and all(n[3] == L.REGEX_FULL for n in regex)
+    # outside the grammar: DQ_E_UNSUPPORTED, pool unchanged
+    size = L.lib.dq_pred_pool_size(P.h)
+    for bad in ("a IN (1, 2)", "a = 'x'", "abs(a) > 1", "a LIKE 'x%'", "1.0D > a", "s > 'x'", "s > 1",
+                "COALESCE(s, 0) > 1", "a BETWEEN 1 AND 2", "'x' = 'y'", "a > 1e", "a > 1.2.3", "s = 'it\\'s'",
+                "a > 9223372036854775808", "a > 0.1234567890123456789", "COALESCE(a, 1, 2) > 0", "a >", "(a > 1"):
+        st, _ = P.add(bad)
+        assert st == L.DQ_E_UNSUPPORTED, bad
+        assert L.lib.dq_last_error(), bad
+        assert L.lib.dq_pred_pool_size(P.h) == size, bad
+    st, _ = P.add("zz > 1")
+    assert st == L.DQ_E_INVALID and L.lib.dq_last_error() == b"no such column: zz"
+    P.close()
+
+
+def test_predicate_pool_python_mapping(dq):
+    """The host wrapper re-indexes the C pool's table columns to plan columns (first reference order)."""
+    from deequ_amd import _lib as L
+    from deequ_amd.analyzers import PlanBuilder
+    from deequ_amd.predicates import UnsupportedPredicate
+
+    b = PlanBuilder([("x", "f64", True), ("y", "i64", False), ("t", "utf8", True)])
+    r = b.pool.add("y > 2 AND x IS NOT NULL")
+    assert b.columns == ["y", "x"]
+    cols = [n[1] for n in b.pool.nodes if n[0] == L.PRED_COLUMN]
+    assert cols == [0, 1] and b.pool.nodes[r][0] == L.PRED_AND
+    b.pool.add("t = 'q'")
+    assert b.columns == ["y", "x", "t"] and b.pool.patterns == ["(?:q)"]
+    with pytest.raises(UnsupportedPredicate):
+        b.pool.add("t > 'q'")
     with pytest.raises(KeyError):
-        PredicatePool(cols).add("zz > 1")
+        b.pool.add("zz > 1")
 
 
 def test_plan_create_without_gpu_reports_error(dq):
