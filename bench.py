@@ -49,6 +49,9 @@ def parse():
     p.add_argument("--config-steps", type=int, default=3)
     p.add_argument("--config-rows", type=int, default=0, help="rows of C2-C4 (0 = BASELINE's 1e9; profiling runs)")
     p.add_argument("--skip-headline", action="store_true", help="profiling runs: only the --configs")
+    p.add_argument("--ingest-rows", type=int, default=62_500_000,
+                   help="rows of the host-resident Arrow C5 batch for the ingestion leg (0 = skip)")
+    p.add_argument("--ingest-reps", type=int, default=4, help="uploads + scans of that batch timed end to end")
     return p.parse_args()
 
 
@@ -203,6 +206,9 @@ def main():
     plan.close()
     del chunks
     torch.cuda.empty_cache()
+    if rank == 0 and world == 1 and args.ingest_rows > 0:
+        out["ingest"] = ingest_timing(args, analyzers)
+        torch.cuda.empty_cache()
     if world == 1 and args.configs:
         out["configs"] = {}
         for cfg in [c for c in args.configs.split(",") if c]:
@@ -368,6 +374,96 @@ def _host_cols(table, n):
             cols.append((c.dtype, c.values[: n * w].cpu().numpy().view({"f64": np.float64, "i64": np.int64,
                                                                         "i32": np.int32}[c.dtype]), None, bm))
     return cols
+
+
+def _arrow_batch(table, n):
+    """The device table's columns as a host-resident pyarrow RecordBatch (zero-copy over numpy buffers)."""
+    import numpy as np
+    import pyarrow as pa
+
+    arrays, names = [], []
+    for name, c in table.columns.items():
+        bm = c.validity[: (n + 7) // 8].cpu().numpy() if c.validity is not None else None
+        vb = pa.py_buffer(bm) if bm is not None else None
+        if c.dtype in ("utf8", "large_utf8"):
+            w = 4 if c.dtype == "utf8" else 8
+            offs = c.offsets[: (n + 1) * w].cpu().numpy()
+            nbytes = int(offs.view(np.int32 if w == 4 else np.int64)[-1])
+            data = c.values[:nbytes].cpu().numpy()
+            arr = pa.Array.from_buffers(pa.string() if w == 4 else pa.large_string(), n,
+                                        [vb, pa.py_buffer(offs), pa.py_buffer(data)], null_count=-1 if bm is not None else 0)
+        else:
+            w = 4 if c.dtype == "i32" else 8
+            t = {"f64": pa.float64(), "i64": pa.int64(), "i32": pa.int32()}[c.dtype]
+            arr = pa.Array.from_buffers(t, n, [vb, pa.py_buffer(c.values[: n * w].cpu().numpy())],
+                                        null_count=-1 if bm is not None else 0)
+        arrays.append(arr)
+        names.append(name)
+    return pa.record_batch(arrays, names=names)
+
+
+def ingest_timing(args, analyzers) -> dict:
+    """C5 from HOST-resident Arrow batches (Arrow C Data Interface -> pinned double-buffered upload ->
+    dq_scan): upload GB/s (host memory -> HBM, CPU staging copy included) and end-to-end rows/s of upload
+    + scan with the copy of chunk k + 1 overlapping the scan of chunk k.  The same host batch is fed
+    --ingest-reps times (rows counted each time)."""
+    import ctypes
+
+    import torch
+
+    from deequ_amd import _lib as L
+    from deequ_amd import synth
+    from deequ_amd.ingest import ArrowScanner, ImportedArray, arrow_schema
+    from deequ_amd.runner import ScanPlan
+
+    n = args.ingest_rows
+    t = synth.c5_table(n, row0=0, seed=42)
+    torch.cuda.synchronize()
+    batch = _arrow_batch(t, n)
+    del t
+    torch.cuda.empty_cache()
+    plan = ScanPlan(analyzers, arrow_schema(batch))
+    hosts = [ImportedArray(batch.column(batch.schema.get_field_index(c))) for c in plan.columns]
+    nbytes = sum(h.host.value_bytes + h.host.validity_bytes + h.host.offset_bytes for h in hosts)
+    for h in hosts:
+        h.close()
+    slot = nbytes + 3 * 256 * len(plan.columns)
+    sc = ArrowScanner(plan, slot, n_slots=2)
+    # upload alone: host -> pinned -> HBM, synchronised
+    sc.scan(batch)  # warm (pinned pages touched, plan allocated)
+    plan.finish()
+    plan.reset()
+    imported = [ImportedArray(batch.column(batch.schema.get_field_index(c))) for c in plan.columns]
+    hc = (type(imported[0].host) * len(imported))(*[i.host for i in imported])
+    views = (L.ColumnView * len(imported))()
+    lib = sc.lib
+    t0 = time.perf_counter()
+    for _ in range(args.ingest_reps):
+        L.check(lib.dq_upload(sc.h, hc, len(imported), views))
+        L.check(lib.dq_upload_release(sc.h, sc.stream))
+    L.check(lib.dq_upload_sync(sc.h))
+    t_up = time.perf_counter() - t0
+    for i in imported:
+        i.close()
+    torch.cuda.synchronize()
+    # end to end: upload k + 1 overlaps scan k
+    plan.reset()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.ingest_reps):
+        sc.scan(batch)
+    plan.finish()
+    torch.cuda.synchronize()
+    t_e2e = time.perf_counter() - t0
+    sc.close()
+    plan.close()
+    reps = args.ingest_reps
+    return {"rows_per_batch": n, "batches": reps, "host_bytes_per_batch": nbytes,
+            "upload_GBps": nbytes * reps / t_up / 1e9,
+            "pcie_gen5_x16_GBps": 64.0,
+            "e2e_rows_per_s": n * reps / t_e2e, "e2e_ms_per_batch": t_e2e / reps * 1e3,
+            "note": "host Arrow batch (pageable numpy buffers) -> CPU threads -> pinned slot -> DMA -> HBM, "
+                    "2 slots; e2e = upload + fused scan + finish, copy of batch k+1 overlapping scan of k"}
 
 
 def cpu_baseline(table, n, threads, min_seconds=10.0):

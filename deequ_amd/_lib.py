@@ -257,6 +257,8 @@ EXPORTED = [
     "dq_abi_version", "dq_last_error", "dq_plan_create", "dq_plan_create_ex", "dq_regex_info", "dq_regex_match_host",
     "dq_pred_pool_create", "dq_pred_pool_add", "dq_pred_pool_add_regex", "dq_pred_pool_size", "dq_pred_pool_nodes",
     "dq_pred_pool_num_patterns", "dq_pred_pool_patterns", "dq_pred_pool_destroy",
+    "dq_arrow_import", "dq_uploader_create", "dq_upload", "dq_upload_fence", "dq_upload_release", "dq_upload_sync",
+    "dq_uploader_destroy",
     "dq_plan_set_stream", "dq_freq_build", "dq_freq_merge", "dq_freq_summarize", "dq_freq_num_groups",
     "dq_freq_export", "dq_freq_destroy", "dq_mutual_information", "dq_approx_quantiles", "dq_freq_top", "dq_scan", "dq_finish",
     "dq_plan_reset", "dq_plan_destroy", "dq_plan_bytes_per_row_x1000", "dq_plan_num_launches",

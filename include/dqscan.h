@@ -135,6 +135,69 @@ typedef struct dq_column_view {
   int64_t reserved; /* must be 0 */
 } dq_column_view;
 
+/* ---- Host ingestion: Arrow C Data Interface batches -> device chunks (no JVM in the data path) ----
+ * The Arrow C Data Interface ABI (arrow.apache.org/docs/format/CDataInterface.html), as exported by
+ * Spark's Arrow conversion, pyarrow (Array._export_to_c), arrow-rs / arrow-cpp. */
+#ifndef ARROW_C_DATA_INTERFACE
+#define ARROW_C_DATA_INTERFACE
+#define ARROW_FLAG_DICTIONARY_ORDERED 1
+#define ARROW_FLAG_NULLABLE 2
+#define ARROW_FLAG_MAP_KEYS_SORTED 4
+struct ArrowSchema {
+  const char* format;
+  const char* name;
+  const char* metadata;
+  int64_t flags;
+  int64_t n_children;
+  struct ArrowSchema** children;
+  struct ArrowSchema* dictionary;
+  void (*release)(struct ArrowSchema*);
+  void* private_data;
+};
+struct ArrowArray {
+  int64_t length;
+  int64_t null_count;
+  int64_t offset;
+  int64_t n_buffers;
+  int64_t n_children;
+  const void** buffers;
+  struct ArrowArray** children;
+  struct ArrowArray* dictionary;
+  void (*release)(struct ArrowArray*);
+  void* private_data;
+};
+#endif /* ARROW_C_DATA_INTERFACE */
+
+/* One column's HOST buffers (what dq_arrow_import finds in an ArrowArray; the caller keeps the Arrow
+ * array alive until dq_upload returns).  Byte counts are the bytes dq_upload copies. */
+typedef struct dq_host_column {
+  int32_t type;            /* enum dq_type */
+  int32_t nullable;        /* 1 iff validity != NULL */
+  int64_t n_rows;
+  const void* values;      /* fixed-width values / UTF8 data bytes */
+  const uint8_t* validity; /* LSB-first bitmap, bit 0 = row 0; NULL = no nulls */
+  const void* offsets;     /* UTF8: n_rows + 1 offsets starting at 0 */
+  int64_t value_bytes, validity_bytes, offset_bytes;
+} dq_host_column;
+/* Map an exported Arrow array (formats g = float64, l = int64, i = int32, u = utf8, U = large_utf8) to
+ * host column buffers.  DQ_E_UNSUPPORTED: other types, nested / dictionary arrays, a slice whose
+ * validity does not start at a byte boundary or whose string offsets do not start at 0 (re-slice). */
+dq_status dq_arrow_import(const struct ArrowSchema* schema, const struct ArrowArray* array, dq_host_column* out);
+/* Pinned, n-buffered host -> device upload.  dq_upload copies one chunk's columns (CPU threads: host ->
+ * pinned slot; DMA on the uploader's own stream: pinned -> device slot) and returns device views of the
+ * slot, valid until the slot is reused n_slots uploads later.  Before scanning, make the scan stream wait
+ * for the copy (dq_upload_fence); after enqueueing the scan, record the slot's release on that stream
+ * (dq_upload_release) -- the DMA of a later chunk into the same slot waits for it.  So with n_slots = 2 the
+ * upload of chunk k + 1 overlaps the scan of chunk k.  host_threads <= 0: up to 16 CPU threads. */
+typedef struct dq_uploader dq_uploader;
+dq_status dq_uploader_create(int32_t device, int32_t n_slots, int64_t slot_bytes, int32_t host_threads,
+                             dq_uploader** out);
+dq_status dq_upload(dq_uploader* u, const dq_host_column* cols, int32_t n_cols, dq_column_view* dev_views);
+dq_status dq_upload_fence(dq_uploader* u, void* hip_stream);
+dq_status dq_upload_release(dq_uploader* u, void* hip_stream);
+dq_status dq_upload_sync(dq_uploader* u);
+void dq_uploader_destroy(dq_uploader* u);
+
 /* The aggregation-result slots of one analyzer (the reference's Row slice at its offset,
  * SURVEY §8b).  has_value[i] = SQL non-null flag of slot i; single-slot analyzers mirror slot 0
  * into has_value[1].  fromAggregationResult yields Some(state) iff both flags are 1 (and, for
