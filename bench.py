@@ -31,7 +31,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md (HBM3E peak 8.0 TB/s)
 # FETCH_SIZE summary of this round's kernels (tools/profile_round.sh -> tools/summarize_prof.py):
 # per-dispatch HBM read bytes of each kernel at the default 125 M-row chunk, gfx950-corrected
-PMC_FILE = os.path.join(ROOT, "profiles", "r1f_pmc.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r2_pmc.json")
 DEFAULT_CHUNK = 125_000_000  # 8 chunks per 1e9 rows; a UTF8 chunk's bytes (~2.0e9) stay < 2 GiB
 
 
@@ -195,7 +195,8 @@ def main():
                      "frac": dom["GBps"] / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": os.path.relpath(PMC_FILE, ROOT) if traffic is not None else None,
                      "kernel": dom_name, "bytes_per_launch": dom["bytes_per_launch"],
-                     "avg_launch_ms": dom["avg_ms"], "launches": dom["launches"], "kernels": kernels},
+                     "avg_launch_ms": dom["avg_ms"], "launches": dom["launches"],
+                     "valu_issue": valu_bound(dom["pmc_name"], dom["avg_ms"]), "kernels": kernels},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1:
@@ -325,8 +326,8 @@ def run_config(cfg, args) -> dict:
     return rec
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the committed FETCH_SIZE pass (None if not profiled)."""
+def pmc_record(kernel):
+    """The committed PMC pass record of `kernel` (FETCH_SIZE bytes, SQ instruction counts per launch), or None."""
     try:
         with open(PMC_FILE) as f:
             recs = json.load(f)["kernels"]
@@ -334,8 +335,31 @@ def pmc_traffic(kernel):
         return None
     for r in recs:
         if r["kernel"] == kernel:
-            return r["hbm_read_bytes_per_call_corrected"]
+            return r
     return None
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed FETCH_SIZE pass (None if not profiled)."""
+    r = pmc_record(kernel)
+    return r["hbm_read_bytes_per_call_corrected"] if r else None
+
+
+# VALU issue model of the HLL kernels (tools/micro/valu_rate_probe.hip, round-1 tools/rates.hip): one wave64
+# integer VALU instruction per 4 SIMD cycles, 1024 SIMDs at 2.4 GHz
+VALU_CYCLES_PER_WAVE_INST = 4.0
+
+
+def valu_bound(kernel, avg_ms):
+    """VALU issue floor of `kernel` from the committed SQ pass: wave-instructions per launch x 4 cycles
+    / (1024 SIMDs x 2.4 GHz), and the fraction of the measured launch it accounts for."""
+    r = pmc_record(kernel)
+    if not r or "SQ_INSTS_VALU_per_call" not in r:
+        return None
+    insts = r["SQ_INSTS_VALU_per_call"]
+    floor_ms = insts * VALU_CYCLES_PER_WAVE_INST / (1024 * 2.4e9) * 1e3
+    return {"valu_insts_per_launch": insts, "issue_floor_ms": floor_ms, "frac_of_launch": floor_ms / avg_ms,
+            "model": "4 SIMD cycles per wave64 VALU instruction, 1024 SIMDs x 2.4 GHz", "source": os.path.relpath(PMC_FILE, ROOT)}
 
 
 def state_io_timing(analyzers, states) -> dict:

@@ -9,7 +9,7 @@ TAG=${1:-r1}
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 mkdir -p gpurun_out profiles
 export TMPDIR=/tmp
-B="bench.py --cpu-sample 0 --configs="
+B="bench.py --cpu-sample 0 --configs= --ingest-rows 0"
 timeout -k 10 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_kt -o kt --output-format csv -- \
   python3 $B --steps 3 --warmup 1 > gpurun_out/prof_kt_bench.json 2> gpurun_out/prof_kt.err || { echo "kt failed $?"; tail -20 gpurun_out/prof_kt.err; exit 2; }
 echo "kt ok"
