@@ -1105,15 +1105,40 @@ __device__ __forceinline__ void pred_atom_cmp(const PredInstr& ins, const AtomBu
   const bool two = ins.col_b >= 0;
   const bool is_int = ins.ctype == CT_INT;
   uint32_t wc = 0;
+  // row group j's 64-bit mask -> word lanes 2 j, 2 j + 1 (lanes 0..15 own the block's 16 words)
+  // v_writelane: the scalar halves go straight into lanes 2 j, 2 j + 1.  The mask usually comes straight
+  // from a v_cmp (VCC): a VALU-written SGPR read by v_writelane needs wait states the compiler cannot
+  // insert for inline asm, hence the s_nop.
+  auto put = [&](int j, uint64_t cm) {
+    const uint32_t lo = (uint32_t)cm, hi = (uint32_t)(cm >> 32);
+    asm volatile("s_nop 4\n\tv_writelane_b32 %0, %1, %2" : "+v"(wc) : "s"(lo), "i"(2 * j));
+    asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(wc) : "s"(hi), "i"(2 * j + 1));
+  };
+  if (is_int) {
+    // integers have no NaN: one compare per row group, the operator chosen once (uniform switch)
+    auto run = [&](auto op) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int64_t x = (int64_t)L.a[j], y = two ? (int64_t)L.b[j] : ins.lit_i;
+        put(j, __builtin_amdgcn_ballot_w64(op(x, y)));
+      }
+    };
+    switch (cmp) {
+      case C_LT: run([](int64_t x, int64_t y) { return x < y; }); break;
+      case C_LE: run([](int64_t x, int64_t y) { return x <= y; }); break;
+      case C_GT: run([](int64_t x, int64_t y) { return x > y; }); break;
+      case C_GE: run([](int64_t x, int64_t y) { return x >= y; }); break;
+      case C_EQ: run([](int64_t x, int64_t y) { return x == y; }); break;
+      case C_NE: run([](int64_t x, int64_t y) { return x != y; }); break;
+      case C_TRUE: wc = ~0u; break;
+      default: wc = 0u; break;
+    }
+  }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
+    if (is_int) break;
     uint64_t lt, eq, gt, an = 0, bn = 0;
-    if (is_int) {
-      const int64_t x = (int64_t)L.a[j], y = two ? (int64_t)L.b[j] : ins.lit_i;
-      lt = __builtin_amdgcn_ballot_w64(x < y);
-      eq = __builtin_amdgcn_ballot_w64(x == y);
-      gt = __builtin_amdgcn_ballot_w64(x > y);
-    } else {
+    {
       const double x = pred_as_double(L.a[j], ins.kind_a), y = two ? pred_as_double(L.b[j], ins.kind_b) : ins.lit_d;
       lt = __builtin_amdgcn_ballot_w64(x < y);
       eq = __builtin_amdgcn_ballot_w64(x == y);
@@ -1122,8 +1147,7 @@ __device__ __forceinline__ void pred_atom_cmp(const PredInstr& ins, const AtomBu
       bn = __builtin_amdgcn_ballot_w64(y != y);
     }
     const uint64_t cm = (lt & Klt) | (eq & Keq) | (gt & Kgt) | (~an & bn & Kbn) | (an & ~bn & Kan) | (an & bn & Kab);
-    // fold row group j into the lane's word (lanes 0..15: word L = rows 32 L .. + 31 of the block)
-    if ((lane >> 1) == j) wc = (lane & 1) ? (uint32_t)(cm >> 32) : (uint32_t)cm;
+    put(j, cm);  // row group j -> the word lanes (lanes 0..15: word L = rows 32 L .. + 31 of the block)
   }
   // NULL operand b -> NULL; NULL a -> the COALESCE fallback result (NULL without one)
   const uint32_t va = L.va, vb = two ? L.vb : ~0u;
@@ -1252,6 +1276,20 @@ __device__ __forceinline__ void pred_atom_regex_utf8(const PredInstr& ins, const
   wn = ins.null_res == NR_NULL ? ~va : 0u;
 }
 
+// One instruction of the program, read from the workgroup's LDS copy and made wave-uniform (SGPRs).  The
+// interpreter used to read each field with scalar loads from global memory inside the block loop: every
+// LDS stack access then also waited for those out-of-order SMEM returns (lgkmcnt(0)), serialising the
+// block on scalar-load latency (rocprof: ~126 SMEM and ~30k wave cycles per 512-row block).
+__device__ __forceinline__ PredInstr uniform_instr(const PredInstr* p) {
+  static_assert(sizeof(PredInstr) % 4 == 0, "PredInstr words");
+  PredInstr r;
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(p);
+  uint32_t* o = reinterpret_cast<uint32_t*>(&r);
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(PredInstr) / 4); ++k) o[k] = __builtin_amdgcn_readfirstlane(w[k]);
+  return r;
+}
+
 // RX: the program holds regex atoms.  Instantiated separately so that the DFA walk's registers (142
 // VGPRs with it, 119 without: 3 vs 4 waves per SIMD) do not cost the plain numeric programs occupancy.
 template <bool RX>
@@ -1259,6 +1297,10 @@ __global__ __launch_bounds__(kBlock) void dq_pred_scan(const PredProgram* __rest
                                                        ScanBitmaps bm, int64_t n_rows, int64_t rows_per_range,
                                                        PredPartial* __restrict__ acc) {
   extern __shared__ uint32_t pred_lds[];
+  __shared__ PredInstr s_instr[kMaxInstr];
+  __shared__ int16_t s_load[kMaxInstr];
+  __shared__ PredCounter s_ctr[kMaxCounters];
+  __shared__ int32_t s_bmroot[kMaxWhere];
   const PredProgram& prog = *prog_g;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1266,6 +1308,13 @@ __global__ __launch_bounds__(kBlock) void dq_pred_scan(const PredProgram* __rest
   PredScratch S(pred_lds + wave * wave_words, prog.stack_depth, prog.n_roots, prog.n_counters);
   const bool wl = lane < 16;  // word lanes
   const int n_instr = prog.n_instr, n_counters = prog.n_counters, n_bitmaps = prog.n_bitmaps, n_loads = prog.n_loads;
+  // the program -> LDS once per workgroup
+  for (int k = threadIdx.x; k < n_instr * (int)(sizeof(PredInstr) / 4); k += kBlock)
+    reinterpret_cast<uint32_t*>(s_instr)[k] = reinterpret_cast<const uint32_t*>(prog.instr)[k];
+  for (int k = threadIdx.x; k < n_loads; k += kBlock) s_load[k] = prog.load_instr[k];
+  for (int k = threadIdx.x; k < n_counters; k += kBlock) s_ctr[k] = prog.counters[k];
+  for (int k = threadIdx.x; k < n_bitmaps; k += kBlock) s_bmroot[k] = prog.bitmap_root[k];
+  __syncthreads();
   if (wl) {
     for (int c = 0; c < n_counters; ++c) { S.ct[(c) * 16 + lane] = 0; S.cn[(c) * 16 + lane] = 0; }
   }
@@ -1282,7 +1331,7 @@ __global__ __launch_bounds__(kBlock) void dq_pred_scan(const PredProgram* __rest
   // buffer g & 1, and the loads of atom g + 1 go into the other buffer before atom g is evaluated.
   AtomBuf B0, B1;
   auto issue = [&](int k, int64_t base, AtomBuf& L) {
-    const PredInstr& ins = prog.instr[prog.load_instr[k]];
+    const PredInstr ins = uniform_instr(&s_instr[__builtin_amdgcn_readfirstlane((int)s_load[k])]);
     if (ins.op == PO_ATOM_CMP) {
       pred_load(cols.values[ins.col_a], ins.kind_a, row0, row1, base, lane, L.a);
       if (ins.col_b >= 0) {
@@ -1303,7 +1352,7 @@ __global__ __launch_bounds__(kBlock) void dq_pred_scan(const PredProgram* __rest
     const uint32_t inr = wr >= row1 ? 0u : (wr + 32 <= row1 ? ~0u : ((1u << (row1 - wr)) - 1u));
     int sp = 0, k = 0;
     for (int i = 0; i < n_instr; ++i) {
-      const PredInstr& ins = prog.instr[i];
+      const PredInstr ins = uniform_instr(&s_instr[i]);
       const int op = ins.op;
       if (op == PO_ATOM_CMP || op == PO_ATOM_ISNULL || op == PO_ATOM_NOTNULL || op == PO_ATOM_REGEX) {
         // next atom: the following one of this block, else the first of the next block
@@ -1361,14 +1410,14 @@ __global__ __launch_bounds__(kBlock) void dq_pred_scan(const PredProgram* __rest
     }
     if (wl) {
       for (int c = 0; c < n_counters; ++c) {
-        const PredCounter pc = prog.counters[c];
+        const PredCounter pc = s_ctr[c];
         const uint32_t tw = (pc.where < 0 ? ~0u : S.rt[(pc.where) * 16 + lane]) & inr;
         S.ct[(c) * 16 + lane] += __popc(S.rt[(pc.pred) * 16 + lane] & tw);
         S.cn[(c) * 16 + lane] += __popc(~S.rn[(pc.pred) * 16 + lane] & tw);
       }
       if (wr < n_rows) {
         for (int b = 0; b < n_bitmaps; ++b)
-          reinterpret_cast<uint32_t*>(bm.where_bits[b])[wr >> 5] = S.rt[prog.bitmap_root[b] * 16 + lane] & inr;
+          reinterpret_cast<uint32_t*>(bm.where_bits[b])[wr >> 5] = S.rt[s_bmroot[b] * 16 + lane] & inr;
       }
     }
   }
