@@ -587,12 +587,19 @@ __global__ __launch_bounds__(kBlock) void dq_pair_mfma_scan(const PairGroup* __r
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       const int bit = 8 * (j >> 1) + (j & 1);
-      const bool sel = ((bit < 32 ? wlo : whi) >> (bit & 31)) & 1u;
+      // multiplicative operands, 8 VALU per step: f = selection as 0.0 / 1.0, z = d f, w = (hi ? d : 1),
+      // A = z w (lo: z, hi: z^2), B = w f (lo: f, hi: z) -- exact (products with 0 / 1).  A non-finite d
+      // (selected, or garbage in an unselected slot: inf * 0) makes the tile non-finite -> refold below.
+      const uint32_t sb = ((bit < 32 ? wlo : whi) >> (bit & 31)) & 1u;
+      const double f = (double)sb;
       const double x = gr.x[j];
-      const double z = sel ? x - sh : 0.0;
-      const double av = hi ? z * z : z;
-      const double bv = hi ? z : (sel ? 1.0 : 0.0);
+      const double d = x - sh;
+      const double z = d * f;
+      const double w = hi ? d : 1.0;
+      const double av = z * w;
+      const double bv = w * f;
       acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+      const bool sel = sb != 0u;
       if (!F64 && kind != CK_F64) isum = (int64_t)((uint64_t)isum + (uint64_t)(sel ? gr.raw[j] : 0));
       if (MINMAX) {
         const double xm = sel ? x : qnan;  // v_min / v_max (IEEE mode) skip a NaN operand: unselected, NaN rows
