@@ -1295,12 +1295,16 @@ __device__ __forceinline__ PredInstr uniform_instr(const PredInstr* p) {
 template <bool RX>
 __global__ __launch_bounds__(kBlock) void dq_pred_scan(const PredProgram* __restrict__ prog_g, ScanCols cols,
                                                        ScanBitmaps bm, int64_t n_rows, int64_t rows_per_range,
-                                                       PredPartial* __restrict__ acc) {
+                                                       PredPartial* __restrict__ acc, ColPartial* __restrict__ col_part,
+                                                       uint32_t* __restrict__ hll_acc) {
   extern __shared__ uint32_t pred_lds[];
   __shared__ PredInstr s_instr[kMaxInstr];
   __shared__ int16_t s_load[kMaxInstr];
   __shared__ PredCounter s_ctr[kMaxCounters];
   __shared__ int32_t s_bmroot[kMaxWhere];
+  __shared__ PredHll s_hll[kMaxPredHll];
+  __shared__ int32_t s_regs[kMaxPredHll * 512];          // fused HLL tasks' registers (q = pw - 1, -1 empty)
+  __shared__ unsigned long long s_hcnt[kMaxPredHll];    // their selected-row counts
   const PredProgram& prog = *prog_g;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1314,7 +1318,51 @@ __global__ __launch_bounds__(kBlock) void dq_pred_scan(const PredProgram* __rest
   for (int k = threadIdx.x; k < n_loads; k += kBlock) s_load[k] = prog.load_instr[k];
   for (int k = threadIdx.x; k < n_counters; k += kBlock) s_ctr[k] = prog.counters[k];
   for (int k = threadIdx.x; k < n_bitmaps; k += kBlock) s_bmroot[k] = prog.bitmap_root[k];
+  const int n_hll = prog.n_hll;
+  for (int k = threadIdx.x; k < n_hll * (int)(sizeof(PredHll) / 4); k += kBlock)
+    reinterpret_cast<uint32_t*>(s_hll)[k] = reinterpret_cast<const uint32_t*>(prog.hll)[k];
+  for (int k = threadIdx.x; k < n_hll * 512; k += kBlock) s_regs[k] = -1;
+  if (threadIdx.x < kMaxPredHll) s_hcnt[threadIdx.x] = 0;
   __syncthreads();
+  uint64_t hcnt[kMaxPredHll] = {0, 0, 0, 0};  // wave-uniform selected-row counts of the fused HLL tasks
+  // ApproxCountDistinct of fused column e from an atom's loaded values (L): rows selected = valid and in
+  // range (the word lanes' validity & in-range words, moved to SGPRs per row group); XXH64 as the column
+  // pass (doubleToLongBits: NaN canonical), branch-free register max, the rare low-word rank exactly.
+  auto hll_block = [&](const PredHll& e, int h, const AtomBuf& L, uint32_t inr) {
+    const uint32_t vw = (e.operand ? L.vb : L.va) & inr;
+    int32_t* regs = s_regs + h * 512;
+    int32_t qmin = 0;
+    uint64_t ms[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)vw, 2 * j);
+      const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)vw, 2 * j + 1);
+      const uint64_t m = ((uint64_t)hi << 32) | lo;
+      ms[j] = m;
+      hcnt[h] += (uint64_t)__builtin_popcountll(m);
+      uint64_t b = e.operand ? L.b[j] : L.a[j];
+      HllKey key;
+      if (e.kind == CK_I32) {
+        key = hll_key_int((uint32_t)b);
+      } else {
+        if (e.kind == CK_F64 && __builtin_bit_cast(double, b) != __builtin_bit_cast(double, b)) b = 0x7FF8000000000000ull;
+        key = hll_key_long(b);
+      }
+      const bool sel = lane_bit(m);
+      qmin = min(qmin, sel ? key.q : 0);
+      atomicMax(reinterpret_cast<int32_t*>(reinterpret_cast<char*>(regs) + key.addr), sel ? key.q : -1);
+    }
+    // rare (2^-23 per value): a rank that needs the hash's low word -- redo the selected values exactly
+    if (__builtin_amdgcn_ballot_w64(qmin < 0) != 0) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {  // unrolled: no indexed register arrays
+        if (!lane_bit(ms[j])) continue;
+        uint64_t b = e.operand ? L.b[j] : L.a[j];
+        if (e.kind == CK_F64 && __builtin_bit_cast(double, b) != __builtin_bit_cast(double, b)) b = 0x7FF8000000000000ull;
+        hll_update(regs, e.kind == CK_I32 ? xxh64_int((uint32_t)b) : xxh64_long(b));
+      }
+    }
+  };
   if (wl) {
     for (int c = 0; c < n_counters; ++c) { S.ct[(c) * 16 + lane] = 0; S.cn[(c) * 16 + lane] = 0; }
   }
@@ -1365,6 +1413,17 @@ __global__ __launch_bounds__(kBlock) void dq_pred_scan(const PredProgram* __rest
         if (op == PO_ATOM_CMP) {
           if ((g & 1u) == 0) pred_atom_cmp(ins, B0, lane, wt, wn);
           else pred_atom_cmp(ins, B1, lane, wt, wn);
+#pragma unroll
+          for (int h = 0; h < kMaxPredHll; ++h) {  // uniform; the first atom loading a fused column hashes it
+            if (h >= n_hll) break;
+            const PredHll e = *reinterpret_cast<const PredHll*>(&s_hll[h]);
+            if (__builtin_amdgcn_readfirstlane(e.instr) != i) continue;
+            PredHll eu;
+            eu.operand = __builtin_amdgcn_readfirstlane(e.operand);
+            eu.kind = __builtin_amdgcn_readfirstlane(e.kind);
+            if ((g & 1u) == 0) hll_block(eu, h, B0, inr);
+            else hll_block(eu, h, B1, inr);
+          }
         } else if (RX && op == PO_ATOM_REGEX) {
           const uint32_t va = (g & 1u) ? B1.va : B0.va;
           if (ins.kind_a == CK_UTF8)
@@ -1421,7 +1480,24 @@ __global__ __launch_bounds__(kBlock) void dq_pred_scan(const PredProgram* __rest
       }
     }
   }
+  // fused HLL tasks: counts (range slot 0 of the task's partials; the plan zeroes the others per scan) and
+  // registers -> one of the kHllCopies accumulator copies (device-scope max, order-free)
+  if (lane == 0) {
+#pragma unroll
+    for (int h = 0; h < kMaxPredHll; ++h)
+      if (h < n_hll) atomicAdd(&s_hcnt[h], (unsigned long long)hcnt[h]);
+  }
   __syncthreads();
+  for (int h = 0; h < n_hll; ++h) {
+    const PredHll e = s_hll[h];
+    if (threadIdx.x == 0)
+      atomicAdd(reinterpret_cast<unsigned long long*>(&col_part[(size_t)e.part * kMaxWG].count), s_hcnt[h]);
+    uint32_t* dst = hll_acc + ((size_t)e.hll_slot * kHllCopies + (blockIdx.x % kHllCopies)) * 512;
+    for (int r = threadIdx.x; r < 512; r += kBlock) {
+      const uint32_t v = (uint32_t)(s_regs[h * 512 + r] + 1);
+      if (v > __builtin_nontemporal_load(dst + r)) atomicMax(dst + r, v);
+    }
+  }
   // workgroup partials -> accumulator (integer atomics: order-free)
   if (threadIdx.x < n_counters) {
     const int c = threadIdx.x;
@@ -1523,14 +1599,14 @@ __global__ void dq_init_acc(ColPartial* col_acc, int32_t ncol, CorrPartial* pair
 // host-side launchers (called from dq_plan.cpp)
 // ------------------------------------------------------------------------------------------
 hipError_t launch_pred_scan(const PredProgram* prog, const ScanCols& cols, const ScanBitmaps& bm, int64_t n_rows,
-                            int64_t rows_per_range, int32_t nranges, PredPartial* acc, int32_t lds_bytes, hipStream_t st,
-                            bool has_regex) {
+                            int64_t rows_per_range, int32_t nranges, PredPartial* acc, ColPartial* col_part,
+                            uint32_t* hll_acc, int32_t lds_bytes, hipStream_t st, bool has_regex) {
   if (has_regex)
     hipLaunchKernelGGL(dq_pred_scan<true>, dim3(nranges), dim3(kBlock), (size_t)lds_bytes, st, prog, cols, bm, n_rows,
-                       rows_per_range, acc);
+                       rows_per_range, acc, col_part, hll_acc);
   else
     hipLaunchKernelGGL(dq_pred_scan<false>, dim3(nranges), dim3(kBlock), (size_t)lds_bytes, st, prog, cols, bm, n_rows,
-                       rows_per_range, acc);
+                       rows_per_range, acc, col_part, hll_acc);
   return hipGetLastError();
 }
 
