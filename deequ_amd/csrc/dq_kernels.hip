@@ -1292,7 +1292,9 @@ __device__ __forceinline__ PredInstr uniform_instr(const PredInstr* p) {
 
 // RX: the program holds regex atoms.  Instantiated separately so that the DFA walk's registers (142
 // VGPRs with it, 119 without: 3 vs 4 waves per SIMD) do not cost the plain numeric programs occupancy.
-template <bool RX>
+// HLL: the program hashes fused HLL-only columns (PredProgram::hll); its own instantiation keeps the hash
+// registers out of the plain interpreter (120 vs 141 VGPRs: 4 vs 3 waves per SIMD).
+template <bool RX, bool HLL>
 __global__ __launch_bounds__(kBlock) void dq_pred_scan(const PredProgram* __restrict__ prog_g, ScanCols cols,
                                                        ScanBitmaps bm, int64_t n_rows, int64_t rows_per_range,
                                                        PredPartial* __restrict__ acc, ColPartial* __restrict__ col_part,
@@ -1318,7 +1320,7 @@ __global__ __launch_bounds__(kBlock) void dq_pred_scan(const PredProgram* __rest
   for (int k = threadIdx.x; k < n_loads; k += kBlock) s_load[k] = prog.load_instr[k];
   for (int k = threadIdx.x; k < n_counters; k += kBlock) s_ctr[k] = prog.counters[k];
   for (int k = threadIdx.x; k < n_bitmaps; k += kBlock) s_bmroot[k] = prog.bitmap_root[k];
-  const int n_hll = prog.n_hll;
+  const int n_hll = HLL ? prog.n_hll : 0;
   for (int k = threadIdx.x; k < n_hll * (int)(sizeof(PredHll) / 4); k += kBlock)
     reinterpret_cast<uint32_t*>(s_hll)[k] = reinterpret_cast<const uint32_t*>(prog.hll)[k];
   for (int k = threadIdx.x; k < n_hll * 512; k += kBlock) s_regs[k] = -1;
@@ -1414,7 +1416,7 @@ __global__ __launch_bounds__(kBlock) void dq_pred_scan(const PredProgram* __rest
           if ((g & 1u) == 0) pred_atom_cmp(ins, B0, lane, wt, wn);
           else pred_atom_cmp(ins, B1, lane, wt, wn);
 #pragma unroll
-          for (int h = 0; h < kMaxPredHll; ++h) {  // uniform; the first atom loading a fused column hashes it
+          for (int h = 0; h < (HLL ? kMaxPredHll : 0); ++h) {  // uniform; the first atom loading a fused column hashes it
             if (h >= n_hll) break;
             const PredHll e = *reinterpret_cast<const PredHll*>(&s_hll[h]);
             if (__builtin_amdgcn_readfirstlane(e.instr) != i) continue;
@@ -1600,13 +1602,18 @@ __global__ void dq_init_acc(ColPartial* col_acc, int32_t ncol, CorrPartial* pair
 // ------------------------------------------------------------------------------------------
 hipError_t launch_pred_scan(const PredProgram* prog, const ScanCols& cols, const ScanBitmaps& bm, int64_t n_rows,
                             int64_t rows_per_range, int32_t nranges, PredPartial* acc, ColPartial* col_part,
-                            uint32_t* hll_acc, int32_t lds_bytes, hipStream_t st, bool has_regex) {
-  if (has_regex)
-    hipLaunchKernelGGL(dq_pred_scan<true>, dim3(nranges), dim3(kBlock), (size_t)lds_bytes, st, prog, cols, bm, n_rows,
-                       rows_per_range, acc, col_part, hll_acc);
-  else
-    hipLaunchKernelGGL(dq_pred_scan<false>, dim3(nranges), dim3(kBlock), (size_t)lds_bytes, st, prog, cols, bm, n_rows,
-                       rows_per_range, acc, col_part, hll_acc);
+                            uint32_t* hll_acc, int32_t lds_bytes, hipStream_t st, bool has_regex, bool has_hll) {
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(nranges), dim3(kBlock), (size_t)lds_bytes, st, prog, cols, bm, n_rows, rows_per_range,
+                       acc, col_part, hll_acc);
+  };
+  if (has_regex) {
+    if (has_hll) go(dq_pred_scan<true, true>);
+    else go(dq_pred_scan<true, false>);
+  } else {
+    if (has_hll) go(dq_pred_scan<false, true>);
+    else go(dq_pred_scan<false, false>);
+  }
   return hipGetLastError();
 }
 

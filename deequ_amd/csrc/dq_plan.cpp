@@ -30,7 +30,7 @@ namespace dq {
 
 hipError_t launch_pred_scan(const PredProgram* prog, const ScanCols& cols, const ScanBitmaps& bm, int64_t n_rows,
                             int64_t rows_per_range, int32_t nranges, PredPartial* acc, ColPartial* col_part,
-                            uint32_t* hll_acc, int32_t lds_bytes, hipStream_t st, bool has_regex);
+                            uint32_t* hll_acc, int32_t lds_bytes, hipStream_t st, bool has_regex, bool has_hll);
 hipError_t launch_column_scan(int32_t variant, const ColTask* tasks, int32_t ntasks, int32_t part_base,
                               const ScanCols& cols, const ScanBitmaps& bm, int64_t n_rows, int64_t rows_per_range,
                               int32_t nranges, ColPartial* partials, uint32_t* hll_acc, hipStream_t st);
@@ -1384,7 +1384,7 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
           const int32_t lds = kWaves * 128 * (p->prog.stack_depth + p->prog.n_roots + p->prog.n_counters) +
                               ((p->prog.regex_words * 2 + 15) & ~15);
           return launch_pred_scan(p->d_prog, sc, bm, n_rows, rpr_pred, nr_pred, p->d_pred_acc, p->d_col_part,
-                                  p->d_hll_acc, lds, p->stream, p->prog.regex_words > 0);
+                                  p->d_hll_acc, lds, p->stream, p->prog.regex_words > 0, p->prog.n_hll > 0);
         }))
       return s;
   // fork: variant launches (and the pair pass) round-robin over the plan stream + side streams
