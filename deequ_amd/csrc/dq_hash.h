@@ -41,7 +41,10 @@ DQ_HD uint64_t rotl64(uint64_t x, int r) {
 #endif
 }
 // x * c + a (mod 2^64) for constants c, a, written so the device code is one v_mad_u64_u32 (low
-// product + addend), two v_mul_lo_u32 (cross products) and one add3.
+// product + addend), two v_mul_lo_u32 (cross products) and one add3.  VOL: the asm is volatile, for
+// the string hash's conditional rounds -- LLVM would otherwise hoist a round out of its exec-masked
+// branch, run it in every lane and select the result afterwards.
+template <bool VOL = false>
 DQ_HD uint64_t mul_add_c(uint64_t x, uint64_t c, uint64_t a) {
   const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -50,11 +53,15 @@ DQ_HD uint64_t mul_add_c(uint64_t x, uint64_t c, uint64_t a) {
   // loop-invariant constant; the VOP3 constant bus takes only the SGPR multiplier).
   uint64_t p, carry;
   uint32_t t1, t2;
-  asm("v_mad_u64_u32 %[p], %[cy], %[xl], %[cl], %[a]\n\t"
-      "v_mul_lo_u32 %[t1], %[xl], %[ch]\n\t"
-      "v_mul_lo_u32 %[t2], %[xh], %[cl]"
-      : [p] "=&v"(p), [cy] "=&s"(carry), [t1] "=&v"(t1), [t2] "=&v"(t2)
-      : [xl] "v"(xl), [xh] "v"(xh), [cl] "s"((uint32_t)c), [ch] "s"((uint32_t)(c >> 32)), [a] "v"(a));
+#define DQ_MUL_BODY                                                                                  \
+  ("v_mad_u64_u32 %[p], %[cy], %[xl], %[cl], %[a]\n\t"                                               \
+   "v_mul_lo_u32 %[t1], %[xl], %[ch]\n\t"                                                             \
+   "v_mul_lo_u32 %[t2], %[xh], %[cl]"                                                                \
+   : [p] "=&v"(p), [cy] "=&s"(carry), [t1] "=&v"(t1), [t2] "=&v"(t2)                                 \
+   : [xl] "v"(xl), [xh] "v"(xh), [cl] "s"((uint32_t)c), [ch] "s"((uint32_t)(c >> 32)), [a] "v"(a))
+  if constexpr (VOL) asm volatile DQ_MUL_BODY;
+  else asm DQ_MUL_BODY;
+#undef DQ_MUL_BODY
   (void)carry;
   const uint32_t hi = (uint32_t)(p >> 32) + t1 + t2;
 #else
@@ -65,14 +72,19 @@ DQ_HD uint64_t mul_add_c(uint64_t x, uint64_t c, uint64_t a) {
 }
 
 // x * c (mod 2^64) for a 32-bit x: one v_mad_u64_u32, one v_mul_lo_u32, one add.
+template <bool VOL = false>
 DQ_HD uint64_t mul32_c(uint32_t x, uint64_t c) {
 #if defined(__HIP_DEVICE_COMPILE__)
   uint64_t p, carry;
   uint32_t t;
-  asm("v_mad_u64_u32 %[p], %[cy], %[x], %[cl], 0\n\t"
-      "v_mul_lo_u32 %[t], %[x], %[ch]"
-      : [p] "=&v"(p), [cy] "=&s"(carry), [t] "=&v"(t)
-      : [x] "v"(x), [cl] "s"((uint32_t)c), [ch] "s"((uint32_t)(c >> 32)));
+#define DQ_MUL_BODY                                                                                  \
+  ("v_mad_u64_u32 %[p], %[cy], %[x], %[cl], 0\n\t"                                                   \
+   "v_mul_lo_u32 %[t], %[x], %[ch]"                                                                  \
+   : [p] "=&v"(p), [cy] "=&s"(carry), [t] "=&v"(t)                                                   \
+   : [x] "v"(x), [cl] "s"((uint32_t)c), [ch] "s"((uint32_t)(c >> 32)))
+  if constexpr (VOL) asm volatile DQ_MUL_BODY;
+  else asm DQ_MUL_BODY;
+#undef DQ_MUL_BODY
   (void)carry;
   return ((uint64_t)((uint32_t)(p >> 32) + t) << 32) | (uint32_t)p;
 #else
@@ -106,57 +118,76 @@ DQ_HD uint64_t xxh64_int_head(uint32_t v) {
 DQ_HD uint64_t xxh64_long(uint64_t v) { return fmix_tail(xxh64_long_head(v)); }
 DQ_HD uint64_t xxh64_int(uint32_t v) { return fmix_tail(xxh64_int_head(v)); }
 
-// Predicated 64-bit move dst = cond ? src : dst.  On the device it is one exec-masked v_mov_b64
-// (s_and_saveexec / s_mov exec around it) instead of two v_cndmask_b32.
-#if defined(__HIP_DEVICE_COMPILE__) && defined(DQ_SEL64_CNDMASK)
-__device__ __forceinline__ void sel64(uint64_t& dst, uint64_t src, bool cond) { dst = cond ? src : dst; }
-#elif defined(__HIP_DEVICE_COMPILE__)
-__device__ __forceinline__ void sel64(uint64_t& dst, uint64_t src, bool cond) {
-  uint64_t save;
-  asm("s_and_saveexec_b64 %[s], %[m]\n\t"
-      "v_mov_b64 %[d], %[x]\n\t"
-      "s_mov_b64 exec, %[s]"
-      : [d] "+v"(dst), [s] "=&s"(save)
-      : [x] "v"(src), [m] "s"(__builtin_amdgcn_ballot_w64(cond))
-      : "scc");  // s_and_saveexec writes SCC
-}
-#else
-inline void sel64(uint64_t& dst, uint64_t src, bool cond) { dst = cond ? src : dst; }
-#endif
-
 struct MulP5 {  // b * P5 for a byte b (host; the kernels read a 256-entry LDS table instead)
   DQ_HD uint64_t operator()(uint32_t b) const { return (uint64_t)b * XP5; }
 };
 
-// XXH64.hashUnsafeBytes of a string of len <= 28 bytes, up to fmix_head.  w[0..7]: the string's
-// bytes as little-endian dwords (bytes past len may hold anything; w[7] is never read for a value
-// that matters).  Branch-free: every lane runs 3 stripe rounds, one 4-byte round and 3 byte rounds
-// and keeps the ones its length needs, so a wave of mixed lengths does not diverge.  The 4-byte
-// round's dword w[2 nw] and the byte rounds' dword w[len >> 2] = w[2 nw + (len >> 2 & 1)] ride
-// along the stripe rounds' predicates as one 64-bit pair (no dynamic register indexing).
-// bp(b) = b * P5 for a byte b.
-template <typename BP>
-DQ_HD uint64_t xxh64_short_head(const uint32_t (&w)[8], uint32_t len, BP bp) {
+// XXH64.hashUnsafeBytes of a string of len <= 28 bytes, up to fmix_head, in the pieces the UTF8
+// kernel runs.  w[0..7]: the string's bytes as little-endian dwords (bytes past len may hold anything;
+// w[7] is never read for a value that matters).  Every round is conditional on the lane's length
+// (on the device: an exec-masked branch, skipped by a wave none of whose lanes needs it), so a wave
+// of mixed lengths does not diverge.  The 4-byte round's dword w[2 nw] and the byte rounds' dword
+// w[len >> 2] = w[2 nw + (len >> 2 & 1)] ride along the stripe rounds as one 64-bit pair (no dynamic
+// register indexing).  bp(b) = b * P5 for a byte b.
+
+// One 8-byte round: h ^= rotl(k1 * P2, 31) * P1; h = rotl(h, 27) * P1 + P4.
+template <bool VOL = false>
+DQ_HD uint64_t xxh64_stripe_round(uint64_t h, uint64_t k1) {
+  return mul_add_c<VOL>(rotl64(h ^ mul_add_c<VOL>(rotl64(mul_add_c<VOL>(k1, XP2, 0), 31), XP1, 0), 27), XP1, XP4);
+}
+
+// The first NR stripe rounds (min(NR, len >> 3) of them): returns h and d4p = {w[2 m], w[2 m + 1]},
+// m = min(NR, len >> 3) -- the tail's dwords for len < 8 NR, else the next stripe word.
+template <int NR>
+DQ_HD uint64_t xxh64_stripes(const uint32_t (&w)[8], uint32_t len, uint64_t& d4p) {
   uint64_t h = kSeed + XP5 + (uint64_t)len;
   const uint32_t nw = len >> 3;
-  uint64_t d4p = ((uint64_t)w[1] << 32) | w[0];  // {w[2 nw], w[2 nw + 1]} after the stripe rounds
+  d4p = ((uint64_t)w[1] << 32) | w[0];
 #pragma unroll
-  for (uint32_t k = 0; k < 3; ++k) {
-    const uint64_t k1 = ((uint64_t)w[2 * k + 1] << 32) | w[2 * k];
-    uint64_t hn = h ^ mul_add_c(rotl64(mul_add_c(k1, XP2, 0), 31), XP1, 0);
-    hn = mul_add_c(rotl64(hn, 27), XP1, XP4);
-    const bool take = k < nw;
-    sel64(h, hn, take);
-    sel64(d4p, ((uint64_t)w[2 * k + 3] << 32) | w[2 * k + 2], take);
+  for (uint32_t k = 0; k < (uint32_t)NR; ++k) {
+    if (k < nw) {
+      h = xxh64_stripe_round<true>(h, ((uint64_t)w[2 * k + 1] << 32) | w[2 * k]);
+      d4p = ((uint64_t)w[2 * k + 3] << 32) | w[2 * k + 2];
+    }
   }
-  const uint32_t d4 = (uint32_t)d4p, d4n = (uint32_t)(d4p >> 32);
+  return h;
+}
+
+// After the stripe rounds: the 4-byte round (len & 4) on the low dword of d4p and the (len & 3) byte
+// rounds on the dword after it, up to fmix_head.  The byte rounds' b * P5 are fetched before any round.
+template <typename BP>
+DQ_HD uint64_t xxh64_tail_head(uint64_t h, uint64_t d4p, uint32_t len, BP bp) {
+  const uint32_t d4 = (uint32_t)d4p;
   const bool has4 = (len & 4u) != 0;
-  sel64(h, mul_add_c(rotl64(h ^ mul32_c(d4, XP1), 23), XP2, XP3), has4);
-  const uint32_t db = has4 ? d4n : d4;
+  const uint32_t db = has4 ? (uint32_t)(d4p >> 32) : d4;
   const uint32_t nb = len & 3u;
+  uint64_t kb[3];
 #pragma unroll
-  for (uint32_t j = 0; j < 3; ++j) sel64(h, mul_add_c(rotl64(h ^ bp((db >> (8 * j)) & 0xFFu), 11), XP1, 0), j < nb);
+  for (uint32_t j = 0; j < 3; ++j) kb[j] = bp((db >> (8 * j)) & 0xFFu);
+  if (has4) h = mul_add_c<true>(rotl64(h ^ mul32_c<true>(d4, XP1), 23), XP2, XP3);
+#pragma unroll
+  for (uint32_t j = 0; j < 3; ++j)
+    if (j < nb) h = mul_add_c<true>(rotl64(h ^ kb[j], 11), XP1, 0);
   return fmix_head(h);
+}
+
+template <typename BP>
+DQ_HD uint64_t xxh64_short_head(const uint32_t (&w)[8], uint32_t len, BP bp) {
+  uint64_t d4p;
+  const uint64_t h = xxh64_stripes<3>(w, len, d4p);
+  return xxh64_tail_head(h, d4p, len, bp);
+}
+
+// The same hash split the way the UTF8 kernel runs it when a string of 24..28 bytes is deferred: two
+// stripe rounds in the block loop, then -- packed with other deferred strings -- the third round on
+// {w4, w5} (= d4p after two rounds) and the tail on {w6, w7}.
+template <typename BP>
+DQ_HD uint64_t xxh64_short_head_split(const uint32_t (&w)[8], uint32_t len, BP bp) {
+  uint64_t d4p;
+  uint64_t h = xxh64_stripes<2>(w, len, d4p);
+  if ((len >> 3) < 3) return xxh64_tail_head(h, d4p, len, bp);
+  h = xxh64_stripe_round<true>(h, d4p);
+  return xxh64_tail_head(h, ((uint64_t)w[7] << 32) | w[6], len, bp);
 }
 
 }  // namespace dq

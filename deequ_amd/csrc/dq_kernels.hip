@@ -600,10 +600,19 @@ struct DtCounts {
 // LDS table p5).  A string that is longer, or whose 32-byte window would cross the end of the chunk's
 // bytes, is flagged in an SGPR mask and rehashed by the general XXH64 loop after the block (rare;
 // ds_max is idempotent, so the block's selected rows are simply redone there).
+//
+// Strings of 24..28 bytes (three stripe rounds; 1 in 17 of C5's 8..24-byte strings) are deferred: the
+// block loop runs two stripe rounds for every lane, and a selected lane that needs the third pushes
+// its state (h, the third stripe word, the tail dword, len) into a per-wave LDS queue (SoA, kDefCap
+// slots); every 64 queued strings are finished together (third round, tail, HLL update), so the third
+// round costs one packed pass per 64 strings instead of a masked round in every lane of every row.
+constexpr uint32_t kDefCap = 128;  // < 64 left after a drain + <= 64 pushed per row group
+constexpr int kDefFields = 6;      // h lo, h hi, w4, w5, w6, len
+
 template <typename OffT, bool HLL, bool DT>
 __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint32_t* validity,
                            const uint32_t* mask, int64_t row0, int64_t row1, int64_t n_rows, ColStats& s,
-                           int32_t* regs, const uint64_t* p5) {
+                           int32_t* regs, const uint64_t* p5, uint32_t* dq) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (row0 >= row1) return;
@@ -650,6 +659,33 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
     return W == 4 ? (uint32_t)l : (l > 28 ? 29u : (uint32_t)l);
   };
   const int32_t win3 = win < 0 ? -1 : (win | 3);  // (rel & ~3) <= win  <=>  rel <= win | 3
+  uint32_t qtail = 0;  // wave-uniform: deferred strings in dq[.][0, qtail)
+  // finish deferred strings [0, n): third stripe round, tail, HLL register max (exact rank when the
+  // high word does not carry it)
+  auto drain = [&](uint32_t n) __attribute__((always_inline)) {
+    if ((uint32_t)lane < n) {
+      const uint64_t h = ((uint64_t)dq[1 * kDefCap + lane] << 32) | dq[0 * kDefCap + lane];
+      const uint64_t k1 = ((uint64_t)dq[3 * kDefCap + lane] << 32) | dq[2 * kDefCap + lane];
+      const uint64_t b = xxh64_tail_head(xxh64_stripe_round(h, k1), (uint64_t)dq[4 * kDefCap + lane],
+                                         dq[5 * kDefCap + lane], bp);
+      const HllKey key = hll_key_from_fmix(b);
+      if (key.q >= 0) atomicMax(reinterpret_cast<int32_t*>(reinterpret_cast<char*>(regs) + key.addr), key.q);
+      else hll_update(regs, fmix_tail(b));
+    }
+  };
+  // the first 64, then the rest moves down (< 64 entries; one wave's LDS ops run in order)
+  auto drain_full = [&]() __attribute__((always_inline)) {
+    drain(64u);
+    const uint32_t rest = qtail - 64u;
+    if ((uint32_t)lane < rest) {
+      uint32_t v[kDefFields];
+#pragma unroll
+      for (int f = 0; f < kDefFields; ++f) v[f] = dq[f * kDefCap + 64 + lane];
+#pragma unroll
+      for (int f = 0; f < kDefFields; ++f) dq[f * kDefCap + lane] = v[f];
+    }
+    qtail = rest;
+  };
   for (int64_t blk = row0; blk < row1; blk += kRowsPerIter) {
     const int64_t base = blk + (int64_t)wave * 512;
     const bool full = blk + kRowsPerIter <= row1;
@@ -681,9 +717,25 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
       wv[7] = d[7];  // only ever feeds the unused half of the tail pair for len >= 24
       if constexpr (DT) dtc.add(dt_class_short(wv, len_of(j), lane_bit(m[j])), lane_bit(m[j]));
       if constexpr (HLL) {
-        const HllKey key = hll_key_from_fmix(xxh64_short_head(wv, len_of(j), bp));
+        uint64_t d4p;
+        const uint64_t h2 = xxh64_stripes<2>(wv, len_of(j), d4p);
+        const uint64_t dm = m[j] & __builtin_amdgcn_ballot_w64(len_of(j) >= 24u);  // needs the third round
+        if (dm != 0) {
+          const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(dm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dm, qtail));
+          if (lane_bit(dm)) {
+            dq[0 * kDefCap + pos] = (uint32_t)h2;
+            dq[1 * kDefCap + pos] = (uint32_t)(h2 >> 32);
+            dq[2 * kDefCap + pos] = (uint32_t)d4p;
+            dq[3 * kDefCap + pos] = (uint32_t)(d4p >> 32);
+            dq[4 * kDefCap + pos] = wv[6];
+            dq[5 * kDefCap + pos] = len_of(j);
+          }
+          qtail += (uint32_t)__builtin_popcountll(dm);
+        }
+        const HllKey key = hll_key_from_fmix(xxh64_tail_head(h2, d4p, len_of(j), bp));
         qmin = min(qmin, key.q);
-        if (lane_bit(m[j])) atomicMax(reinterpret_cast<int32_t*>(reinterpret_cast<char*>(regs) + key.addr), key.q);
+        if (lane_bit(m[j] & ~dm)) atomicMax(reinterpret_cast<int32_t*>(reinterpret_cast<char*>(regs) + key.addr), key.q);
+        if (qtail >= 64u) drain_full();
       }
       load_offsets(blk + kRowsPerIter, j);  // unconditional: past row1 the descriptor reads 0
       a = an;
@@ -708,6 +760,9 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
       }
       qmin = 0;
     }
+  }
+  if constexpr (HLL) {
+    if (qtail != 0) drain(qtail);
   }
   if (lane == 0) s.count += cnt_w;
   if constexpr (DT) dtc.flush(s);
@@ -761,7 +816,7 @@ __device__ void run_numeric(const ColTask& t, const ScanCols& cols, const ScanBi
 template <int V>
 __device__ __forceinline__ void run_variant(const ColTask& t, const ScanCols& cols, const uint32_t* mask, int64_t row0,
                                             int64_t row1, int64_t n_rows, ColStats& s, int32_t* regs,
-                                            const uint64_t* p5) {
+                                            const uint64_t* p5, uint32_t* dq) {
   const void* v = cols.values[t.col];
   const uint32_t* val = cols.validity[t.col];
   if constexpr (V == CV_VALIDITY) validity_range(val, mask, row0, row1, s);
@@ -778,15 +833,23 @@ __device__ __forceinline__ void run_variant(const ColTask& t, const ScanCols& co
   else if constexpr (V == CV_UTF8_H || V == CV_UTF8_D || V == CV_UTF8_HD)
     utf8_range<int32_t, V != CV_UTF8_D, V != CV_UTF8_H>(
         reinterpret_cast<const uint8_t*>(v), reinterpret_cast<const int32_t*>(cols.offsets[t.col]), val, mask, row0,
-        row1, n_rows, s, regs, p5);
+        row1, n_rows, s, regs, p5, dq);
   else
     utf8_range<int64_t, V != CV_LUTF8_D, V != CV_LUTF8_H>(
         reinterpret_cast<const uint8_t*>(v), reinterpret_cast<const int64_t*>(cols.offsets[t.col]), val, mask, row0,
-        row1, n_rows, s, regs, p5);
+        row1, n_rows, s, regs, p5, dq);
 }
 
+// Minimum waves per SIMD the register allocator must leave room for (0 = no constraint); a
+// diagnostic build switch for the issue-bound string hash variants.
+#ifndef DQ_STR_WAVES
+#define DQ_STR_WAVES 0
+#endif
 template <int V>
-__global__ __launch_bounds__(kBlock) void dq_column_scan(const ColTask* __restrict__ tasks, int32_t ntasks,
+constexpr int kMinWaves = V == CV_UTF8_H && DQ_STR_WAVES > 0 ? DQ_STR_WAVES : 1;
+
+template <int V>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kMinWaves<V>))) void dq_column_scan(const ColTask* __restrict__ tasks, int32_t ntasks,
                                                          int32_t part_base, ScanCols cols, ScanBitmaps bm,
                                                          int64_t n_rows, int64_t rows_per_range,
                                                          ColPartial* __restrict__ partials,
@@ -796,6 +859,7 @@ __global__ __launch_bounds__(kBlock) void dq_column_scan(const ColTask* __restri
   constexpr bool kStr = V == CV_UTF8_H || V == CV_LUTF8_H || V == CV_UTF8_HD || V == CV_LUTF8_HD;
   __shared__ int32_t regs[kHll ? 512 : 1];  // q = pw - 1, -1 = empty (see hll_q_exact)
   __shared__ uint64_t p5[kStr ? 256 : 1];   // b * P5 for the byte rounds of the string hash
+  __shared__ uint32_t dfq[kStr ? kWaves * kDefFields * kDefCap : 1];  // deferred 24..28-byte strings
   __shared__ ColStats red[kWaves];
   const int32_t ti = blockIdx.x % ntasks;
   const int32_t range = blockIdx.x / ntasks;
@@ -811,7 +875,8 @@ __global__ __launch_bounds__(kBlock) void dq_column_scan(const ColTask* __restri
   ColStats s;
   stats_init(s);
   const uint32_t* mask = t.where >= 0 ? reinterpret_cast<const uint32_t*>(bm.where_bits[t.where]) : nullptr;
-  run_variant<V>(t, cols, mask, row0, row1, n_rows, s, regs, p5);
+  run_variant<V>(t, cols, mask, row0, row1, n_rows, s, regs, p5,
+                 dfq + (kStr ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * kDefFields * kDefCap : 0));
   block_reduce_store(s, partials + (size_t)(part_base + ti) * kMaxWG + range, red);
   if constexpr (kHll) {
     // registers only grow: merge into the plan accumulator with device-scope atomicMax, skipping

@@ -1,6 +1,7 @@
 // Host build of the kernels' XXH64 formulations (deequ_amd/csrc/dq_hash.h), driven by
 // tests/test_hash_formulation.py against the golden vectors.  Reads "len hex" lines on stdin and
-// prints the signed hash of fmix_tail(xxh64_short_head()) for every byte alignment 0..3 of the string,
+// prints the signed hash of fmix_tail(xxh64_short_head()) and of the split (deferred-round) form
+// xxh64_short_head_split() for every byte alignment 0..3 of the string,
 // fed as the UTF8 kernel feeds it: two aligned 16-byte loads realigned with alignbit, and garbage
 // (0xA5) in the bytes past the string.
 #include <cstdio>
@@ -26,7 +27,8 @@ int main() {
       for (int k = 0; k < 7; ++k) w[k] = dq::alignbit32(d[k + 1], d[k], sh);
       w[7] = d[7];
       const uint64_t h = dq::fmix_tail(dq::xxh64_short_head(w, (uint32_t)len, dq::MulP5{}));
-      std::printf("%lld%c", (long long)h, align == 3 ? '\n' : ' ');
+      const uint64_t hs = dq::fmix_tail(dq::xxh64_short_head_split(w, (uint32_t)len, dq::MulP5{}));
+      std::printf("%lld %lld%c", (long long)h, (long long)hs, align == 3 ? '\n' : ' ');
     }
   }
   std::printf("LONG %lld INT %lld\n", (long long)dq::xxh64_long(42u), (long long)dq::xxh64_int(7u));

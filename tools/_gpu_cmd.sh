@@ -1,4 +1,8 @@
-cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export TMPDIR=/tmp && \
-timeout -k 10 600 python tools/sweep.py > gpurun_out/sweep.log 2>&1; echo sweep rc=$?; cat gpurun_out/sweep.log | grep case; \
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof1 -o prof --output-format csv -- python bench.py --rows 125000000 --steps 3 --warmup 1 --cpu-sample 0 > gpurun_out/bench_prof.json 2>&1; echo prof rc=$?; \
-SKIP_BENCH=1 bash tools/gpu_check.sh
+set -o pipefail
+cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/t2.log 2>&1; rc=$?; tail -3 gpurun_out/t2.log; [ $rc -eq 0 ] || exit $rc
+for v in A B C; do
+  if [ $v = B ]; then L=""; else L=$PWD/build_variants/lib$v.so; fi
+  DQ_LIB_PATH=$L timeout -k 10 200 python -u tools/sweep.py 125000000 utf8x4_hll > gpurun_out/sw_$v.log 2>&1 || exit $?
+  echo "$v: $(tail -1 gpurun_out/sw_$v.log)"
+done
