@@ -450,21 +450,49 @@ hipError_t launch_pair_lane_scan(const PairWaveTask* tasks, int32_t ntasks, cons
 // VALU kernel above (per-task column duplication, SALU slot control) and the LDS tile + column pass pair.
 // ================================================================================================
 typedef double dq_d4 __attribute__((ext_vector_type(4)));
+#ifndef DQ_PAIR_SLOTS
+#define DQ_PAIR_SLOTS 3
+#endif
+constexpr int kStageSlots = DQ_PAIR_SLOTS;  // LDS-DMA group slots per wave (kStageSlots - 1 groups in flight beside the fold)
 
 // F64: every column of every group is fp64; MINMAX: a fused moments task feeds Minimum / Maximum
-template <bool F64, bool MINMAX>
-__global__ __launch_bounds__(kBlock) void dq_pair_mfma_scan(const PairGroup* __restrict__ groups, int32_t ngroups,
+// GLDS (with F64): full groups staged through LDS by DMA (every column 16-byte aligned: the host checks)
+template <bool F64, bool MINMAX, bool GLDS = false>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GLDS ? 3 : 1))) void dq_pair_mfma_scan(const PairGroup* __restrict__ groups, int32_t ngroups,
                                                             ScanCols cols, ScanBitmaps bm, const uint32_t* ones,
                                                             int64_t n_rows, int64_t rows_per_range, int32_t nranges,
                                                             CorrPartial* __restrict__ pair_part,
                                                             ColPartial* __restrict__ col_part) {
   __shared__ double shift_s[kTileCols];
-  __shared__ double tile[kWaves][16][17];  // the waves' C tiles (+1: bank spread)
-  __shared__ uint32_t cnt_s[kWaves][kTileCols][kTileCols];
-  __shared__ int64_t nan_s[kWaves][kTileCols], pinf_s[kWaves][kTileCols], ninf_s[kWaves][kTileCols];
-  __shared__ int64_t isum_s[kWaves][kTileCols];
-  __shared__ double lo_s[kWaves][kTileCols], hi_s[kWaves][kTileCols];
-  __shared__ uint64_t poison_s[kWaves];
+  // the workgroup merge's arrays share LDS with the DMA stage slots (GLDS: used only after every wave has
+  // left its group loop -- a barrier separates them)
+  struct MergeLds {
+    double tile[kWaves][16][17];  // the waves' C tiles (+1: bank spread)
+    uint32_t cnt_s[kWaves][kTileCols][kTileCols];
+    int64_t nan_s[kWaves][kTileCols], pinf_s[kWaves][kTileCols], ninf_s[kWaves][kTileCols];
+    int64_t isum_s[kWaves][kTileCols];
+    double lo_s[kWaves][kTileCols], hi_s[kWaves][kTileCols];
+    uint64_t poison_s[kWaves];
+  };
+  struct StageLds {
+    double x[kWaves][kStageSlots][kTileCols * 64];  // [column][row] of a 64-row group
+    uint32_t w[kWaves][kStageSlots][64];             // selection words (lanes 0..17 of the DMA)
+  };
+  constexpr size_t kSmem = GLDS && sizeof(StageLds) > sizeof(MergeLds) ? sizeof(StageLds) : sizeof(MergeLds);
+  __shared__ __attribute__((aligned(16))) char smem[kSmem];
+  MergeLds& ml = *reinterpret_cast<MergeLds*>(smem);
+  StageLds& sl = *reinterpret_cast<StageLds*>(smem);
+  auto& tile = ml.tile;
+  auto& cnt_s = ml.cnt_s;
+  auto& nan_s = ml.nan_s;
+  auto& pinf_s = ml.pinf_s;
+  auto& ninf_s = ml.ninf_s;
+  auto& isum_s = ml.isum_s;
+  auto& lo_s = ml.lo_s;
+  auto& hi_s = ml.hi_s;
+  auto& poison_s = ml.poison_s;
+  auto& stage_x = sl.x;
+  auto& stage_w = sl.w;
   const int gi = blockIdx.x % ngroups, range = blockIdx.x / ngroups;
   const PairGroup& g = groups[gi];
   const int nc = g.ncols;
@@ -525,13 +553,17 @@ __global__ __launch_bounds__(kBlock) void dq_pair_mfma_scan(const PairGroup* __r
   gu32 where_v = (gu32)where;
   asm volatile("" : "+v"(where_v));
 
-  dq_d4 acc = {0.0, 0.0, 0.0, 0.0};
+  // two tiles, even / odd steps: consecutive MFMAs do not wait for each other's accumulator
+  dq_d4 acc = {0.0, 0.0, 0.0, 0.0}, accb = {0.0, 0.0, 0.0, 0.0};
+  // w = hi ? d : 1 as one FMA: d * hd + omh (exact for finite d)
+  const double hd = hi ? 1.0 : 0.0, omh = hi ? 0.0 : 1.0;
   uint32_t cnt = 0;           // rows selected in both a and b (lane (a, b)); a == b: the column count
   bool poison = false;        // pair (a, b) met a selected NaN / +-inf of column a in a row selected in b
   int64_t nanv = 0, pinfv = 0, ninfv = 0, isum = 0;  // column c's rows of slot rs (lanes with hi == 0)
   double lo = __builtin_bit_cast(double, 0x7FF0000000000000ull), hiv = __builtin_bit_cast(double, 0xFFF0000000000000ull);
   const double qnan = __builtin_bit_cast(double, 0x7FF8000000000000ull);
 
+  typedef double d2 __attribute__((ext_vector_type(2)));
   struct Grp {
     double x[16];
     int64_t raw[F64 ? 1 : 16];
@@ -550,7 +582,6 @@ __global__ __launch_bounds__(kBlock) void dq_pair_mfma_scan(const PairGroup* __r
     gr.wb[1] = two ? vb[w + 1] : 0u;
     gr.wm[1] = two ? where_v[w + 1] : 0u;
     if (VEC && !TAIL) {
-      typedef double d2 __attribute__((ext_vector_type(2)));
       const d2* p = reinterpret_cast<const d2*>(colp) + ((base >> 1) + rs);
 #pragma unroll
       for (int t = 0; t < 8; ++t) {
@@ -574,53 +605,85 @@ __global__ __launch_bounds__(kBlock) void dq_pair_mfma_scan(const PairGroup* __r
   // group proves there was none; otherwise (rare) the group is folded again from the saved tile with the
   // non-finite values kept out, counted, and their pairs poisoned.  Min / max / integral sums are taken
   // once, in the fast path (min / max see the same values either way; NaN is skipped by v_min / v_max).
-  auto fold = [&](int64_t base, const Grp& gr, auto tail_tag) __attribute__((always_inline)) {
+  // wa_raw / wb_raw / wm_raw: the 64-row selection words (column a, column b, `where`); xpair(t): this
+  // lane's values of steps 2 t and 2 t + 1; rawv(j): the integral value of step j (!F64)
+  auto fold = [&](int64_t base, uint64_t wa_raw, uint64_t wb_raw, uint64_t wm_raw, auto xpair, auto rawv,
+                  auto tail_tag) __attribute__((always_inline)) {
     constexpr bool TAIL = decltype(tail_tag)::value;
-    uint64_t wm = ((uint64_t)gr.wm[1] << 32) | gr.wm[0];
+    uint64_t wm = wm_raw;
     if (TAIL && base + 64 > row1) wm &= (1ull << (row1 - base)) - 1ull;
-    const uint64_t wa = live ? (((uint64_t)gr.wa[1] << 32) | gr.wa[0]) & wm : 0ull;
-    const uint64_t wb = live_b ? (((uint64_t)gr.wb[1] << 32) | gr.wb[0]) & wm : 0ull;
+    const uint64_t wa = live ? wa_raw & wm : 0ull;
+    const uint64_t wb = live_b ? wb_raw & wm : 0ull;
     cnt += (uint32_t)__builtin_popcountll(wa & wb);
     const uint64_t wr = wa >> (2 * rs);  // step j's bit: 8 (j >> 1) + (j & 1)
     const uint32_t wlo = (uint32_t)wr, whi = (uint32_t)(wr >> 32);
-    const dq_d4 acc0 = acc;
+    const dq_d4 acc0 = acc, accb0 = accb;
+    // Operands are prepared kPrepBatch steps at a time and their MFMAs issued after them as one batch: a
+    // step's VALU chain (bfe -> cvt -> mul -> mul) interleaved 1:1 with the MFMAs leaves every f64 result's
+    // latency exposed (the other wave's MFMA cannot cover it: no co-issue), batched the chains overlap.
+#ifndef DQ_PAIR_BATCH
+#define DQ_PAIR_BATCH 4
+#endif
+    constexpr int kPrepBatch = DQ_PAIR_BATCH;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int bit = 8 * (j >> 1) + (j & 1);
-      // multiplicative operands, 8 VALU per step: f = selection as 0.0 / 1.0, z = d f, w = (hi ? d : 1),
-      // A = z w (lo: z, hi: z^2), B = w f (lo: f, hi: z) -- exact (products with 0 / 1).  A non-finite d
-      // (selected, or garbage in an unselected slot: inf * 0) makes the tile non-finite -> refold below.
-      const uint32_t sb = ((bit < 32 ? wlo : whi) >> (bit & 31)) & 1u;
-      const double f = (double)sb;
-      const double x = gr.x[j];
-      const double d = x - sh;
-      const double z = d * f;
-      const double w = hi ? d : 1.0;
-      const double av = z * w;
-      const double bv = w * f;
-      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
-      const bool sel = sb != 0u;
-      if (!F64 && kind != CK_F64) isum = (int64_t)((uint64_t)isum + (uint64_t)(sel ? gr.raw[j] : 0));
-      if (MINMAX) {
-        const double xm = sel ? x : qnan;  // v_min / v_max (IEEE mode) skip a NaN operand: unselected, NaN rows
-        lo = hw_min(lo, xm);
-        hiv = hw_max(hiv, xm);
+    for (int j0 = 0; j0 < 16; j0 += kPrepBatch) {
+      double av[kPrepBatch], bv[kPrepBatch], xb[kPrepBatch];
+#pragma unroll
+      for (int t = 0; t < kPrepBatch / 2; ++t) {
+        const d2 v = xpair(j0 / 2 + t);
+        xb[2 * t] = v.x;
+        xb[2 * t + 1] = v.y;
       }
+#pragma unroll
+      for (int jj = 0; jj < kPrepBatch; ++jj) {
+        const int j = j0 + jj;
+        const int bit = 8 * (j >> 1) + (j & 1);
+        // multiplicative operands, 7 VALU per step: f = selection as 0.0 / 1.0, z = d f, w = (hi ? d : 1),
+        // A = z w (lo: z, hi: z^2), B = w f (lo: f, hi: z) -- exact (products with 0 / 1).  A non-finite d
+        // (selected, or garbage in an unselected slot: inf * 0) makes the tile non-finite -> refold below.
+        const uint32_t sb = ((bit < 32 ? wlo : whi) >> (bit & 31)) & 1u;
+        // (f built from the bit with integer ops instead of v_cvt_f64_u32: 2.09 vs 2.04 ms per 125 M rows)
+        const double f = (double)sb;
+        const double x = xb[jj];
+        const double d = x - sh;
+        const double z = d * f;
+        const double w = __builtin_fma(d, hd, omh);
+        av[jj] = z * w;
+        bv[jj] = w * f;
+        const bool sel = sb != 0u;
+        if (!F64 && kind != CK_F64) isum = (int64_t)((uint64_t)isum + (uint64_t)(sel ? rawv(j) : 0));
+        if (MINMAX) {
+          const double xm = sel ? x : qnan;  // v_min / v_max (IEEE mode) skip a NaN operand: unselected, NaN rows
+          lo = hw_min(lo, xm);
+          hiv = hw_max(hiv, xm);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int jj = 0; jj < kPrepBatch; ++jj) {
+        if (jj & 1) accb = __builtin_amdgcn_mfma_f64_16x16x4f64(av[jj], bv[jj], accb, 0, 0, 0);
+        else acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[jj], bv[jj], acc, 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
     }
     const bool tile_fin = __builtin_isfinite(acc[0]) && __builtin_isfinite(acc[1]) && __builtin_isfinite(acc[2]) &&
-                          __builtin_isfinite(acc[3]);
+                          __builtin_isfinite(acc[3]) && __builtin_isfinite(accb[0]) && __builtin_isfinite(accb[1]) &&
+                          __builtin_isfinite(accb[2]) && __builtin_isfinite(accb[3]);
     if (__builtin_amdgcn_ballot_w64(!tile_fin) != 0) {  // rare (unrolled: no indexed register arrays)
       acc = acc0;
+      accb = accb0;
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
         const int bit = 8 * (j >> 1) + (j & 1);
         const bool sel = ((bit < 32 ? wlo : whi) >> (bit & 31)) & 1u;
-        const double x = gr.x[j];
+        const d2 xp = xpair(j >> 1);
+        const double x = (j & 1) ? xp.y : xp.x;
         const bool fin = __builtin_isfinite(x);
         const double z = sel && fin ? x - sh : 0.0;
         const double av = hi ? z * z : z;
         const double bv = hi ? z : (sel ? 1.0 : 0.0);
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+        if (j & 1) accb = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, accb, 0, 0, 0);
+        else acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
         const bool nf = sel && !fin;
         const uint64_t m = __builtin_amdgcn_ballot_w64(nf && !hi);  // lane a + 16 rs: column a, row slot rs
         if (m == 0) continue;
@@ -637,6 +700,12 @@ __global__ __launch_bounds__(kBlock) void dq_pair_mfma_scan(const PairGroup* __r
     }
   };
 
+  auto fold_regs = [&](int64_t base, const Grp& gr, auto tail_tag) __attribute__((always_inline)) {
+    fold(base, ((uint64_t)gr.wa[1] << 32) | gr.wa[0], ((uint64_t)gr.wb[1] << 32) | gr.wb[0],
+         ((uint64_t)gr.wm[1] << 32) | gr.wm[0], [&](int t) { return d2{gr.x[2 * t], gr.x[2 * t + 1]}; },
+         [&](int j) { return gr.raw[F64 ? 0 : j]; }, tail_tag);
+  };
+
   // full groups, software-pipelined over two buffers: the next group's loads fly while this one folds.  The
   // prefetch is unconditional (the last one re-reads the current group) so every path into a fold has the
   // same loads in flight and the wait before it stays a partial vmcnt, not a drain.
@@ -647,28 +716,95 @@ __global__ __launch_bounds__(kBlock) void dq_pair_mfma_scan(const PairGroup* __r
     Grp b0, b1;
     if (base >= full_end) return;
     load(base, b0, vec_tag, std::false_type{});
+    // sched_barrier: the scheduler would otherwise sink the prefetch behind most of the fold's MFMAs,
+    // leaving only the last steps to cover its latency
     while (true) {
       load(base + kStride < full_end ? base + kStride : base, b1, vec_tag, std::false_type{});
-      fold(base, b0, std::false_type{});
+      __builtin_amdgcn_sched_barrier(0);
+      fold_regs(base, b0, std::false_type{});
       base += kStride;
       if (base >= full_end) break;
       load(base + kStride < full_end ? base + kStride : base, b0, vec_tag, std::false_type{});
-      fold(base, b1, std::false_type{});
+      __builtin_amdgcn_sched_barrier(0);
+      fold_regs(base, b1, std::false_type{});
       base += kStride;
       if (base >= full_end) break;
     }
   };
-  if (vec16) run_full(std::true_type{});
+  // LDS-DMA staged full groups (aligned fp64 columns): a group's 8 columns x 64 rows go HBM -> LDS with
+  // 4 global_load_lds_dwordx4 (lane l: column 2 k + (l >> 5), rows 2 (l & 31), +1 -> LDS [column][row],
+  // lane-linear) and its selection words with one global_load_lds_dword (lanes 0..15: 2 words of each
+  // column's validity, 16..17: `where`).  No VGPRs hold a group in flight, so the wave keeps kStageSlots - 1
+  // groups in flight beside the fold at the occupancy of the fold alone.  Only this wave reads its slots.
+  // The DMAs are asm (hipcc does not count them): the waits are explicit vmcnt, with no other vector
+  // memory instruction in the loop.
+  auto run_glds = [&]() __attribute__((always_inline)) {
+    if (base >= full_end) return;
+    const char* srcx[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int cc = 2 * k + (lane >> 5);
+      srcx[k] = reinterpret_cast<const char*>(cols.values[g.cols[cc < nc ? cc : 0]]) + (size_t)(2 * (lane & 31)) * 8;
+    }
+    const uint32_t* srcw;
+    {
+      const int cc = lane < 16 ? lane >> 1 : 0;
+      const uint32_t* vv = cols.validity[g.cols[cc < nc ? cc : 0]];
+      srcw = lane < 16 ? (vv ? vv : ones) + (lane & 1) : (lane < 18 ? where + (lane - 16) : ones);
+    }
+    auto stage = [&](int64_t gb, int slot) __attribute__((always_inline)) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const char* src = srcx[k] + gb * 8;
+        const uint32_t dst = (uint32_t)(uintptr_t)&stage_x[wave][slot][k * 128];
+        uint32_t keep;
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
+      }
+      const uint32_t* srcb = srcw + (gb >> 5);
+      const uint32_t dstb = (uint32_t)(uintptr_t)&stage_w[wave][slot][0];
+      uint32_t keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(srcb), "s"(dstb) : "memory");
+    };
+    constexpr int D = kStageSlots - 1;  // groups in flight beside the fold
+    auto wait_dma = [](int groups_after) __attribute__((always_inline)) {  // 5 DMAs per group
+      if (groups_after >= 2) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+      else if (groups_after == 1) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    };
+    static_assert(D >= 1 && D <= 2, "wait_dma covers up to 2 groups in flight");
+    int slot = 0;
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+      if (d == 0 || base + d * kStride < full_end) stage(base + d * kStride, d);
+    while (true) {
+      const int64_t ahead = base + D * kStride;
+      if (ahead < full_end) stage(ahead, slot + D < kStageSlots ? slot + D : slot + D - kStageSlots);
+      const int64_t left = (full_end - base - 1) / kStride;  // this wave's groups after the current one
+      wait_dma(left < D ? (int)left : D);
+      const uint64_t* wl = reinterpret_cast<const uint64_t*>(&stage_w[wave][slot][0]);
+      const d2* xs = reinterpret_cast<const d2*>(&stage_x[wave][slot][c * 64 + 2 * rs]);
+      fold(base, wl[c], wl[pb], wl[8], [&](int t) { return xs[4 * t]; }, [&](int) { return (int64_t)0; },
+           std::false_type{});
+      base += kStride;
+      slot = slot + 1 < kStageSlots ? slot + 1 : 0;
+      if (base >= full_end) break;
+    }
+  };
+  if constexpr (GLDS && F64) run_glds();
+  else if (vec16) run_full(std::true_type{});
   else run_full(std::false_type{});
   if (base < row1) {
     Grp bt;
     load(base, bt, std::false_type{}, std::true_type{});
-    fold(base, bt, std::true_type{});
+    fold_regs(base, bt, std::true_type{});
   }
 
   // ---- workgroup merge (fixed order: waves 0..3) and the per-range partials
+  if constexpr (GLDS) __syncthreads();  // every wave is done with the stage slots the merge arrays overlay
 #pragma unroll
-  for (int r = 0; r < 4; ++r) tile[wave][(lane >> 4) + 4 * r][lane & 15] = acc[r];
+  for (int r = 0; r < 4; ++r) tile[wave][(lane >> 4) + 4 * r][lane & 15] = acc[r] + accb[r];
   cnt_s[wave][lane >> 3][lane & 7] = cnt;  // [b][a]
   {
     const uint64_t pz = __builtin_amdgcn_ballot_w64(poison);
@@ -771,13 +907,16 @@ __global__ __launch_bounds__(kBlock) void dq_pair_mfma_scan(const PairGroup* __r
 hipError_t launch_pair_mfma_scan(const PairGroup* groups, int32_t ngroups, const ScanCols& cols,
                                  const ScanBitmaps& bm, const uint32_t* ones, int64_t n_rows, int64_t rows_per_range,
                                  int32_t nranges, CorrPartial* pair_part, ColPartial* col_part, bool all_f64,
-                                 bool minmax, hipStream_t st) {
+                                 bool minmax, bool glds, hipStream_t st) {
   const uint32_t blocks = (uint32_t)ngroups * (uint32_t)nranges;
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(kBlock), 0, st, groups, ngroups, cols, bm, ones, n_rows, rows_per_range,
                        nranges, pair_part, col_part);
   };
-  if (all_f64) {
+  if (all_f64 && glds) {
+    if (minmax) go(dq_pair_mfma_scan<true, true, true>);
+    else go(dq_pair_mfma_scan<true, false, true>);
+  } else if (all_f64) {
     if (minmax) go(dq_pair_mfma_scan<true, true>);
     else go(dq_pair_mfma_scan<true, false>);
   } else {

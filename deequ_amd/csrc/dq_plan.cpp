@@ -44,7 +44,7 @@ hipError_t launch_pair_lane_scan(const PairWaveTask* tasks, int32_t ntasks, cons
 hipError_t launch_pair_mfma_scan(const PairGroup* groups, int32_t ngroups, const ScanCols& cols,
                                  const ScanBitmaps& bm, const uint32_t* ones, int64_t n_rows, int64_t rows_per_range,
                                  int32_t nranges, CorrPartial* pair_part, ColPartial* col_part, bool all_f64,
-                                 bool minmax, hipStream_t st);
+                                 bool minmax, bool glds, hipStream_t st);
 hipError_t launch_finalize(int32_t ncol, int32_t nranges_col, const ColPartial* col_part, ColPartial* col_acc,
                            int32_t npair, int32_t nranges_pair, const CorrPartial* pair_part, CorrPartial* pair_acc,
                            int32_t has_pred, int32_t nranges_pred, const PredPartial* pred_part, PredPartial* pred_acc,
@@ -1413,10 +1413,15 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
   }
   if (!p->mfma_groups.empty()) {
     hipStream_t st = stream_for(li++);
+    // LDS-DMA staging needs every column of every group 16-byte aligned (a table sliced at an odd row is not)
+    static const bool glds_env = !(std::getenv("DQ_PAIR_GLDS") && std::getenv("DQ_PAIR_GLDS")[0] == '0');
+    bool glds = glds_env && p->mfma_all_f64;
+    for (const PairGroup& g : p->mfma_groups)
+      for (int c = 0; c < g.ncols && glds; ++c) glds = ((uintptr_t)sc.values[g.cols[c]] & 15u) == 0;
     if (dq_status s = timed(p, 2, st, [&] {
           return launch_pair_mfma_scan(p->d_mfma_groups, (int32_t)p->mfma_groups.size(), sc, bm, p->d_ones, n_rows,
                                        rpr_col, nr_col, p->d_pair_part, p->d_col_part, p->mfma_all_f64,
-                                       p->mfma_minmax, st);
+                                       p->mfma_minmax, glds, st);
         }))
       return s;
   }
