@@ -1413,9 +1413,10 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
   }
   if (!p->mfma_groups.empty()) {
     hipStream_t st = stream_for(li++);
-    // LDS-DMA staging needs every column of every group 16-byte aligned (a table sliced at an odd row is not)
-    static const bool glds_env = !(std::getenv("DQ_PAIR_GLDS") && std::getenv("DQ_PAIR_GLDS")[0] == '0');
-    bool glds = glds_env && p->mfma_all_f64;
+    // LDS-DMA staging of all-fp64 groups (dq_scan already requires 16-byte aligned value buffers; checked
+    // again here since the kernel's DMA assumes it); DQ_PAIR_GLDS=0 selects the register-staged kernel
+    const char* glds_env = std::getenv("DQ_PAIR_GLDS");
+    bool glds = !(glds_env && glds_env[0] == '0') && p->mfma_all_f64;
     for (const PairGroup& g : p->mfma_groups)
       for (int c = 0; c < g.ncols && glds; ++c) glds = ((uintptr_t)sc.values[g.cols[c]] & 15u) == 0;
     if (dq_status s = timed(p, 2, st, [&] {

@@ -166,3 +166,44 @@ def test_c4_complete_pair_set_deterministic(dq):
     an += [dq.Mean(c) for c in names] + [dq.StandardDeviation(c) for c in names]
     runs = [[bytes(s) for s in scan_results(t, an)] for _ in range(2)]
     assert runs[0] == runs[1]
+
+
+def _f64_only(n, seed, special):
+    rng = np.random.default_rng(seed)
+    z0 = rng.normal(size=n)
+    cols = {}
+    for c in range(8):
+        cols[f"f{c}"] = ("f64", 0.5 * z0 + rng.normal(size=n) + 10.0 * c, rng.random(n) > 0.1 * (c % 3))
+    cols["w"] = ("i64", rng.integers(-3, 10, n), rng.random(n) > 0.05)
+    if special and n > 10:
+        for name, k in (("f2", 0), ("f6", 1)):
+            f = cols[name][1]
+            f[rng.integers(0, n, 2 + k)] = np.nan
+            f[rng.integers(0, n, 1)] = np.inf
+            f[rng.integers(0, n, 1 + k)] = -np.inf
+    return cols
+
+
+@pytest.mark.parametrize("n", [0, 1, 63, 64, 65, 255, 257, 4095, 4097, 100_003])
+@pytest.mark.parametrize("where", [None, "w > 2"])
+@pytest.mark.parametrize("glds", ["1", "0"])
+def test_all_f64_pair_pass_vs_oracle(dq, n, where, glds, monkeypatch):
+    """All-fp64 pair groups: the LDS-DMA staged Correlation pass (default) and the register-staged one
+    (DQ_PAIR_GLDS=0) vs the oracle with NaN / +-inf (the refold path), `where`, and sizes around the 64-row
+    group and the 4-wave stride."""
+    from deequ_amd.runner import scan_states
+    from deequ_amd.table import column_from_numpy
+
+    monkeypatch.setenv("DQ_PAIR_GLDS", glds)
+    cols = _f64_only(n, n * 5 + 11 + (where is not None), special=(n % 2 == 1))
+    tbl = dq.Table([column_from_numpy(k, t, v, m) for k, (t, v, m) in cols.items()])
+    names = [f"f{c}" for c in range(8)]
+    an = [dq.Correlation(names[i], names[j], where) for i in range(8) for j in range(i + 1, 8)]
+    for c in names:
+        an += [dq.Mean(c, where), dq.StandardDeviation(c, where), dq.Minimum(c, where), dq.Maximum(c, where),
+               dq.Sum(c, where)]
+    states = scan_states(tbl, an)
+    wm = None
+    if where is not None:
+        wm = cols["w"][2] & (cols["w"][1] > 2)
+    _check(dq, cols, states, an, n, wm)
