@@ -359,7 +359,7 @@ def valu_bound(kernel, avg_ms):
     insts = r["SQ_INSTS_VALU_per_call"]
     floor_ms = insts * VALU_CYCLES_PER_WAVE_INST / (1024 * 2.4e9) * 1e3
     return {"valu_insts_per_launch": insts, "issue_floor_ms": floor_ms, "frac_of_launch": floor_ms / avg_ms,
-            "model": "4 SIMD cycles per wave64 VALU instruction, 1024 SIMDs x 2.4 GHz", "source": os.path.relpath(PMC_FILE, ROOT)}
+            "model": "4 SIMD cycles per wave64 VALU instruction (measured 4.5 at 4 waves/SIMD, 3.0-3.3 at 8: tools/micro/valu_rate_probe.hip), 1024 SIMDs x 2.4 GHz", "source": os.path.relpath(PMC_FILE, ROOT)}
 
 
 def state_io_timing(analyzers, states) -> dict:

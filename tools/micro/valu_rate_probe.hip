@@ -37,6 +37,12 @@ BODY(k_cndmask, asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(u[j]) : "v"(
 BODY(k_bfe, asm volatile("v_bfe_u32 %0, %0, 3, 8" : "+v"(u[j])))
 BODY(k_perm, asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(u[j]) : "v"(u[(j + 1) & 15]), "s"(k)))
 
+// fp64 ops (the Correlation pass's operand prep): 8 independent 64-bit chains per wave
+BODY(k_add_f64, asm volatile("v_add_f64 %0, %0, %1" : "+v"(w[j & 7]) : "v"(w[(j + 1) & 7])))
+BODY(k_mul_f64, asm volatile("v_mul_f64 %0, %0, %1" : "+v"(w[j & 7]) : "v"(w[(j + 1) & 7])))
+BODY(k_fma_f64, asm volatile("v_fma_f64 %0, %0, %1, %0" : "+v"(w[j & 7]) : "v"(w[(j + 1) & 7])))
+BODY(k_cvt_f64_u32, asm volatile("v_cvt_f64_u32 %0, %1" : "=v"(w[j & 7]) : "v"(u[j])))
+
 typedef void (*KF)(uint32_t*, int, long long*);
 void run(const char* name, KF f, int wps = 4, int threads = 256) {
   uint32_t* out; long long* cyc;
@@ -59,5 +65,7 @@ int main() {
   run("v_mul_hi_u32", k_mul_hi); run("v_mul_u32_u24", k_mul_u24); run("v_mad_u64_u32", k_mad_u64);
   run("v_mad_u32_u24", k_mad_u32_u24); run("v_lshl_add_u64", k_lshl_add_u64); run("v_mov_b64", k_mov_b64);
   run("v_cndmask_b32", k_cndmask); run("v_bfe_u32", k_bfe); run("v_perm_b32", k_perm);
+  run("v_add_f64", k_add_f64); run("v_mul_f64", k_mul_f64); run("v_fma_f64", k_fma_f64);
+  run("v_cvt_f64_u32", k_cvt_f64_u32); run("v_mul_f64", k_mul_f64, 2, 256); run("v_mul_f64", k_mul_f64, 8, 256);
   return 0;
 }
