@@ -666,30 +666,37 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
   int32_t qmin = 0;
   DtCounts dtc;
   const auto bp = [p5](uint32_t b) { return p5[b]; };
-  // Software pipeline: string j + 1's 32 bytes are in flight while string j is hashed, and right
-  // after row j is hashed its registers take the next block's offsets of row j (a whole block of
-  // slack; vmcnt retires in order, so every load is awaited about one row after it was issued).
-  // Each row's exec-masked ds_max ends a basic block, so the order written here is the issue order;
-  // the prefetch is unconditional (a conditional one makes the wait counts of both paths merge).
-  OffT ra[8], rb[8];  // offsets o0, o1 of the lane's 8 rows (then: o0 and len)
+  // Software pipeline over the lane's rows j = 0..7 of each block, continuing into the next block:
+  // row j + 4's offsets are loaded into the ring slot row j frees (kOffRing = 4 rows of offsets in
+  // registers, loaded 4 rows before use), and the 32-byte windows of rows j + 1 .. j + kStrAhead are in
+  // flight while row j is hashed.  Each row's exec-masked ds_max ends a basic block, so the order written
+  // here is the issue order; the prefetches are unconditional (past row1 the descriptors read 0: a
+  // conditional one makes the wait counts of both paths merge).
+  constexpr int kOffRing = 4;
+  OffT ra[kOffRing], rb[kOffRing];  // offsets o0, o1 of rows j .. j + 3 (slot = row & 3)
   auto load_offsets = [&](int64_t blk, int j) {
     const int soff = (int)((blk + (int64_t)wave * 512 - row0 + j * 64) * W);
+    const int q = j & (kOffRing - 1);
     if constexpr (W == 4) {
-      ra[j] = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(orsrc, lane * 4, soff, 0);
-      rb[j] = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(orsrc, lane * 4 + 4, soff, 0);
+      ra[q] = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(orsrc, lane * 4, soff, 0);
+      rb[q] = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(orsrc, lane * 4 + 4, soff, 0);
     } else {
       const auto a0 = __builtin_amdgcn_raw_buffer_load_b64(orsrc, lane * 8, soff, 0);
       const auto a1 = __builtin_amdgcn_raw_buffer_load_b64(orsrc, lane * 8 + 8, soff, 0);
-      ra[j] = (int64_t)(((uint64_t)a0[1] << 32) | a0[0]);
-      rb[j] = (int64_t)(((uint64_t)a1[1] << 32) | a1[0]);
+      ra[q] = (int64_t)(((uint64_t)a0[1] << 32) | a0[0]);
+      rb[q] = (int64_t)(((uint64_t)a1[1] << 32) | a1[0]);
     }
   };
 #pragma unroll
-  for (int j = 0; j < 8; ++j) load_offsets(row0, j);
-  // o0 rel. to the window (low 2 bits = the string's byte alignment) and len of row j
-  auto rel_of = [&](int j) -> uint32_t { return W == 4 ? (uint32_t)ra[j] : (uint32_t)((int64_t)ra[j] - lo); };
+  for (int j = 0; j < kOffRing; ++j) load_offsets(row0, j);
+  // o0 rel. to the window (low 2 bits = the string's byte alignment) and len of the row in slot j & 3
+  auto rel_of = [&](int j) -> uint32_t {
+    const int q = j & (kOffRing - 1);
+    return W == 4 ? (uint32_t)ra[q] : (uint32_t)((int64_t)ra[q] - lo);
+  };
   auto len_of = [&](int j) -> uint32_t {
-    const int64_t l = (int64_t)rb[j] - (int64_t)ra[j];
+    const int q = j & (kOffRing - 1);
+    const int64_t l = (int64_t)rb[q] - (int64_t)ra[q];
     return W == 4 ? (uint32_t)l : (l > 28 ? 29u : (uint32_t)l);
   };
   const int32_t win3 = win < 0 ? -1 : (win | 3);  // (rel & ~3) <= win  <=>  rel <= win | 3
@@ -735,15 +742,14 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
     uint64_t slow = 0;  // OR of the selected rows that need the general hash
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      cnt_w += __builtin_popcountll(m[j]);
-      const uint64_t fastm = __builtin_amdgcn_ballot_w64(len_of(j) <= 28u && (int32_t)rel_of(j) <= win3);
-      slow |= m[j] & ~fastm;
-      m[j] &= fastm;
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      // string (j + kStrAhead) & 7 -- of the next block once j + kStrAhead >= 8, whose offsets row j's
-      // registers took after that row was hashed: the windows stay in flight across block boundaries
+      {  // selected rows that take the fast path (row j's offsets are in its ring slot)
+        cnt_w += __builtin_popcountll(m[j]);
+        const uint64_t fastm = __builtin_amdgcn_ballot_w64(len_of(j) <= 28u && (int32_t)rel_of(j) <= win3);
+        slow |= m[j] & ~fastm;
+        m[j] &= fastm;
+      }
+      // the window of row j + kStrAhead (of the next block once j + kStrAhead >= 8): its offsets are in
+      // ring slot (j + kStrAhead) & 3, so the windows stay in flight across block boundaries
       u32x4 an, cn;
       {
         const int32_t offn = (int32_t)(rel_of((j + kStrAhead) & 7) & ~3u);
@@ -779,7 +785,9 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
         if (lane_bit(m[j] & ~dm)) atomicMax(reinterpret_cast<int32_t*>(reinterpret_cast<char*>(regs) + key.addr), key.q);
         if (qtail >= 64u) drain_full();
       }
-      load_offsets(blk + kRowsPerIter, j);  // unconditional: past row1 the descriptor reads 0
+      // row j + 4 into the slot row j frees (of the next block for j >= 4)
+      if (j + kOffRing < 8) load_offsets(blk, j + kOffRing);
+      else load_offsets(blk + kRowsPerIter, j + kOffRing - 8);
 #pragma unroll
       for (int q = 0; q + 1 < kStrAhead; ++q) {
         win_a[q] = win_a[q + 1];
@@ -890,7 +898,7 @@ __device__ __forceinline__ void run_variant(const ColTask& t, const ScanCols& co
 // Minimum waves per SIMD the register allocator must leave room for (0 = no constraint); a
 // diagnostic build switch for the issue-bound string hash variants.
 #ifndef DQ_STR_WAVES
-#define DQ_STR_WAVES 0
+#define DQ_STR_WAVES 6  // 80 VGPRs with the 4-row offset ring (81 unconstrained: 5 waves); A/B within 1 %
 #endif
 // fp64 / int64 stats+HLL: 6 waves per SIMD (80 VGPRs; the 2 spilled registers are reloaded only in the
 // prologue / epilogue): f64 1.538 -> 1.522 ms per 125 M rows x 8 columns against the unconstrained 82
