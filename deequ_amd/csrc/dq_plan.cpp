@@ -444,6 +444,11 @@ struct dq_plan {
   std::vector<hipStream_t> side;          // concurrency - 1 extra streams
   std::vector<hipEvent_t> side_done;
   hipEvent_t fork_ev = nullptr;
+  // the predicate pass on its own stream, concurrent with the column / pair launches, when no `where`
+  // bitmap (the only thing those launches read from it) is produced: its load-latency-bound interpreter
+  // then overlaps the VALU-bound hash passes (DQ_PRED_CONCURRENT=0: serial on the plan stream)
+  hipStream_t pred_stream = nullptr;
+  hipEvent_t pred_fork_ev = nullptr, pred_done_ev = nullptr;
   PredProgram prog{};
   std::vector<std::string> patterns;      // DQ_PRED_REGEX patterns (dq_plan_create_ex)
   std::vector<uint16_t> regex_blob;       // their compiled DFAs
@@ -525,6 +530,11 @@ static dq_status timed(dq_plan* p, int kernel, hipStream_t st, F fn) {
 }
 
 static dq_status free_plan_mem(dq_plan* p) {
+  if (p->pred_stream) (void)hipStreamDestroy(p->pred_stream);
+  if (p->pred_fork_ev) (void)hipEventDestroy(p->pred_fork_ev);
+  if (p->pred_done_ev) (void)hipEventDestroy(p->pred_done_ev);
+  p->pred_stream = nullptr;
+  p->pred_fork_ev = p->pred_done_ev = nullptr;
   for (hipStream_t st : p->side) (void)hipStreamDestroy(st);
   for (hipEvent_t ev : p->side_done) (void)hipEventDestroy(ev);
   if (p->fork_ev) (void)hipEventDestroy(p->fork_ev);
@@ -1219,6 +1229,12 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
       p->concurrency, std::max<int32_t>(1, (int32_t)p->groups.size() + (p->pair_groups.empty() ? 0 : 1) +
                                                (p->lane_tasks.empty() ? 0 : 1) + (p->mfma_groups.empty() ? 0 : 1)));
   HIP_TRY(hipEventCreateWithFlags(&p->fork_ev, hipEventDisableTiming));
+  const char* pc = std::getenv("DQ_PRED_CONCURRENT");
+  if (p->has_pred && p->prog.n_bitmaps == 0 && !(pc && pc[0] == '0')) {
+    HIP_TRY(hipStreamCreateWithFlags(&p->pred_stream, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&p->pred_fork_ev, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&p->pred_done_ev, hipEventDisableTiming));
+  }
   for (int32_t k = 1; k < p->concurrency; ++k) {
     hipStream_t st;
     hipEvent_t ev;
@@ -1379,14 +1395,22 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
   for (int32_t h = 0; h < p->prog.n_hll; ++h)
     HIP_TRY(hipMemsetAsync(p->d_col_part + (size_t)p->prog.hll[h].part * kMaxWG, 0, (size_t)nr_col * sizeof(ColPartial),
                            p->stream));
-  if (p->has_pred)
-    if (dq_status s = timed(p, 0, p->stream, [&] {
+  if (p->has_pred) {
+    hipStream_t pst = p->stream;
+    if (p->pred_stream) {  // fork: the predicate pass beside the column / pair launches
+      HIP_TRY(hipEventRecord(p->pred_fork_ev, p->stream));
+      HIP_TRY(hipStreamWaitEvent(p->pred_stream, p->pred_fork_ev, 0));
+      pst = p->pred_stream;
+    }
+    if (dq_status s = timed(p, 0, pst, [&] {
           const int32_t lds = kWaves * 128 * (p->prog.stack_depth + p->prog.n_roots + p->prog.n_counters) +
                               ((p->prog.regex_words * 2 + 15) & ~15);
           return launch_pred_scan(p->d_prog, sc, bm, n_rows, rpr_pred, nr_pred, p->d_pred_acc, p->d_col_part,
-                                  p->d_hll_acc, lds, p->stream, p->prog.regex_words > 0, p->prog.n_hll > 0);
+                                  p->d_hll_acc, lds, pst, p->prog.regex_words > 0, p->prog.n_hll > 0);
         }))
       return s;
+    if (p->pred_stream) HIP_TRY(hipEventRecord(p->pred_done_ev, p->pred_stream));
+  }
   // fork: variant launches (and the pair pass) round-robin over the plan stream + side streams
   const int32_t K = p->concurrency;
   if (K > 1) {
@@ -1440,6 +1464,7 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
       HIP_TRY(hipStreamWaitEvent(p->stream, p->side_done[k - 1], 0));
     }
   }
+  if (p->has_pred && p->pred_stream) HIP_TRY(hipStreamWaitEvent(p->stream, p->pred_done_ev, 0));
   if (dq_status s = timed(p, 3, p->stream, [&] {
         return launch_finalize((int32_t)p->col_tasks.size(), nr_col, p->d_col_part, p->d_col_acc,
                                (int32_t)p->pair_tasks.size(), nr_col, p->d_pair_part, p->d_pair_acc,
