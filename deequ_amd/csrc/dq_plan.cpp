@@ -444,9 +444,10 @@ struct dq_plan {
   std::vector<hipStream_t> side;          // concurrency - 1 extra streams
   std::vector<hipEvent_t> side_done;
   hipEvent_t fork_ev = nullptr;
-  // the predicate pass on its own stream, concurrent with the column / pair launches, when no `where`
-  // bitmap (the only thing those launches read from it) is produced: its load-latency-bound interpreter
-  // then overlaps the VALU-bound hash passes (DQ_PRED_CONCURRENT=0: serial on the plan stream)
+  // DQ_PRED_CONCURRENT=1: the predicate pass on its own stream, concurrent with the column / pair
+  // launches, when no `where` bitmap (the only thing those launches read from it) is produced.  Opt-in:
+  // its waves (120 VGPRs, 4 per SIMD) can hold the SIMDs the hash passes need, so the gain depends on
+  // dispatch order -- C3 29.17 -> 28.55 ms on one box, 35.1 ms on another
   hipStream_t pred_stream = nullptr;
   hipEvent_t pred_fork_ev = nullptr, pred_done_ev = nullptr;
   PredProgram prog{};
@@ -1229,8 +1230,8 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
       p->concurrency, std::max<int32_t>(1, (int32_t)p->groups.size() + (p->pair_groups.empty() ? 0 : 1) +
                                                (p->lane_tasks.empty() ? 0 : 1) + (p->mfma_groups.empty() ? 0 : 1)));
   HIP_TRY(hipEventCreateWithFlags(&p->fork_ev, hipEventDisableTiming));
-  const char* pc = std::getenv("DQ_PRED_CONCURRENT");
-  if (p->has_pred && p->prog.n_bitmaps == 0 && !(pc && pc[0] == '0')) {
+  const char* pc = std::getenv("DQ_PRED_CONCURRENT");  // opt-in: see the plan field's note
+  if (p->has_pred && p->prog.n_bitmaps == 0 && pc && pc[0] == '1') {
     HIP_TRY(hipStreamCreateWithFlags(&p->pred_stream, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&p->pred_fork_ev, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&p->pred_done_ev, hipEventDisableTiming));
