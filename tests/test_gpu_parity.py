@@ -238,6 +238,29 @@ def test_utf8_hll_edge_lengths(dq, n, large):
         assert_state_close(got[an], ref)
 
 
+@pytest.mark.parametrize("lens", [(24, 28), (23, 25), (8, 24)])
+@pytest.mark.parametrize("n", [63, 4097, 100_003])
+def test_utf8_hll_deferred_third_round(dq, n, lens):
+    """The UTF8 pass defers a selected string of 24..28 bytes (third stripe round) to a per-wave LDS queue
+    finished 64 at a time: every lane deferred (24..28 bytes: a drain per row group), a boundary mix, and
+    C5's 8..24-byte lengths, with nulls and a `where`, vs the oracle's HLL registers."""
+    from deequ_amd.runner import scan_states
+    from deequ_amd.table import column_from_numpy, utf8_column
+
+    rng = np.random.default_rng(77 + n + lens[0])
+    strs = [None if rng.random() < 0.1 else bytes(rng.integers(0, 256, int(rng.integers(lens[0], lens[1] + 1)),
+                                                              dtype=np.uint8)) for _ in range(n)]
+    a = rng.integers(-5, 5, n).astype(np.int64)
+    t = dq.Table([utf8_column("s", strs), column_from_numpy("a", "i64", a, np.ones(n, bool))])
+    analyzers = [dq.ApproxCountDistinct("s"), dq.ApproxCountDistinct("s", "a > 0")]
+    got = scan_states(t, analyzers)
+    valid = np.array([s is not None for s in strs])
+    ocols = {"s": O.OColumn("utf8", strs, valid), "a": O.OColumn("i64", a, np.ones(n, bool))}
+    for an in analyzers:
+        ref = O.compute_state((type(an).__name__, an.column, an.where), ocols, n)
+        assert_state_close(got[an], ref)
+
+
 def test_chunked_equals_single_scan(dq):
     """dq_scan over row chunks (chunk_index order) == one scan (PartitionedTableIntegrationTest analogue)."""
     from deequ_amd import synth
