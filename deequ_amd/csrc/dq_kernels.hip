@@ -1215,6 +1215,10 @@ __device__ __forceinline__ uint32_t pred_valid_word(const uint32_t* v, int64_t b
 struct AtomBuf {
   uint64_t a[8], b[8];
   uint32_t va, vb;
+  // what the buffer holds (wave-uniform): block base, columns of a / b (-1: none), values loaded (CMP)
+  int64_t t_base = -1;
+  int32_t t_col_a = -1, t_col_b = -1;
+  bool t_vals = false;
 };
 
 // One ATOM_CMP for a block from its loads: the lane's 32-bit TRUE / NULL words (lanes 0..15).
@@ -1506,18 +1510,39 @@ __global__ __launch_bounds__(kBlock) void dq_pred_scan(const PredProgram* __rest
   // Two-deep pipeline over the atoms, across blocks: atom g (a wave-uniform running count) uses
   // buffer g & 1, and the loads of atom g + 1 go into the other buffer before atom g is evaluated.
   AtomBuf B0, B1;
-  auto issue = [&](int k, int64_t base, AtomBuf& L) {
+  // Loads of atom k of the block at `base` into L; C is the buffer of the atom evaluated meanwhile (the
+  // previous atom): a column it already holds for the same block is copied, not re-read -- C3 reads i1 in
+  // three consecutive atoms and i3 in two, and those re-reads missed L2 (FETCH_SIZE 1.41x algorithmic).
+  auto issue = [&](int k, int64_t base, AtomBuf& L, const AtomBuf& C) {
     const PredInstr ins = uniform_instr(&s_instr[__builtin_amdgcn_readfirstlane((int)s_load[k])]);
-    if (ins.op == PO_ATOM_CMP) {
-      pred_load(cols.values[ins.col_a], ins.kind_a, row0, row1, base, lane, L.a);
-      if (ins.col_b >= 0) {
-        pred_load(cols.values[ins.col_b], ins.kind_b, row0, row1, base, lane, L.b);
-        L.vb = pred_valid_word(cols.validity[ins.col_b], base, n_rows, lane);
+    const bool same_blk = C.t_base == base;
+    auto fetch = [&](int col, int kind, bool vals, uint64_t (&dst)[8], uint32_t& vdst) __attribute__((always_inline)) {
+      if (same_blk && col == C.t_col_a && (C.t_vals || !vals)) {
+        if (vals) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) dst[j] = C.a[j];
+        }
+        vdst = C.va;
+      } else if (same_blk && col == C.t_col_b && C.t_vals) {
+        if (vals) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) dst[j] = C.b[j];
+        }
+        vdst = C.vb;
+      } else {
+        if (vals) pred_load(cols.values[col], kind, row0, row1, base, lane, dst);
+        vdst = pred_valid_word(cols.validity[col], base, n_rows, lane);
       }
-    }
-    L.va = pred_valid_word(cols.validity[ins.col_a], base, n_rows, lane);
+    };
+    const bool cmp = ins.op == PO_ATOM_CMP;
+    if (cmp && ins.col_b >= 0) fetch(ins.col_b, ins.kind_b, true, L.b, L.vb);
+    fetch(ins.col_a, ins.kind_a, cmp, L.a, L.va);
+    L.t_base = base;
+    L.t_col_a = ins.col_a;
+    L.t_col_b = cmp ? ins.col_b : -1;
+    L.t_vals = cmp;
   };
-  if (n_loads > 0) issue(0, row0 + (int64_t)wave * 512, B0);
+  if (n_loads > 0) issue(0, row0 + (int64_t)wave * 512, B0, B1);
   uint32_t g = 0;
 
   for (int64_t blk = row0; blk < row1; blk += kRowsPerIter) {
@@ -1536,8 +1561,8 @@ __global__ __launch_bounds__(kBlock) void dq_pred_scan(const PredProgram* __rest
         const int64_t bn = k + 1 < n_loads ? base : base + kRowsPerIter;
         uint32_t wt, wn;
         const AtomBuf& cur = (g & 1u) ? B1 : B0;
-        if ((g & 1u) == 0) issue(kn, bn, B1);
-        else issue(kn, bn, B0);
+        if ((g & 1u) == 0) issue(kn, bn, B1, B0);
+        else issue(kn, bn, B0, B1);
         if (op == PO_ATOM_CMP) {
           if ((g & 1u) == 0) pred_atom_cmp(ins, B0, lane, wt, wn);
           else pred_atom_cmp(ins, B1, lane, wt, wn);
