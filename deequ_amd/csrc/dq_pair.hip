@@ -451,14 +451,20 @@ hipError_t launch_pair_lane_scan(const PairWaveTask* tasks, int32_t ntasks, cons
 // ================================================================================================
 typedef double dq_d4 __attribute__((ext_vector_type(4)));
 #ifndef DQ_PAIR_SLOTS
-#define DQ_PAIR_SLOTS 3
+#define DQ_PAIR_SLOTS 2
+#endif
+// waves per SIMD the LDS-DMA kernel's registers must allow: 2 slots (35 KB per workgroup) let 4
+// workgroups share a CU, and 4 waves (128 VGPRs, 8 spilled) measured 1.80 -> 1.76 ms per 125 M rows
+// against 3 slots at 3 waves (52 KB, 136 VGPRs)
+#ifndef DQ_PAIR_WAVES
+#define DQ_PAIR_WAVES 4
 #endif
 constexpr int kStageSlots = DQ_PAIR_SLOTS;  // LDS-DMA group slots per wave (kStageSlots - 1 groups in flight beside the fold)
 
 // F64: every column of every group is fp64; MINMAX: a fused moments task feeds Minimum / Maximum
 // GLDS (with F64): full groups staged through LDS by DMA (every column 16-byte aligned: the host checks)
 template <bool F64, bool MINMAX, bool GLDS = false>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GLDS ? 3 : 1))) void dq_pair_mfma_scan(const PairGroup* __restrict__ groups, int32_t ngroups,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GLDS ? DQ_PAIR_WAVES : 1))) void dq_pair_mfma_scan(const PairGroup* __restrict__ groups, int32_t ngroups,
                                                             ScanCols cols, ScanBitmaps bm, const uint32_t* ones,
                                                             int64_t n_rows, int64_t rows_per_range, int32_t nranges,
                                                             CorrPartial* __restrict__ pair_part,
