@@ -744,7 +744,10 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
     for (int j = 0; j < 8; ++j) {
       {  // selected rows that take the fast path (row j's offsets are in its ring slot)
         cnt_w += __builtin_popcountll(m[j]);
-        const uint64_t fastm = __builtin_amdgcn_ballot_w64(len_of(j) <= 28u && (int32_t)rel_of(j) <= win3);
+        // the compares' own masks (llvm.amdgcn.icmp; signedness from the predicate) ANDed in SGPRs: a
+        // ballot of the combined bool materialises it in a VGPR and compares again (2 VALU per row)
+        const uint64_t fastm = __builtin_amdgcn_uicmp(len_of(j), 28u, 37 /* ICMP_ULE */) &
+                               __builtin_amdgcn_uicmp(rel_of(j), (uint32_t)win3, 41 /* ICMP_SLE: signed */);
         slow |= m[j] & ~fastm;
         m[j] &= fastm;
       }
