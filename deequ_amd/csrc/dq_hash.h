@@ -71,6 +71,30 @@ DQ_HD uint64_t mul_add_c(uint64_t x, uint64_t c, uint64_t a) {
   return ((uint64_t)hi << 32) | (uint32_t)p;
 }
 
+// x * c (mod 2^64): mul_add_c with the addend an inline 0 (no zero register pair kept live)
+template <bool VOL = false>
+DQ_HD uint64_t mul_c(uint64_t x, uint64_t c) {
+  const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint64_t p, carry;
+  uint32_t t1, t2;
+#define DQ_MUL_BODY                                                                                  \
+  ("v_mad_u64_u32 %[p], %[cy], %[xl], %[cl], 0\n\t"                                                  \
+   "v_mul_lo_u32 %[t1], %[xl], %[ch]\n\t"                                                             \
+   "v_mul_lo_u32 %[t2], %[xh], %[cl]"                                                                \
+   : [p] "=&v"(p), [cy] "=&s"(carry), [t1] "=&v"(t1), [t2] "=&v"(t2)                                 \
+   : [xl] "v"(xl), [xh] "v"(xh), [cl] "s"((uint32_t)c), [ch] "s"((uint32_t)(c >> 32)))
+  if constexpr (VOL) asm volatile DQ_MUL_BODY;
+  else asm DQ_MUL_BODY;
+#undef DQ_MUL_BODY
+  (void)carry;
+  const uint32_t hi = (uint32_t)(p >> 32) + t1 + t2;
+  return ((uint64_t)hi << 32) | (uint32_t)p;
+#else
+  return x * c;
+#endif
+}
+
 // x * c (mod 2^64) for a 32-bit x: one v_mad_u64_u32, one v_mul_lo_u32, one add.
 template <bool VOL = false>
 DQ_HD uint64_t mul32_c(uint32_t x, uint64_t c) {
@@ -96,7 +120,7 @@ DQ_HD uint64_t mul32_c(uint32_t x, uint64_t c) {
 // fmix_tail(fmix_head(h)).  The HLL kernels only need the high word of fmix_tail, hi32(b * P3).
 DQ_HD uint64_t fmix_head(uint64_t h) {
   h ^= h >> 33;
-  h = mul_add_c(h, XP2, 0);
+  h = mul_c(h, XP2);
   return h ^ (h >> 29);
 }
 DQ_HD uint64_t fmix_tail(uint64_t b) {
@@ -107,8 +131,8 @@ DQ_HD uint64_t fmix64(uint64_t h) { return fmix_tail(fmix_head(h)); }
 
 // XXH64.hashLong / hashInt (seed 42) up to fmix_head
 DQ_HD uint64_t xxh64_long_head(uint64_t v) {
-  const uint64_t k = rotl64(mul_add_c(v, XP2, 0), 31);
-  const uint64_t h = mul_add_c(k, XP1, 0) ^ (kSeed + XP5 + 8);
+  const uint64_t k = rotl64(mul_c(v, XP2), 31);
+  const uint64_t h = mul_c(k, XP1) ^ (kSeed + XP5 + 8);
   return fmix_head(mul_add_c(rotl64(h, 27), XP1, XP4));
 }
 DQ_HD uint64_t xxh64_int_head(uint32_t v) {
@@ -133,7 +157,7 @@ struct MulP5 {  // b * P5 for a byte b (host; the kernels read a 256-entry LDS t
 // One 8-byte round: h ^= rotl(k1 * P2, 31) * P1; h = rotl(h, 27) * P1 + P4.
 template <bool VOL = false>
 DQ_HD uint64_t xxh64_stripe_round(uint64_t h, uint64_t k1) {
-  return mul_add_c<VOL>(rotl64(h ^ mul_add_c<VOL>(rotl64(mul_add_c<VOL>(k1, XP2, 0), 31), XP1, 0), 27), XP1, XP4);
+  return mul_add_c<VOL>(rotl64(h ^ mul_c<VOL>(rotl64(mul_c<VOL>(k1, XP2), 31), XP1), 27), XP1, XP4);
 }
 
 // The first NR stripe rounds (min(NR, len >> 3) of them): returns h and d4p = {w[2 m], w[2 m + 1]},
@@ -167,7 +191,7 @@ DQ_HD uint64_t xxh64_tail_head(uint64_t h, uint64_t d4p, uint32_t len, BP bp) {
   if (has4) h = mul_add_c<true>(rotl64(h ^ mul32_c<true>(d4, XP1), 23), XP2, XP3);
 #pragma unroll
   for (uint32_t j = 0; j < 3; ++j)
-    if (j < nb) h = mul_add_c<true>(rotl64(h ^ kb[j], 11), XP1, 0);
+    if (j < nb) h = mul_c<true>(rotl64(h ^ kb[j], 11), XP1);
   return fmix_head(h);
 }
 
