@@ -74,8 +74,8 @@ DQ_HD uint64_t mul_add_c(uint64_t x, uint64_t c, uint64_t a) {
 // x * c (mod 2^64): mul_add_c with the addend an inline 0 (no zero register pair kept live)
 template <bool VOL = false>
 DQ_HD uint64_t mul_c(uint64_t x, uint64_t c) {
-  const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
 #if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
   uint64_t p, carry;
   uint32_t t1, t2;
 #define DQ_MUL_BODY                                                                                  \

@@ -61,10 +61,6 @@ __device__ __forceinline__ uint64_t bits64_tail(const uint32_t* bm, int64_t base
   if (base + 64 > row1) x &= (1ull << (row1 - base)) - 1ull;
   return x;
 }
-// the same for a whole 64-row group below row1: one s_load_dwordx2
-__device__ __forceinline__ uint64_t bits64(const uint32_t* bm, int64_t base) {
-  return load_word64(bm, base >> 5);
-}
 
 // value of row `idx` of a column (values pointer at row 0 of the chunk), as double; raw = the int64 value
 struct PosLoad {
