@@ -45,6 +45,12 @@ enum ColVariant : int32_t {
 };
 constexpr int kNumVariants = 17;
 
+// per-variant row-range counts of one scan (dq_finalize merges nr[i] partials for tasks [first, end))
+struct FinRanges {
+  int32_t n;
+  int32_t first[kNumVariants], end[kNumVariants], nr[kNumVariants];
+};
+
 struct ColTask {
   int32_t variant;   // ColVariant
   int32_t col;       // column index

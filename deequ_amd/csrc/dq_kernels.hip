@@ -1679,14 +1679,17 @@ __global__ __launch_bounds__(kBlock) void dq_finalize(int32_t ncol, int32_t nran
                                                       const CorrPartial* __restrict__ pair_part,
                                                       CorrPartial* __restrict__ pair_acc, int32_t has_pred,
                                                       int32_t nranges_pred, const PredPartial* __restrict__ pred_part,
-                                                      PredPartial* __restrict__ pred_acc) {
+                                                      PredPartial* __restrict__ pred_acc, FinRanges fr) {
   __shared__ ColStats cs[kBlock];
   __shared__ CorrStats ps[kBlock];
   const int b = blockIdx.x, tid = threadIdx.x;
   if (b < ncol) {
+    int32_t nr = nranges_col;  // the variant launch's own range count, if it had one
+    for (int i = 0; i < fr.n; ++i)
+      if (b >= fr.first[i] && b < fr.end[i]) nr = fr.nr[i];
     ColStats s;
     stats_init(s);
-    for (int r = tid; r < nranges_col; r += kBlock) stats_merge(s, stats_load(col_part + (size_t)b * kMaxWG + r));
+    for (int r = tid; r < nr; r += kBlock) stats_merge(s, stats_load(col_part + (size_t)b * kMaxWG + r));
     cs[tid] = s;
     __syncthreads();
     for (int stride = kBlock / 2; stride >= 1; stride >>= 1) {
@@ -1806,11 +1809,11 @@ hipError_t launch_pair_tile_scan(const PairGroup* groups, int32_t ngroups, const
 hipError_t launch_finalize(int32_t ncol, int32_t nranges_col, const ColPartial* col_part, ColPartial* col_acc,
                            int32_t npair, int32_t nranges_pair, const CorrPartial* pair_part, CorrPartial* pair_acc,
                            int32_t has_pred, int32_t nranges_pred, const PredPartial* pred_part, PredPartial* pred_acc,
-                           hipStream_t st) {
+                           const FinRanges& fr, hipStream_t st) {
   const uint32_t nb = (uint32_t)(ncol + npair + (has_pred ? 1 : 0));
   if (nb == 0) return hipSuccess;
   hipLaunchKernelGGL(dq_finalize, dim3(nb), dim3(kBlock), 0, st, ncol, nranges_col, col_part, col_acc, npair,
-                     nranges_pair, pair_part, pair_acc, has_pred, nranges_pred, pred_part, pred_acc);
+                     nranges_pair, pair_part, pair_acc, has_pred, nranges_pred, pred_part, pred_acc, fr);
   return hipGetLastError();
 }
 

@@ -47,7 +47,7 @@ hipError_t launch_pair_mfma_scan(const PairGroup* groups, int32_t ngroups, const
                                  bool minmax, bool glds, hipStream_t st);
 hipError_t launch_finalize(int32_t ncol, int32_t nranges_col, const ColPartial* col_part, ColPartial* col_acc,
                            int32_t npair, int32_t nranges_pair, const CorrPartial* pair_part, CorrPartial* pair_acc,
-                           int32_t has_pred, int32_t nranges_pred, const PredPartial* pred_part, PredPartial* pred_acc,
+                           int32_t has_pred, int32_t nranges_pred, const PredPartial* pred_part, PredPartial* pred_acc, const FinRanges& fr,
                            hipStream_t st);
 hipError_t launch_init_acc(ColPartial* col_acc, int32_t ncol, CorrPartial* pair_acc, int32_t npair, hipStream_t st);
 
@@ -1384,9 +1384,42 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
     return e ? std::max<int64_t>(256, std::atoll(e)) : (int64_t)kTargetWGs;
   }();
   const int64_t want = std::max<int64_t>(64, std::min<int64_t>(kMaxWG, target / std::max<int64_t>(1, min_launch)));
-  int32_t nr_col = (int32_t)std::min<int64_t>(want, ceil_div(n_rows, kRowsPerIter));
-  int64_t rpr_col = ceil_div(ceil_div(n_rows, nr_col), kRowsPerIter) * kRowsPerIter;
-  nr_col = (int32_t)ceil_div(n_rows, rpr_col);
+  // rows per range and range count for `want` ranges
+  auto size_ranges = [&](int64_t w, int64_t& rpr, int32_t& nr) {
+    nr = (int32_t)std::min<int64_t>(w, ceil_div(n_rows, kRowsPerIter));
+    rpr = ceil_div(ceil_div(n_rows, nr), kRowsPerIter) * kRowsPerIter;
+    nr = (int32_t)ceil_div(n_rows, rpr);
+  };
+  int32_t nr_col;
+  int64_t rpr_col;
+  size_ranges(want, rpr_col, nr_col);
+  // per-variant workgroup counts: the string hash balances better with twice the ranges (uneven string
+  // lengths, deferred-round drains): utf8_hll 1.979 -> 1.949 ms per 125 M x 4 on the C5 headline (A/B
+  // twice, DQ_VARIANT_RANGES=0 for the common size); halving the fp64 hash's ranges measured no change.
+  // scale > 0: want x scale ranges, < 0: want / -scale
+  auto variant_scale = [](int32_t v) -> int32_t {
+    if (v == CV_UTF8_H || v == CV_LUTF8_H || v == CV_UTF8_HD || v == CV_LUTF8_HD) return 2;
+    return 1;
+  };
+  static const bool per_variant = !(std::getenv("DQ_VARIANT_RANGES") && std::getenv("DQ_VARIANT_RANGES")[0] == '0');
+  FinRanges fr{};
+  std::vector<std::pair<int64_t, int32_t>> vr(p->groups.size());  // (rows per range, ranges) per variant group
+  for (size_t gi = 0; gi < p->groups.size(); ++gi) {
+    const auto& g = p->groups[gi];
+    const int32_t sc_v = per_variant ? variant_scale(g.variant) : 1;
+    if (sc_v == 1) {
+      vr[gi] = {rpr_col, nr_col};
+      continue;
+    }
+    const int64_t w = sc_v > 0 ? want * sc_v : want / -sc_v;
+    size_ranges(std::max<int64_t>(64, std::min<int64_t>(kMaxWG, w)), vr[gi].first, vr[gi].second);
+    if (fr.n < kNumVariants) {
+      fr.first[fr.n] = g.first;
+      fr.end[fr.n] = g.first + g.count;
+      fr.nr[fr.n] = vr[gi].second;
+      ++fr.n;
+    }
+  }
   // predicate pass: ~2048 workgroups of whole 2048-row iterations (HBM-bound; counters leave by atomics)
   int32_t nr_pred = (int32_t)std::min<int64_t>(2048, ceil_div(n_rows, kRowsPerIter));
   int64_t rpr_pred = ceil_div(ceil_div(n_rows, nr_pred), kRowsPerIter) * kRowsPerIter;
@@ -1420,11 +1453,12 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
   }
   int32_t li = 0;
   auto stream_for = [&](int32_t i) { return (K > 1 && i % K) ? p->side[i % K - 1] : p->stream; };
-  for (const auto& g : p->groups) {
+  for (size_t gi = 0; gi < p->groups.size(); ++gi) {
+    const auto& g = p->groups[gi];
     hipStream_t st = stream_for(li++);
     if (dq_status s = timed(p, 16 + g.variant, st, [&] {
-          return launch_column_scan(g.variant, p->d_col_tasks + g.first, g.count, g.first, sc, bm, n_rows, rpr_col,
-                                    nr_col, p->d_col_part, p->d_hll_acc, st);
+          return launch_column_scan(g.variant, p->d_col_tasks + g.first, g.count, g.first, sc, bm, n_rows,
+                                    vr[gi].first, vr[gi].second, p->d_col_part, p->d_hll_acc, st);
         }))
       return s;
   }
@@ -1470,7 +1504,7 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
         return launch_finalize((int32_t)p->col_tasks.size(), nr_col, p->d_col_part, p->d_col_acc,
                                (int32_t)p->pair_tasks.size(), nr_col, p->d_pair_part, p->d_pair_acc,
                                0 /* the predicate pass accumulates itself */, nr_pred, p->d_pred_part, p->d_pred_acc,
-                               p->stream);
+                               fr, p->stream);
       }))
     return s;
   p->total_rows += n_rows;
