@@ -31,7 +31,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md (HBM3E peak 8.0 TB/s)
 # FETCH_SIZE summary of this round's kernels (tools/profile_round.sh -> tools/summarize_prof.py):
 # per-dispatch HBM read bytes of each kernel at the default 125 M-row chunk, gfx950-corrected
-PMC_FILE = os.path.join(ROOT, "profiles", "r2i_pmc.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r2j_pmc.json")
 DEFAULT_CHUNK = 125_000_000  # 8 chunks per 1e9 rows; a UTF8 chunk's bytes (~2.0e9) stay < 2 GiB
 
 
@@ -145,6 +145,9 @@ def main():
         host_ms["append"] += (time.perf_counter() - a) * 1e3
         return states
 
+    # timing on for the warm-up too, so its hipEvent pool is filled outside the timed region (events are created
+    # only when the pool is empty); enabling again below zeroes the counters and keeps the pool
+    plan.enable_timing(True)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -301,6 +304,7 @@ def run_config(cfg, args) -> dict:
             plan.scan(t)
         return plan.finish()
 
+    plan.enable_timing(True)  # warm-up step fills the hipEvent pool (see main)
     step()
     torch.cuda.synchronize()
     plan.enable_timing(True)
