@@ -1427,8 +1427,12 @@ __device__ __forceinline__ PredInstr uniform_instr(const PredInstr* p) {
 // VGPRs with it, 119 without: 3 vs 4 waves per SIMD) do not cost the plain numeric programs occupancy.
 // HLL: the program hashes fused HLL-only columns (PredProgram::hll); its own instantiation keeps the hash
 // registers out of the plain interpreter (120 vs 141 VGPRs: 4 vs 3 waves per SIMD).
+#ifndef DQ_PRED_WAVES
+#define DQ_PRED_WAVES 1  // occupancy floor of the plain program (1 = unconstrained, 120 VGPRs / 4 waves).  5 and 6
+                         // spill (96 VGPRs + 120 B, 80 + 184 B scratch): 0.96 -> 1.56 / 2.43 ms per 125 M rows
+#endif
 template <bool RX, bool HLL>
-__global__ __launch_bounds__(kBlock) void dq_pred_scan(const PredProgram* __restrict__ prog_g, ScanCols cols,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(!RX && !HLL ? DQ_PRED_WAVES : 1))) void dq_pred_scan(const PredProgram* __restrict__ prog_g, ScanCols cols,
                                                        ScanBitmaps bm, int64_t n_rows, int64_t rows_per_range,
                                                        PredPartial* __restrict__ acc, ColPartial* __restrict__ col_part,
                                                        uint32_t* __restrict__ hll_acc) {
