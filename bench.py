@@ -32,7 +32,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md (HBM3E peak 8.0 TB/s)
 # FETCH_SIZE summary of this round's kernels (tools/profile_round.sh -> tools/summarize_prof.py):
 # per-dispatch HBM read bytes of each kernel at the default 125 M-row chunk, gfx950-corrected
-PMC_FILE = os.path.join(ROOT, "profiles", "r2j_pmc.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r2m_pmc.json")
 DEFAULT_CHUNK = 125_000_000  # 8 chunks per 1e9 rows; a UTF8 chunk's bytes (~2.0e9) stay < 2 GiB
 
 
@@ -148,7 +148,11 @@ def main():
 
     # timing on for the warm-up too, so its hipEvent pool is filled outside the timed region (events are created
     # only when the pool is empty); enabling again below zeroes the counters and keeps the pool
+    # the collector runs (and is then switched off, as timeit does) before the warm-up, not between it and
+    # the timed steps: a ~50 ms idle GPU there drops its clocks and the first timed step ran ~7 % slower
     plan.enable_timing(True)
+    gc.collect()
+    gc.disable()
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -157,8 +161,6 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    gc.collect()
-    gc.disable()  # as timeit does: no collector pass lands inside the timed steps
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -309,13 +311,13 @@ def run_config(cfg, args) -> dict:
         return plan.finish()
 
     plan.enable_timing(True)  # warm-up steps fill the hipEvent pool (see main)
-    for _ in range(2):  # the first two steps after table generation run ~7% slower kernels (clock ramp, C3 trace)
+    gc.collect()
+    gc.disable()
+    for _ in range(2):  # kernels right after table generation / an idle GPU run ~7 % slower (clock ramp, C3 trace)
         step()
     torch.cuda.synchronize()
     plan.enable_timing(True)
     k = max(1, args.config_steps)
-    gc.collect()
-    gc.disable()
     step_ms = []
     t0 = time.perf_counter()
     for _ in range(k):
@@ -330,7 +332,7 @@ def run_config(cfg, args) -> dict:
     algo = plan.bytes_per_row() * n + (str_bytes if cfg == "c3" else 0)
     dom_name, dom = max(kernels.items(), key=lambda kv: kv[1]["ms_total"])
     rec = {"workload": desc, "rows": n, "analyzers": len(analyzers), "ms_per_step": dt * 1e3, "rows_per_s": n / dt,
-           "step_ms": [round(x, 3) for x in step_ms],
+           "step_ms": [round(x, 3) for x in step_ms], "ms_per_step_median": sorted(step_ms)[len(step_ms) // 2],
            "hbm_frac_of_step": algo / dt / 1e9 / HBM_PEAK_GBS,
            "roofline": {"kernel": dom_name, "achieved": dom["GBps"], "frac": dom["GBps"] / HBM_PEAK_GBS,
                         "avg_launch_ms": dom["avg_ms"], "bytes_per_launch": dom["bytes_per_launch"]},

@@ -1525,6 +1525,8 @@ dq_status dq_finish(dq_plan* p, dq_state* out) {
   if (!pair.empty()) HIP_TRY(hipMemcpyAsync(pair.data(), p->d_pair_acc, pair.size() * sizeof(CorrPartial), hipMemcpyDeviceToHost, p->stream));
   if (p->has_pred) HIP_TRY(hipMemcpyAsync(&pred, p->d_pred_acc, sizeof(PredPartial), hipMemcpyDeviceToHost, p->stream));
   HIP_TRY(hipStreamSynchronize(p->stream));
+  // timed launches of this scan -> counters, their events back to the pool (no hipEventCreate in later scans)
+  if (dq_status s = resolve_timing(p)) return s;
 
   const int64_t rows = p->total_rows;
   const double nan = std::numeric_limits<double>::quiet_NaN();
