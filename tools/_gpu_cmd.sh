@@ -1,10 +1,6 @@
 set -o pipefail
-cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
+cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out profiles
 export TMPDIR=/tmp
-B="python -u bench.py --skip-headline --configs c3 --cpu-sample 0 --ingest-rows 0 --config-steps 6"
-for w in 2048 1024 4096 8192 16384 2048; do
-  DQ_PRED_WGS=$w timeout -k 10 200 $B > gpurun_out/pw_$w.json 2>/dev/null || exit $?
-  python3 -c "
-import json; d=json.loads(open('gpurun_out/pw_$w.json').read().strip().splitlines()[-1])['configs']['c3']
-print('$w', round(d['ms_per_step_median'],2), {k:round(x['avg_ms'],3) for k,x in d['kernels'].items()})"
-done
+TAG=r2o STEPS="tests" bash tools/gpu_r2.sh && \
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/smoke_r2o.log 2>&1 && \
+TAG=r2o STEPS="bench" bash tools/gpu_r2.sh
