@@ -1,6 +1,10 @@
 set -o pipefail
-cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out profiles
+cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
 export TMPDIR=/tmp
-TAG=r2o STEPS="tests" bash tools/gpu_r2.sh && \
-timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/smoke_r2o.log 2>&1 && \
-TAG=r2o STEPS="bench" bash tools/gpu_r2.sh
+B="python -u bench.py --configs= --cpu-sample 0 --ingest-rows 0 --steps 8"
+for s in 1 2 3 1 2; do
+  DQ_COLUMN_STREAMS=$s timeout -k 10 200 $B > gpurun_out/cs_$s.json 2>/dev/null || exit $?
+  python3 -c "
+import json; d=json.loads(open('gpurun_out/cs_$s.json').read().strip().splitlines()[-1])
+print('$s', round(d['value']/1e10,4), round(d['ms_per_step'],2))"
+done
