@@ -1397,8 +1397,14 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
   // lengths, deferred-round drains): utf8_hll 1.979 -> 1.949 ms per 125 M x 4 on the C5 headline (A/B
   // twice, DQ_VARIANT_RANGES=0 for the common size); halving the fp64 hash's ranges measured no change.
   // scale > 0: want x scale ranges, < 0: want / -scale
+  static const int32_t str_scale = [] {
+    // tuning override (diagnostic); utf8_hll per 125 M x 4 on one box: x1 1.979, x2 1.951 / 1.956,
+    // x3 1.963 / 1.964, x4 1.965 ms
+    const char* e = std::getenv("DQ_STR_RANGE_SCALE");
+    return e ? std::max(1, std::min(8, std::atoi(e))) : 2;
+  }();
   auto variant_scale = [](int32_t v) -> int32_t {
-    if (v == CV_UTF8_H || v == CV_LUTF8_H || v == CV_UTF8_HD || v == CV_LUTF8_HD) return 2;
+    if (v == CV_UTF8_H || v == CV_LUTF8_H || v == CV_UTF8_HD || v == CV_LUTF8_HD) return str_scale;
     return 1;
   };
   static const bool per_variant = !(std::getenv("DQ_VARIANT_RANGES") && std::getenv("DQ_VARIANT_RANGES")[0] == '0');
