@@ -36,7 +36,7 @@ PMC_FILE = os.path.join(ROOT, "profiles", "r2m_pmc.json")
 DEFAULT_CHUNK = 125_000_000  # 8 chunks per 1e9 rows; a UTF8 chunk's bytes (~2.0e9) stay < 2 GiB
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
@@ -53,7 +53,9 @@ def parse():
     p.add_argument("--ingest-rows", type=int, default=62_500_000,
                    help="rows of the host-resident Arrow C5 batch for the ingestion leg (0 = skip)")
     p.add_argument("--ingest-reps", type=int, default=4, help="uploads + scans of that batch timed end to end")
-    return p.parse_args()
+    p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                   help="process group for N > 1 (nccl = RCCL over xGMI; gloo: launcher tests with ranks sharing a GPU)")
+    return p.parse_args(argv)
 
 
 def launch_ranks(args) -> int:
@@ -103,7 +105,10 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local % max(1, torch.cuda.device_count())))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local % max(1, torch.cuda.device_count())))
+        else:
+            dist.init_process_group("gloo")
 
     from deequ_amd import _lib as L
     from deequ_amd import distributed, synth
@@ -196,7 +201,8 @@ def main():
         "config": {"workload": "C5 fused 16-col profile scan (8 f64 + 4 i64 + 4 utf8, 10% nulls) + state merge "
                                "+ incremental StateLoader append",
                    "rows_per_gpu": n_total, "chunk_rows": chunk, "analyzers": len(analyzers),
-                   "parallelism": f"row-shard x{world}"},
+                   "parallelism": f"row-shard x{world}",
+                   "collective": (f"{args.dist_backend} all-gather of the state slot sets" if world > 1 else None)},
         "hbm_frac_of_step": (algo_bytes_per_step / (elapsed / args.steps)) / 1e9 / HBM_PEAK_GBS,
         "rank_merge_ms_per_step": host_ms["merge"] / args.steps if world > 1 else 0.0,
         "append_ms_per_step": host_ms["append"] / args.steps,

@@ -483,3 +483,51 @@ void dqo_exact_comoments(int kx, const void* x, const uint8_t* vx, int ky, const
   for (int k = 0; k < 5; ++k) { out[1 + 2 * k] = s[k].hi; out[2 + 2 * k] = s[k].lo; }
   free(acc);
 }
+
+/*
+ * HLL registers of a large column on several threads (full-scale parity): partitions fold into private
+ * registers, merged by max (order-free, so the result equals dqo_hll_registers).  Also counts the rows
+ * that reach the GPU kernels' rare paths (test reporting only): paths[0] = selected rows whose hash has
+ * bits 54..32 zero (the rank needs the low word: exact redo), paths[1] = selected strings longer than 28
+ * bytes, paths[2] = selected strings whose 32-byte window (from the dword holding their first byte)
+ * crosses the end of the chunk's string bytes (both take the general XXH64 loop).
+ */
+void dqo_hll_registers_mt(int kind, const void* values, const void* offsets, const uint8_t* validity,
+                          const uint8_t* mask, int64_t n, int nthreads, uint8_t* regs /* [512], accumulated */,
+                          int64_t* paths /* [3] */) {
+  int nb = 1024;
+  uint8_t* pr = (uint8_t*)calloc((size_t)nb, 512);
+  int64_t* pc = (int64_t*)calloc((size_t)nb * 3, sizeof(int64_t));
+  int64_t total = 0;
+  if (kind == K_UTF8) total = ((const int32_t*)offsets)[n];
+  if (kind == K_LARGE_UTF8) total = ((const int64_t*)offsets)[n];
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 1)
+#endif
+  for (int b = 0; b < nb; ++b) {
+    int64_t lo = part_bound(n, b, nb), hi = part_bound(n, b + 1, nb);
+    uint8_t* r = pr + (size_t)b * 512;
+    int64_t* c = pc + 3 * b;
+    for (int64_t i = lo; i < hi; ++i) {
+      if (!bit(validity, i) || !bit(mask, i)) continue;
+      uint64_t h = hash_row(kind, values, offsets, i);
+      hll_add(r, h);
+      c[0] += ((h >> 32) & 0x7FFFFFu) == 0;
+      if (kind == K_UTF8 || kind == K_LARGE_UTF8) {
+        int64_t o0 = kind == K_UTF8 ? ((const int32_t*)offsets)[i] : ((const int64_t*)offsets)[i];
+        int64_t o1 = kind == K_UTF8 ? ((const int32_t*)offsets)[i + 1] : ((const int64_t*)offsets)[i + 1];
+        c[1] += o1 - o0 > 28;
+        c[2] += o1 - o0 <= 28 && (o0 & ~(int64_t)3) + 32 > total;
+      }
+    }
+  }
+  paths[0] = paths[1] = paths[2] = 0;
+  for (int b = 0; b < nb; ++b) {
+    const uint8_t* r = pr + (size_t)b * 512;
+    for (int i = 0; i < 512; ++i) if (r[i] > regs[i]) regs[i] = r[i];
+    for (int k = 0; k < 3; ++k) paths[k] += pc[3 * b + k];
+  }
+  free(pr);
+  free(pc);
+}

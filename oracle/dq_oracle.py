@@ -886,6 +886,154 @@ class OracleExpr:
         raise ValueError(kind)
 
 
+class NpPredicate:
+    """OracleExpr's semantics vectorised with numpy, for the numeric predicates of the full-scale parity
+    runs (Compliance over 1e9 rows; the per-row evaluator above is the reference at small n and
+    tests/test_oracle.py checks the two agree).  cols: {name: (dtype, values ndarray, valid bool ndarray)}
+    with numeric dtypes only.
+
+    Value model: (kind, v, notnull), kind in {int, dec, dbl, bool, null}; int / dec hold int64 arrays (a
+    column, or an integral decimal coalesced into one) or Python ints / Fractions (literals).  int vs dec
+    compares exactly (Spark 2.2 widens LongType vs DECIMAL to a decimal); anything vs double compares in
+    double with NaN as the largest value (nanSafe ordering), as _cmp does.
+    """
+
+    def __init__(self, text: str):
+        self.expr = OracleExpr(text)
+
+    def eval_bool(self, cols: dict, n: int):
+        """(TRUE rows, non-NULL rows) as bool arrays."""
+        kind, v, nn = self._ev(self.expr.ast, cols, n)
+        if kind == "null":
+            z = np.zeros(n, dtype=bool)
+            return z, z
+        assert kind == "bool", self.expr.text
+        return np.broadcast_to(np.asarray(v, dtype=bool), (n,)) & nn, nn
+
+    def _ev(self, e, cols, n):
+        from fractions import Fraction
+
+        kind = e[0]
+        if kind == "lit":
+            typ, v = e[1], e[2]
+            if typ == "null":
+                return "null", None, np.zeros(n, dtype=bool)
+            if typ == "str":
+                raise NotImplementedError("string literal")
+            return typ, v, np.ones(n, dtype=bool)
+        if kind == "col":
+            dtype, vals, valid = cols[e[1]]
+            if dtype == "f64":
+                return "dbl", np.asarray(vals, dtype=np.float64), np.asarray(valid, dtype=bool)
+            if dtype in ("i64", "i32"):
+                return "int", np.asarray(vals, dtype=np.int64), np.asarray(valid, dtype=bool)
+            raise NotImplementedError(dtype)
+        if kind == "coalesce":
+            parts = [self._ev(a, cols, n) for a in e[1]]
+            typ = _widen([p[0] for p in parts if p[0] != "null"])
+            if typ in ("int", "dec"):
+                vals, np_t = np.zeros(n, dtype=np.int64), np.int64
+            elif typ == "dbl":
+                vals, np_t = np.zeros(n, dtype=np.float64), np.float64
+            else:
+                raise NotImplementedError(typ)
+            nn = np.zeros(n, dtype=bool)
+            for pk, pv, pn in parts:
+                if pk == "null":
+                    continue
+                if typ != "dbl" and isinstance(pv, Fraction):
+                    if pv.denominator != 1:
+                        raise NotImplementedError("non-integral decimal in COALESCE over an integral column")
+                    pv = int(pv)
+                take = ~nn & pn
+                src = np.broadcast_to(np.asarray(float(pv) if typ == "dbl" and not isinstance(pv, np.ndarray) else pv,
+                                                 dtype=np_t), (n,))
+                vals[take] = src[take].astype(np_t)
+                nn |= pn
+            return typ, vals, nn
+        if kind == "cmp":
+            op = e[1]
+            ak, av, an = self._ev(e[2], cols, n)
+            bk, bv, bn = self._ev(e[3], cols, n)
+            nn = an & bn
+            if ak == "null" or bk == "null":
+                return "bool", np.zeros(n, dtype=bool), np.zeros(n, dtype=bool)
+            if "dbl" in (ak, bk):
+                return "bool", _np_cmp_dbl(op, _as_f64(av), _as_f64(bv)) & nn, nn
+            return "bool", _np_cmp_exact(op, av, bv, n) & nn, nn
+        if kind == "in":
+            ak, av, an = self._ev(e[1], cols, n)
+            t = np.zeros(n, dtype=bool)
+            anynull = ~an
+            for it in e[2]:
+                ik, iv, inn = self._ev(it, cols, n)
+                if ik == "null":
+                    anynull = anynull | ~inn
+                    continue
+                eq = _np_cmp_dbl("=", _as_f64(av), _as_f64(iv)) if "dbl" in (ak, ik) else _np_cmp_exact("=", av, iv, n)
+                t |= eq & an & inn
+                anynull = anynull | ~inn
+            return "bool", t, t | ~anynull
+        if kind in ("and", "or"):
+            _, av, an = self._ev(e[1], cols, n)
+            _, bv, bn = self._ev(e[2], cols, n)
+            a_t, b_t = np.asarray(av, dtype=bool) & an, np.asarray(bv, dtype=bool) & bn
+            a_f, b_f = ~np.asarray(av, dtype=bool) & an, ~np.asarray(bv, dtype=bool) & bn
+            t, f = (a_t & b_t, a_f | b_f) if kind == "and" else (a_t | b_t, a_f & b_f)
+            return "bool", t, t | f
+        if kind == "not":
+            _, av, an = self._ev(e[1], cols, n)
+            return "bool", ~np.asarray(av, dtype=bool) & an, an
+        if kind in ("isnull", "isnotnull"):
+            _, _, an = self._ev(e[1], cols, n)
+            return "bool", (~an if kind == "isnull" else an.copy()), np.ones(n, dtype=bool)
+        raise NotImplementedError(kind)
+
+
+def _as_f64(v):
+    return v.astype(np.float64) if isinstance(v, np.ndarray) else np.float64(float(v))
+
+
+def _np_cmp_dbl(op, x, y):
+    xn, yn = np.isnan(x), np.isnan(y)
+    with np.errstate(invalid="ignore"):
+        c = np.where(xn | yn, np.where(xn & yn, 0, np.where(xn, 1, -1)), (x > y).astype(np.int8) - (x < y))
+    return {"<": c < 0, "<=": c <= 0, ">": c > 0, ">=": c >= 0, "=": c == 0, "!=": c != 0}[op]
+
+
+def _np_cmp_exact(op, x, y, n):
+    """integers (int64 arrays) / exact literals (int, Fraction) compared exactly"""
+    import math as _m
+    from fractions import Fraction
+
+    if not isinstance(x, np.ndarray) and not isinstance(y, np.ndarray):
+        c = (x > y) - (x < y)
+        r = {"<": c < 0, "<=": c <= 0, ">": c > 0, ">=": c >= 0, "=": c == 0, "!=": c != 0}[op]
+        return np.full(n, r, dtype=bool)
+    if not isinstance(x, np.ndarray):  # literal op array  ->  array op' literal
+        op = {"<": ">", "<=": ">=", ">": "<", ">=": "<=", "=": "=", "!=": "!="}[op]
+        x, y = y, x
+    if isinstance(y, np.ndarray):
+        return {"<": x < y, "<=": x <= y, ">": x > y, ">=": x >= y, "=": x == y, "!=": x != y}[op]
+    q = Fraction(y)
+    lo, hi = -(1 << 63), (1 << 63) - 1
+    fl, ce = _m.floor(q), _m.ceil(q)
+
+    def bound(b):  # clamp an integer bound into int64 (comparisons with out-of-range bounds saturate)
+        return np.int64(min(max(b, lo), hi))
+
+    if op == "<":
+        return x < bound(ce) if ce <= hi else np.ones(n, dtype=bool)
+    if op == ">=":
+        return x >= bound(ce) if ce <= hi else np.zeros(n, dtype=bool)
+    if op == "<=":
+        return x <= bound(fl) if fl >= lo else np.zeros(n, dtype=bool)
+    if op == ">":
+        return x > bound(fl) if fl >= lo else np.ones(n, dtype=bool)
+    eq = (x == bound(fl)) if (q.denominator == 1 and lo <= fl <= hi) else np.zeros(n, dtype=bool)
+    return eq if op == "=" else ~eq
+
+
 def _widen(types):
     types = [t for t in types if t != "null"]
     if not types:

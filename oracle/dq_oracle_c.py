@@ -44,6 +44,7 @@ def lib():
         L.dqo_corr.argtypes = [ctypes.c_int, vp, u8p, ctypes.c_int, vp, u8p, u8p, ctypes.c_int64,
                                ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
         L.dqo_hll_registers.argtypes = [ctypes.c_int, vp, vp, u8p, u8p, ctypes.c_int64, vp]
+        L.dqo_hll_registers_mt.argtypes = [ctypes.c_int, vp, vp, u8p, u8p, ctypes.c_int64, ctypes.c_int, vp, vp]
         L.dqo_count_bits.restype = ctypes.c_int64
         L.dqo_count_bits.argtypes = [u8p, u8p, ctypes.c_int64]
         L.dqo_profile_scan.argtypes = [ctypes.c_int, vp, vp, vp, vp, ctypes.c_int64, ctypes.c_int,
@@ -83,6 +84,16 @@ def hll_registers(kind, values, offsets, validity, mask, n) -> np.ndarray:
     regs = np.zeros(512, dtype=np.uint8)
     lib().dqo_hll_registers(KINDS[kind], _p(values), _p(offsets), _p(validity), _p(mask), n, _p(regs))
     return regs
+
+
+def hll_registers_mt(kind, values, offsets, validity, mask, n, nthreads, regs=None):
+    """(registers accumulated into `regs`, {redo, long, window}: rows reaching the kernels' rare paths)."""
+    if regs is None:
+        regs = np.zeros(512, dtype=np.uint8)
+    paths = np.zeros(3, dtype=np.int64)
+    lib().dqo_hll_registers_mt(KINDS[kind], _p(values), _p(offsets), _p(validity), _p(mask), n, nthreads, _p(regs),
+                               _p(paths))
+    return regs, {"redo": int(paths[0]), "long": int(paths[1]), "window": int(paths[2])}
 
 
 def profile_scan(cols, n, nparts, nthreads):

@@ -165,3 +165,28 @@ def test_state_bytes_and_identifier():
     assert img[:4] == bytes.fromhex("00000028") and len(img) == 44 and img[-1] == 5
     # scala.util.hashing.MurmurHash3.stringHash("", 42) == avalanche(42 ^ 0)
     assert isinstance(O.murmur3_string_hash("Size(None)"), int)
+
+
+def test_vectorised_predicates_match_the_row_evaluator():
+    """NpPredicate (the full-scale runs' Compliance oracle) == OracleExpr row by row, incl. C3's predicates,
+    decimal literals against int64 (exact), COALESCE, NULL logic, IN, doubles with NaN."""
+    rng = np.random.default_rng(3)
+    n = 4000
+    i0 = rng.integers(-2000, 2000, n).astype(np.int64)
+    i1 = rng.integers(-5, 1200, n).astype(np.int64)
+    i1[::97] = (1 << 62) + 7
+    f = rng.normal(0, 5, n)
+    f[::53] = np.nan
+    cols = {"i0": ("i64", i0, rng.random(n) > 0.1), "i1": ("i64", i1, rng.random(n) > 0.2),
+            "i2": ("i64", rng.integers(-3, 3, n).astype(np.int64), rng.random(n) > 0.1),
+            "i3": ("i64", rng.integers(-3, 3, n).astype(np.int64), rng.random(n) > 0.3),
+            "f": ("f64", f, rng.random(n) > 0.1)}
+    preds = ["i0 >= 0", "`i1` IS NULL OR (`i1` >= 10.0 AND `i1` <= 1000.0)", "i2 < i3", "COALESCE(i3, 0.0) >= 0",
+             "i0 > 2.5", "i0 <= -3.5", "i0 = 7.0", "i0 != 7.5", "i1 < 4611686018427387911", "f >= 0.5",
+             "f < i0", "NOT (i2 = i3) OR f IS NULL", "i0 IN (1, 2, 3.0)", "f > 1e0 AND i3 IS NOT NULL",
+             "COALESCE(f, i0) > 0", "i2 >= NULL", "i0 < 1e30", "i0 > -99999999999999999999.5"]
+    ocols = {k: O.OColumn(t, v, valid) for k, (t, v, valid) in cols.items()}
+    for p in preds:
+        t_ref, nn_ref = O.OracleExpr(p).eval_bool(ocols, n)
+        t_np, nn_np = O.NpPredicate(p).eval_bool(cols, n)
+        assert (t_ref == t_np).all() and (nn_ref == nn_np).all(), p
