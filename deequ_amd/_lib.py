@@ -8,6 +8,8 @@ from __future__ import annotations
 import ctypes
 import os
 
+ABI_VERSION = 2  # include/dqscan.h DQ_ABI_VERSION
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DQ_LIB_PATH") or os.path.join(_HERE, "libdqscan.so")  # override: diagnostic A/B builds
 
@@ -245,8 +247,8 @@ def _load():
     L.dq_state_from_bytes.argtypes = [c.c_int32, c.c_char_p, c.c_int64, P(State)]
     L.dq_state_identifier.restype = c.c_int32
     L.dq_state_identifier.argtypes = [c.c_char_p]
-    if L.dq_abi_version() != 1:
-        raise ImportError(f"libdqscan ABI {L.dq_abi_version()} != 1")
+    if L.dq_abi_version() != ABI_VERSION:
+        raise ImportError(f"libdqscan ABI {L.dq_abi_version()} != {ABI_VERSION}")
     return L
 
 

@@ -41,12 +41,50 @@ int32_t type_of_format(const char* f) {
   return 0;
 }
 
-// parallel memcpy of a list of (dst, src, bytes) pieces over up to `threads` CPU threads
+// parallel copy of a list of pieces over up to `threads` CPU threads.  A piece is a memcpy, or -- for an
+// Arrow slice -- a rebase of its string offsets (minus the slice's first offset) or a shift of its
+// validity bitmap (the slice's row 0 at bit `shift` of the first source byte).
 struct Piece {
   char* dst;
   const char* src;
-  int64_t bytes;
+  int64_t bytes;           // destination bytes
+  int kind = 0;            // 0 memcpy, 1 int32 offsets - base, 2 int64 offsets - base, 3 bitmap >> shift
+  int64_t base = 0;        // kinds 1, 2
+  int shift = 0;           // kind 3 (1..7)
+  int64_t src_bytes = 0;   // kind 3: readable source bytes
 };
+
+void copy_part(const Piece& p, int64_t a, int64_t b) {  // destination bytes [a, b) of piece p
+  switch (p.kind) {
+    case 0: std::memcpy(p.dst + a, p.src + a, (size_t)(b - a)); break;
+    case 1: {
+      const int32_t base = (int32_t)p.base;
+      for (int64_t i = a / 4; i < b / 4; ++i) {
+        int32_t v;
+        std::memcpy(&v, p.src + 4 * i, 4);
+        v -= base;
+        std::memcpy(p.dst + 4 * i, &v, 4);
+      }
+      break;
+    }
+    case 2:
+      for (int64_t i = a / 8; i < b / 8; ++i) {
+        int64_t v;
+        std::memcpy(&v, p.src + 8 * i, 8);
+        v -= p.base;
+        std::memcpy(p.dst + 8 * i, &v, 8);
+      }
+      break;
+    default: {
+      const uint8_t* src = reinterpret_cast<const uint8_t*>(p.src);
+      for (int64_t i = a; i < b; ++i) {
+        const uint32_t lo = src[i], hi = i + 1 < p.src_bytes ? src[i + 1] : 0u;
+        p.dst[i] = (char)(uint8_t)((lo >> p.shift) | (hi << (8 - p.shift)));
+      }
+    }
+  }
+}
+
 void parallel_copy(const std::vector<Piece>& pieces, int threads) {
   int64_t total = 0;
   for (const Piece& p : pieces) total += p.bytes;
@@ -54,16 +92,20 @@ void parallel_copy(const std::vector<Piece>& pieces, int threads) {
   const int n = (int)std::max<int64_t>(1, std::min<int64_t>(threads, total / kGrain));
   if (n <= 1) {
     for (const Piece& p : pieces)
-      if (p.bytes) std::memcpy(p.dst, p.src, (size_t)p.bytes);
+      if (p.bytes) copy_part(p, 0, p.bytes);
     return;
   }
-  // split the concatenated byte range [0, total) into n contiguous shares
+  // split the concatenated byte range [0, total) into n contiguous shares; inside a piece the share
+  // boundaries are rounded down to 8 bytes (whole offsets), the same way on both sides of a boundary
   auto work = [&](int t) {
     const int64_t lo = total * t / n, hi = total * (t + 1) / n;
     int64_t at = 0;
     for (const Piece& p : pieces) {
-      const int64_t a = std::max(lo, at), b = std::min(hi, at + p.bytes);
-      if (a < b) std::memcpy(p.dst + (a - at), p.src + (a - at), (size_t)(b - a));
+      if (at + p.bytes > lo && at < hi) {
+        const int64_t a = lo <= at ? 0 : ((lo - at) & ~int64_t(7));
+        const int64_t b = hi >= at + p.bytes ? p.bytes : ((hi - at) & ~int64_t(7));
+        if (a < b) copy_part(p, a, b);
+      }
       at += p.bytes;
       if (at >= hi) break;
     }
@@ -106,18 +148,25 @@ dq_status dq_arrow_import(const struct ArrowSchema* schema, const struct ArrowAr
                      (long long)array->n_buffers);
   const int64_t n = array->length, off = array->offset;
   if (n < 0 || off < 0) return set_error(DQ_E_INVALID, "Arrow array with negative length / offset");
-  const uint8_t* validity = static_cast<const uint8_t*>(array->buffers[0]);
-  if (array->null_count == 0) validity = nullptr;  // buffers[0] may be NULL then
-  if (validity && (off & 7) != 0)
-    return set_error(DQ_E_UNSUPPORTED,
-                     "Arrow array slice at row offset %lld: validity bit 0 is not row 0 (re-slice at a multiple of 8)",
-                     (long long)off);
   dq_host_column c{};
   c.type = type;
-  c.nullable = validity ? 1 : 0;
   c.n_rows = n;
+  if (n == 0) {  // producers may export NULL buffers for an empty array: touch none
+    *out = c;
+    return DQ_OK;
+  }
+  const uint8_t* validity = static_cast<const uint8_t*>(array->buffers[0]);
+  if (array->null_count == 0) validity = nullptr;  // buffers[0] may be NULL then
+  if (array->null_count != 0 && !validity && array->null_count != -1)
+    return set_error(DQ_E_INVALID, "Arrow array with %lld nulls and no validity buffer", (long long)array->null_count);
+  if (!array->buffers[1]) return set_error(DQ_E_INVALID, "Arrow array of format '%s' without its %s buffer",
+                                           schema->format, str ? "offsets" : "values");
+  c.nullable = validity ? 1 : 0;
+  // a slice (RecordBatch.slice, to_batches(max_chunksize)): row 0 is bit off % 8 of byte off / 8; dq_upload
+  // shifts the bitmap into place while it copies
   c.validity = validity ? validity + off / 8 : nullptr;
   c.validity_bytes = validity ? (n + 7) / 8 : 0;
+  c.validity_bit = validity ? (int32_t)(off & 7) : 0;
   if (!str) {
     const int64_t w = type == DQ_TYPE_I32 ? 4 : 8;
     c.values = static_cast<const char*>(array->buffers[1]) + off * w;
@@ -135,13 +184,14 @@ dq_status dq_arrow_import(const struct ArrowSchema* schema, const struct ArrowAr
       o0 = reinterpret_cast<const int64_t*>(offs)[0];
       o1 = reinterpret_cast<const int64_t*>(offs)[n];
     }
-    if (o0 != 0)
-      return set_error(DQ_E_UNSUPPORTED, "Arrow string slice whose first offset is %lld (dq offsets start at 0)",
-                       (long long)o0);
+    if (o0 < 0 || o1 < o0) return set_error(DQ_E_INVALID, "Arrow string offsets %lld..%lld", (long long)o0, (long long)o1);
+    if (o1 > o0 && !array->buffers[2]) return set_error(DQ_E_INVALID, "Arrow string array without its data buffer");
+    // a slice's offsets start at o0: dq_upload copies the bytes from o0 and writes offsets - o0
     c.offsets = offs;
     c.offset_bytes = (n + 1) * w;
-    c.values = array->buffers[2];
-    c.value_bytes = o1;
+    c.offset_base = o0;
+    c.values = o1 > o0 ? static_cast<const char*>(array->buffers[2]) + o0 : nullptr;
+    c.value_bytes = o1 - o0;
   }
   *out = c;
   return DQ_OK;
@@ -189,6 +239,8 @@ dq_status dq_upload(dq_uploader* u, const dq_host_column* cols, int32_t n_cols, 
   std::vector<int64_t> pos(3 * (size_t)n_cols, -1);
   for (int32_t c = 0; c < n_cols; ++c) {
     const dq_host_column& h = cols[c];
+    if (h.validity_bit < 0 || h.validity_bit > 7 || h.offset_base < 0)
+      return set_error(DQ_E_INVALID, "dq_upload: column %d: bad slice rebase", c);
     const void* src[3] = {h.values, h.validity, h.offsets};
     const int64_t len[3] = {h.value_bytes, h.validity_bytes, h.offset_bytes};
     for (int k = 0; k < 3; ++k) {
@@ -209,9 +261,20 @@ dq_status dq_upload(dq_uploader* u, const dq_host_column* cols, int32_t n_cols, 
     const dq_host_column& h = cols[c];
     const void* src[3] = {h.values, h.validity, h.offsets};
     const int64_t len[3] = {h.value_bytes, h.validity_bytes, h.offset_bytes};
-    for (int k = 0; k < 3; ++k)
-      if (pos[3 * (size_t)c + k] >= 0)
-        pieces.push_back({u->pinned[(size_t)s] + pos[3 * (size_t)c + k], static_cast<const char*>(src[k]), len[k]});
+    for (int k = 0; k < 3; ++k) {
+      if (pos[3 * (size_t)c + k] < 0) continue;
+      Piece p{u->pinned[(size_t)s] + pos[3 * (size_t)c + k], static_cast<const char*>(src[k]), len[k]};
+      if (k == 1 && h.validity_bit) {
+        p.kind = 3;
+        p.shift = h.validity_bit;
+        p.src_bytes = (h.validity_bit + h.n_rows + 7) / 8;
+      }
+      if (k == 2 && h.offset_base) {
+        p.kind = h.type == DQ_TYPE_UTF8 ? 1 : 2;
+        p.base = h.offset_base;
+      }
+      pieces.push_back(p);
+    }
   }
   parallel_copy(pieces, u->threads);
   // the scan that last read the device slot must have passed its release before the DMA overwrites it

@@ -255,28 +255,33 @@ dq_status state_combine(const dq_state& a, const dq_state& b, dq_state& o) {
            [&] { o.u.ratio.count = wrap_add(a.u.ratio.count, b.u.ratio.count); });
       break;
     // integral columns: Spark's partial buffers hold the LongType sum, the final merge adds them (wrapping)
-    // and the CAST to double comes last -- adding the cast doubles would differ once a shard's sum wraps
+    // and the CAST to double comes last -- adding the cast doubles would differ once a shard's sum wraps.
+    // A partial that is already a double (a deserialized or Analyzers.merge-d state: SumState / MeanState
+    // hold doubles, Sum.scala:27-29, Mean.scala:27-31) combines by double addition.
     case DQ_OP_SUM:
-      if (a.integral != b.integral) return set_error(DQ_E_STATE, "dq_state_combine: integral and double Sum partials");
-      pick(0, [] {}, [&] { o.u.sum = b.u.sum; }, [&] {
-        if (a.integral) {
+      pick(0, [] {}, [&] { o.u.sum = b.u.sum; o.integral = b.integral; }, [&] {
+        if (a.integral && b.integral) {
           o.u.sum.partial = wrap_add(a.u.sum.partial, b.u.sum.partial);
           o.u.sum.sum = (double)o.u.sum.partial;
         } else {
           o.u.sum.sum = a.u.sum.sum + b.u.sum.sum;
+          o.u.sum.partial = 0;
+          o.integral = 0;
         }
       });
       break;
     case DQ_OP_MEAN:
-      if (a.integral != b.integral) return set_error(DQ_E_STATE, "dq_state_combine: integral and double Mean partials");
-      pick(0, [] {}, [&] { o.u.mean.sum = b.u.mean.sum; o.u.mean.partial = b.u.mean.partial; }, [&] {
-        if (a.integral) {
-          o.u.mean.partial = wrap_add(a.u.mean.partial, b.u.mean.partial);
-          o.u.mean.sum = (double)o.u.mean.partial;
-        } else {
-          o.u.mean.sum = a.u.mean.sum + b.u.mean.sum;
-        }
-      });
+      pick(0, [] {}, [&] { o.u.mean.sum = b.u.mean.sum; o.u.mean.partial = b.u.mean.partial; o.integral = b.integral; },
+           [&] {
+             if (a.integral && b.integral) {
+               o.u.mean.partial = wrap_add(a.u.mean.partial, b.u.mean.partial);
+               o.u.mean.sum = (double)o.u.mean.partial;
+             } else {
+               o.u.mean.sum = a.u.mean.sum + b.u.mean.sum;
+               o.u.mean.partial = 0;
+               o.integral = 0;
+             }
+           });
       pick(1, [] {}, [&] { o.u.mean.count = b.u.mean.count; },
            [&] { o.u.mean.count = wrap_add(a.u.mean.count, b.u.mean.count); });
       break;

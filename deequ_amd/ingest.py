@@ -43,7 +43,8 @@ ArrowArrayC._fields_ = [("length", ctypes.c_int64), ("null_count", ctypes.c_int6
 class HostColumn(ctypes.Structure):
     _fields_ = [("type", ctypes.c_int32), ("nullable", ctypes.c_int32), ("n_rows", ctypes.c_int64),
                 ("values", ctypes.c_void_p), ("validity", ctypes.c_void_p), ("offsets", ctypes.c_void_p),
-                ("value_bytes", ctypes.c_int64), ("validity_bytes", ctypes.c_int64), ("offset_bytes", ctypes.c_int64)]
+                ("value_bytes", ctypes.c_int64), ("validity_bytes", ctypes.c_int64), ("offset_bytes", ctypes.c_int64),
+                ("offset_base", ctypes.c_int64), ("validity_bit", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 def _bind():

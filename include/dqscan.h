@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define DQ_ABI_VERSION 1
+#define DQ_ABI_VERSION 2  /* 2: dq_state.reserved[0] = integral flag + Sum / Mean int64 partials; ingestion, pool and state-array entry points */
 
 typedef int32_t dq_status;
 #define DQ_OK 0
@@ -169,19 +169,23 @@ struct ArrowArray {
 #endif /* ARROW_C_DATA_INTERFACE */
 
 /* One column's HOST buffers (what dq_arrow_import finds in an ArrowArray; the caller keeps the Arrow
- * array alive until dq_upload returns).  Byte counts are the bytes dq_upload copies. */
+ * array alive until dq_upload returns).  Byte counts are the bytes dq_upload writes to the device. */
 typedef struct dq_host_column {
   int32_t type;            /* enum dq_type */
   int32_t nullable;        /* 1 iff validity != NULL */
   int64_t n_rows;
-  const void* values;      /* fixed-width values / UTF8 data bytes */
-  const uint8_t* validity; /* LSB-first bitmap, bit 0 = row 0; NULL = no nulls */
-  const void* offsets;     /* UTF8: n_rows + 1 offsets starting at 0 */
+  const void* values;      /* fixed-width values / UTF8 data bytes (from the first string's first byte) */
+  const uint8_t* validity; /* LSB-first bitmap: row 0 is bit validity_bit of byte 0; NULL = no nulls */
+  const void* offsets;     /* UTF8: n_rows + 1 offsets; offsets[0] == offset_base */
   int64_t value_bytes, validity_bytes, offset_bytes;
+  int64_t offset_base;     /* subtracted from every offset by dq_upload (an Arrow slice's first offset) */
+  int32_t validity_bit;    /* 0..7: dq_upload shifts the bitmap so that row 0 lands on bit 0 */
+  int32_t reserved;
 } dq_host_column;
 /* Map an exported Arrow array (formats g = float64, l = int64, i = int32, u = utf8, U = large_utf8) to
- * host column buffers.  DQ_E_UNSUPPORTED: other types, nested / dictionary arrays, a slice whose
- * validity does not start at a byte boundary or whose string offsets do not start at 0 (re-slice). */
+ * host column buffers; slices at any row offset are rebased by dq_upload.  DQ_E_UNSUPPORTED: other
+ * types, nested / dictionary arrays.  DQ_E_INVALID: a required buffer is NULL (an empty array may
+ * export NULL buffers: it maps to an empty column). */
 dq_status dq_arrow_import(const struct ArrowSchema* schema, const struct ArrowArray* array, dq_host_column* out);
 /* Pinned, n-buffered host -> device upload.  dq_upload copies one chunk's columns (CPU threads: host ->
  * pinned slot; DMA on the uploader's own stream: pinned -> device slot) and returns device views of the

@@ -31,7 +31,7 @@ def test_header_symbols_exported(dq):
     for name in declared:
         assert hasattr(L.lib, name), name
     assert declared == set(L.EXPORTED)
-    assert L.lib.dq_abi_version() == 1
+    assert L.lib.dq_abi_version() == L.ABI_VERSION == 2
 
 
 def test_struct_layouts(dq):
@@ -259,3 +259,45 @@ def test_plan_create_without_gpu_reports_error(dq):
     h = ctypes.c_void_p()
     rc = L.lib.dq_plan_create(specs, 1, sch, 0, None, 0, 0, ctypes.byref(h))
     assert rc != L.DQ_OK and L.lib.dq_last_error()
+
+
+def test_combine_integral_with_double_partials(dq):
+    """dq_state_combine of Sum / Mean slot sets: two fresh integral partials add as wrapping int64 (Spark's
+    LongType partial buffers); a partial that is already a double (deserialized, or Analyzers.merge-d with a
+    loaded state) combines with a fresh integral one by double addition instead of failing."""
+    import ctypes
+
+    from deequ_amd import _lib as L
+
+    def mk(op, integral, partial, sum_, count=0):
+        s = L.State()
+        s.op = op
+        s.has_value[0] = s.has_value[1] = 1
+        s.integral = integral
+        if op == L.OP_SUM:
+            s.u.sum.sum, s.u.sum.partial = sum_, partial
+        else:
+            s.u.mean.sum, s.u.mean.partial, s.u.mean.count = sum_, partial, count
+        return s
+
+    big = (1 << 63) - 5
+    for op in (L.OP_SUM, L.OP_MEAN):
+        out = L.State()
+        # two integral partials: the int64 sum wraps before the cast (Spark), not the doubles
+        L.check(L.lib.dq_state_combine(ctypes.byref(mk(op, 1, big, float(big), 1)), ctypes.byref(mk(op, 1, 10, 10.0, 2)),
+                                       ctypes.byref(out)))
+        u = out.u.sum if op == L.OP_SUM else out.u.mean
+        assert out.integral == 1 and u.partial == big + 10 - (1 << 64) and u.sum == float(big + 10 - (1 << 64))
+        # integral + double (either order): double addition, the result is a double partial
+        for a, b in ((mk(op, 1, 7, 7.0, 1), mk(op, 0, 0, 2.5, 1)), (mk(op, 0, 0, 2.5, 1), mk(op, 1, 7, 7.0, 1))):
+            L.check(L.lib.dq_state_combine(ctypes.byref(a), ctypes.byref(b), ctypes.byref(out)))
+            u = out.u.sum if op == L.OP_SUM else out.u.mean
+            assert out.integral == 0 and u.sum == 9.5
+            if op == L.OP_MEAN:
+                assert out.u.mean.count == 2
+        # a NULL side takes the other's partial and kind
+        a = mk(op, 1, 4, 4.0, 1)
+        nul = mk(op, 0, 0, 0.0, 0)
+        nul.has_value[0] = 0
+        L.check(L.lib.dq_state_combine(ctypes.byref(nul), ctypes.byref(a), ctypes.byref(out)))
+        assert out.integral == 1 and (out.u.sum if op == L.OP_SUM else out.u.mean).partial == 4

@@ -207,3 +207,27 @@ def test_all_f64_pair_pass_vs_oracle(dq, n, where, glds, monkeypatch):
     if where is not None:
         wm = cols["w"][2] & (cols["w"][1] > 2)
     _check(dq, cols, states, an, n, wm)
+
+
+@pytest.mark.parametrize("n", [4097, 200_003])
+def test_pair_pass_drift_and_offset_columns(dq, n):
+    """Columns whose first rows are not representative of the rest: a linear trend around 1e9, a sorted
+    column, a large offset with unit noise, and a first 64 / 128-row block far from everything after it
+    (the pass's shifted sums take their shift from a range's first rows).  Correlation, Mean,
+    StandardDeviation vs the oracle (Spark's sequential update order) within the fp64 bar."""
+    from deequ_amd.runner import scan_states
+    from deequ_amd.table import column_from_numpy
+
+    rng = np.random.default_rng(n)
+    i = np.arange(n, dtype=np.float64)
+    noise = rng.normal(size=n)
+    cols = {"trend": 1e9 + i, "sorted": np.sort(rng.normal(0, 1000, n)), "offset": 1e12 + noise,
+            "step64": np.where(i < 64, 0.0, 1e9 + noise), "step128": np.where(i < 128, -1e6, 3e8 + 0.5 * i + noise),
+            "mixed": 0.5 * (1e9 + i) + 3.0 * noise}
+    valid = {k: rng.random(n) > 0.05 for k in cols}
+    tbl = dq.Table([column_from_numpy(k, "f64", v, valid[k]) for k, v in cols.items()])
+    names = list(cols)
+    an = [dq.Correlation(names[a], names[b]) for a in range(len(names)) for b in range(a + 1, len(names))]
+    for c in names:
+        an += [dq.Mean(c), dq.StandardDeviation(c)]
+    _check(dq, {k: ("f64", v, valid[k]) for k, v in cols.items()}, scan_states(tbl, an), an, n, None)
