@@ -1,0 +1,47 @@
+"""Host C++ under AddressSanitizer + UndefinedBehaviorSanitizer (CPU only).
+
+`make -C deequ_amd asan` builds build/asan/libdqscan.so with the planner, predicate compiler, state I/O,
+regex compiler and Arrow import instrumented (-fsanitize=address,undefined, no recovery); the kernels'
+objects are the normal ones -- the GPU sanitizer is not available on this pool.  The CPU tests that
+drive that code (the ctypes boundary tests, the regex compiler tests, the Arrow import tests and the
+hypothesis fuzz of tests/test_fuzz_host.py) then run in a child process that preloads the sanitizer
+runtime and loads the instrumented library (DQ_LIB_PATH); any report fails the test.
+"""
+from __future__ import annotations
+
+import glob
+import os
+import subprocess
+import sys
+
+import pytest
+
+from tests.conftest import ROOT
+
+ASAN_LIB = os.path.join(ROOT, "deequ_amd", "build", "asan", "libdqscan.so")
+TESTS = ["tests/test_fuzz_host.py", "tests/test_boundary.py", "tests/test_regex.py", "tests/test_ingest.py",
+         "tests/test_oracle.py"]
+
+
+def _runtime():
+    hits = sorted(glob.glob("/opt/rocm/lib/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so"))
+    return hits[-1] if hits else None
+
+
+def test_host_code_clean_under_asan_ubsan():
+    rt = _runtime()
+    if rt is None:
+        pytest.skip("no clang ASan runtime in this image")
+    if not os.path.exists(ASAN_LIB):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "deequ_amd"), "asan"], check=True)
+    syms = subprocess.run(["nm", "-D", ASAN_LIB], capture_output=True, text=True).stdout
+    assert "__asan_report" in syms and "__ubsan_handle" in syms, "library is not instrumented"
+    env = dict(os.environ)
+    env.update(LD_PRELOAD=rt, DQ_LIB_PATH=ASAN_LIB,
+               ASAN_OPTIONS="detect_leaks=0:abort_on_error=1:halt_on_error=1",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
+    out = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-m", "not gpu", "-p", "no:cacheprovider"] + TESTS,
+                         cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
+    text = out.stdout + out.stderr
+    assert out.returncode == 0, text[-4000:]
+    assert "AddressSanitizer" not in text and "runtime error:" not in text, text[-4000:]
