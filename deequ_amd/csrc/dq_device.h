@@ -65,10 +65,9 @@ struct PairTask {
   int32_t pad[3];
 };
 
-// Correlation pairs sharing <= 8 distinct columns and one `where`: one LDS row tile serves them all.
+// Correlation pairs sharing <= 8 distinct columns and one `where` (host-side planning unit; staged together).
 constexpr int kTileCols = 8;
 constexpr int kTilePairs = 32;
-constexpr int kTileRows = 512;
 struct PairGroup {
   int32_t ncols;
   int32_t npairs;
@@ -77,28 +76,32 @@ struct PairGroup {
   int32_t cols[kTileCols];          // plan column indices
   int32_t kinds[kTileCols];         // CK_F64 / CK_I64 / CK_I32
   int8_t pi[kTilePairs], pj[kTilePairs];  // local column index of x / y per pair
-  int32_t mom_task[kTileCols];      // MFMA pass: column-moments task fused for local column c, or -1
 };
 
-// Lane-per-row Correlation pass (dq_pair.hip): one wave task = up to kLaneCols columns of a pair group, the
-// active slots of the fixed pattern of all kLaneSlots pairs over those positions, and the column-moment
-// tasks (Mean / StandardDeviation / Sum / Min / Max of the same rows and `where`) of positions
-// 0 .. kLaneMoments-1, fused so each column is read from HBM once for its correlations AND its moments.
-constexpr int kLaneCols = 5;
-constexpr int kLaneSlots = 10;
-constexpr int kLaneMoments = 2;
-constexpr int kLaneSlotA[kLaneSlots] = {0, 0, 0, 0, 1, 1, 1, 2, 2, 3};
-constexpr int kLaneSlotB[kLaneSlots] = {1, 2, 3, 4, 2, 3, 4, 3, 4, 4};
+// Correlation pass (dq_pair.hip).  A workgroup task is one pair group (<= 8 columns, one `where`) and two
+// wave tasks.  Wave w's position p holds the group's local column (p + w) % 8; both waves run the same
+// fixed pattern of kPairSlots slots over their 8 positions, and the two rotations of that pattern are
+// every pair of 8 columns exactly once (28 = 2 x 14).  The column-moment tasks (Mean / StandardDeviation /
+// Sum / Min / Max of the same rows and `where`) sit at the even positions (local column c: wave c % 2,
+// position c - c % 2), fused so each column is read from HBM once for its correlations AND its moments.
+constexpr int kPairWaves = 2;
+constexpr int kPairPos = 8;
+constexpr int kPairSlots = 14;
+constexpr int kPairMoments = 4;              // at positions 0, 2, 4, 6
+constexpr int kPairSlotA[kPairSlots] = {0, 2, 4, 6, 0, 2, 4, 6, 0, 2, 4, 6, 0, 2};
+constexpr int kPairSlotB[kPairSlots] = {1, 3, 5, 7, 2, 4, 6, 0, 3, 5, 7, 1, 4, 6};
 struct PairWaveTask {
-  int32_t ncols;                   // positions in use (0: an idle padding task)
   int32_t where;                   // where-bitmap index or -1
-  uint32_t pair_mask;              // bit q: slot q (positions kLaneSlotA[q], kLaneSlotB[q]) is a pair task
-  uint32_t mom_mask;               // bit p: position p has a column-moments task
-  uint32_t swap_mask;              // bit q: the pair task's first column is position kLaneSlotB[q]
-  int32_t cols[kLaneCols];         // plan column indices
-  int32_t kinds[kLaneCols];        // CK_F64 / CK_I64 / CK_I32
-  int32_t pair_out[kLaneSlots];    // pair-task index of each active slot
-  int32_t mom_out[kLaneMoments];   // column-task index of each moments position
+  uint32_t pair_mask;              // bit q: slot q (positions kPairSlotA[q], kPairSlotB[q]) is a pair task
+  uint32_t mom_mask;               // bit m: position 2 m has a column-moments task
+  uint32_t swap_mask;              // bit q: the pair task's first column is position kPairSlotB[q]
+  int32_t cols[kPairPos];          // plan column indices (an unused position repeats a used column)
+  int32_t kinds[kPairPos];         // CK_F64 / CK_I64 / CK_I32
+  int32_t pair_out[kPairSlots];    // pair-task index of each active slot
+  int32_t mom_out[kPairMoments];   // column-task index of each moments position
+};
+struct PairWG {
+  PairWaveTask wave[kPairWaves];
 };
 
 // Per-workgroup partial of one column task.  Moments are Chan-mergeable (n, mean, m2).

@@ -6,10 +6,9 @@
 //                     Compliance / conditional-count counters, and `where` TRUE bitmaps.
 //   2. dq_column_scan<V>: single-column tasks (Completeness, Sum, Mean, StandardDeviation,
 //                     Minimum, Maximum, ApproxCountDistinct), one launch per variant V (column kind x
-//                     accumulators), optionally spread over several HIP streams so HBM-bound and
-//                     VALU-bound (XXH64) variants run side by side on the 256 CUs.
-//   3. dq_pair_tile_scan (only if Correlations exist): co-moments of up to 32 column pairs per
-//                     launch group from one LDS tile of their (<= 8) columns.
+//                     accumulators).
+//   3. dq_pair_stage_scan (dq_pair.hip, only if Correlations exist): co-moments of the pair groups
+//                     (<= 8 columns staged HBM -> LDS once) fused with the moments of their columns.
 //   4. dq_finalize:   fixed-order merge of the per-workgroup partials, then in-order merge into
 //                     the plan's accumulators (chunk order) -> results are deterministic.
 // Streaming loads are 16 B per lane (global_load_dwordx4) for 8-/4-byte columns; there are no
@@ -980,164 +979,6 @@ __device__ __forceinline__ void corr_merge(CorrStats& a, const CorrStats& b) {
   a.n = n;
 }
 
-__device__ __forceinline__ double load_as_double(const void* p, int kind, int64_t row) {
-  if (kind == CK_F64) return reinterpret_cast<const double*>(p)[row];
-  if (kind == CK_I64) return (double)reinterpret_cast<const int64_t*>(p)[row];
-  return (double)reinterpret_cast<const int32_t*>(p)[row];
-}
-
-// ------------------------------------------------------------------------------------------
-// Kernel 3b: Correlation pair groups over an LDS row tile.  Each 512-row tile of the group's
-// (<= 8) columns is read from HBM once (16-byte loads, converted to double, validity & where
-// folded into per-column bit rows); then thread t owns pair t % 32 over the 64 tile rows of
-// group t / 32 and folds them in 8-row chunks (shifted co-moment sums, Chan merge, one division
-// per chunk).  Column stride kTileStride (516 doubles) puts the 8 columns of one tile row on
-// distinct LDS banks.
-// ------------------------------------------------------------------------------------------
-constexpr int kTileStride = kTileRows + 4;
-
-__global__ __launch_bounds__(kBlock) void dq_pair_tile_scan(const PairGroup* __restrict__ groups, int32_t ngroups,
-                                                            ScanCols cols, ScanBitmaps bm, int64_t n_rows,
-                                                            int64_t rows_per_range, CorrPartial* __restrict__ partials) {
-  __shared__ double tile[kTileCols * kTileStride];
-  __shared__ uint32_t vbits[kTileCols][kTileRows / 32];
-  __shared__ CorrStats red[kWaves][kTilePairs];
-  const int32_t gi = blockIdx.x % ngroups;
-  const int32_t range = blockIdx.x / ngroups;
-  const PairGroup& g = groups[gi];
-  const int ncols = g.ncols, npairs = g.npairs;
-  const int64_t row0 = (int64_t)range * rows_per_range;
-  int64_t row1 = row0 + rows_per_range;
-  if (row1 > n_rows) row1 = n_rows;
-  const uint32_t* mask = g.where >= 0 ? reinterpret_cast<const uint32_t*>(bm.where_bits[g.where]) : nullptr;
-  const int tid = threadIdx.x;
-  const int p = tid % kTilePairs, grp = tid / kTilePairs;  // 8 row groups of 64 tile rows
-  const bool active = p < npairs;
-  const int ci = active ? g.pi[p] : 0, cj = active ? g.pj[p] : 0;
-  CorrStats s = {0, 0, 0, 0, 0, 0};
-
-  for (int64_t t0 = row0; t0 < row1; t0 += kTileRows) {
-    const bool full = t0 + kTileRows <= row1;
-    // ---- stage the tile: each thread converts rows 2*tid, 2*tid+1 of every column
-    for (int c = 0; c < ncols; ++c) {
-      const void* src = cols.values[g.cols[c]];
-      const int kind = g.kinds[c];
-      const int64_t r = t0 + 2 * tid;
-      double a = 0.0, b = 0.0;
-      if (full) {
-        if (kind == CK_F64 || kind == CK_I64) {
-          const u32x4 v4 = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(reinterpret_cast<const int64_t*>(src) + r));
-          const uint64_t ua = ((uint64_t)v4.y << 32) | v4.x, ub = ((uint64_t)v4.w << 32) | v4.z;
-          if (kind == CK_F64) { a = __longlong_as_double((long long)ua); b = __longlong_as_double((long long)ub); }
-          else { a = (double)(int64_t)ua; b = (double)(int64_t)ub; }
-        } else {
-          const int2 v2 = *reinterpret_cast<const int2*>(reinterpret_cast<const int32_t*>(src) + r);
-          a = (double)v2.x; b = (double)v2.y;
-        }
-      } else {
-        if (r < row1) a = load_as_double(src, kind, r);
-        if (r + 1 < row1) b = load_as_double(src, kind, r + 1);
-      }
-      tile[c * kTileStride + 2 * tid] = a;
-      tile[c * kTileStride + 2 * tid + 1] = b;
-    }
-    if (tid < kTileCols * (kTileRows / 32)) {
-      const int c = tid / (kTileRows / 32), w = tid % (kTileRows / 32);
-      if (c < ncols) {
-        const int64_t widx = (t0 >> 5) + w;
-        uint32_t bits = word_or_ones(cols.validity[g.cols[c]], widx) & word_or_ones(mask, widx);
-        const int64_t r = t0 + 32 * w;
-        if (r >= row1) bits = 0;
-        else if (r + 32 > row1) bits &= (1u << (row1 - r)) - 1u;
-        vbits[c][w] = bits;
-      }
-    }
-    __syncthreads();
-    // ---- fold: this thread's pair over its 64 rows as shifted sums around the pair's running means
-    // (exec-masked accumulation: a row that is not valid in both columns costs no VALU work), then one
-    // Chan merge per tile (rcp + Newton step instead of a division)
-    if (active) {
-      double sx = s.xa, sy = s.ya;
-      if (s.n == 0.0) {  // still-empty pair: its first valid row of this tile group is the shift
-        bool found = false;
-#pragma unroll 1
-        for (int k = 0; k < 8 && !found; ++k) {
-          const int rr = grp * 64 + k * 8;
-          const uint32_t bits = ((vbits[ci][rr >> 5] & vbits[cj][rr >> 5]) >> (rr & 31)) & 0xFFu;
-          if (bits) {
-            const int j = __builtin_ctz(bits);
-            sx = tile[ci * kTileStride + rr + j];
-            sy = tile[cj * kTileStride + rr + j];
-            found = true;
-          }
-        }
-      }
-      double Sx = 0.0, Sy = 0.0, Sxy = 0.0, Sxx = 0.0, Syy = 0.0;
-      int32_t kc = 0;
-#pragma unroll 1
-      for (int k = 0; k < 8; ++k) {
-        const int rr = grp * 64 + k * 8;
-        const uint32_t bits = ((vbits[ci][rr >> 5] & vbits[cj][rr >> 5]) >> (rr & 31)) & 0xFFu;
-        if (__builtin_amdgcn_ballot_w64(bits != 0) == 0) continue;  // wave-uniform skip
-        double x[8], y[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          x[j] = tile[ci * kTileStride + rr + j];
-          y[j] = tile[cj * kTileStride + rr + j];
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const uint64_t m = __builtin_amdgcn_ballot_w64((bits >> j) & 1u);
-          double dx, dy;
-          uint64_t save;
-          asm volatile(
-              "s_and_saveexec_b64 %[save], %[m]\n\t"
-              "v_add_f64 %[dx], %[x], -%[sx]\n\t"
-              "v_add_f64 %[dy], %[y], -%[sy]\n\t"
-              "v_add_u32 %[k], 1, %[k]\n\t"
-              "v_add_f64 %[Sx], %[Sx], %[dx]\n\t"
-              "v_add_f64 %[Sy], %[Sy], %[dy]\n\t"
-              "v_fma_f64 %[Sxy], %[dx], %[dy], %[Sxy]\n\t"
-              "v_fma_f64 %[Sxx], %[dx], %[dx], %[Sxx]\n\t"
-              "v_fma_f64 %[Syy], %[dy], %[dy], %[Syy]\n\t"
-              "s_mov_b64 exec, %[save]"
-              : [Sx] "+v"(Sx), [Sy] "+v"(Sy), [Sxy] "+v"(Sxy), [Sxx] "+v"(Sxx), [Syy] "+v"(Syy), [k] "+v"(kc),
-                [dx] "=&v"(dx), [dy] "=&v"(dy), [save] "=&s"(save)
-              : [x] "v"(x[j]), [y] "v"(y[j]), [sx] "v"(sx), [sy] "v"(sy), [m] "s"(m)
-              : "scc");
-        }
-      }
-      if (kc != 0) {
-        const double n2 = s.n + (double)kc;
-        const double r = rcp_nr(n2);
-        const double qx = Sx * r, qy = Sy * r;
-        s.xa = sx + qx; s.ya = sy + qy;
-        s.ck = s.ck + __builtin_fma(-Sx, qy, Sxy);
-        s.xm = s.xm + __builtin_fma(-Sx, qx, Sxx);
-        s.ym = s.ym + __builtin_fma(-Sy, qy, Syy);
-        s.n = n2;
-      }
-    }
-    __syncthreads();
-  }
-  // ---- reduce the 8 row groups of each pair in fixed order: lanes p and p + 32 of a wave, then waves
-  {
-    CorrStats o;
-    o.n = __shfl_xor(s.n, 32); o.xa = __shfl_xor(s.xa, 32); o.ya = __shfl_xor(s.ya, 32);
-    o.ck = __shfl_xor(s.ck, 32); o.xm = __shfl_xor(s.xm, 32); o.ym = __shfl_xor(s.ym, 32);
-    corr_merge(s, o);
-  }
-  const int lane = tid & 63, wave = tid >> 6;
-  if (lane < kTilePairs) red[wave][lane] = s;
-  __syncthreads();
-  if (tid < npairs) {
-    CorrStats a = red[0][tid];
-    for (int w = 1; w < kWaves; ++w) corr_merge(a, red[w][tid]);
-    CorrPartial* q = partials + (size_t)(g.first_pair + tid) * kMaxWG + range;
-    q->n = a.n; q->xa = a.xa; q->ya = a.ya; q->ck = a.ck; q->xm = a.xm; q->ym = a.ym; q->pad0 = 0; q->pad1 = 0;
-  }
-}
-
 // ------------------------------------------------------------------------------------------
 // Kernel 1: predicate program (three-valued logic) -- Compliance / conditional counts and `where`
 // bitmaps (Compliance.scala:37-53, Analyzer.scala:404-408).  A wave takes 512-row blocks (lane l:
@@ -1802,13 +1643,6 @@ hipError_t launch_column_scan(int32_t variant, const ColTask* tasks, int32_t nta
   return hipGetLastError();
 }
 
-hipError_t launch_pair_tile_scan(const PairGroup* groups, int32_t ngroups, const ScanCols& cols,
-                                 const ScanBitmaps& bm, int64_t n_rows, int64_t rows_per_range, int32_t nranges,
-                                 CorrPartial* partials, hipStream_t st) {
-  hipLaunchKernelGGL(dq_pair_tile_scan, dim3((uint32_t)ngroups * (uint32_t)nranges), dim3(kBlock), 0, st, groups,
-                     ngroups, cols, bm, n_rows, rows_per_range, partials);
-  return hipGetLastError();
-}
 
 hipError_t launch_finalize(int32_t ncol, int32_t nranges_col, const ColPartial* col_part, ColPartial* col_acc,
                            int32_t npair, int32_t nranges_pair, const CorrPartial* pair_part, CorrPartial* pair_acc,

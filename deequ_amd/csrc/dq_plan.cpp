@@ -34,17 +34,10 @@ hipError_t launch_pred_scan(const PredProgram* prog, const ScanCols& cols, const
 hipError_t launch_column_scan(int32_t variant, const ColTask* tasks, int32_t ntasks, int32_t part_base,
                               const ScanCols& cols, const ScanBitmaps& bm, int64_t n_rows, int64_t rows_per_range,
                               int32_t nranges, ColPartial* partials, uint32_t* hll_acc, hipStream_t st);
-hipError_t launch_pair_tile_scan(const PairGroup* groups, int32_t ngroups, const ScanCols& cols,
-                                 const ScanBitmaps& bm, int64_t n_rows, int64_t rows_per_range, int32_t nranges,
-                                 CorrPartial* partials, hipStream_t st);
-hipError_t launch_pair_lane_scan(const PairWaveTask* tasks, int32_t ntasks, const ScanCols& cols,
-                                 const ScanBitmaps& bm, const uint32_t* ones, int64_t n_rows, int64_t rows_per_range,
-                                 int32_t nranges, CorrPartial* pair_part, ColPartial* col_part, bool all_f64,
-                                 hipStream_t st);
-hipError_t launch_pair_mfma_scan(const PairGroup* groups, int32_t ngroups, const ScanCols& cols,
-                                 const ScanBitmaps& bm, const uint32_t* ones, int64_t n_rows, int64_t rows_per_range,
-                                 int32_t nranges, CorrPartial* pair_part, ColPartial* col_part, bool all_f64,
-                                 bool minmax, bool glds, hipStream_t st);
+hipError_t launch_pair_scan(const PairWG* wgs, int32_t nwg, const ScanCols& cols, const ScanBitmaps& bm,
+                            const uint32_t* ones, int64_t n_rows, int64_t rows_per_range, int32_t nranges,
+                            CorrPartial* pair_part, ColPartial* col_part, int32_t* redo, bool all_f64, bool minmax,
+                            hipStream_t st);
 hipError_t launch_finalize(int32_t ncol, int32_t nranges_col, const ColPartial* col_part, ColPartial* col_acc,
                            int32_t npair, int32_t nranges_pair, const CorrPartial* pair_part, CorrPartial* pair_acc,
                            int32_t has_pred, int32_t nranges_pred, const PredPartial* pred_part, PredPartial* pred_acc, const FinRanges& fr,
@@ -433,23 +426,10 @@ struct dq_plan {
   struct Group { int32_t variant, first, count; };
   std::vector<Group> groups;              // one column-scan launch per variant group
   std::vector<PairTask> pair_tasks;      // sorted by pair group
-  std::vector<PairGroup> pair_groups;     // <= 8 columns / <= 32 pairs / one where each (LDS-tile kernel)
-  std::vector<PairWaveTask> lane_tasks;   // pair groups planned for the lane-per-row kernel (dq_pair.hip)
-  int32_t n_fused = 0;                    // column tasks computed by the lane pair kernel (sorted last)
-  bool lane_all_f64 = true;               // every lane task column is fp64 (the conversion-free instantiation)
-  std::vector<PairGroup> mfma_groups;     // pair groups of the matrix-core Gram kernel (dq_pair.hip), moments fused
-  bool mfma_all_f64 = true;
-  bool mfma_minmax = false;               // a fused moments task feeds Minimum / Maximum
-  int32_t concurrency = 1;                // HIP streams the variant launches are spread over
-  std::vector<hipStream_t> side;          // concurrency - 1 extra streams
-  std::vector<hipEvent_t> side_done;
-  hipEvent_t fork_ev = nullptr;
-  // DQ_PRED_CONCURRENT=1: the predicate pass on its own stream, concurrent with the column / pair
-  // launches, when no `where` bitmap (the only thing those launches read from it) is produced.  Opt-in:
-  // its waves (120 VGPRs, 4 per SIMD) can hold the SIMDs the hash passes need, so the gain depends on
-  // dispatch order -- C3 29.17 -> 28.55 ms on one box, 35.1 ms on another
-  hipStream_t pred_stream = nullptr;
-  hipEvent_t pred_fork_ev = nullptr, pred_done_ev = nullptr;
+  std::vector<PairWG> pair_wgs;          // Correlation pass workgroup tasks (dq_pair.hip), moments fused
+  int32_t n_fused = 0;                    // column tasks computed by the pair pass (sorted last)
+  bool pair_all_f64 = true;               // every pair-group column is fp64 (the conversion-free instantiations)
+  bool pair_minmax = false;               // a fused moments task feeds Minimum / Maximum
   PredProgram prog{};
   std::vector<std::string> patterns;      // DQ_PRED_REGEX patterns (dq_plan_create_ex)
   std::vector<uint16_t> regex_blob;       // their compiled DFAs
@@ -460,9 +440,8 @@ struct dq_plan {
   // device memory
   ColTask* d_col_tasks = nullptr;
   PairTask* d_pair_tasks = nullptr;
-  PairGroup* d_pair_groups = nullptr;
-  PairWaveTask* d_lane_tasks = nullptr;
-  PairGroup* d_mfma_groups = nullptr;
+  PairWG* d_pair_wgs = nullptr;
+  int32_t* d_pair_redo = nullptr;         // [pair_wgs][kPairWaves][kMaxWG] ranges left to the checked fold
   PredProgram* d_prog = nullptr;
   ColPartial* d_col_part = nullptr;
   CorrPartial* d_pair_part = nullptr;
@@ -473,7 +452,7 @@ struct dq_plan {
   PredPartial* d_pred_acc = nullptr;
   uint64_t* d_where_bits[kMaxWhere] = {nullptr};
   int64_t where_cap_words = 0;
-  uint32_t* d_ones = nullptr;  // all-ones bitmap (lane pair pass: columns without validity, tasks without where)
+  uint32_t* d_ones = nullptr;  // all-ones bitmap (pair pass: columns without validity, groups without where)
   int64_t ones_cap_words = 0;
 
   int64_t total_rows = 0;
@@ -531,22 +510,12 @@ static dq_status timed(dq_plan* p, int kernel, hipStream_t st, F fn) {
 }
 
 static dq_status free_plan_mem(dq_plan* p) {
-  if (p->pred_stream) (void)hipStreamDestroy(p->pred_stream);
-  if (p->pred_fork_ev) (void)hipEventDestroy(p->pred_fork_ev);
-  if (p->pred_done_ev) (void)hipEventDestroy(p->pred_done_ev);
-  p->pred_stream = nullptr;
-  p->pred_fork_ev = p->pred_done_ev = nullptr;
-  for (hipStream_t st : p->side) (void)hipStreamDestroy(st);
-  for (hipEvent_t ev : p->side_done) (void)hipEventDestroy(ev);
-  if (p->fork_ev) (void)hipEventDestroy(p->fork_ev);
-  p->side.clear();
-  p->side_done.clear();
   for (auto& q : p->pending) { p->ev_pool.push_back(q.a); p->ev_pool.push_back(q.b); }
   p->pending.clear();
   for (hipEvent_t e : p->ev_pool) (void)hipEventDestroy(e);
   p->ev_pool.clear();
-  void* ptrs[] = {p->d_col_tasks, p->d_pair_tasks, p->d_pair_groups, p->d_lane_tasks, p->d_mfma_groups, p->d_prog, p->d_col_part, p->d_pair_part,
-                  p->d_pred_part, p->d_col_acc, p->d_hll_acc, p->d_pair_acc, p->d_pred_acc, p->d_regex};
+  void* ptrs[] = {p->d_col_tasks, p->d_pair_tasks, p->d_pair_wgs, p->d_prog, p->d_col_part, p->d_pair_part,
+                  p->d_pred_part, p->d_col_acc, p->d_hll_acc, p->d_pair_acc, p->d_pred_acc, p->d_regex, p->d_pair_redo};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   for (int i = 0; i < kMaxWhere; ++i)
@@ -572,178 +541,75 @@ static dq_status dmalloc(T** ptr, size_t bytes) {
   return DQ_OK;
 }
 
-// Plan one pair group for the lane-per-row kernel (dq_pair.hip): cover its pairs with the fewest column
-// subsets of kLaneCols local columns (one wave task each; every pair of 8 columns fits 4 subsets of 5), put
-// each fusable moments column -- a stats-only column task of the group's columns and `where` -- at position
-// 0 / 1 of a task holding it (extra moments-only tasks if the covers have no room), and hand every pair to
-// the least-loaded task covering it.  Returns false when the group cannot be planned this way.
-static bool plan_lane_tasks(const dq_plan* p, const PairGroup& g, std::vector<PairWaveTask>& out,
-                            std::vector<int>& fused) {
-  const int k = g.ncols;
-  if (k < 2 || k > kTileCols || g.npairs < 1) return false;
-  std::vector<int32_t> mom_task(k, -1);
-  for (int c = 0; c < k; ++c)
+// Plan one pair group for the Correlation pass (dq_pair.hip): wave w's position p holds local column
+// (p + w) % 8, so every pair of two distinct columns has exactly one (wave, slot) of the fixed pattern; the
+// slot computes (position A, position B) and a pair whose first column sits at B swaps x / y on output.
+// Each fusable moments column -- a stats-only column task of the group's columns and `where` -- goes to
+// its even position (column c: wave c % 2, position c - c % 2).  Pairs the group cannot hold (x with
+// itself, or (y, x) beside (x, y): one slot per unordered pair) become one- / two-column workgroup tasks of
+// their own.
+static void plan_pair_wgs(const dq_plan* p, const PairGroup& g, std::vector<PairWG>& out, std::vector<int>& fused) {
+  auto blank = [&](const int32_t* lcols, int nl) {  // wave tasks over local columns lcols[0 .. nl)
+    PairWG wg;
+    std::memset(&wg, 0, sizeof(wg));
+    for (int w = 0; w < kPairWaves; ++w) {
+      PairWaveTask& t = wg.wave[w];
+      t.where = g.where;
+      for (int q = 0; q < kPairPos; ++q) {
+        const int l = (q + w) % kPairPos;
+        const int c = lcols[l < nl ? l : 0];  // an unused position repeats a used column (loaded, never read)
+        t.cols[q] = g.cols[c];
+        t.kinds[q] = g.kinds[c];
+      }
+      for (int q = 0; q < kPairSlots; ++q) t.pair_out[q] = -1;
+      for (int k = 0; k < kPairMoments; ++k) t.mom_out[k] = -1;
+    }
+    return wg;
+  };
+  auto place = [&](PairWG& wg, int a, int b, int32_t pair) {  // local positions of the first / second column
+    for (int w = 0; w < kPairWaves; ++w) {
+      const int pa = (a - w + kPairPos) % kPairPos, pb = (b - w + kPairPos) % kPairPos;
+      for (int q = 0; q < kPairSlots; ++q) {
+        const bool fwd = kPairSlotA[q] == pa && kPairSlotB[q] == pb, rev = kPairSlotA[q] == pb && kPairSlotB[q] == pa;
+        if (!fwd && !rev) continue;
+        PairWaveTask& t = wg.wave[w];
+        if ((t.pair_mask >> q) & 1u) return false;
+        t.pair_mask |= 1u << q;
+        if (rev) t.swap_mask |= 1u << q;
+        t.pair_out[q] = pair;
+        return true;
+      }
+    }
+    return false;
+  };
+  int32_t ident[kPairPos];
+  for (int c = 0; c < kPairPos; ++c) ident[c] = c;
+  PairWG wg = blank(ident, g.ncols);
+  std::vector<int> extra;
+  for (int q = 0; q < g.npairs; ++q)
+    if (g.pi[q] == g.pj[q] || !place(wg, g.pi[q], g.pj[q], g.first_pair + q)) extra.push_back(q);
+  for (int c = 0; c < g.ncols; ++c)
     for (size_t t = 0; t < p->col_tasks.size(); ++t) {
       const ColTask& ct = p->col_tasks[t];
       if (ct.col == g.cols[c] && ct.where == g.where && !fused[t] &&
-          (ct.variant == CV_F64_S || ct.variant == CV_I64_S || ct.variant == CV_I32_S))
-        mom_task[c] = (int32_t)t;
-    }
-  auto pbit = [](int a, int b) { return a < b ? 1ull << (a * 8 + b) : 1ull << (b * 8 + a); };
-  uint64_t need = 0;
-  for (int q = 0; q < g.npairs; ++q) need |= pbit(g.pi[q], g.pj[q]);
-  const int sz = std::min(k, kLaneCols);
-  std::vector<uint32_t> subs;
-  std::vector<uint64_t> cov;
-  for (uint32_t m = 1; m < (1u << k); ++m) {
-    if (__builtin_popcount(m) != sz) continue;
-    uint64_t c = 0;
-    for (int a = 0; a < k; ++a)
-      for (int b = a + 1; b < k; ++b)
-        if (((m >> a) & 1u) && ((m >> b) & 1u)) c |= pbit(a, b);
-    if ((c & need) == 0) continue;
-    subs.push_back(m);
-    cov.push_back(c & need);
-  }
-  // moments matching: column -> one task holding it, at most kLaneMoments per task (augmenting paths)
-  auto match = [&](const std::vector<uint32_t>& tasks, std::vector<int>& col_of_slot) {
-    col_of_slot.assign(tasks.size() * kLaneMoments, -1);
-    int matched = 0;
-    for (int c = 0; c < k; ++c) {
-      if (mom_task[c] < 0) continue;
-      std::vector<char> seen(col_of_slot.size(), 0);
-      std::function<bool(int)> aug = [&](int col) {
-        for (size_t t = 0; t < tasks.size(); ++t) {
-          if (!((tasks[t] >> col) & 1u)) continue;
-          for (int sl = 0; sl < kLaneMoments; ++sl) {
-            const size_t i = t * kLaneMoments + sl;
-            if (seen[i]) continue;
-            seen[i] = 1;
-            if (col_of_slot[i] < 0 || aug(col_of_slot[i])) { col_of_slot[i] = col; return true; }
-          }
-        }
-        return false;
-      };
-      if (aug(c)) ++matched;
-    }
-    return matched;
-  };
-  const int n_mom = (int)std::count_if(mom_task.begin(), mom_task.end(), [](int32_t t) { return t >= 0; });
-  std::vector<uint32_t> best;
-  std::vector<int> best_slots;
-  int best_matched = -1;
-  const int ns = (int)subs.size();
-  for (int T = 1; T <= 4 && best.empty(); ++T) {
-    std::vector<int> idx(T);
-    for (int i = 0; i < T; ++i) idx[i] = i;
-    while (T <= ns) {
-      uint64_t c = 0;
-      for (int i : idx) c |= cov[i];
-      if ((c & need) == need) {
-        std::vector<uint32_t> tasks;
-        for (int i : idx) tasks.push_back(subs[i]);
-        std::vector<int> slots;
-        const int mt = match(tasks, slots);
-        if (mt > best_matched) { best = tasks; best_slots = slots; best_matched = mt; }
-        if (mt == n_mom) break;
+          (ct.variant == CV_F64_S || ct.variant == CV_I64_S || ct.variant == CV_I32_S)) {
+        PairWaveTask& w = wg.wave[c % 2];
+        const int k = (c - c % 2) / 2;
+        w.mom_mask |= 1u << k;
+        w.mom_out[k] = (int32_t)t;
+        fused[t] = 1;
+        break;
       }
-      int i = T - 1;  // next combination
-      while (i >= 0 && idx[i] == ns - T + i) --i;
-      if (i < 0) break;
-      ++idx[i];
-      for (int j = i + 1; j < T; ++j) idx[j] = idx[j - 1] + 1;
     }
+  if (wg.wave[0].pair_mask | wg.wave[0].mom_mask | wg.wave[1].pair_mask | wg.wave[1].mom_mask) out.push_back(wg);
+  for (int q : extra) {  // slot (0, 1) of wave 0 of a task holding the pair's column(s) at positions 0, 1
+    const int32_t lc[2] = {g.pi[q], g.pj[q]};
+    PairWG e = blank(lc, 2);
+    PairWaveTask& t = e.wave[0];
+    t.pair_mask = 1u;
+    t.pair_out[0] = g.first_pair + q;
+    out.push_back(e);
   }
-  if (best.empty()) return false;
-  // position lists: matched moments columns first, then the rest of the subset
-  std::vector<std::vector<int>> pos(best.size());
-  std::vector<int> task_moms(best.size(), 0);
-  for (size_t t = 0; t < best.size(); ++t) {
-    for (int sl = 0; sl < kLaneMoments; ++sl)
-      if (best_slots[t * kLaneMoments + sl] >= 0) { pos[t].push_back(best_slots[t * kLaneMoments + sl]); task_moms[t]++; }
-    for (int c = 0; c < k; ++c)
-      if (((best[t] >> c) & 1u) && std::find(pos[t].begin(), pos[t].end(), c) == pos[t].end()) pos[t].push_back(c);
-  }
-  std::vector<char> mom_done(k, 0);
-  for (int v : best_slots)
-    if (v >= 0) mom_done[v] = 1;
-  for (int c = 0; c < k;) {  // unmatched moments columns: moments-only tasks
-    if (mom_task[c] < 0 || mom_done[c]) { ++c; continue; }
-    std::vector<int> ps{c};
-    mom_done[c] = 1;
-    for (int d = c + 1; d < k && (int)ps.size() < kLaneMoments; ++d)
-      if (mom_task[d] >= 0 && !mom_done[d]) { ps.push_back(d); mom_done[d] = 1; }
-    best.push_back(0);
-    pos.push_back(ps);
-    task_moms.push_back((int)ps.size());
-  }
-  std::vector<PairWaveTask> tasks(pos.size());
-  std::vector<int> load(pos.size(), 0);
-  for (size_t t = 0; t < pos.size(); ++t) {
-    PairWaveTask& w = tasks[t];
-    std::memset(&w, 0, sizeof(w));
-    w.ncols = (int32_t)pos[t].size();
-    w.where = g.where;
-    for (int i = 0; i < kLaneCols; ++i) {  // unused positions repeat position 0 (loaded, never used)
-      const int l = pos[t][i < w.ncols ? i : 0];
-      w.cols[i] = g.cols[l];
-      w.kinds[i] = g.kinds[l];
-    }
-    for (int i = 0; i < kLaneSlots; ++i) w.pair_out[i] = -1;
-    for (int i = 0; i < kLaneMoments; ++i) w.mom_out[i] = -1;
-    for (int i = 0; i < task_moms[t]; ++i) {
-      w.mom_mask |= 1u << i;
-      w.mom_out[i] = mom_task[pos[t][i]];
-    }
-    load[t] = 4 * task_moms[t] + w.ncols;
-  }
-  auto slot_of = [](int a, int b) {
-    for (int i = 0; i < kLaneSlots; ++i)
-      if (kLaneSlotA[i] == std::min(a, b) && kLaneSlotB[i] == std::max(a, b)) return i;
-    return -1;
-  };
-  for (int q = 0; q < g.npairs; ++q) {
-    int bt = -1, ba = -1, bb = -1;
-    for (size_t t = 0; t < pos.size(); ++t) {
-      auto ia = std::find(pos[t].begin(), pos[t].end(), (int)g.pi[q]);
-      auto ib = std::find(pos[t].begin(), pos[t].end(), (int)g.pj[q]);
-      if (ia == pos[t].end() || ib == pos[t].end()) continue;
-      const int sl = slot_of((int)(ia - pos[t].begin()), (int)(ib - pos[t].begin()));
-      if ((tasks[t].pair_mask >> sl) & 1u) continue;  // e.g. Correlation(a, b) and Correlation(b, a)
-      if (bt < 0 || load[t] < load[bt]) { bt = (int)t; ba = (int)(ia - pos[t].begin()); bb = (int)(ib - pos[t].begin()); }
-    }
-    if (bt < 0) {  // no covering task with the slot free: a two-column task of its own
-      PairWaveTask w;
-      std::memset(&w, 0, sizeof(w));
-      w.ncols = 2;
-      w.where = g.where;
-      for (int i = 0; i < kLaneCols; ++i) {
-        const int l = i == 1 ? g.pj[q] : g.pi[q];
-        w.cols[i] = g.cols[l];
-        w.kinds[i] = g.kinds[l];
-      }
-      for (int i = 0; i < kLaneSlots; ++i) w.pair_out[i] = -1;
-      for (int i = 0; i < kLaneMoments; ++i) w.mom_out[i] = -1;
-      tasks.push_back(w);
-      pos.push_back({(int)g.pi[q], (int)g.pj[q]});
-      load.push_back(2);
-      bt = (int)tasks.size() - 1;
-      ba = 0;
-      bb = 1;
-    }
-    const int slot = slot_of(ba, bb);
-    if (slot < 0) return false;
-    // the slot computes (position a, position b); a pair whose first column sits at b swaps x / y on output
-    if (ba > bb) tasks[bt].swap_mask |= 1u << slot;
-    tasks[bt].pair_mask |= 1u << slot;
-    tasks[bt].pair_out[slot] = g.first_pair + q;
-    load[bt] += 5;
-  }
-  for (size_t t = 0; t < pos.size(); ++t)
-    for (int i = 0; i < kLaneMoments; ++i)
-      if ((tasks[t].mom_mask >> i) & 1u) fused[tasks[t].mom_out[i]] = 1;
-  out = tasks;
-  return true;
 }
 
 static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred) {
@@ -940,7 +806,8 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
     }
   }
 
-  // correlation pairs -> groups sharing one LDS row tile (greedy, per where bitmap)
+  // correlation pairs -> groups of <= kTileCols columns and one `where` (greedy), staged together
+  std::vector<PairGroup> pair_groups;
   {
     std::vector<int32_t> order;
     std::vector<PairGroup> groups;
@@ -979,73 +846,17 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
       new_index[order[k]] = (int32_t)k;
     }
     p->pair_tasks.swap(sorted);
-    p->pair_groups.swap(groups);
+    pair_groups.swap(groups);
     for (SpecOut& o : p->outs)
       if (o.pair_task >= 0) o.pair_task = new_index[o.pair_task];
   }
 
-  // pair groups -> the matrix-core Gram kernel (default) or lane-per-row wave tasks (dq_pair.hip), with the
-  // groups' stats-only column tasks fused in; DQ_PAIR_KERNEL=lane|tile selects the older kernels (A/B tests)
+  // pair groups -> workgroup tasks of the Correlation pass (dq_pair.hip): the group's pairs and its
+  // stats-only column tasks (Mean / StdDev / Sum / Min / Max of the same `where`) over two wave tasks
   std::vector<int> fused(p->col_tasks.size(), 0);
-  {
-    const char* kern = std::getenv("DQ_PAIR_KERNEL");
-    const bool tile_only = std::getenv("DQ_PAIR_TILE") != nullptr || (kern && std::strcmp(kern, "tile") == 0);
-    const bool lane = kern && std::strcmp(kern, "lane") == 0;
-    std::vector<PairGroup> tile_groups;
-    for (PairGroup g : p->pair_groups) {
-      std::vector<PairWaveTask> w;
-      if (!tile_only && !lane && g.ncols >= 1) {
-        for (int c = 0; c < kTileCols; ++c) g.mom_task[c] = -1;
-        for (int c = 0; c < g.ncols; ++c)
-          for (size_t t = 0; t < p->col_tasks.size(); ++t) {
-            const ColTask& ct = p->col_tasks[t];
-            if (ct.col == g.cols[c] && ct.where == g.where && !fused[t] &&
-                (ct.variant == CV_F64_S || ct.variant == CV_I64_S || ct.variant == CV_I32_S)) {
-              g.mom_task[c] = (int32_t)t;
-              fused[t] = 1;
-              break;
-            }
-          }
-        for (int c = 0; c < g.ncols; ++c) p->mfma_all_f64 = p->mfma_all_f64 && g.kinds[c] == CK_F64;
-        p->mfma_groups.push_back(g);
-      } else if (!tile_only && plan_lane_tasks(p, g, w, fused)) {
-        while (w.size() % kWaves) w.push_back(PairWaveTask{});  // idle padding: 4 tasks of one range per workgroup
-        p->lane_tasks.insert(p->lane_tasks.end(), w.begin(), w.end());
-      } else {
-        tile_groups.push_back(g);
-      }
-    }
-    p->pair_groups.swap(tile_groups);
-    for (const PairWaveTask& w : p->lane_tasks)
-      for (int c = 0; c < w.ncols; ++c) p->lane_all_f64 = p->lane_all_f64 && w.kinds[c] == CK_F64;
-    // idle padding tasks still need valid column indices for nothing: they return before any load
-  }
-
-  // HLL-only column tasks (no `where`) of columns whose values an ATOM_CMP of the predicate program already
-  // loads can be hashed inside the predicate pass (one read of the column for both).  Opt-in
-  // (DQ_PRED_HLL=1): measured on C3 the fused pass takes 2.04 ms per 125 M rows against 0.99 + 0.66 ms for
-  // the predicate pass plus the separate i64 HLL launch -- the interpreter's occupancy (3 waves/SIMD with
-  // the hash registers) costs more than the second read of the columns saves.
-  std::vector<int32_t> pred_hll_tasks;  // original task indices, in fusion order
-  {
-    const char* ph = std::getenv("DQ_PRED_HLL");
-    const bool pred_used = !root_code.empty() && (!counter_of.empty() || !bitmap_of.empty());
-    if (pred_used && ph && std::strcmp(ph, "1") == 0) {
-      std::vector<char> loaded(ncols, 0);
-      for (const auto& rc : root_code)
-        for (const PredInstr& ins : rc)
-          if (ins.op == PO_ATOM_CMP) {
-            if (ins.col_a >= 0) loaded[ins.col_a] = 1;
-            if (ins.col_b >= 0) loaded[ins.col_b] = 1;
-          }
-      for (size_t t = 0; t < p->col_tasks.size() && (int)pred_hll_tasks.size() < kMaxPredHll; ++t) {
-        const ColTask& ct = p->col_tasks[t];
-        if (fused[t] || ct.where >= 0 || !loaded[ct.col]) continue;
-        if (ct.variant != CV_F64_H && ct.variant != CV_I64_H && ct.variant != CV_I32_H) continue;
-        fused[t] = 2;
-        pred_hll_tasks.push_back((int32_t)t);
-      }
-    }
+  for (const PairGroup& g : pair_groups) {
+    plan_pair_wgs(p, g, p->pair_wgs, fused);
+    for (int c = 0; c < g.ncols; ++c) p->pair_all_f64 = p->pair_all_f64 && g.kinds[c] == CK_F64;
   }
 
   // sort column tasks by (fused into the pair pass, variant) (stable), remap the analyzers' and lane tasks'
@@ -1066,17 +877,14 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
     p->col_tasks.swap(sorted);
     for (SpecOut& o : p->outs)
       if (o.col_task >= 0) o.col_task = new_index[o.col_task];
-    for (PairWaveTask& w : p->lane_tasks)
-      for (int k = 0; k < kLaneMoments; ++k)
-        if ((w.mom_mask >> k) & 1u) w.mom_out[k] = new_index[w.mom_out[k]];
-    for (int32_t& t : pred_hll_tasks) t = new_index[t];
-    for (PairGroup& g : p->mfma_groups)
-      for (int c = 0; c < g.ncols; ++c)
-        if (g.mom_task[c] >= 0) {
-          g.mom_task[c] = new_index[g.mom_task[c]];
-          for (const SpecOut& o : p->outs)
-            if (o.col_task == g.mom_task[c] && (o.op == DQ_OP_MIN || o.op == DQ_OP_MAX)) p->mfma_minmax = true;
-        }
+    for (PairWG& wg : p->pair_wgs)
+      for (PairWaveTask& w : wg.wave)
+        for (int k = 0; k < kPairMoments; ++k)
+          if ((w.mom_mask >> k) & 1u) {
+            w.mom_out[k] = new_index[w.mom_out[k]];
+            for (const SpecOut& o : p->outs)
+              if (o.col_task == w.mom_out[k] && (o.op == DQ_OP_MIN || o.op == DQ_OP_MAX)) p->pair_minmax = true;
+          }
     for (int32_t k = 0; k < (int32_t)p->col_tasks.size(); ++k) {
       if (fused[order[k]]) break;  // fused tasks sort last: their partials come from the pair pass
       if (p->groups.empty() || p->groups.back().variant != p->col_tasks[k].variant)
@@ -1118,21 +926,6 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
     for (auto& kv : counter_of) prog.counters[kv.second] = PredCounter{kv.first.first, kv.first.second};
     prog.n_bitmaps = (int32_t)bitmap_of.size();
     for (auto& kv : bitmap_of) prog.bitmap_root[kv.second] = kv.first;
-    for (int32_t t : pred_hll_tasks) {  // the first ATOM_CMP loading the column hashes it
-      const ColTask& ct = p->col_tasks[(size_t)t];
-      for (int32_t i = 0; i < prog.n_instr; ++i) {
-        const PredInstr& ins = prog.instr[i];
-        if (ins.op != PO_ATOM_CMP || (ins.col_a != ct.col && ins.col_b != ct.col)) continue;
-        PredHll& e = prog.hll[prog.n_hll++];
-        e.instr = i;
-        e.operand = ins.col_a == ct.col ? 0 : 1;
-        e.kind = ins.col_a == ct.col ? ins.kind_a : ins.kind_b;
-        e.part = t;
-        e.hll_slot = ct.hll_slot;
-        e.pad = 0;
-        break;
-      }
-    }
   }
 
   // algorithmic bytes per row: each (column, buffer) read once
@@ -1181,23 +974,18 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
     p->pred_bytes_x1000 = bytes_of(pv, pn);
     p->pair_bytes_x1000 = bytes_of(qv, qn);
   }
-  p->launches_per_scan = (p->has_pred ? 1 : 0) + (int32_t)p->groups.size() + (p->pair_groups.empty() ? 0 : 1) +
-                         (p->lane_tasks.empty() ? 0 : 1) + (p->mfma_groups.empty() ? 0 : 1) +
+  p->launches_per_scan = (p->has_pred ? 1 : 0) + (int32_t)p->groups.size() + (p->pair_wgs.empty() ? 0 : 1) +
                          ((p->col_tasks.size() + p->pair_tasks.size()) ? 1 : 0);
 
   // device allocations
   const size_t nct = p->col_tasks.size(), npt = p->pair_tasks.size();
   if (dq_status s = dmalloc(&p->d_col_tasks, nct * sizeof(ColTask))) return s;
   if (dq_status s = dmalloc(&p->d_pair_tasks, npt * sizeof(PairTask))) return s;
-  if (dq_status s = dmalloc(&p->d_pair_groups, p->pair_groups.size() * sizeof(PairGroup))) return s;
-  if (dq_status s = dmalloc(&p->d_lane_tasks, p->lane_tasks.size() * sizeof(PairWaveTask))) return s;
-  if (dq_status s = dmalloc(&p->d_mfma_groups, p->mfma_groups.size() * sizeof(PairGroup))) return s;
-  if (!p->mfma_groups.empty())
-    HIP_TRY(hipMemcpyAsync(p->d_mfma_groups, p->mfma_groups.data(), p->mfma_groups.size() * sizeof(PairGroup),
+  if (dq_status s = dmalloc(&p->d_pair_wgs, p->pair_wgs.size() * sizeof(PairWG))) return s;
+  if (!p->pair_wgs.empty())
+    HIP_TRY(hipMemcpyAsync(p->d_pair_wgs, p->pair_wgs.data(), p->pair_wgs.size() * sizeof(PairWG),
                            hipMemcpyHostToDevice, p->stream));
-  if (!p->lane_tasks.empty())
-    HIP_TRY(hipMemcpyAsync(p->d_lane_tasks, p->lane_tasks.data(), p->lane_tasks.size() * sizeof(PairWaveTask),
-                           hipMemcpyHostToDevice, p->stream));
+  if (dq_status s = dmalloc(&p->d_pair_redo, p->pair_wgs.size() * kPairWaves * kMaxWG * sizeof(int32_t))) return s;
   if (dq_status s = dmalloc(&p->d_prog, sizeof(PredProgram))) return s;
   if (dq_status s = dmalloc(&p->d_col_part, nct * kMaxWG * sizeof(ColPartial))) return s;
   if (dq_status s = dmalloc(&p->d_pair_part, npt * kMaxWG * sizeof(CorrPartial))) return s;
@@ -1208,9 +996,6 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
   if (dq_status s = dmalloc(&p->d_pred_acc, sizeof(PredPartial))) return s;
   if (nct) HIP_TRY(hipMemcpyAsync(p->d_col_tasks, p->col_tasks.data(), nct * sizeof(ColTask), hipMemcpyHostToDevice, p->stream));
   if (npt) HIP_TRY(hipMemcpyAsync(p->d_pair_tasks, p->pair_tasks.data(), npt * sizeof(PairTask), hipMemcpyHostToDevice, p->stream));
-  if (!p->pair_groups.empty())
-    HIP_TRY(hipMemcpyAsync(p->d_pair_groups, p->pair_groups.data(), p->pair_groups.size() * sizeof(PairGroup),
-                           hipMemcpyHostToDevice, p->stream));
   if (p->regex_blob.size() > (size_t)kMaxRegexWords)
     return set_error(DQ_E_UNSUPPORTED, "compiled patterns need %zu KB (LDS budget %d KB)",
                      p->regex_blob.size() * 2 / 1024, kMaxRegexWords * 2 / 1024);
@@ -1224,26 +1009,6 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
   HIP_TRY(hipMemcpyAsync(p->d_prog, &p->prog, sizeof(PredProgram), hipMemcpyHostToDevice, p->stream));
   if (dq_status s = reset_acc(p)) return s;
   HIP_TRY(hipStreamSynchronize(p->stream));
-  // concurrency: DQ_COLUMN_STREAMS (default 1) streams for the variant launches
-  if (const char* e = std::getenv("DQ_COLUMN_STREAMS")) p->concurrency = std::max(1, std::min(8, std::atoi(e)));
-  p->concurrency = std::min<int32_t>(
-      p->concurrency, std::max<int32_t>(1, (int32_t)p->groups.size() + (p->pair_groups.empty() ? 0 : 1) +
-                                               (p->lane_tasks.empty() ? 0 : 1) + (p->mfma_groups.empty() ? 0 : 1)));
-  HIP_TRY(hipEventCreateWithFlags(&p->fork_ev, hipEventDisableTiming));
-  const char* pc = std::getenv("DQ_PRED_CONCURRENT");  // opt-in: see the plan field's note
-  if (p->has_pred && p->prog.n_bitmaps == 0 && pc && pc[0] == '1') {
-    HIP_TRY(hipStreamCreateWithFlags(&p->pred_stream, hipStreamNonBlocking));
-    HIP_TRY(hipEventCreateWithFlags(&p->pred_fork_ev, hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&p->pred_done_ev, hipEventDisableTiming));
-  }
-  for (int32_t k = 1; k < p->concurrency; ++k) {
-    hipStream_t st;
-    hipEvent_t ev;
-    HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-    HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    p->side.push_back(st);
-    p->side_done.push_back(ev);
-  }
   return DQ_OK;
 }
 
@@ -1354,8 +1119,8 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
   }
   ScanBitmaps bm{};
   for (int b = 0; b < kMaxWhere; ++b) bm.where_bits[b] = p->d_where_bits[b];
-  // all-ones bitmap standing in for a missing validity / where bitmap in the lane pair pass
-  if ((!p->lane_tasks.empty() || !p->mfma_groups.empty()) && words + 1 > p->ones_cap_words) {
+  // all-ones bitmap standing in for a missing validity / where bitmap in the pair pass
+  if (!p->pair_wgs.empty() && words + 1 > p->ones_cap_words) {
     HIP_TRY(hipStreamSynchronize(p->stream));
     if (p->d_ones) (void)hipFree(p->d_ones);
     p->d_ones = nullptr;
@@ -1369,21 +1134,11 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
   // so the smallest launch still has ~kTargetWGs workgroups (load balance over 256 CUs)
   int64_t min_launch = 0;
   for (const auto& g : p->groups) min_launch = min_launch ? std::min<int64_t>(min_launch, g.count) : g.count;
-  if (!p->pair_groups.empty())
-    min_launch = min_launch ? std::min<int64_t>(min_launch, (int64_t)p->pair_groups.size()) : (int64_t)p->pair_groups.size();
-  if (!p->lane_tasks.empty()) {  // workgroups of the lane pair launch per row range
-    const int64_t wg = (int64_t)p->lane_tasks.size() / kWaves;
+  if (!p->pair_wgs.empty()) {
+    const int64_t wg = (int64_t)p->pair_wgs.size();
     min_launch = min_launch ? std::min<int64_t>(min_launch, wg) : wg;
   }
-  if (!p->mfma_groups.empty()) {
-    const int64_t wg = (int64_t)p->mfma_groups.size();
-    min_launch = min_launch ? std::min<int64_t>(min_launch, wg) : wg;
-  }
-  static const int64_t target = [] {
-    const char* e = std::getenv("DQ_TARGET_WGS");  // tuning override (diagnostic)
-    return e ? std::max<int64_t>(256, std::atoll(e)) : (int64_t)kTargetWGs;
-  }();
-  const int64_t want = std::max<int64_t>(64, std::min<int64_t>(kMaxWG, target / std::max<int64_t>(1, min_launch)));
+  const int64_t want = std::max<int64_t>(64, std::min<int64_t>(kMaxWG, kTargetWGs / std::max<int64_t>(1, min_launch)));
   // rows per range and range count for `want` ranges
   auto size_ranges = [&](int64_t w, int64_t& rpr, int32_t& nr) {
     nr = (int32_t)std::min<int64_t>(w, ceil_div(n_rows, kRowsPerIter));
@@ -1394,31 +1149,21 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
   int64_t rpr_col;
   size_ranges(want, rpr_col, nr_col);
   // per-variant workgroup counts: the string hash balances better with twice the ranges (uneven string
-  // lengths, deferred-round drains): utf8_hll 1.979 -> 1.949 ms per 125 M x 4 on the C5 headline (A/B
-  // twice, DQ_VARIANT_RANGES=0 for the common size); halving the fp64 hash's ranges measured no change.
-  // scale > 0: want x scale ranges, < 0: want / -scale
-  static const int32_t str_scale = [] {
-    // tuning override (diagnostic); utf8_hll per 125 M x 4 on one box: x1 1.979, x2 1.951 / 1.956,
-    // x3 1.963 / 1.964, x4 1.965 ms
-    const char* e = std::getenv("DQ_STR_RANGE_SCALE");
-    return e ? std::max(1, std::min(8, std::atoi(e))) : 2;
-  }();
+  // lengths, deferred-round drains): utf8_hll 1.979 -> 1.949 ms per 125 M x 4 on the C5 headline (x3 1.963,
+  // x4 1.965 ms); halving the fp64 hash's ranges measured no change
   auto variant_scale = [](int32_t v) -> int32_t {
-    if (v == CV_UTF8_H || v == CV_LUTF8_H || v == CV_UTF8_HD || v == CV_LUTF8_HD) return str_scale;
-    return 1;
+    return v == CV_UTF8_H || v == CV_LUTF8_H || v == CV_UTF8_HD || v == CV_LUTF8_HD ? 2 : 1;
   };
-  static const bool per_variant = !(std::getenv("DQ_VARIANT_RANGES") && std::getenv("DQ_VARIANT_RANGES")[0] == '0');
   FinRanges fr{};
   std::vector<std::pair<int64_t, int32_t>> vr(p->groups.size());  // (rows per range, ranges) per variant group
   for (size_t gi = 0; gi < p->groups.size(); ++gi) {
     const auto& g = p->groups[gi];
-    const int32_t sc_v = per_variant ? variant_scale(g.variant) : 1;
+    const int32_t sc_v = variant_scale(g.variant);
     if (sc_v == 1) {
       vr[gi] = {rpr_col, nr_col};
       continue;
     }
-    const int64_t w = sc_v > 0 ? want * sc_v : want / -sc_v;
-    size_ranges(std::max<int64_t>(64, std::min<int64_t>(kMaxWG, w)), vr[gi].first, vr[gi].second);
+    size_ranges(std::max<int64_t>(64, std::min<int64_t>(kMaxWG, want * sc_v)), vr[gi].first, vr[gi].second);
     if (fr.n < kNumVariants) {
       fr.first[fr.n] = g.first;
       fr.end[fr.n] = g.first + g.count;
@@ -1426,91 +1171,39 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
       ++fr.n;
     }
   }
-  // predicate pass: ~2048 workgroups of whole 2048-row iterations (HBM-bound; counters leave by atomics)
-  static const int64_t pred_wgs = [] {
-    // tuning override (diagnostic): 1024-16384 workgroups measured within 2 % of 2048 on C3 (0.954-0.978 ms)
-    const char* e = std::getenv("DQ_PRED_WGS");
-    return e ? std::max<int64_t>(64, std::min<int64_t>(65536, std::atoll(e))) : (int64_t)2048;
-  }();
-  int32_t nr_pred = (int32_t)std::min<int64_t>(pred_wgs, ceil_div(n_rows, kRowsPerIter));
+  // predicate pass: ~2048 workgroups of whole 2048-row iterations (HBM-bound; counters leave by atomics;
+  // 1024-16384 workgroups measured within 2 % on C3)
+  int32_t nr_pred = (int32_t)std::min<int64_t>(2048, ceil_div(n_rows, kRowsPerIter));
   int64_t rpr_pred = ceil_div(ceil_div(n_rows, nr_pred), kRowsPerIter) * kRowsPerIter;
   nr_pred = (int32_t)ceil_div(n_rows, rpr_pred);
 
-  // fused HLL tasks (counted by the predicate pass into range slot 0): empty partials for every range
-  for (int32_t h = 0; h < p->prog.n_hll; ++h)
-    HIP_TRY(hipMemsetAsync(p->d_col_part + (size_t)p->prog.hll[h].part * kMaxWG, 0, (size_t)nr_col * sizeof(ColPartial),
-                           p->stream));
+  // every launch on the plan's stream, in order (the C5 variant launches spread over 2-3 streams measured the
+  // same step time: each launch fills the chip)
   if (p->has_pred) {
-    hipStream_t pst = p->stream;
-    if (p->pred_stream) {  // fork: the predicate pass beside the column / pair launches
-      HIP_TRY(hipEventRecord(p->pred_fork_ev, p->stream));
-      HIP_TRY(hipStreamWaitEvent(p->pred_stream, p->pred_fork_ev, 0));
-      pst = p->pred_stream;
-    }
-    if (dq_status s = timed(p, 0, pst, [&] {
+    if (dq_status s = timed(p, 0, p->stream, [&] {
           const int32_t lds = kWaves * 128 * (p->prog.stack_depth + p->prog.n_roots + p->prog.n_counters) +
                               ((p->prog.regex_words * 2 + 15) & ~15);
           return launch_pred_scan(p->d_prog, sc, bm, n_rows, rpr_pred, nr_pred, p->d_pred_acc, p->d_col_part,
-                                  p->d_hll_acc, lds, pst, p->prog.regex_words > 0, p->prog.n_hll > 0);
+                                  p->d_hll_acc, lds, p->stream, p->prog.regex_words > 0, p->prog.n_hll > 0);
         }))
       return s;
-    if (p->pred_stream) HIP_TRY(hipEventRecord(p->pred_done_ev, p->pred_stream));
   }
-  // fork: variant launches (and the pair pass) round-robin over the plan stream + side streams
-  const int32_t K = p->concurrency;
-  if (K > 1) {
-    HIP_TRY(hipEventRecord(p->fork_ev, p->stream));
-    for (hipStream_t st : p->side) HIP_TRY(hipStreamWaitEvent(st, p->fork_ev, 0));
-  }
-  int32_t li = 0;
-  auto stream_for = [&](int32_t i) { return (K > 1 && i % K) ? p->side[i % K - 1] : p->stream; };
   for (size_t gi = 0; gi < p->groups.size(); ++gi) {
     const auto& g = p->groups[gi];
-    hipStream_t st = stream_for(li++);
-    if (dq_status s = timed(p, 16 + g.variant, st, [&] {
+    if (dq_status s = timed(p, 16 + g.variant, p->stream, [&] {
           return launch_column_scan(g.variant, p->d_col_tasks + g.first, g.count, g.first, sc, bm, n_rows,
-                                    vr[gi].first, vr[gi].second, p->d_col_part, p->d_hll_acc, st);
+                                    vr[gi].first, vr[gi].second, p->d_col_part, p->d_hll_acc, p->stream);
         }))
       return s;
   }
-  if (!p->lane_tasks.empty()) {
-    hipStream_t st = stream_for(li++);
-    if (dq_status s = timed(p, 2, st, [&] {
-          return launch_pair_lane_scan(p->d_lane_tasks, (int32_t)p->lane_tasks.size(), sc, bm, p->d_ones, n_rows, rpr_col,
-                                       nr_col, p->d_pair_part, p->d_col_part, p->lane_all_f64, st);
+  if (!p->pair_wgs.empty()) {
+    if (dq_status s = timed(p, 2, p->stream, [&] {
+          return launch_pair_scan(p->d_pair_wgs, (int32_t)p->pair_wgs.size(), sc, bm, p->d_ones, n_rows, rpr_col,
+                                  nr_col, p->d_pair_part, p->d_col_part, p->d_pair_redo, p->pair_all_f64,
+                                  p->pair_minmax, p->stream);
         }))
       return s;
   }
-  if (!p->mfma_groups.empty()) {
-    hipStream_t st = stream_for(li++);
-    // LDS-DMA staging of all-fp64 groups (dq_scan already requires 16-byte aligned value buffers; checked
-    // again here since the kernel's DMA assumes it); DQ_PAIR_GLDS=0 selects the register-staged kernel
-    const char* glds_env = std::getenv("DQ_PAIR_GLDS");
-    bool glds = !(glds_env && glds_env[0] == '0') && p->mfma_all_f64;
-    for (const PairGroup& g : p->mfma_groups)
-      for (int c = 0; c < g.ncols && glds; ++c) glds = ((uintptr_t)sc.values[g.cols[c]] & 15u) == 0;
-    if (dq_status s = timed(p, 2, st, [&] {
-          return launch_pair_mfma_scan(p->d_mfma_groups, (int32_t)p->mfma_groups.size(), sc, bm, p->d_ones, n_rows,
-                                       rpr_col, nr_col, p->d_pair_part, p->d_col_part, p->mfma_all_f64,
-                                       p->mfma_minmax, glds, st);
-        }))
-      return s;
-  }
-  if (!p->pair_groups.empty()) {
-    hipStream_t st = stream_for(li++);
-    if (dq_status s = timed(p, 2, st, [&] {
-          return launch_pair_tile_scan(p->d_pair_groups, (int32_t)p->pair_groups.size(), sc, bm, n_rows, rpr_col,
-                                       nr_col, p->d_pair_part, st);
-        }))
-      return s;
-  }
-  if (K > 1) {  // join
-    for (int32_t k = 1; k < K; ++k) {
-      HIP_TRY(hipEventRecord(p->side_done[k - 1], p->side[k - 1]));
-      HIP_TRY(hipStreamWaitEvent(p->stream, p->side_done[k - 1], 0));
-    }
-  }
-  if (p->has_pred && p->pred_stream) HIP_TRY(hipStreamWaitEvent(p->stream, p->pred_done_ev, 0));
   if (dq_status s = timed(p, 3, p->stream, [&] {
         return launch_finalize((int32_t)p->col_tasks.size(), nr_col, p->d_col_part, p->d_col_acc,
                                (int32_t)p->pair_tasks.size(), nr_col, p->d_pair_part, p->d_pair_acc,

@@ -902,41 +902,3 @@ def test_histogram_vs_oracle(dq, n):
             assert want[k] == v.absolute and v.ratio == v.absolute / n, (col, k)
         h5 = dq.Histogram(col, None, 5).calculate(data).value.get()
         assert sorted((v.absolute for v in h5.values.values()), reverse=True) == top[:5], col
-
-
-@pytest.mark.parametrize("n", [1, 513, 300_007])
-def test_pred_pass_fused_hll_equals_column_pass(dq, n, monkeypatch):
-    """With DQ_PRED_HLL=1, ApproxCountDistinct of columns the predicate pass already loads is hashed there
-    (one read of the column): registers, counts and Completeness are bit-identical to the column pass
-    (the default) and the HLL estimate equals the oracle's; the plan drops the HLL column launch."""
-    from deequ_amd.runner import ScanPlan, scan_states
-    from deequ_amd.table import column_from_numpy
-
-    rng = np.random.default_rng(77 + n)
-    a = rng.integers(-1000, 1000, n)
-    b = rng.integers(-50, 50, n).astype(np.int32)
-    x = rng.normal(size=n)
-    if n > 10:
-        x[rng.integers(0, n, 3)] = np.nan
-    va, vx = rng.random(n) > 0.1, rng.random(n) > 0.2
-    t = dq.Table([column_from_numpy("a", "i64", a, va), column_from_numpy("b", "i32", b, np.ones(n, bool), nullable=False),
-                  column_from_numpy("x", "f64", x, vx)])
-    an = [dq.Compliance("c1", "a > 0 AND b < 10"), dq.Compliance("c2", "x >= 0.5 OR a IS NULL"),
-          dq.ApproxCountDistinct("a"), dq.ApproxCountDistinct("b"), dq.ApproxCountDistinct("x"), dq.Completeness("a"),
-          dq.Completeness("x"), dq.Size()]
-    monkeypatch.setenv("DQ_PRED_HLL", "1")
-    plan = ScanPlan(an, t.schema)
-    fused_launches = plan.num_launches()
-    plan.close()
-    fused = scan_states(t, an)
-    monkeypatch.setenv("DQ_PRED_HLL", "0")
-    plan = ScanPlan(an, t.schema)
-    plain_launches = plan.num_launches()
-    plan.close()
-    plain = scan_states(t, an)
-    assert fused_launches < plain_launches, (fused_launches, plain_launches)
-    for k in an:
-        assert fused[k] == plain[k] or (fused[k] is None and plain[k] is None), (k, fused[k], plain[k])
-    ocols = {"a": O.OColumn("i64", a, va), "b": O.OColumn("i32", b, np.ones(n, bool)), "x": O.OColumn("f64", x, vx)}
-    for k in an[2:5]:
-        assert_state_close(fused[k], O.compute_state((type(k).__name__, k.column, k.where), ocols, n))
