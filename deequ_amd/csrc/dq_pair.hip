@@ -36,6 +36,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 #include "dq_device.h"
 #include "dq_lane.h"
@@ -121,6 +122,13 @@ __device__ double range_shift(const char* col, int kind, const uint32_t* vb, con
   return 0.0;
 }
 
+// LDS ring of the fp64 path, per workgroup: kRing slots of one 64-row group -- the 8 columns (512 bytes each)
+// and the 18 selection words; 9 slots = 37 KB, 4 workgroups per CU
+constexpr int kRing = 9;
+constexpr int kSlotBytes = 8 * 512 + 128;
+constexpr int kSlotMaskWord = 8 * 128;  // dword index of the selection words in a slot
+
+
 // per-lane sums of one wave task over its range
 struct PairAcc {
   double s[kPairSlots][5];  // Sa, Sb, Sab, Saa, Sbb over rows selected in both positions (z = x - shift)
@@ -205,13 +213,130 @@ __device__ __forceinline__ void fold(PairAcc& A, const int64_t (&raw)[kPairPos],
   }
 }
 
+// The unchecked fold of one 64-row group (every selected value assumed finite; a non-finite one shows in
+// the sums and sends the range to the checked fold): z = x - shift in every lane, then each pair's five
+// sums under exec = m(a) & m(b) -- the rows selected in both positions, so nothing is zeroed -- and each
+// moments position's under exec = m(c).  One asm statement per update group, exec restored to all lanes
+// at its end (the compiler never sees a partial exec).
+__device__ __forceinline__ void pair_update2(double (&a)[5], double (&b)[5], double za, double zb, double zc, double zd,
+                                             uint64_t ma, uint64_t mb, uint64_t mc, uint64_t md) {
+  asm volatile(
+      "s_and_b64 exec, %[ma], %[mb]\n\t"
+      "v_add_f64 %[a0], %[a0], %[za]\n\t"
+      "v_add_f64 %[a1], %[a1], %[zb]\n\t"
+      "v_fma_f64 %[a2], %[za], %[zb], %[a2]\n\t"
+      "v_fma_f64 %[a3], %[za], %[za], %[a3]\n\t"
+      "v_fma_f64 %[a4], %[zb], %[zb], %[a4]\n\t"
+      "s_and_b64 exec, %[mc], %[md]\n\t"
+      "v_add_f64 %[b0], %[b0], %[zc]\n\t"
+      "v_add_f64 %[b1], %[b1], %[zd]\n\t"
+      "v_fma_f64 %[b2], %[zc], %[zd], %[b2]\n\t"
+      "v_fma_f64 %[b3], %[zc], %[zc], %[b3]\n\t"
+      "v_fma_f64 %[b4], %[zd], %[zd], %[b4]\n\t"
+      "s_mov_b64 exec, -1"
+      : [a0] "+v"(a[0]), [a1] "+v"(a[1]), [a2] "+v"(a[2]), [a3] "+v"(a[3]), [a4] "+v"(a[4]), [b0] "+v"(b[0]),
+        [b1] "+v"(b[1]), [b2] "+v"(b[2]), [b3] "+v"(b[3]), [b4] "+v"(b[4])
+      : [za] "v"(za), [zb] "v"(zb), [zc] "v"(zc), [zd] "v"(zd), [ma] "s"(ma), [mb] "s"(mb), [mc] "s"(mc), [md] "s"(md)
+      : "scc");
+}
+// the four moments positions 0, 2, 4, 6 in one statement
+template <bool MINMAX>
+__device__ __forceinline__ void moment_update4(PairAcc& A, const double (&z)[kPairPos], const double (&x)[kPairPos],
+                                               const uint64_t (&m)[kPairPos]) {
+  if constexpr (MINMAX) {
+    asm volatile(
+        "s_mov_b64 exec, %[m0]\n\t"
+        "v_add_f64 %[s0], %[s0], %[z0]\n\t"
+        "v_fma_f64 %[t0], %[z0], %[z0], %[t0]\n\t"
+        "v_min_f64 %[l0], %[l0], %[x0]\n\t"
+        "v_max_f64 %[h0], %[h0], %[x0]\n\t"
+        "s_mov_b64 exec, %[m1]\n\t"
+        "v_add_f64 %[s1], %[s1], %[z1]\n\t"
+        "v_fma_f64 %[t1], %[z1], %[z1], %[t1]\n\t"
+        "v_min_f64 %[l1], %[l1], %[x1]\n\t"
+        "v_max_f64 %[h1], %[h1], %[x1]\n\t"
+        "s_mov_b64 exec, %[m2]\n\t"
+        "v_add_f64 %[s2], %[s2], %[z2]\n\t"
+        "v_fma_f64 %[t2], %[z2], %[z2], %[t2]\n\t"
+        "v_min_f64 %[l2], %[l2], %[x2]\n\t"
+        "v_max_f64 %[h2], %[h2], %[x2]\n\t"
+        "s_mov_b64 exec, %[m3]\n\t"
+        "v_add_f64 %[s3], %[s3], %[z3]\n\t"
+        "v_fma_f64 %[t3], %[z3], %[z3], %[t3]\n\t"
+        "v_min_f64 %[l3], %[l3], %[x3]\n\t"
+        "v_max_f64 %[h3], %[h3], %[x3]\n\t"
+        "s_mov_b64 exec, -1"
+        : [s0] "+v"(A.sd[0]), [t0] "+v"(A.sdd[0]), [l0] "+v"(A.lo[0]), [h0] "+v"(A.hi[0]), [s1] "+v"(A.sd[1]),
+          [t1] "+v"(A.sdd[1]), [l1] "+v"(A.lo[1]), [h1] "+v"(A.hi[1]), [s2] "+v"(A.sd[2]), [t2] "+v"(A.sdd[2]),
+          [l2] "+v"(A.lo[2]), [h2] "+v"(A.hi[2]), [s3] "+v"(A.sd[3]), [t3] "+v"(A.sdd[3]), [l3] "+v"(A.lo[3]),
+          [h3] "+v"(A.hi[3])
+        : [z0] "v"(z[0]), [z1] "v"(z[2]), [z2] "v"(z[4]), [z3] "v"(z[6]), [x0] "v"(x[0]), [x1] "v"(x[2]),
+          [x2] "v"(x[4]), [x3] "v"(x[6]), [m0] "s"(m[0]), [m1] "s"(m[2]), [m2] "s"(m[4]), [m3] "s"(m[6]));
+  } else {
+    asm volatile(
+        "s_mov_b64 exec, %[m0]\n\t"
+        "v_add_f64 %[s0], %[s0], %[z0]\n\t"
+        "v_fma_f64 %[t0], %[z0], %[z0], %[t0]\n\t"
+        "s_mov_b64 exec, %[m1]\n\t"
+        "v_add_f64 %[s1], %[s1], %[z1]\n\t"
+        "v_fma_f64 %[t1], %[z1], %[z1], %[t1]\n\t"
+        "s_mov_b64 exec, %[m2]\n\t"
+        "v_add_f64 %[s2], %[s2], %[z2]\n\t"
+        "v_fma_f64 %[t2], %[z2], %[z2], %[t2]\n\t"
+        "s_mov_b64 exec, %[m3]\n\t"
+        "v_add_f64 %[s3], %[s3], %[z3]\n\t"
+        "v_fma_f64 %[t3], %[z3], %[z3], %[t3]\n\t"
+        "s_mov_b64 exec, -1"
+        : [s0] "+v"(A.sd[0]), [t0] "+v"(A.sdd[0]), [s1] "+v"(A.sd[1]), [t1] "+v"(A.sdd[1]), [s2] "+v"(A.sd[2]),
+          [t2] "+v"(A.sdd[2]), [s3] "+v"(A.sd[3]), [t3] "+v"(A.sdd[3])
+        : [z0] "v"(z[0]), [z1] "v"(z[2]), [z2] "v"(z[4]), [z3] "v"(z[6]), [m0] "s"(m[0]), [m1] "s"(m[2]),
+          [m2] "s"(m[4]), [m3] "s"(m[6]));
+  }
+}
+template <int Q, int N>
+struct SlotLoop {
+  template <typename F>
+  __device__ __forceinline__ static void run(F&& f) {
+    f(std::integral_constant<int, Q>{});
+    SlotLoop<Q + 1, N>::run(f);
+  }
+};
+template <int N>
+struct SlotLoop<N, N> {
+  template <typename F>
+  __device__ __forceinline__ static void run(F&&) {}
+};
+template <bool F64, bool MINMAX>
+__device__ __forceinline__ void fold_fast(PairAcc& A, const int64_t (&raw)[kPairPos], const uint64_t (&m)[kPairPos],
+                                          const double (&shift)[kPairPos], const int (&kind)[kPairPos]) {
+  double x[kPairPos], z[kPairPos];
+#pragma unroll
+  for (int p = 0; p < kPairPos; ++p) {
+    x[p] = F64 ? __builtin_bit_cast(double, raw[p]) : raw_to_double(raw[p], kind[p]);
+    z[p] = x[p] - shift[p];
+  }
+  static_assert(kPairSlots % 2 == 0, "slots go in twos");
+  SlotLoop<0, kPairSlots / 2>::run([&](auto qc) {
+    constexpr int q = 2 * decltype(qc)::value;
+    constexpr int a = kPairSlotA[q], b = kPairSlotB[q], c = kPairSlotA[q + 1], d = kPairSlotB[q + 1];
+    pair_update2(A.s[q], A.s[q + 1], z[a], z[b], z[c], z[d], m[a], m[b], m[c], m[d]);
+  });
+  moment_update4<MINMAX>(A, z, x, m);
+  if constexpr (!F64) {
+#pragma unroll
+    for (int k = 0; k < kPairMoments; ++k)
+      if (kind[2 * k] != CK_F64 && lane_bit(m[2 * k])) A.is[k] = (int64_t)((uint64_t)A.is[k] + (uint64_t)raw[2 * k]);
+  }
+}
+
 // One wave task over one row range: fold every 64-row group, then (CHECKED or all sums finite) the counts
 // and the CorrPartial / ColPartial records.  Returns false (nothing written) when an unchecked fold met a
 // non-finite sum.
-template <bool CHECKED, bool F64, bool MINMAX>
+template <bool CHECKED, bool F64, bool MINMAX, bool RING>
 __device__ __forceinline__ bool pair_range(const PairWaveTask& T, const ScanCols& cols, const uint32_t* where,
                                            const uint32_t* ones, int64_t row0, int64_t row1, int32_t range,
-                                           CorrPartial* __restrict__ pair_part, ColPartial* __restrict__ col_part) {
+                                           CorrPartial* __restrict__ pair_part, ColPartial* __restrict__ col_part,
+                                           int64_t* ring, bool active) {
   const int lane = threadIdx.x & 63;
   // everything from here on in range-local rows [0, nr): base pointers moved to row0 (a multiple of 64)
   const int64_t nr = row1 - row0;
@@ -243,9 +368,135 @@ __device__ __forceinline__ bool pair_range(const PairWaveTask& T, const ScanCols
   }
   A.poison = 0;
 
+  const int64_t nfull = nr >> 6;
+  if constexpr (RING) {
+    // ---- full groups through the workgroup's LDS ring (kRing slots, one 64-row group each): the two waves
+    // stage each group together, wave 0 the group's columns 0-3 and the where / column 0-3 selection words,
+    // wave 1 columns 4-7 and their selection words -- five DMA loads each (global_load_lds; lanes 0-31
+    // bring 16 bytes = 2 rows of a column, one lane per selection dword), kRing - 2 groups ahead of the
+    // fold, no VGPRs held.  One s_barrier per group: past it the partner's loads of group g have landed
+    // (each wave waits for its own first) and the partner has folded group g - 1, so the slot of group g - 2
+    // may be restaged.
+    static_assert(F64 && !CHECKED, "the ring path stages fp64 values");
+    constexpr int D = kRing - 2;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)ring);
+    const bool has_where = T.where >= 0;
+    // selection dwords of a slot: 0, 1 = where, 2 + 2 c, 3 + 2 c = column c.  Wave 0 stages dwords 0-9
+    // (lanes 0-9), wave 1 dwords 10-17 (lanes 0-7); wave w's position p is column p + w (mod 8).
+    const uint32_t* mp;
+    if (wave == 0) {
+      mp = ww;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (lane >> 1 == c + 1) mp = vw[c];
+    } else {
+      mp = vw[3];
+#pragma unroll
+      for (int c = 1; c < 4; ++c)
+        if (lane >> 1 == c) mp = vw[3 + c];
+    }
+    mp += lane & 1;
+    const uint64_t mexec = wave == 0 ? 0x3FFull : 0xFFull;
+    const uint32_t moff = 4096u + (wave == 0 ? 0u : 40u);
+    // the four columns this wave stages: wave 0 positions 0-3, wave 1 positions 3-6 (= columns 4-7)
+    const char* dp[4];
+    const int p0 = wave == 0 ? 0 : 3;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dp[k] = reinterpret_cast<const char*>(cols.values[T.cols[p0 + k]]) + row0 * 8;
+    const uint32_t dcol = wave == 0 ? 0u : 2048u;  // LDS byte offset of the first staged column
+    auto dma = [&](int64_t g, uint32_t slot) __attribute__((always_inline)) {
+      const uint32_t gc = (uint32_t)(g < nfull ? g : nfull - 1);
+      const uint32_t voff = gc * 512u + (uint32_t)lane * 16u;
+      const uint32_t d = lds0 + slot * (uint32_t)kSlotBytes + dcol;
+      const uint32_t dm = lds0 + slot * (uint32_t)kSlotBytes + moff;
+      const uint32_t* ma = mp + 2 * gc;
+      uint32_t keep;
+      uint64_t sv;
+      asm volatile(
+          "s_mov_b32 %[keep], m0\n\t"
+          "s_mov_b64 %[sv], exec\n\t"
+          "s_mov_b32 exec_hi, 0\n\t"
+          "s_mov_b32 m0, %[d]\n\t"
+          "s_nop 0\n\t"
+          "global_load_lds_dwordx4 %[vo], %[b0]\n\t"
+          "s_add_u32 m0, %[d], 0x200\n\t"
+          "s_nop 0\n\t"
+          "global_load_lds_dwordx4 %[vo], %[b1]\n\t"
+          "s_add_u32 m0, %[d], 0x400\n\t"
+          "s_nop 0\n\t"
+          "global_load_lds_dwordx4 %[vo], %[b2]\n\t"
+          "s_add_u32 m0, %[d], 0x600\n\t"
+          "s_nop 0\n\t"
+          "global_load_lds_dwordx4 %[vo], %[b3]\n\t"
+          "s_mov_b64 exec, %[me]\n\t"
+          "s_mov_b32 m0, %[dm]\n\t"
+          "s_nop 0\n\t"
+          "global_load_lds_dword %[ma], off\n\t"
+          "s_mov_b64 exec, %[sv]\n\t"
+          "s_mov_b32 m0, %[keep]"
+          : [keep] "=&s"(keep), [sv] "=&s"(sv)
+          : [vo] "v"(voff), [d] "s"(d), [dm] "s"(dm), [me] "s"(mexec), [b0] "s"(dp[0]), [b1] "s"(dp[1]),
+            [b2] "s"(dp[2]), [b3] "s"(dp[3]), [ma] "v"(ma)
+          : "memory", "scc");
+    };
+    // this wave's positions: ring column (p + wave) % 8; selection words: lanes 0, 1 of the first read =
+    // where, lanes 2 p, 2 p + 1 of the second = position p
+    const int64_t* xs0 = ring + lane;
+    const uint32_t* ms0 = reinterpret_cast<const uint32_t*>(ring) + kSlotMaskWord;
+    const int mlw = lane & 1, mlc = lane < 16 ? 2 + ((2 * wave + lane) & 15) : 0;
+    auto one = [&](int64_t g, uint32_t slot) __attribute__((always_inline)) {
+      dma(g + D, slot + D < (uint32_t)kRing ? slot + D : slot + D - kRing);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(5 * D) : "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      const int64_t* xs = xs0 + slot * (kSlotBytes / 8);
+      const uint32_t* ms = ms0 + slot * (kSlotBytes / 4);
+      int64_t b[kPairPos];
+      if (wave == 0) {
+#pragma unroll
+        for (int p = 0; p < kPairPos; ++p) b[p] = xs[p * 64];
+      } else {
+#pragma unroll
+        for (int p = 0; p < kPairPos; ++p) b[p] = xs[((p + 1) % kPairPos) * 64];
+      }
+      const uint32_t mc = ms[mlc];
+      auto word = [](uint32_t v, int i) {
+        return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(v, i + 1) << 32) | (uint32_t)__builtin_amdgcn_readlane(v, i);
+      };
+      uint64_t m[kPairPos];
+#pragma unroll
+      for (int p = 0; p < kPairPos; ++p) m[p] = word(mc, 2 * p);
+      if (has_where) {
+        const uint64_t wm = word(ms[mlw], 0);
+#pragma unroll
+        for (int p = 0; p < kPairPos; ++p) m[p] &= wm;
+      }
+      if (active) fold_fast<true, MINMAX>(A, b, m, shift, kind);
+    };
+    if (nfull > 0) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) dma(d, (uint32_t)d);
+      uint32_t slot = 0;
+      for (int64_t g = 0; g < nfull; ++g) {
+        one(g, slot);
+        slot = slot + 1 == kRing ? 0 : slot + 1;
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may outlive the workgroup (its LDS is reused)
+    }
+    if (!active) return true;
+    // the column pointers again for the tail and the counts (reloaded, not held in SGPRs through the loop)
+    const PairWaveTask* tp = &T;  // laundered: the column indices are loaded again (never &cols: that copies
+    asm volatile("" : "+s"(tp));  // the kernel-argument struct to scratch)
+#pragma unroll
+    for (int p = 0; p < kPairPos; ++p) {
+      const int c = tp->cols[p];
+      vw[p] = (cols.validity[c] ? cols.validity[c] : ones) + (row0 >> 5);
+      vp[p] = reinterpret_cast<const char*>(cols.values[c]) + row0 * 8;
+    }
+  } else {
   // ---- full groups: values two groups ahead of the fold (three rotating buffers; two with Min / Max or
   // conversions, for VGPRs), masks by scalar loads; 32-bit offsets from the scalar base pointers
-  const int64_t nfull = nr >> 6;
   auto load = [&](int64_t (&b)[kPairPos], int64_t g) __attribute__((always_inline)) {
     const uint32_t li = (uint32_t)(g < nfull ? g : nfull - 1) * 64u + (uint32_t)lane;
 #pragma unroll
@@ -258,7 +509,8 @@ __device__ __forceinline__ bool pair_range(const PairWaveTask& T, const ScanCols
     uint64_t m[kPairPos];
 #pragma unroll
     for (int p = 0; p < kPairPos; ++p) m[p] = sword_at(vw[p], off) & wm;
-    fold<CHECKED, F64, MINMAX>(A, b, m, shift, kind);
+    if constexpr (CHECKED) fold<true, F64, MINMAX>(A, b, m, shift, kind);
+    else fold_fast<F64, MINMAX>(A, b, m, shift, kind);
   };
   if (nfull > 0) {
     int64_t b0[kPairPos], b1[kPairPos];
@@ -285,6 +537,7 @@ __device__ __forceinline__ bool pair_range(const PairWaveTask& T, const ScanCols
     }
     if (g < nfull) step(b0, g);
     if (g + 1 < nfull) step(b1, g + 1);
+  }
   }
   // ---- the range's last rows (< 64; only at the end of the scan)
   const int64_t tb = nfull * 64;
@@ -403,8 +656,9 @@ __device__ __forceinline__ bool pair_range(const PairWaveTask& T, const ScanCols
 }  // namespace
 
 // F64: every position fp64 (no conversions, no integral sums).  MINMAX: a moments task feeds Min / Max.
-// Two waves per SIMD (<= 256 VGPRs): the other wave's VALU hides this one's scalar work and load waits.
-template <bool F64, bool MINMAX>
+// RING: fp64 values staged through the per-wave LDS ring (16-byte aligned columns).  Two waves per SIMD
+// (<= 256 VGPRs): the other wave's VALU hides this one's scalar work and waits.
+template <bool F64, bool MINMAX, bool RING>
 __global__ __launch_bounds__(64 * kPairWaves) __attribute__((amdgpu_waves_per_eu(2))) void dq_pair_scan(
     const PairWG* __restrict__ wgs, int32_t nwg, ScanCols cols, ScanBitmaps bm, const uint32_t* ones, int64_t n_rows,
     int64_t rows_per_range, CorrPartial* __restrict__ pair_part, ColPartial* __restrict__ col_part,
@@ -412,11 +666,19 @@ __global__ __launch_bounds__(64 * kPairWaves) __attribute__((amdgpu_waves_per_eu
   const int gi = blockIdx.x % nwg, range = blockIdx.x / nwg;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const PairWaveTask& T = wgs[gi].wave[wave];
-  if ((T.pair_mask | T.mom_mask) == 0) return;
+  const bool active = (T.pair_mask | T.mom_mask) != 0;
+  // the ring path's waves stage the group together: an idle wave still stages its half
+  if (RING ? !active && (wgs[gi].wave[wave ^ 1].pair_mask | wgs[gi].wave[wave ^ 1].mom_mask) == 0 : !active) return;
   const int64_t row0 = (int64_t)range * rows_per_range;
   const int64_t row1 = row0 + rows_per_range < n_rows ? row0 + rows_per_range : n_rows;
   const uint32_t* where = T.where >= 0 ? reinterpret_cast<const uint32_t*>(bm.where_bits[T.where]) : ones;
-  const bool done = pair_range<false, F64, MINMAX>(T, cols, where, ones, row0, row1, range, pair_part, col_part);
+  int64_t* ring = nullptr;
+  if constexpr (RING) {
+    __shared__ __attribute__((aligned(16))) int64_t ring_lds[kRing * kSlotBytes / 8];
+    ring = ring_lds;
+  }
+  const bool done = pair_range<false, F64, MINMAX, RING>(T, cols, where, ones, row0, row1, range, pair_part,
+                                                          col_part, ring, active);
   if ((threadIdx.x & 63) == 0) redo[((size_t)gi * kPairWaves + wave) * kMaxWG + range] = done ? 0 : 1;
 }
 
@@ -435,24 +697,28 @@ __global__ __launch_bounds__(64 * kPairWaves) void dq_pair_redo(const PairWG* __
   const int64_t row0 = (int64_t)range * rows_per_range;
   const int64_t row1 = row0 + rows_per_range < n_rows ? row0 + rows_per_range : n_rows;
   const uint32_t* where = T.where >= 0 ? reinterpret_cast<const uint32_t*>(bm.where_bits[T.where]) : ones;
-  (void)pair_range<true, false, true>(T, cols, where, ones, row0, row1, range, pair_part, col_part);
+  (void)pair_range<true, false, true, false>(T, cols, where, ones, row0, row1, range, pair_part, col_part, nullptr,
+                                             true);
 }
 
 hipError_t launch_pair_scan(const PairWG* wgs, int32_t nwg, const ScanCols& cols, const ScanBitmaps& bm,
                             const uint32_t* ones, int64_t n_rows, int64_t rows_per_range, int32_t nranges,
-                            CorrPartial* pair_part, ColPartial* col_part, int32_t* redo, bool all_f64, bool minmax,
-                            hipStream_t st) {
+                            CorrPartial* pair_part, ColPartial* col_part, int32_t* redo, bool all_f64, bool ring,
+                            bool minmax, hipStream_t st) {
   const uint32_t blocks = (uint32_t)nwg * (uint32_t)nranges;
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(64 * kPairWaves), 0, st, wgs, nwg, cols, bm, ones, n_rows,
                        rows_per_range, pair_part, col_part, redo);
   };
-  if (all_f64) {
-    if (minmax) go(dq_pair_scan<true, true>);
-    else go(dq_pair_scan<true, false>);
+  if (all_f64 && ring) {
+    if (minmax) go(dq_pair_scan<true, true, true>);
+    else go(dq_pair_scan<true, false, true>);
+  } else if (all_f64) {
+    if (minmax) go(dq_pair_scan<true, true, false>);
+    else go(dq_pair_scan<true, false, false>);
   } else {
-    if (minmax) go(dq_pair_scan<false, true>);
-    else go(dq_pair_scan<false, false>);
+    if (minmax) go(dq_pair_scan<false, true, false>);
+    else go(dq_pair_scan<false, false, false>);
   }
   hipLaunchKernelGGL(dq_pair_redo, dim3(blocks), dim3(64 * kPairWaves), 0, st, wgs, nwg, cols, bm, ones, n_rows,
                      rows_per_range, pair_part, col_part, (const int32_t*)redo);

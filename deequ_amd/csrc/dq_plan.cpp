@@ -36,8 +36,8 @@ hipError_t launch_column_scan(int32_t variant, const ColTask* tasks, int32_t nta
                               int32_t nranges, ColPartial* partials, uint32_t* hll_acc, hipStream_t st);
 hipError_t launch_pair_scan(const PairWG* wgs, int32_t nwg, const ScanCols& cols, const ScanBitmaps& bm,
                             const uint32_t* ones, int64_t n_rows, int64_t rows_per_range, int32_t nranges,
-                            CorrPartial* pair_part, ColPartial* col_part, int32_t* redo, bool all_f64, bool minmax,
-                            hipStream_t st);
+                            CorrPartial* pair_part, ColPartial* col_part, int32_t* redo, bool all_f64, bool ring,
+                            bool minmax, hipStream_t st);
 hipError_t launch_finalize(int32_t ncol, int32_t nranges_col, const ColPartial* col_part, ColPartial* col_acc,
                            int32_t npair, int32_t nranges_pair, const CorrPartial* pair_part, CorrPartial* pair_acc,
                            int32_t has_pred, int32_t nranges_pred, const PredPartial* pred_part, PredPartial* pred_acc, const FinRanges& fr,
@@ -1197,9 +1197,14 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
       return s;
   }
   if (!p->pair_wgs.empty()) {
+    // the LDS-ring path's 16-byte DMA needs 16-byte aligned fp64 columns (dq_scan's contract; checked here)
+    bool ring = p->pair_all_f64;
+    for (const PairWG& wg : p->pair_wgs)
+      for (const PairWaveTask& t : wg.wave)
+        for (int c = 0; c < kPairPos && ring; ++c) ring = ((uintptr_t)sc.values[t.cols[c]] & 15u) == 0;
     if (dq_status s = timed(p, 2, p->stream, [&] {
           return launch_pair_scan(p->d_pair_wgs, (int32_t)p->pair_wgs.size(), sc, bm, p->d_ones, n_rows, rpr_col,
-                                  nr_col, p->d_pair_part, p->d_col_part, p->d_pair_redo, p->pair_all_f64,
+                                  nr_col, p->d_pair_part, p->d_col_part, p->d_pair_redo, p->pair_all_f64, ring,
                                   p->pair_minmax, p->stream);
         }))
       return s;
