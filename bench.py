@@ -206,12 +206,7 @@ def main():
         "hbm_frac_of_step": (algo_bytes_per_step / (elapsed / args.steps)) / 1e9 / HBM_PEAK_GBS,
         "rank_merge_ms_per_step": host_ms["merge"] / args.steps if world > 1 else 0.0,
         "append_ms_per_step": host_ms["append"] / args.steps,
-        "roofline": {"bound": "hbm", "achieved": dom["GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": dom["GBps"] / HBM_PEAK_GBS, "traffic": traffic,
-                     "traffic_source": os.path.relpath(PMC_FILE, ROOT) if traffic is not None else None,
-                     "kernel": dom_name, "bytes_per_launch": dom["bytes_per_launch"],
-                     "avg_launch_ms": dom["avg_ms"], "launches": dom["launches"],
-                     "valu_issue": valu_bound(dom["pmc_name"], dom["avg_ms"]), "kernels": kernels},
+        "roofline": roofline(dom_name, dom, traffic, kernels),
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1:
@@ -384,6 +379,28 @@ def valu_bound(kernel, avg_ms):
     floor_ms = insts * VALU_CYCLES_PER_WAVE_INST / (1024 * 2.4e9) * 1e3
     return {"valu_insts_per_launch": insts, "issue_floor_ms": floor_ms, "frac_of_launch": floor_ms / avg_ms,
             "model": "4 SIMD cycles per wave64 VALU instruction (measured 4.5 at 4 waves/SIMD, 3.0-3.3 at 8: tools/micro/valu_rate_probe.hip), 1024 SIMDs x 2.4 GHz", "source": os.path.relpath(PMC_FILE, ROOT)}
+
+
+def roofline(dom_name, dom, traffic, kernels) -> dict:
+    """The dominant kernel against the bound that binds it.  Both floors per launch: HBM = algorithmic
+    bytes / 8 TB/s; VALU issue = wave64 VALU instructions (committed SQ pass) x 4 cycles / (1024 SIMDs x
+    2.4 GHz).  The larger floor is the roofline (`bound`); `achieved` / `peak` / `frac` are in its unit
+    (GB/s, or wave-instructions per second for VALU), the other bound is reported beside it."""
+    hbm = {"achieved": dom["GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": dom["GBps"] / HBM_PEAK_GBS,
+           "floor_ms": dom["bytes_per_launch"] / (HBM_PEAK_GBS * 1e9) * 1e3}
+    valu = valu_bound(dom["pmc_name"], dom["avg_ms"])
+    out = {"kernel": dom_name, "bytes_per_launch": dom["bytes_per_launch"], "avg_launch_ms": dom["avg_ms"],
+           "launches": dom["launches"], "traffic": traffic,
+           "traffic_source": os.path.relpath(PMC_FILE, ROOT) if traffic is not None else None}
+    if valu is not None and valu["issue_floor_ms"] > hbm["floor_ms"]:
+        peak = 1024 * 2.4e9 / VALU_CYCLES_PER_WAVE_INST
+        out.update(bound="valu", achieved=valu["valu_insts_per_launch"] / (dom["avg_ms"] / 1e3), peak=peak,
+                   unit="wave64 VALU instructions/s", frac=valu["frac_of_launch"], valu_issue=valu, hbm=hbm)
+    else:
+        out.update(bound="hbm", achieved=hbm["achieved"], peak=hbm["peak"], unit="GB/s", frac=hbm["frac"],
+                   valu_issue=valu, hbm=hbm)
+    out["kernels"] = kernels
+    return out
 
 
 def state_io_timing(analyzers, states) -> dict:
