@@ -56,12 +56,17 @@ class HdfsStateProvider(StateLoader, StatePersister):
         return f"{self.locationPrefix}-{identifier(analyzer)}.bin"
 
     def persist(self, analyzer, state):
-        c = state_to_c(state, analyzer._lower_op())
-        n = L.lib.dq_state_to_bytes(ctypes.byref(c), None, 0)
-        if n < 0:
-            L.check(int(n))
-        buf = (ctypes.c_uint8 * n)()
-        L.lib.dq_state_to_bytes(ctypes.byref(c), buf, n)
+        from .quantiles import ApproxQuantileState
+
+        if isinstance(state, ApproxQuantileState):  # ApproximatePercentile.serializer (StateProvider.scala:126-129)
+            buf = state.percentileDigest.serialize()
+        else:
+            c = state_to_c(state, analyzer._lower_op())
+            n = L.lib.dq_state_to_bytes(ctypes.byref(c), None, 0)
+            if n < 0:
+                L.check(int(n))
+            buf = (ctypes.c_uint8 * n)()
+            L.lib.dq_state_to_bytes(ctypes.byref(c), buf, n)
         path = self._path(analyzer)
         if os.path.exists(path) and not self.allowOverwrite:
             raise FileExistsError(f"File {path} already exists!")  # DfsUtils.writeToFileOnDfs
@@ -74,6 +79,10 @@ class HdfsStateProvider(StateLoader, StatePersister):
             return None
         with open(path, "rb") as f:
             data = f.read()
+        from .quantiles import ApproxQuantileState, PercentileDigest, _QuantileBase
+
+        if isinstance(analyzer, _QuantileBase):  # StateProvider.scala:165-167
+            return ApproxQuantileState(PercentileDigest.deserialize(data))
         out = L.State()
         L.check(L.lib.dq_state_from_bytes(analyzer._lower_op(), data, len(data), ctypes.byref(out)))
         return state_from_c(out)

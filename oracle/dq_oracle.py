@@ -1590,6 +1590,27 @@ def state_to_bytes(state) -> bytes:
 # (AnalyzerTests.scala:533-565); GK's own order-dependent pick is not restated (parity vs GK
 # unpinned -- any value inside its bound is a correct ApproxQuantile).
 # --------------------------------------------------------------------------------------
+def gk_digest_exact(values: np.ndarray, valid: np.ndarray, relative_error: float) -> Tuple[int, List[Tuple[float, int, int]]]:
+    """(count, sampled) of the quantile state the GPU path builds (deequ_amd/quantiles.py module doc): the
+    exact order statistics at ranks 1, 1 + s, ..., n with s = max(1, floor(2 e n)), e = 1 / (1 / relErr)
+    (StatefulApproxQuantile's accuracy round trip, DeequFunctions.scala:63-71), g = rank gaps, delta = 0."""
+    v = np.asarray(values)[np.asarray(valid, bool)]
+    n = len(v)
+    if n == 0:
+        return 0, []
+    e = 0.0 if relative_error == 0.0 else 1.0 / (1.0 / relative_error)
+    s = max(1, int(math.floor(2 * e * n)))
+    ranks = list(range(1, n + 1, s))
+    if ranks[-1] != n:
+        ranks.append(n)
+    vals = approx_quantiles_exact(values, valid, [(r - 0.5) / n for r in ranks], 0.0)
+    out, prev = [], 0
+    for r, x in zip(ranks, vals):
+        out.append((x, r - prev, 0))
+        prev = r
+    return n, out
+
+
 def approx_quantiles_exact(values: np.ndarray, valid: np.ndarray, quantiles: Sequence[float],
                            relative_error: float = 0.01) -> Optional[List[float]]:
     v = np.asarray(values)[np.asarray(valid, bool)]

@@ -1,7 +1,8 @@
 """ApproxQuantile / ApproxQuantiles (ApproxQuantile.scala:49-103, ApproxQuantiles.scala:30-105).
 
 CPU: the oracle against the reference's own band tests (AnalyzerTests.scala:533-565) and the
-parameter checks' messages (:567-600).  GPU (`-m gpu`): dq_approx_quantiles through the C ABI
+parameter checks' messages (:567-600); the quantile state's digest (serializer layout and round trip as
+StateProviderTest.scala:118-139 checks it, IncrementalAnalyzerTest.scala:176-199's merge, GK's rank bound).  GPU (`-m gpu`): dq_approx_quantiles through the C ABI
 against the oracle's exact order statistic, bit-exact (it is a selection, no arithmetic), over f64
 with NaN / +-inf / -0.0 / nulls, i64, i32, several chunks, all-null and ragged sizes.
 """
@@ -147,3 +148,119 @@ def test_gpu_quantiles_chunks_nulls_and_reference_bands(dq):
     assert dq.ApproxQuantile("x", 0.5).calculate(t0).value.isFailure
     m = dq.ApproxQuantiles("x", [0.1, 0.5]).calculate(t0)
     assert m.value.isSuccess and m.value.get() == {}, m
+
+
+# ---- ApproxQuantileState: the GK digest (Spark 2.2.2 QuantileSummaries / PercentileDigestSerializer restated;
+# parity unpinned beyond the reference's StateProviderTest / IncrementalAnalyzerTest cases and GK's rank bound)
+
+def _digest(values, valid, err):
+    from deequ_amd.quantiles import PercentileDigest, QuantileSummaries, spark_relative_error
+
+    n, sampled = O.gk_digest_exact(values, valid, err)
+    return PercentileDigest(QuantileSummaries(10000, spark_relative_error(err), sampled, n))
+
+
+def test_digest_serializer_layout_and_round_trip():
+    from deequ_amd.quantiles import PercentileDigest
+
+    d = _digest(np.array([3.0, -1.0, 2.5]), np.ones(3, bool), 0.01)
+    img = d.serialize()
+    # compressThreshold int, relativeError double, count long, length int, then (value double, g int, delta int)
+    assert img[:4] == (10000).to_bytes(4, "big") and img[12:20] == (3).to_bytes(8, "big")
+    assert img[20:24] == (3).to_bytes(4, "big") and len(img) == 24 + 3 * 16
+    assert img[24:40] == bytes.fromhex("bff0000000000000") + (1).to_bytes(4, "big") + (0).to_bytes(4, "big")
+    back = PercentileDigest.deserialize(img)  # StateProviderTest.assertCorrectlyApproxQuantileState
+    s, c = d.quantileSummaries, back.quantileSummaries
+    assert (s.compressThreshold, s.relativeError, s.count, s.sampled) == (c.compressThreshold, c.relativeError,
+                                                                             c.count, c.sampled)
+    with pytest.raises(ValueError):
+        PercentileDigest.deserialize(img[:-1])
+
+
+def test_incremental_merge_reference_case():
+    # IncrementalAnalyzerTest.scala:176-199: median of first = (0, 1, 2) merged with second = (-2, -1) is 0.0,
+    # the same as over the union
+    first = _digest(np.array([0.0, 1.0, 2.0]), np.ones(3, bool), 0.01)
+    second = _digest(np.array([-2.0, -1.0]), np.ones(2, bool), 0.01)
+    union = _digest(np.array([0.0, 1.0, 2.0, -2.0, -1.0]), np.ones(5, bool), 0.01)
+    assert first.merge(second).getPercentiles([0.5]) == [0.0] == union.getPercentiles([0.5])
+
+
+@pytest.mark.parametrize("err", [0.01, 0.05, 0.2])
+def test_digest_queries_within_gk_bound(err):
+    rng = np.random.default_rng(int(err * 1000))
+    x = rng.normal(size=20_000)
+    srt = np.sort(x)
+    parts = np.array_split(x, 5)
+    single = _digest(x, np.ones(len(x), bool), err)
+    merged = _digest(parts[0], np.ones(len(parts[0]), bool), err)
+    for p in parts[1:]:
+        merged = merged.merge(_digest(p, np.ones(len(p), bool), err))
+    n = len(x)
+    for q in np.linspace(0.0, 1.0, 41):
+        target = min(n, max(1, math.ceil(q * n)))
+        for dg, slack in ((single, math.ceil(err * n) + 1), (merged, 2 * math.ceil(err * n) + 1)):
+            v = dg.getPercentiles([q])[0]
+            lo, hi = np.searchsorted(srt, v, "left") + 1, np.searchsorted(srt, v, "right")
+            assert lo - slack <= target <= hi + slack, (err, q, v, lo, hi, target)
+    assert merged.quantileSummaries.count == n
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["f64", "i64", "i32"])
+def test_gpu_digest_matches_exact_ranks(dq, dtype):
+    from deequ_amd.quantiles import device_digest
+    from deequ_amd.table import column_from_numpy
+
+    rng = np.random.default_rng(11 + len(dtype))
+    n = 123_457
+    if dtype == "f64":
+        v = _f64_data(rng, n)
+    elif dtype == "i64":
+        v = rng.integers(-(1 << 40), 1 << 40, n, dtype=np.int64)
+    else:
+        v = rng.integers(-(1 << 31), (1 << 31) - 1, n, dtype=np.int64).astype(np.int32)
+    valid = rng.random(n) >= 0.1
+    cuts = [0, 50_000, 50_000, 99_999, n]
+    parts = [dq.Table([column_from_numpy("x", dtype, v[a:b], valid[a:b])]) for a, b in zip(cuts, cuts[1:])]
+    for err in (0.01, 0.1, 0.5):
+        got = device_digest(parts, "x", err).quantileSummaries
+        cnt, want = O.gk_digest_exact(v, valid, err)
+        assert got.count == cnt and len(got.sampled) == len(want)
+        assert all(_same(a[0], b[0]) and a[1:] == b[1:] for a, b in zip(got.sampled, want)), (dtype, err)
+
+
+@pytest.mark.gpu
+def test_gpu_quantile_state_persist_load_and_aggregate(dq, tmp_path):
+    from deequ_amd.quantiles import ApproxQuantileState
+    from deequ_amd.state_provider import HdfsStateProvider, InMemoryStateProvider
+    from deequ_amd.table import column_from_numpy
+
+    rng = np.random.default_rng(5)
+    x = rng.normal(size=40_000)
+    ok = rng.random(len(x)) >= 0.05
+    a_t = dq.Table([column_from_numpy("price", "f64", x[:25_000], ok[:25_000])])
+    b_t = dq.Table([column_from_numpy("price", "f64", x[25_000:], ok[25_000:])])
+    an = dq.ApproxQuantile("price", 0.5)
+    hdfs = HdfsStateProvider(str(tmp_path / "q"), allowOverwrite=True)
+    mem = InMemoryStateProvider()
+    for prov in (hdfs, mem):
+        m_a = an.calculate(a_t, saveStatesWith=prov)
+        st = prov.load(an)
+        assert isinstance(st, ApproxQuantileState) and st == an.computeStateFrom(a_t)
+        assert m_a.value.get() == st.percentileDigest.getPercentiles([0.5])[0]
+        # the second batch aggregated with the first: the metric of the merged digest
+        m_ab = an.calculate(b_t, aggregateWith=prov)
+        merged = an.computeStateFrom(b_t).sum(st)
+        assert m_ab.value.get() == merged.percentileDigest.getPercentiles([0.5])[0]
+        srt = np.sort(x[ok])
+        rank = np.searchsorted(srt, m_ab.value.get()) + 1
+        assert abs(rank - math.ceil(0.5 * len(srt))) <= 2 * math.ceil(0.01 * len(srt)) + 1
+    qs = dq.ApproxQuantiles("price", [0.1, 0.9])
+    m = qs.calculate(a_t, saveStatesWith=mem)
+    assert set(m.value.get()) == {"0.1", "0.9"} and isinstance(mem.load(qs), ApproxQuantileState)
+    # all NULL: ApproxQuantile's state is None (EmptyStateException), ApproxQuantiles' an empty digest
+    t0 = dq.Table([column_from_numpy("price", "f64", x[:10], np.zeros(10, bool))])
+    assert an.calculate(t0, saveStatesWith=InMemoryStateProvider()).value.isFailure
+    m0 = qs.calculate(t0, saveStatesWith=InMemoryStateProvider())
+    assert m0.value.isSuccess and m0.value.get() == {}
