@@ -165,18 +165,6 @@ struct PredCounter {
   int32_t where;  // root slot or -1
 };
 
-// ApproxCountDistinct of a column the predicate pass already loads (HLL-only column task, no `where`),
-// computed inside the predicate pass instead of a second read in the column pass
-constexpr int kMaxPredHll = 4;
-struct PredHll {
-  int32_t instr;     // the first ATOM_CMP instruction loading the column's values
-  int32_t operand;   // 0: its col_a, 1: its col_b
-  int32_t kind;      // CK_F64 / CK_I64 / CK_I32
-  int32_t part;      // column task index (partial / accumulator slot)
-  int32_t hll_slot;  // the task's HLL accumulator
-  int32_t pad;
-};
-
 struct PredProgram {
   const uint16_t* regex;           // device: concatenated DFAs (n_states, n_classes, start, flags,
                                    // cls[256], acc_end[n_states], trans[n_states][n_classes])
@@ -187,8 +175,6 @@ struct PredProgram {
   int32_t n_loads;                 // atoms (the instructions that read a column)
   int32_t n_roots;                 // root slots stored by the program
   int32_t stack_depth;             // max operand stack depth (<= kPredStack)
-  int32_t n_hll;                   // fused HLL tasks (PredHll)
-  PredHll hll[kMaxPredHll];
   int16_t load_instr[kMaxInstr];   // their instruction indices, in program order
   int32_t bitmap_root[kMaxWhere];  // root slot whose TRUE bits fill where-bitmap i
   PredCounter counters[kMaxCounters];

@@ -760,6 +760,8 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
       }
       const u32x4 a = win_a[0], c = win_c[0];
       const uint32_t d[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+      // (byte-granular unaligned window loads instead of this realignment -- 8 fewer VALU per string --
+      // measured 2.70-2.73 vs 1.90-1.92 ms per 125 M rows x 4: the unaligned 16-byte loads are address-bound)
       const uint32_t sh = rel_of(j) << 3;  // v_alignbit reads the low 5 bits: (o0 & 3) * 8
       uint32_t wv[8];
 #pragma unroll
@@ -1065,8 +1067,10 @@ struct AtomBuf {
   bool t_vals = false;
 };
 
-// One ATOM_CMP for a block from its loads: the lane's 32-bit TRUE / NULL words (lanes 0..15).
-__device__ __forceinline__ void pred_atom_cmp(const PredInstr& ins, const AtomBuf& L, int lane, uint32_t& wt,
+// One ATOM_CMP for a block from its operands' raw values (a, b: rows base + 64 j + lane) and validity words:
+// the lane's 32-bit TRUE / NULL words (lanes 0..15).
+__device__ __forceinline__ void pred_atom_cmp(const PredInstr& ins, const uint64_t (&La)[8], uint32_t Lva,
+                                              const uint64_t (&Lb)[8], uint32_t Lvb, int lane, uint32_t& wt,
                                               uint32_t& wn) {
   // result = (lt & Klt) | (eq & Keq) | (gt & Kgt) | NaN terms (Spark: NaN = NaN, NaN > all)
   const int cmp = ins.cmp;
@@ -1093,7 +1097,7 @@ __device__ __forceinline__ void pred_atom_cmp(const PredInstr& ins, const AtomBu
     auto run = [&](auto op) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int64_t x = (int64_t)L.a[j], y = two ? (int64_t)L.b[j] : ins.lit_i;
+        const int64_t x = (int64_t)La[j], y = two ? (int64_t)Lb[j] : ins.lit_i;
         put(j, __builtin_amdgcn_ballot_w64(op(x, y)));
       }
     };
@@ -1113,7 +1117,7 @@ __device__ __forceinline__ void pred_atom_cmp(const PredInstr& ins, const AtomBu
     if (is_int) break;
     uint64_t lt, eq, gt, an = 0, bn = 0;
     {
-      const double x = pred_as_double(L.a[j], ins.kind_a), y = two ? pred_as_double(L.b[j], ins.kind_b) : ins.lit_d;
+      const double x = pred_as_double(La[j], ins.kind_a), y = two ? pred_as_double(Lb[j], ins.kind_b) : ins.lit_d;
       lt = __builtin_amdgcn_ballot_w64(x < y);
       eq = __builtin_amdgcn_ballot_w64(x == y);
       gt = __builtin_amdgcn_ballot_w64(x > y);
@@ -1124,10 +1128,15 @@ __device__ __forceinline__ void pred_atom_cmp(const PredInstr& ins, const AtomBu
     put(j, cm);  // row group j -> the word lanes (lanes 0..15: word L = rows 32 L .. + 31 of the block)
   }
   // NULL operand b -> NULL; NULL a -> the COALESCE fallback result (NULL without one)
-  const uint32_t va = L.va, vb = two ? L.vb : ~0u;
+  const uint32_t va = Lva, vb = two ? Lvb : ~0u;
   const uint32_t nr_true = ins.null_res == NR_TRUE ? ~0u : 0u, nr_null = ins.null_res == NR_NULL ? ~0u : 0u;
   wt = (va & vb & wc) | (~va & vb & nr_true);
   wn = ~vb | (~va & nr_null);
+}
+
+__device__ __forceinline__ void pred_atom_cmp(const PredInstr& ins, const AtomBuf& L, int lane, uint32_t& wt,
+                                              uint32_t& wn) {
+  pred_atom_cmp(ins, L.a, L.va, L.b, L.vb, lane, wt, wn);
 }
 
 // One ATOM_REGEX for a block (PatternMatch.scala:48-49 / RLIKE): lane l walks the search DFA (staged in
@@ -1264,27 +1273,109 @@ __device__ __forceinline__ PredInstr uniform_instr(const PredInstr* p) {
   return r;
 }
 
+// The fields an ATOM_CMP evaluation reads (cmp, ctype, null_res, col_b, kinds, literals), wave-uniform: 10
+// readfirstlanes instead of the whole instruction's 14 (the block loop decodes every instruction per block).
+__device__ __forceinline__ PredInstr uniform_cmp_fields(const PredInstr* p) {
+  PredInstr r{};
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(p);
+  uint32_t* o = reinterpret_cast<uint32_t*>(&r);
+  constexpr int kF[10] = {1, 2, 3, 5, 6, 7, 8, 9, 10, 11};
+  static_assert(offsetof(PredInstr, lit_d) == 40 && offsetof(PredInstr, col_b) == 20, "PredInstr layout");
+#pragma unroll
+  for (int k = 0; k < 10; ++k) o[kF[k]] = __builtin_amdgcn_readfirstlane(w[kF[k]]);
+  return r;
+}
+
+// Compact per-instruction words staged in LDS by the interpreter, one readfirstlane each:
+//   op word:   op | null_res << 8 | slot << 16            (every instruction; logic ops need nothing else)
+//   load word: op | (col_a + 1) << 4 | (col_b + 1) << 12 | kind_a << 20 | kind_b << 24   (atoms)
+__device__ __forceinline__ uint32_t pred_op_word(const PredInstr& ins) {
+  return (uint32_t)ins.op | (uint32_t)ins.null_res << 8 | (uint32_t)ins.slot << 16;
+}
+__device__ __forceinline__ uint32_t pred_load_word(const PredInstr& ins) {
+  return (uint32_t)ins.op | (uint32_t)(ins.col_a + 1) << 4 | (uint32_t)(ins.col_b + 1) << 12 | (uint32_t)ins.kind_a << 20 |
+         (uint32_t)ins.kind_b << 24;
+}
+
+// Three-valued logic ops of the program on the wave's 16 word lanes (operand stack in LDS):
+// CONST / AND / OR / NOT / STORE (w: the op word); atoms push their own results.
+__device__ __forceinline__ void pred_logic_op(uint32_t w, const PredScratch& S, int& sp, int lane) {
+  const int op = (int)(w & 0xFFu), null_res = (int)((w >> 8) & 0xFFu), slot = (int)(w >> 16);
+  const bool wl = lane < 16;
+  if (op == PO_CONST) {
+    if (wl) { S.st[(sp) * 16 + lane] = null_res == NR_TRUE ? ~0u : 0u; S.sn[(sp) * 16 + lane] = null_res == NR_NULL ? ~0u : 0u; }
+    ++sp;
+  } else if (op == PO_AND || op == PO_OR) {
+    if (wl) {
+      const uint32_t at = S.st[(sp - 2) * 16 + lane], an = S.sn[(sp - 2) * 16 + lane];
+      const uint32_t bt = S.st[(sp - 1) * 16 + lane], bn = S.sn[(sp - 1) * 16 + lane];
+      const uint32_t af = ~at & ~an, bf = ~bt & ~bn;
+      const uint32_t rt = op == PO_AND ? (at & bt) : (at | bt);
+      const uint32_t rf = op == PO_AND ? (af | bf) : (af & bf);
+      S.st[(sp - 2) * 16 + lane] = rt;
+      S.sn[(sp - 2) * 16 + lane] = ~rt & ~rf;
+    }
+    --sp;
+  } else if (op == PO_NOT) {
+    if (wl) {
+      const uint32_t at = S.st[(sp - 1) * 16 + lane], an = S.sn[(sp - 1) * 16 + lane];
+      S.st[(sp - 1) * 16 + lane] = ~at & ~an;
+    }
+  } else if (op == PO_STORE) {
+    if (wl) { S.rt[(slot) * 16 + lane] = S.st[(sp - 1) * 16 + lane]; S.rn[(slot) * 16 + lane] = S.sn[(sp - 1) * 16 + lane]; }
+    --sp;
+  }
+}
+
+// End of a block: counters (TRUE / NOT NULL of each (predicate, where) pair over the in-range rows) and
+// the `where` bitmaps, on the word lanes (wr = first row of the lane's word).
+__device__ __forceinline__ void pred_block_out(const PredScratch& S, const PredCounter* s_ctr, int n_counters,
+                                               const int32_t* s_bmroot, int n_bitmaps, const ScanBitmaps& bm,
+                                               int64_t wr, uint32_t inr, int64_t n_rows, int lane) {
+  if (lane >= 16) return;
+  for (int c = 0; c < n_counters; ++c) {
+    const PredCounter pc = s_ctr[c];
+    const uint32_t tw = (pc.where < 0 ? ~0u : S.rt[(pc.where) * 16 + lane]) & inr;
+    S.ct[(c) * 16 + lane] += __popc(S.rt[(pc.pred) * 16 + lane] & tw);
+    S.cn[(c) * 16 + lane] += __popc(~S.rn[(pc.pred) * 16 + lane] & tw);
+  }
+  if (wr < n_rows) {
+    for (int b = 0; b < n_bitmaps; ++b)
+      reinterpret_cast<uint32_t*>(bm.where_bits[b])[wr >> 5] = S.rt[s_bmroot[b] * 16 + lane] & inr;
+  }
+}
+
+// Workgroup partials -> accumulator (integer atomics: order-free); waits for every wave's counters.
+__device__ __forceinline__ void pred_counters_out(const uint32_t* pred_lds, int wave_words, const PredProgram& prog,
+                                                  PredPartial* acc) {
+  __syncthreads();
+  if (threadIdx.x < prog.n_counters) {
+    const int c = threadIdx.x;
+    int64_t t = 0, nn = 0;
+    for (int w = 0; w < kWaves; ++w)
+      for (int l = 0; l < 16; ++l) {
+        const PredScratch W(const_cast<uint32_t*>(pred_lds) + w * wave_words, prog.stack_depth, prog.n_roots,
+                            prog.n_counters);
+        t += W.ct[c * 16 + l];
+        nn += W.cn[c * 16 + l];
+      }
+    atomicAdd(reinterpret_cast<unsigned long long*>(&acc->t[c]), (unsigned long long)t);
+    atomicAdd(reinterpret_cast<unsigned long long*>(&acc->nn[c]), (unsigned long long)nn);
+  }
+}
+
 // RX: the program holds regex atoms.  Instantiated separately so that the DFA walk's registers (142
 // VGPRs with it, 119 without: 3 vs 4 waves per SIMD) do not cost the plain numeric programs occupancy.
-// HLL: the program hashes fused HLL-only columns (PredProgram::hll); its own instantiation keeps the hash
-// registers out of the plain interpreter (120 vs 141 VGPRs: 4 vs 3 waves per SIMD).
-#ifndef DQ_PRED_WAVES
-#define DQ_PRED_WAVES 1  // occupancy floor of the plain program (1 = unconstrained, 120 VGPRs / 4 waves).  5 and 6
-                         // spill (96 VGPRs + 120 B, 80 + 184 B scratch): 0.96 -> 1.56 / 2.43 ms per 125 M rows
-#endif
-template <bool RX, bool HLL>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(!RX && !HLL ? DQ_PRED_WAVES : 1))) void dq_pred_scan(const PredProgram* __restrict__ prog_g, ScanCols cols,
+template <bool RX>
+__global__ __launch_bounds__(kBlock) void dq_pred_scan(const PredProgram* __restrict__ prog_g, ScanCols cols,
                                                        ScanBitmaps bm, int64_t n_rows, int64_t rows_per_range,
-                                                       PredPartial* __restrict__ acc, ColPartial* __restrict__ col_part,
-                                                       uint32_t* __restrict__ hll_acc) {
+                                                       PredPartial* __restrict__ acc) {
   extern __shared__ uint32_t pred_lds[];
   __shared__ PredInstr s_instr[kMaxInstr];
-  __shared__ int16_t s_load[kMaxInstr];
+  __shared__ uint32_t s_op[kMaxInstr];    // op words (pred_op_word)
+  __shared__ uint32_t s_ldw[kMaxInstr];   // atom k's load word (pred_load_word)
   __shared__ PredCounter s_ctr[kMaxCounters];
   __shared__ int32_t s_bmroot[kMaxWhere];
-  __shared__ PredHll s_hll[kMaxPredHll];
-  __shared__ int32_t s_regs[kMaxPredHll * 512];          // fused HLL tasks' registers (q = pw - 1, -1 empty)
-  __shared__ unsigned long long s_hcnt[kMaxPredHll];    // their selected-row counts
   const PredProgram& prog = *prog_g;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1295,54 +1386,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(!RX && !
   // the program -> LDS once per workgroup
   for (int k = threadIdx.x; k < n_instr * (int)(sizeof(PredInstr) / 4); k += kBlock)
     reinterpret_cast<uint32_t*>(s_instr)[k] = reinterpret_cast<const uint32_t*>(prog.instr)[k];
-  for (int k = threadIdx.x; k < n_loads; k += kBlock) s_load[k] = prog.load_instr[k];
+  for (int k = threadIdx.x; k < n_instr; k += kBlock) s_op[k] = pred_op_word(prog.instr[k]);
+  for (int k = threadIdx.x; k < n_loads; k += kBlock) s_ldw[k] = pred_load_word(prog.instr[prog.load_instr[k]]);
   for (int k = threadIdx.x; k < n_counters; k += kBlock) s_ctr[k] = prog.counters[k];
   for (int k = threadIdx.x; k < n_bitmaps; k += kBlock) s_bmroot[k] = prog.bitmap_root[k];
-  const int n_hll = HLL ? prog.n_hll : 0;
-  for (int k = threadIdx.x; k < n_hll * (int)(sizeof(PredHll) / 4); k += kBlock)
-    reinterpret_cast<uint32_t*>(s_hll)[k] = reinterpret_cast<const uint32_t*>(prog.hll)[k];
-  for (int k = threadIdx.x; k < n_hll * 512; k += kBlock) s_regs[k] = -1;
-  if (threadIdx.x < kMaxPredHll) s_hcnt[threadIdx.x] = 0;
   __syncthreads();
-  uint64_t hcnt[kMaxPredHll] = {0, 0, 0, 0};  // wave-uniform selected-row counts of the fused HLL tasks
-  // ApproxCountDistinct of fused column e from an atom's loaded values (L): rows selected = valid and in
-  // range (the word lanes' validity & in-range words, moved to SGPRs per row group); XXH64 as the column
-  // pass (doubleToLongBits: NaN canonical), branch-free register max, the rare low-word rank exactly.
-  auto hll_block = [&](const PredHll& e, int h, const AtomBuf& L, uint32_t inr) {
-    const uint32_t vw = (e.operand ? L.vb : L.va) & inr;
-    int32_t* regs = s_regs + h * 512;
-    int32_t qmin = 0;
-    uint64_t ms[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)vw, 2 * j);
-      const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)vw, 2 * j + 1);
-      const uint64_t m = ((uint64_t)hi << 32) | lo;
-      ms[j] = m;
-      hcnt[h] += (uint64_t)__builtin_popcountll(m);
-      uint64_t b = e.operand ? L.b[j] : L.a[j];
-      HllKey key;
-      if (e.kind == CK_I32) {
-        key = hll_key_int((uint32_t)b);
-      } else {
-        if (e.kind == CK_F64 && __builtin_bit_cast(double, b) != __builtin_bit_cast(double, b)) b = 0x7FF8000000000000ull;
-        key = hll_key_long(b);
-      }
-      const bool sel = lane_bit(m);
-      qmin = min(qmin, sel ? key.q : 0);
-      atomicMax(reinterpret_cast<int32_t*>(reinterpret_cast<char*>(regs) + key.addr), sel ? key.q : -1);
-    }
-    // rare (2^-23 per value): a rank that needs the hash's low word -- redo the selected values exactly
-    if (__builtin_amdgcn_ballot_w64(qmin < 0) != 0) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {  // unrolled: no indexed register arrays
-        if (!lane_bit(ms[j])) continue;
-        uint64_t b = e.operand ? L.b[j] : L.a[j];
-        if (e.kind == CK_F64 && __builtin_bit_cast(double, b) != __builtin_bit_cast(double, b)) b = 0x7FF8000000000000ull;
-        hll_update(regs, e.kind == CK_I32 ? xxh64_int((uint32_t)b) : xxh64_long(b));
-      }
-    }
-  };
   if (wl) {
     for (int c = 0; c < n_counters; ++c) { S.ct[(c) * 16 + lane] = 0; S.cn[(c) * 16 + lane] = 0; }
   }
@@ -1362,7 +1410,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(!RX && !
   // previous atom): a column it already holds for the same block is copied, not re-read -- C3 reads i1 in
   // three consecutive atoms and i3 in two, and those re-reads missed L2 (FETCH_SIZE 1.41x algorithmic).
   auto issue = [&](int k, int64_t base, AtomBuf& L, const AtomBuf& C) {
-    const PredInstr ins = uniform_instr(&s_instr[__builtin_amdgcn_readfirstlane((int)s_load[k])]);
+    const uint32_t lw = __builtin_amdgcn_readfirstlane(s_ldw[k]);
+    const int op = (int)(lw & 15u), col_a = (int)((lw >> 4) & 0xFFu) - 1, col_b = (int)((lw >> 12) & 0xFFu) - 1;
+    const int kind_a = (int)((lw >> 20) & 15u), kind_b = (int)((lw >> 24) & 15u);
     const bool same_blk = C.t_base == base;
     auto fetch = [&](int col, int kind, bool vals, uint64_t (&dst)[8], uint32_t& vdst) __attribute__((always_inline)) {
       if (same_blk && col == C.t_col_a && (C.t_vals || !vals)) {
@@ -1382,12 +1432,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(!RX && !
         vdst = pred_valid_word(cols.validity[col], base, n_rows, lane);
       }
     };
-    const bool cmp = ins.op == PO_ATOM_CMP;
-    if (cmp && ins.col_b >= 0) fetch(ins.col_b, ins.kind_b, true, L.b, L.vb);
-    fetch(ins.col_a, ins.kind_a, cmp, L.a, L.va);
+    const bool cmp = op == PO_ATOM_CMP;
+    if (cmp && col_b >= 0) fetch(col_b, kind_b, true, L.b, L.vb);
+    fetch(col_a, kind_a, cmp, L.a, L.va);
     L.t_base = base;
-    L.t_col_a = ins.col_a;
-    L.t_col_b = cmp ? ins.col_b : -1;
+    L.t_col_a = col_a;
+    L.t_col_b = cmp ? col_b : -1;
     L.t_vals = cmp;
   };
   if (n_loads > 0) issue(0, row0 + (int64_t)wave * 512, B0, B1);
@@ -1401,8 +1451,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(!RX && !
     const uint32_t inr = wr >= row1 ? 0u : (wr + 32 <= row1 ? ~0u : ((1u << (row1 - wr)) - 1u));
     int sp = 0, k = 0;
     for (int i = 0; i < n_instr; ++i) {
-      const PredInstr ins = uniform_instr(&s_instr[i]);
-      const int op = ins.op;
+      const uint32_t ow = __builtin_amdgcn_readfirstlane(s_op[i]);
+      const int op = (int)(ow & 0xFFu);
       if (op == PO_ATOM_CMP || op == PO_ATOM_ISNULL || op == PO_ATOM_NOTNULL || op == PO_ATOM_REGEX) {
         // next atom: the following one of this block, else the first of the next block
         const int kn = k + 1 < n_loads ? k + 1 : 0;
@@ -1412,20 +1462,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(!RX && !
         if ((g & 1u) == 0) issue(kn, bn, B1, B0);
         else issue(kn, bn, B0, B1);
         if (op == PO_ATOM_CMP) {
+          const PredInstr ins = uniform_cmp_fields(&s_instr[i]);
           if ((g & 1u) == 0) pred_atom_cmp(ins, B0, lane, wt, wn);
           else pred_atom_cmp(ins, B1, lane, wt, wn);
-#pragma unroll
-          for (int h = 0; h < (HLL ? kMaxPredHll : 0); ++h) {  // uniform; the first atom loading a fused column hashes it
-            if (h >= n_hll) break;
-            const PredHll e = *reinterpret_cast<const PredHll*>(&s_hll[h]);
-            if (__builtin_amdgcn_readfirstlane(e.instr) != i) continue;
-            PredHll eu;
-            eu.operand = __builtin_amdgcn_readfirstlane(e.operand);
-            eu.kind = __builtin_amdgcn_readfirstlane(e.kind);
-            if ((g & 1u) == 0) hll_block(eu, h, B0, inr);
-            else hll_block(eu, h, B1, inr);
-          }
         } else if (RX && op == PO_ATOM_REGEX) {
+          const PredInstr ins = uniform_instr(&s_instr[i]);
           const uint32_t va = (g & 1u) ? B1.va : B0.va;
           if (ins.kind_a == CK_UTF8)
             pred_atom_regex_utf8(ins, dfa_lds + ins.lit_i, reinterpret_cast<const uint8_t*>(cols.values[ins.col_a]),
@@ -1444,74 +1485,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(!RX && !
         ++k;
         if (wl) { S.st[(sp) * 16 + lane] = wt; S.sn[(sp) * 16 + lane] = wn; }
         ++sp;
-      } else if (op == PO_CONST) {
-        if (wl) { S.st[(sp) * 16 + lane] = ins.null_res == NR_TRUE ? ~0u : 0u; S.sn[(sp) * 16 + lane] = ins.null_res == NR_NULL ? ~0u : 0u; }
-        ++sp;
-      } else if (op == PO_AND || op == PO_OR) {
-        if (wl) {
-          const uint32_t at = S.st[(sp - 2) * 16 + lane], an = S.sn[(sp - 2) * 16 + lane];
-          const uint32_t bt = S.st[(sp - 1) * 16 + lane], bn = S.sn[(sp - 1) * 16 + lane];
-          const uint32_t af = ~at & ~an, bf = ~bt & ~bn;
-          const uint32_t rt = op == PO_AND ? (at & bt) : (at | bt);
-          const uint32_t rf = op == PO_AND ? (af | bf) : (af & bf);
-          S.st[(sp - 2) * 16 + lane] = rt;
-          S.sn[(sp - 2) * 16 + lane] = ~rt & ~rf;
-        }
-        --sp;
-      } else if (op == PO_NOT) {
-        if (wl) {
-          const uint32_t at = S.st[(sp - 1) * 16 + lane], an = S.sn[(sp - 1) * 16 + lane];
-          S.st[(sp - 1) * 16 + lane] = ~at & ~an;
-        }
-      } else if (op == PO_STORE) {
-        if (wl) { S.rt[(ins.slot) * 16 + lane] = S.st[(sp - 1) * 16 + lane]; S.rn[(ins.slot) * 16 + lane] = S.sn[(sp - 1) * 16 + lane]; }
-        --sp;
+      } else {
+        pred_logic_op(ow, S, sp, lane);
       }
     }
-    if (wl) {
-      for (int c = 0; c < n_counters; ++c) {
-        const PredCounter pc = s_ctr[c];
-        const uint32_t tw = (pc.where < 0 ? ~0u : S.rt[(pc.where) * 16 + lane]) & inr;
-        S.ct[(c) * 16 + lane] += __popc(S.rt[(pc.pred) * 16 + lane] & tw);
-        S.cn[(c) * 16 + lane] += __popc(~S.rn[(pc.pred) * 16 + lane] & tw);
-      }
-      if (wr < n_rows) {
-        for (int b = 0; b < n_bitmaps; ++b)
-          reinterpret_cast<uint32_t*>(bm.where_bits[b])[wr >> 5] = S.rt[s_bmroot[b] * 16 + lane] & inr;
-      }
-    }
+    pred_block_out(S, s_ctr, n_counters, s_bmroot, n_bitmaps, bm, wr, inr, n_rows, lane);
   }
-  // fused HLL tasks: counts (range slot 0 of the task's partials; the plan zeroes the others per scan) and
-  // registers -> one of the kHllCopies accumulator copies (device-scope max, order-free)
-  if (lane == 0) {
-#pragma unroll
-    for (int h = 0; h < kMaxPredHll; ++h)
-      if (h < n_hll) atomicAdd(&s_hcnt[h], (unsigned long long)hcnt[h]);
-  }
-  __syncthreads();
-  for (int h = 0; h < n_hll; ++h) {
-    const PredHll e = s_hll[h];
-    if (threadIdx.x == 0)
-      atomicAdd(reinterpret_cast<unsigned long long*>(&col_part[(size_t)e.part * kMaxWG].count), s_hcnt[h]);
-    uint32_t* dst = hll_acc + ((size_t)e.hll_slot * kHllCopies + (blockIdx.x % kHllCopies)) * 512;
-    for (int r = threadIdx.x; r < 512; r += kBlock) {
-      const uint32_t v = (uint32_t)(s_regs[h * 512 + r] + 1);
-      if (v > __builtin_nontemporal_load(dst + r)) atomicMax(dst + r, v);
-    }
-  }
-  // workgroup partials -> accumulator (integer atomics: order-free)
-  if (threadIdx.x < n_counters) {
-    const int c = threadIdx.x;
-    int64_t t = 0, nn = 0;
-    for (int w = 0; w < kWaves; ++w)
-      for (int l = 0; l < 16; ++l) {
-        const PredScratch W(pred_lds + w * wave_words, prog.stack_depth, prog.n_roots, prog.n_counters);
-        t += W.ct[c * 16 + l];
-        nn += W.cn[c * 16 + l];
-      }
-    atomicAdd(reinterpret_cast<unsigned long long*>(&acc->t[c]), (unsigned long long)t);
-    atomicAdd(reinterpret_cast<unsigned long long*>(&acc->nn[c]), (unsigned long long)nn);
-  }
+  pred_counters_out(pred_lds, wave_words, prog, acc);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1603,19 +1583,14 @@ __global__ void dq_init_acc(ColPartial* col_acc, int32_t ncol, CorrPartial* pair
 // host-side launchers (called from dq_plan.cpp)
 // ------------------------------------------------------------------------------------------
 hipError_t launch_pred_scan(const PredProgram* prog, const ScanCols& cols, const ScanBitmaps& bm, int64_t n_rows,
-                            int64_t rows_per_range, int32_t nranges, PredPartial* acc, ColPartial* col_part,
-                            uint32_t* hll_acc, int32_t lds_bytes, hipStream_t st, bool has_regex, bool has_hll) {
-  auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3(nranges), dim3(kBlock), (size_t)lds_bytes, st, prog, cols, bm, n_rows, rows_per_range,
-                       acc, col_part, hll_acc);
-  };
-  if (has_regex) {
-    if (has_hll) go(dq_pred_scan<true, true>);
-    else go(dq_pred_scan<true, false>);
-  } else {
-    if (has_hll) go(dq_pred_scan<false, true>);
-    else go(dq_pred_scan<false, false>);
-  }
+                            int64_t rows_per_range, int32_t nranges, PredPartial* acc, int32_t lds_bytes, hipStream_t st,
+                            bool has_regex) {
+  if (has_regex)
+    hipLaunchKernelGGL(dq_pred_scan<true>, dim3(nranges), dim3(kBlock), (size_t)lds_bytes, st, prog, cols, bm, n_rows,
+                       rows_per_range, acc);
+  else
+    hipLaunchKernelGGL(dq_pred_scan<false>, dim3(nranges), dim3(kBlock), (size_t)lds_bytes, st, prog, cols, bm, n_rows,
+                       rows_per_range, acc);
   return hipGetLastError();
 }
 

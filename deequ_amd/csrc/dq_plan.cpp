@@ -29,8 +29,8 @@
 namespace dq {
 
 hipError_t launch_pred_scan(const PredProgram* prog, const ScanCols& cols, const ScanBitmaps& bm, int64_t n_rows,
-                            int64_t rows_per_range, int32_t nranges, PredPartial* acc, ColPartial* col_part,
-                            uint32_t* hll_acc, int32_t lds_bytes, hipStream_t st, bool has_regex, bool has_hll);
+                            int64_t rows_per_range, int32_t nranges, PredPartial* acc, int32_t lds_bytes, hipStream_t st,
+                            bool has_regex);
 hipError_t launch_column_scan(int32_t variant, const ColTask* tasks, int32_t ntasks, int32_t part_base,
                               const ScanCols& cols, const ScanBitmaps& bm, int64_t n_rows, int64_t rows_per_range,
                               int32_t nranges, ColPartial* partials, uint32_t* hll_acc, hipStream_t st);
@@ -806,6 +806,40 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
     }
   }
 
+  // predicate program: roots in slot order, each followed by STORE
+  p->has_pred = !root_code.empty() && (!counter_of.empty() || !bitmap_of.empty());
+  PredProgram& prog = p->prog;
+  std::memset(&prog, 0, sizeof(prog));
+  if (p->has_pred) {
+    std::vector<PredInstr> code;
+    for (size_t r = 0; r < root_code.size(); ++r) {
+      for (const PredInstr& ins : root_code[r]) code.push_back(ins);
+      PredInstr st{};
+      st.op = PO_STORE; st.slot = (int32_t)r; st.col_a = st.col_b = -1;
+      code.push_back(st);
+    }
+    if ((int32_t)code.size() > kMaxInstr) return set_error(DQ_E_UNSUPPORTED, "predicate program too long (%zu)", code.size());
+    int depth = 0, max_depth = 0;
+    for (const PredInstr& ins : code) {
+      depth += (ins.op == PO_AND || ins.op == PO_OR || ins.op == PO_STORE) ? -1 : (ins.op == PO_NOT ? 0 : 1);
+      max_depth = std::max(max_depth, depth);
+    }
+    if (max_depth > kPredStack)
+      return set_error(DQ_E_UNSUPPORTED, "predicate nesting needs a stack of %d (at most %d)", max_depth, kPredStack);
+    prog.stack_depth = std::max(1, max_depth);
+    prog.n_roots = (int32_t)root_code.size();
+    prog.n_instr = (int32_t)code.size();
+    std::copy(code.begin(), code.end(), prog.instr);
+    for (int32_t i = 0; i < prog.n_instr; ++i)
+      if (prog.instr[i].op == PO_ATOM_CMP || prog.instr[i].op == PO_ATOM_ISNULL || prog.instr[i].op == PO_ATOM_NOTNULL ||
+          prog.instr[i].op == PO_ATOM_REGEX)
+        prog.load_instr[prog.n_loads++] = (int16_t)i;
+    prog.n_counters = (int32_t)counter_of.size();
+    for (auto& kv : counter_of) prog.counters[kv.second] = PredCounter{kv.first.first, kv.first.second};
+    prog.n_bitmaps = (int32_t)bitmap_of.size();
+    for (auto& kv : bitmap_of) prog.bitmap_root[kv.second] = kv.first;
+  }
+
   // correlation pairs -> groups of <= kTileCols columns and one `where` (greedy), staged together
   std::vector<PairGroup> pair_groups;
   {
@@ -892,40 +926,6 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
       p->groups.back().count++;
     }
     p->n_fused = (int32_t)std::count_if(fused.begin(), fused.end(), [](int f) { return f != 0; });
-  }
-
-  // predicate program: roots in slot order, each followed by STORE
-  p->has_pred = !root_code.empty() && (!counter_of.empty() || !bitmap_of.empty());
-  PredProgram& prog = p->prog;
-  std::memset(&prog, 0, sizeof(prog));
-  if (p->has_pred) {
-    std::vector<PredInstr> code;
-    for (size_t r = 0; r < root_code.size(); ++r) {
-      for (const PredInstr& ins : root_code[r]) code.push_back(ins);
-      PredInstr st{};
-      st.op = PO_STORE; st.slot = (int32_t)r; st.col_a = st.col_b = -1;
-      code.push_back(st);
-    }
-    if ((int32_t)code.size() > kMaxInstr) return set_error(DQ_E_UNSUPPORTED, "predicate program too long (%zu)", code.size());
-    int depth = 0, max_depth = 0;
-    for (const PredInstr& ins : code) {
-      depth += (ins.op == PO_AND || ins.op == PO_OR || ins.op == PO_STORE) ? -1 : (ins.op == PO_NOT ? 0 : 1);
-      max_depth = std::max(max_depth, depth);
-    }
-    if (max_depth > kPredStack)
-      return set_error(DQ_E_UNSUPPORTED, "predicate nesting needs a stack of %d (at most %d)", max_depth, kPredStack);
-    prog.stack_depth = std::max(1, max_depth);
-    prog.n_roots = (int32_t)root_code.size();
-    prog.n_instr = (int32_t)code.size();
-    std::copy(code.begin(), code.end(), prog.instr);
-    for (int32_t i = 0; i < prog.n_instr; ++i)
-      if (prog.instr[i].op == PO_ATOM_CMP || prog.instr[i].op == PO_ATOM_ISNULL || prog.instr[i].op == PO_ATOM_NOTNULL ||
-          prog.instr[i].op == PO_ATOM_REGEX)
-        prog.load_instr[prog.n_loads++] = (int16_t)i;
-    prog.n_counters = (int32_t)counter_of.size();
-    for (auto& kv : counter_of) prog.counters[kv.second] = PredCounter{kv.first.first, kv.first.second};
-    prog.n_bitmaps = (int32_t)bitmap_of.size();
-    for (auto& kv : bitmap_of) prog.bitmap_root[kv.second] = kv.first;
   }
 
   // algorithmic bytes per row: each (column, buffer) read once
@@ -1183,8 +1183,8 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
     if (dq_status s = timed(p, 0, p->stream, [&] {
           const int32_t lds = kWaves * 128 * (p->prog.stack_depth + p->prog.n_roots + p->prog.n_counters) +
                               ((p->prog.regex_words * 2 + 15) & ~15);
-          return launch_pred_scan(p->d_prog, sc, bm, n_rows, rpr_pred, nr_pred, p->d_pred_acc, p->d_col_part,
-                                  p->d_hll_acc, lds, p->stream, p->prog.regex_words > 0, p->prog.n_hll > 0);
+          return launch_pred_scan(p->d_prog, sc, bm, n_rows, rpr_pred, nr_pred, p->d_pred_acc, lds, p->stream,
+                                  p->prog.regex_words > 0);
         }))
       return s;
   }
