@@ -32,7 +32,8 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md (HBM3E peak 8.0 TB/s)
 # FETCH_SIZE summary of this round's kernels (tools/profile_round.sh -> tools/summarize_prof.py):
 # per-dispatch HBM read bytes of each kernel at the default 125 M-row chunk, gfx950-corrected
-PMC_FILE = os.path.join(ROOT, "profiles", "r2m_pmc.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r3b_pmc.json")
+CLOCK_FILE = os.path.join(ROOT, "profiles", "r3_clock.json")  # tools/clock_probe.sh: held clock per kernel
 DEFAULT_CHUNK = 125_000_000  # 8 chunks per 1e9 rows; a UTF8 chunk's bytes (~2.0e9) stay < 2 GiB
 
 
@@ -377,8 +378,22 @@ def valu_bound(kernel, avg_ms):
         return None
     insts = r["SQ_INSTS_VALU_per_call"]
     floor_ms = insts * VALU_CYCLES_PER_WAVE_INST / (1024 * 2.4e9) * 1e3
-    return {"valu_insts_per_launch": insts, "issue_floor_ms": floor_ms, "frac_of_launch": floor_ms / avg_ms,
-            "model": "4 SIMD cycles per wave64 VALU instruction (measured 4.5 at 4 waves/SIMD, 3.0-3.3 at 8: tools/micro/valu_rate_probe.hip), 1024 SIMDs x 2.4 GHz", "source": os.path.relpath(PMC_FILE, ROOT)}
+    out = {"valu_insts_per_launch": insts, "issue_floor_ms": floor_ms, "frac_of_launch": floor_ms / avg_ms,
+           "model": "4 SIMD cycles per wave64 VALU instruction, 1024 SIMDs x 2.4 GHz (nominal peak clock)",
+           "source": os.path.relpath(PMC_FILE, ROOT)}
+    # the clock the chip holds under this kernel (GRBM_GUI_ACTIVE / 8 XCDs / duration, committed probe): the
+    # issue floor at that clock is what the launch can reach with its instruction count
+    try:
+        with open(CLOCK_FILE) as f:
+            clk = json.load(f).get("void " + kernel)
+    except (OSError, ValueError):
+        clk = None
+    if clk:
+        ghz = clk["effective_clock_GHz"]
+        held_ms = insts * VALU_CYCLES_PER_WAVE_INST / (1024 * ghz * 1e9) * 1e3
+        out.update(held_clock_GHz=ghz, issue_floor_ms_at_held_clock=held_ms, frac_at_held_clock=held_ms / avg_ms,
+                   clock_source=os.path.relpath(CLOCK_FILE, ROOT))
+    return out
 
 
 def roofline(dom_name, dom, traffic, kernels) -> dict:
