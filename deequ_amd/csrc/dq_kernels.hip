@@ -285,9 +285,9 @@ __device__ __forceinline__ void block_masks(const uint32_t* validity, const uint
 // are accumulated as shifted sums sd = sum(x - shift), sdd = sum((x - shift)^2), k under the selection
 // mask -- exec-masked updates, so an unselected row costs no VALU work -- and merged into the lane's
 // running (n, mean, m2) with Chan's formula (StandardDeviation.scala:37-44) every kChunkBlocks blocks:
-// one reciprocal per 32 values.  shift is the lane's running mean, so the shifted sums stay small;
+// one reciprocal per 64 values.  shift is the lane's running mean, so the shifted sums stay small;
 // a lane with nothing yet takes its first selected value.
-constexpr int kChunkBlocks = 4;
+constexpr int kChunkBlocks = 8;
 
 struct LaneMoments {
   double shift, sd, sdd;
@@ -387,14 +387,20 @@ __device__ __forceinline__ void masked_moments(LaneMoments& a, double& lo, doubl
 template <int KIND, bool STATS, bool HLL, bool NANS>
 __device__ __forceinline__ void numeric_block(const double (&x)[8], const uint64_t (&bits)[8], const uint64_t (&m)[8],
                                               const uint64_t (&mm)[8], const uint64_t (&nanm)[8], ColStats& s,
-                                              LaneMoments& a, int32_t* regs, int32_t& qmin) {
+                                              LaneMoments& a, int32_t* regs, int32_t& qmin, bool& started) {
   if (STATS) {
-    // still-empty lanes take the block's first selected value as their shift (wave-uniform branch)
-    if (__builtin_amdgcn_ballot_w64(s.n == 0.0 && a.k == 0) != 0) {
-      double first = a.shift;
+    // still-empty lanes take the block's first selected value as their shift (wave-uniform branch); once no
+    // lane is empty at a block's start the check is skipped for the rest of the range (`started`, uniform).
+    // Not for fp64: its loop is at the 6-wave register budget, and the flag spilled it (1.47 -> 2.16 ms).
+    if (KIND == CK_F64 || !started) {
+      if (__builtin_amdgcn_ballot_w64(s.n == 0.0 && a.k == 0) != 0) {
+        double first = a.shift;
 #pragma unroll
-      for (int j = 7; j >= 0; --j) first = lane_bit(mm[j]) ? x[j] : first;
-      if (s.n == 0.0 && a.k == 0) a.shift = first;
+        for (int j = 7; j >= 0; --j) first = lane_bit(mm[j]) ? x[j] : first;
+        if (s.n == 0.0 && a.k == 0) a.shift = first;
+      } else {
+        started = true;
+      }
     }
   }
 #pragma unroll
@@ -451,6 +457,7 @@ __device__ void numeric_range(const void* values, const uint32_t* validity, cons
   int64_t cnt_w = 0;  // wave-uniform count of selected rows (HLL-only variant)
   LaneMoments a{0.0, 0.0, 0.0, 0, 0};
   int32_t qmin = 0;
+  bool started = false;  // every lane has its moments shift (wave-uniform)
   int nb = 0;
   // (the block's loads software-pipelined one block ahead measured slower: 107 VGPRs for f64 stats+HLL,
   // 4 waves per SIMD instead of 5, 1.51 -> 1.59 ms per 125 M rows x 8 columns)
@@ -529,7 +536,7 @@ __device__ void numeric_range(const void* values, const uint32_t* validity, cons
       }
     } else {
       const uint64_t nanm[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      numeric_block<KIND, STATS, HLL, false>(x, bits, m, m, nanm, s, a, regs, qmin);
+      numeric_block<KIND, STATS, HLL, false>(x, bits, m, m, nanm, s, a, regs, qmin, started);
     }
     if (STATS && (nb % kChunkBlocks) == kChunkBlocks - 1) moments_flush<KIND>(s, a);
   }
@@ -762,10 +769,11 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
       const uint32_t d[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
       // (byte-granular unaligned window loads instead of this realignment -- 8 fewer VALU per string --
       // measured 2.70-2.73 vs 1.90-1.92 ms per 125 M rows x 4: the unaligned 16-byte loads are address-bound)
-      const uint32_t sh = rel_of(j) << 3;  // v_alignbit reads the low 5 bits: (o0 & 3) * 8
+      // v_alignbyte reads the byte shift from the low 2 bits of rel = o0 & 3 (v_alignbit would need rel << 3)
+      const uint32_t sh = rel_of(j);
       uint32_t wv[8];
 #pragma unroll
-      for (int k = 0; k < 7; ++k) wv[k] = alignbit32(d[k + 1], d[k], sh);
+      for (int k = 0; k < 7; ++k) wv[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
       wv[7] = d[7];  // only ever feeds the unused half of the tail pair for len >= 24
       if constexpr (DT) dtc.add(dt_class_short(wv, len_of(j), lane_bit(m[j])), lane_bit(m[j]));
       if constexpr (HLL) {
