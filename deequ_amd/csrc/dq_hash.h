@@ -182,7 +182,7 @@ DQ_HD uint64_t xxh64_stripes(const uint32_t (&w)[8], uint32_t len, uint64_t& d4p
 template <typename BP>
 DQ_HD uint64_t xxh64_tail_head(uint64_t h, uint64_t d4p, uint32_t len, BP bp) {
   const uint32_t d4 = (uint32_t)d4p;
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(DQ_JIT)
   // one compare for both uses (the select and the exec-masked round): written as a bool, LLVM emits an
   // eq compare for one and a ne compare for the other
   const bool has4 = __builtin_amdgcn_inverse_ballot_w64(__builtin_amdgcn_uicmp(len & 4u, 0u, 33 /* ICMP_NE */));

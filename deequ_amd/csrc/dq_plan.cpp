@@ -24,6 +24,7 @@
 
 #include "dq_device.h"
 #include "dq_internal.h"
+#include "dq_pred_jit.h"
 #include "dq_regex.h"
 
 namespace dq {
@@ -436,6 +437,12 @@ struct dq_plan {
   uint16_t* d_regex = nullptr;
   int32_t n_hll = 0;
   bool has_pred = false;
+  // the predicate pass compiled for this program (dq_pred_jit.cpp), or null: the interpreter runs it
+  hipFunction_t pred_jit = nullptr;
+  std::vector<int32_t> pred_jit_cols;                   // its slots' plan columns
+  std::vector<int32_t> pred_jit_hll_task, pred_jit_hll_slot;  // fused HLL tasks (post-sort index) / accumulators
+  int32_t pred_fused_first = 0, pred_fused_count = 0;  // those tasks sort last (after the pair-fused ones)
+  std::string pred_jit_note;                            // why the interpreter runs (diagnostic)
 
   // device memory
   ColTask* d_col_tasks = nullptr;
@@ -840,6 +847,44 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
     for (auto& kv : bitmap_of) prog.bitmap_root[kv.second] = kv.first;
   }
 
+  // the predicate program compiled into its own kernel when the generator takes it; HLL-only tasks (no
+  // `where`) on its columns are hashed there (fused = 2) instead of re-reading the column in the column pass
+  std::vector<int> pred_fused(p->col_tasks.size(), 0);
+  if (p->has_pred) {
+    std::vector<int32_t> kinds(ncols);
+    for (int c = 0; c < ncols; ++c) kinds[c] = kind_of(p->schema[c].type);
+    if (pred_jit_eligible(p->prog, kinds.data(), ncols)) {
+      std::vector<int32_t> slots;
+      (void)pred_jit_source(p->prog, kinds.data(), slots, {});
+      std::vector<PredJitHll> hll;
+      std::vector<int32_t> tasks;
+      for (size_t t = 0; t < p->col_tasks.size() && hll.size() < 8; ++t) {
+        const ColTask& ct = p->col_tasks[t];
+        if (ct.where >= 0 || (ct.variant != CV_F64_H && ct.variant != CV_I64_H && ct.variant != CV_I32_H)) continue;
+        for (size_t i = 0; i < slots.size(); ++i)
+          if (slots[i] == ct.col) {
+            hll.push_back(PredJitHll{(int32_t)i});
+            tasks.push_back((int32_t)t);
+          }
+      }
+      const std::string src = pred_jit_source(p->prog, kinds.data(), slots, hll);
+      std::string err;
+      p->pred_jit = src.empty() ? nullptr : pred_jit_compile(src, err);
+      if (p->pred_jit) {
+        p->pred_jit_cols = slots;
+        p->pred_jit_hll_task = tasks;
+        for (int32_t t : tasks) {
+          pred_fused[t] = 2;
+          p->pred_jit_hll_slot.push_back(p->col_tasks[t].hll_slot);
+        }
+      } else {
+        p->pred_jit_note = src.empty() ? "generator declined the program" : err;
+      }
+    } else {
+      p->pred_jit_note = "program not eligible (regex / string atoms or > 8 columns)";
+    }
+  }
+
   // correlation pairs -> groups of <= kTileCols columns and one `where` (greedy), staged together
   std::vector<PairGroup> pair_groups;
   {
@@ -887,7 +932,7 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
 
   // pair groups -> workgroup tasks of the Correlation pass (dq_pair.hip): the group's pairs and its
   // stats-only column tasks (Mean / StdDev / Sum / Min / Max of the same `where`) over two wave tasks
-  std::vector<int> fused(p->col_tasks.size(), 0);
+  std::vector<int> fused(pred_fused);
   for (const PairGroup& g : pair_groups) {
     plan_pair_wgs(p, g, p->pair_wgs, fused);
     for (int c = 0; c < g.ncols; ++c) p->pair_all_f64 = p->pair_all_f64 && g.kinds[c] == CK_F64;
@@ -919,8 +964,11 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
             for (const SpecOut& o : p->outs)
               if (o.col_task == w.mom_out[k] && (o.op == DQ_OP_MIN || o.op == DQ_OP_MAX)) p->pair_minmax = true;
           }
+    for (int32_t& t : p->pred_jit_hll_task) t = new_index[t];
+    p->pred_fused_count = (int32_t)std::count(fused.begin(), fused.end(), 2);
+    p->pred_fused_first = (int32_t)p->col_tasks.size() - p->pred_fused_count;
     for (int32_t k = 0; k < (int32_t)p->col_tasks.size(); ++k) {
-      if (fused[order[k]]) break;  // fused tasks sort last: their partials come from the pair pass
+      if (fused[order[k]]) break;  // fused tasks sort last: their partials come from the pair / predicate pass
       if (p->groups.empty() || p->groups.back().variant != p->col_tasks[k].variant)
         p->groups.push_back({p->col_tasks[k].variant, k, 0});
       p->groups.back().count++;
@@ -1177,10 +1225,37 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
   int64_t rpr_pred = ceil_div(ceil_div(n_rows, nr_pred), kRowsPerIter) * kRowsPerIter;
   nr_pred = (int32_t)ceil_div(n_rows, rpr_pred);
 
+  // HLL tasks hashed by the compiled predicate pass: one partial per predicate-pass range
+  if (p->pred_fused_count > 0 && fr.n < kNumVariants) {
+    fr.first[fr.n] = p->pred_fused_first;
+    fr.end[fr.n] = p->pred_fused_first + p->pred_fused_count;
+    fr.nr[fr.n] = nr_pred;
+    ++fr.n;
+  }
+
   // every launch on the plan's stream, in order (the C5 variant launches spread over 2-3 streams measured the
   // same step time: each launch fills the chip)
   if (p->has_pred) {
     if (dq_status s = timed(p, 0, p->stream, [&] {
+          if (p->pred_jit) {
+            PredJitArgs a{};
+            for (size_t i = 0; i < p->pred_jit_cols.size(); ++i) {
+              a.values[i] = reinterpret_cast<const char*>(sc.values[p->pred_jit_cols[i]]);
+              a.validity[i] = sc.validity[p->pred_jit_cols[i]];
+            }
+            for (int b = 0; b < kMaxWhere && b < 8; ++b) a.where_bits[b] = bm.where_bits[b];
+            a.n_rows = n_rows;
+            a.rows_per_range = rpr_pred;
+            a.acc_t = reinterpret_cast<unsigned long long*>(p->d_pred_acc->t);
+            a.acc_nn = reinterpret_cast<unsigned long long*>(p->d_pred_acc->nn);
+            a.col_part = reinterpret_cast<char*>(p->d_col_part);
+            a.hll_acc = p->d_hll_acc;
+            for (size_t h = 0; h < p->pred_jit_hll_task.size(); ++h) {
+              a.hll_task[h] = p->pred_jit_hll_task[h];
+              a.hll_slot[h] = p->pred_jit_hll_slot[h];
+            }
+            return pred_jit_launch(p->pred_jit, a, nr_pred, p->stream);
+          }
           const int32_t lds = kWaves * 128 * (p->prog.stack_depth + p->prog.n_roots + p->prog.n_counters) +
                               ((p->prog.regex_words * 2 + 15) & ~15);
           return launch_pred_scan(p->d_prog, sc, bm, n_rows, rpr_pred, nr_pred, p->d_pred_acc, lds, p->stream,
@@ -1416,6 +1491,14 @@ int64_t dq_plan_variant_bytes_per_row_x1000(const dq_plan* p, int32_t variant) {
   return b;
 }
 int32_t dq_plan_num_launches(const dq_plan* p) { return p ? p->launches_per_scan : 0; }
+
+int32_t dq_plan_pred_compiled(const dq_plan* p, char* note, int32_t cap) {
+  if (note && cap > 0) {
+    const std::string n = !p ? "plan is NULL" : (!p->has_pred ? "no predicates" : p->pred_jit_note);
+    std::snprintf(note, (size_t)cap, "%s", n.c_str());
+  }
+  return p && p->pred_jit ? 1 : 0;
+}
 
 int64_t dq_plan_kernel_bytes_per_row_x1000(const dq_plan* p, int32_t kernel) {
   if (!p) return 0;

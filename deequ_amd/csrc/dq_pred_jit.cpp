@@ -1,0 +1,483 @@
+// dq_pred_jit.cpp -- the predicate pass compiled per plan (host C++; hipRTC for gfx950).
+//
+// The reference evaluates Compliance / `where` predicates with Spark's whole-stage code generation: each
+// `expr(...)` becomes straight-line Java bytecode inside the one aggregation pass (AnalysisRunner.scala:303,
+// Compliance.scala:37-53).  This is the same idea on the GPU.  dq_pred_scan interprets the postfix program
+// per 512-row block (SQ counters: ~108 VALU + ~130 SALU per 64-row group for C3's four predicates, most of
+// it decoding instructions and walking an LDS operand stack); for a program whose atoms are comparisons /
+// IS [NOT] NULL on numeric columns the plan instead emits a kernel with the program unrolled into it:
+//   * per wave, 512-row blocks (lane l: rows base + 64 j + l), each column's values loaded once per block;
+//   * per 64-row group j: every atom is one ballot of a per-lane comparison (literals folded in), its
+//     three-valued TRUE / NULL masks are 64-bit scalars, AND / OR / NOT are scalar mask ops, the counters
+//     are scalar popcounts and a `where` root's TRUE mask is stored as its bitmap word;
+//   * an HLL-only ApproxCountDistinct (no `where`) on a program column is hashed from the same registers
+//     (XXH64 seed 42, the column pass's formulation, dq_hash.h), so that column is read from HBM once.
+// The source is generated from the PredProgram the interpreter would run, compiled once per distinct source
+// and device (hipRTC, in-process cache; comgr keeps its own on-disk cache), and launched in place of
+// dq_pred_scan.  A program the generator does not take (regex atoms, strings, > 8 columns) or a failed
+// compile keeps the interpreter and the column pass's HLL tasks.
+#include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
+
+#include <cinttypes>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "dq_device.h"
+#include "dq_pred_jit.h"
+
+namespace dq {
+
+namespace {
+
+// XXH64 pieces of dq_hash.h (its text, embedded at build time: build/dq_hash_src.inc)
+const char* kHashSrc =
+#include "dq_hash_src.inc"
+    ;
+
+const char* kPreamble = R"DQJIT(
+#define DQ_JIT 1
+typedef unsigned int uint32_t;
+typedef int int32_t;
+typedef unsigned long long uint64_t;
+typedef long long int64_t;
+typedef unsigned long long uintptr_t;
+typedef const __attribute__((address_space(4))) uint32_t* dq_const_u32s;
+)DQJIT";
+
+const char* kHelpers = R"DQJIT(
+namespace dqj {
+using namespace dq;
+struct Args {
+  const char* values[8];
+  const uint32_t* validity[8];
+  uint64_t* where_bits[8];
+  int64_t n_rows, rows_per_range;
+  unsigned long long* acc_t;
+  unsigned long long* acc_nn;
+  char* col_part;
+  uint32_t* hll_acc;
+  int32_t hll_task[8];
+  int32_t hll_slot[8];
+};
+// (hipRTC does not declare __builtin_amdgcn_inverse_ballot_w64: the lane's bit as a VALU test, and the hot
+// exec-masked register max in asm)
+__device__ __forceinline__ bool lane_bit(uint64_t m) { return (m >> __lane_id()) & 1ull; }
+// ds_max_i32 under exec = m: LDS register max of the selected rows (regs_lds = the array's LDS address);
+// the kernel waits for these (lgkmcnt) before its closing barrier
+__device__ __forceinline__ void ds_max_masked(uint64_t m, uint32_t addr, int32_t q) {
+  uint64_t save;
+  asm volatile("s_and_saveexec_b64 %0, %1\n\tds_max_i32 %2, %3\n\ts_mov_b64 exec, %0"
+               : "=&s"(save) : "s"(m), "v"(addr), "v"(q) : "memory", "scc");
+}
+// bits of rows [r, r + 64) of a bitmap (scalar loads), clipped to rows below row1; all ones without one
+__device__ __forceinline__ uint64_t mask64(const uint32_t* bm, int64_t r, int64_t row1) {
+  if (r >= row1) return 0;
+  uint64_t x = ~0ull;
+  if (bm) {
+    const int64_t w = r >> 5;
+    const bool two = r + 32 < row1;
+    x = ((uint64_t)(two ? ((dq_const_u32s)bm)[w + 1] : 0u) << 32) | ((dq_const_u32s)bm)[w];
+  }
+  if (r + 64 > row1) x &= (1ull << (row1 - r)) - 1ull;
+  return x;
+}
+// validity words of a block (lanes 0..15: rows base + 32 l .. + 31) through a bounds-checked descriptor over
+// the chunk's bitmap (past it: 0); all ones without a bitmap.  The 64-bit mask of row group j is then two
+// readlanes: scalar loads of every group's words, hoisted by the compiler, overflowed the scalar file.
+__device__ __forceinline__ uint32_t valid_words(const uint32_t* bm, int64_t base, int64_t n_rows, int lane) {
+  if (!bm) return ~0u;
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc((void*)bm, (short)0, (int)(((n_rows + 31) >> 5) * 4), 0x00020000);
+  return __builtin_amdgcn_raw_buffer_load_b32(r, (lane & 15) * 4, (int)((base >> 5) * 4), 0);
+}
+__device__ __forceinline__ uint64_t group_mask(uint32_t w, int j) {
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)w, 2 * j + 1) << 32) |
+         (uint32_t)__builtin_amdgcn_readlane((int)w, 2 * j);
+}
+// Spark's ordering of doubles (nanSafeCompare): NaN = NaN, NaN above everything
+__device__ __forceinline__ int spark_cmp(double a, double b) {
+  const bool an = a != a, bn = b != b;
+  if (an || bn) return (an && bn) ? 0 : (an ? 1 : -1);
+  return (a > b) - (a < b);
+}
+__device__ __forceinline__ int32_t ffbh_raw(uint32_t x) {
+  int32_t r;
+  asm("v_ffbh_u32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+// HLL key from the XXH64 state before its last multiply (dq_kernels.hip hll_key_from_fmix): register byte
+// offset and q = pw - 1, or -1 when the rank needs the hash's low word (redone exactly)
+__device__ __forceinline__ void hll_key(uint64_t b, uint32_t& addr, int32_t& q) {
+  const uint32_t bl = (uint32_t)b, bh = (uint32_t)(b >> 32);
+  const uint32_t hi = __umulhi(bl, (uint32_t)XP3) + bl * (uint32_t)(XP3 >> 32) + bh * (uint32_t)XP3;
+  addr = (hi >> 21) & 0x7FCu;
+  q = ffbh_raw(hi << 9);
+}
+__device__ __forceinline__ void hll_exact(int32_t* regs, uint64_t x) {
+  atomicMax(&regs[(uint32_t)(x >> 55)], (int32_t)__clzll((long long)((x << 9) | 256ull)));
+}
+}  // namespace dqj
+)DQJIT";
+
+std::string u64lit(uint64_t v) {
+  char b[40];
+  std::snprintf(b, sizeof b, "0x%016" PRIx64 "ull", v);
+  return b;
+}
+
+// value expression of slot s row group j as int64 / double
+std::string as_int(int s, int kind) {
+  const std::string v = "v" + std::to_string(s) + "[j]";
+  return kind == CK_I32 ? "(int64_t)(int32_t)(uint32_t)" + v : "(int64_t)" + v;
+}
+std::string as_dbl(int s, int kind) {
+  const std::string v = "v" + std::to_string(s) + "[j]";
+  if (kind == CK_F64) return "__longlong_as_double((long long)" + v + ")";
+  return "(double)" + as_int(s, kind);
+}
+const char* cmp_op(int c) {
+  switch (c) {
+    case C_LT: return "<";
+    case C_LE: return "<=";
+    case C_GT: return ">";
+    case C_GE: return ">=";
+    case C_EQ: return "==";
+    default: return "!=";
+  }
+}
+
+}  // namespace
+
+bool pred_jit_eligible(const PredProgram& prog, const int32_t* col_kind, int32_t ncols) {
+  if (prog.regex_words > 0 || prog.n_loads == 0) return false;
+  std::vector<int32_t> cols;
+  for (int i = 0; i < prog.n_instr; ++i) {
+    const PredInstr& ins = prog.instr[i];
+    if (ins.op == PO_ATOM_REGEX) return false;
+    if (ins.op != PO_ATOM_CMP && ins.op != PO_ATOM_ISNULL && ins.op != PO_ATOM_NOTNULL) continue;
+    for (int32_t c : {ins.col_a, ins.col_b}) {
+      if (c < 0) continue;
+      if (c >= ncols) return false;
+      const int k = col_kind[c];
+      if (k != CK_F64 && k != CK_I64 && k != CK_I32) return false;
+      bool seen = false;
+      for (int32_t x : cols) seen = seen || x == c;
+      if (!seen) cols.push_back(c);
+    }
+  }
+  return !cols.empty() && cols.size() <= 8;
+}
+
+// The kernel source of `prog`; slot_col receives the program's distinct columns in slot order (the order of
+// PredJitArgs::values / validity); fused HLL task h hashes slot hll[h].slot (its task and accumulator come
+// in PredJitArgs::hll_task / hll_slot, so the source does not depend on task numbering).
+std::string pred_jit_source(const PredProgram& prog, const int32_t* col_kind, std::vector<int32_t>& slot_col,
+                            const std::vector<PredJitHll>& hll) {
+  slot_col.clear();
+  auto slot_of = [&](int32_t c) {
+    for (size_t i = 0; i < slot_col.size(); ++i)
+      if (slot_col[i] == c) return (int)i;
+    slot_col.push_back(c);
+    return (int)slot_col.size() - 1;
+  };
+  for (int i = 0; i < prog.n_instr; ++i) {
+    const PredInstr& ins = prog.instr[i];
+    if (ins.op != PO_ATOM_CMP && ins.op != PO_ATOM_ISNULL && ins.op != PO_ATOM_NOTNULL) continue;
+    slot_of(ins.col_a);
+    if (ins.col_b >= 0) slot_of(ins.col_b);
+  }
+  const int ns = (int)slot_col.size();
+  std::vector<bool> need_vals(ns, false);
+  for (int i = 0; i < prog.n_instr; ++i) {
+    const PredInstr& ins = prog.instr[i];
+    if (ins.op != PO_ATOM_CMP) continue;
+    if (ins.cmp >= C_LT && ins.cmp <= C_NE) {
+      need_vals[slot_of(ins.col_a)] = true;
+      if (ins.col_b >= 0) need_vals[slot_of(ins.col_b)] = true;
+    }
+  }
+  for (const PredJitHll& h : hll) need_vals[h.slot] = true;
+  const int nh = (int)hll.size();
+
+  std::string s;
+  s.reserve(16384);
+  s += kPreamble;
+  s += kHashSrc;
+  s += kHelpers;
+  s += "extern \"C\" __global__ __launch_bounds__(256) void dq_pred_jit(dqj::Args A) {\n";
+  s += "  using namespace dq; using namespace dqj;\n";
+  s += "  __shared__ int32_t regs[" + std::to_string(nh > 0 ? nh * 512 : 1) + "];\n";
+  s += "  __shared__ unsigned long long hcnt[" + std::to_string(nh > 0 ? nh : 1) + "];\n";
+  if (nh > 0) {
+    s += "  for (int i = threadIdx.x; i < " + std::to_string(nh * 512) + "; i += 256) regs[i] = -1;\n";
+    s += "  if (threadIdx.x < " + std::to_string(nh) + ") hcnt[threadIdx.x] = 0;\n";
+    s += "  __syncthreads();\n";
+  }
+  s += "  const int lane = threadIdx.x & 63;\n";
+  s += "  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n";
+  s += "  const int64_t row0 = (int64_t)blockIdx.x * A.rows_per_range;\n";
+  s += "  const int64_t row1 = row0 + A.rows_per_range < A.n_rows ? row0 + A.rows_per_range : A.n_rows;\n";
+  for (int i = 0; i < ns; ++i) {
+    const int k = col_kind[slot_col[i]];
+    const int sz = k == CK_I32 ? 4 : 8;
+    s += "  const uint32_t* vb" + std::to_string(i) + " = A.validity[" + std::to_string(i) + "];\n";
+    if (need_vals[i])
+      s += "  const __amdgpu_buffer_rsrc_t vr" + std::to_string(i) +
+           " = __builtin_amdgcn_make_buffer_rsrc((void*)(A.values[" + std::to_string(i) + "] + row0 * " +
+           std::to_string(sz) + "), (short)0, (int)((row1 - row0) * " + std::to_string(sz) + "), 0x00020000);\n";
+  }
+  for (int c = 0; c < prog.n_counters; ++c) s += "  uint64_t ct" + std::to_string(c) + " = 0, cn" + std::to_string(c) + " = 0;\n";
+  for (int h = 0; h < nh; ++h) s += "  uint64_t hc" + std::to_string(h) + " = 0;\n";
+  s += "  for (int64_t blk = row0; blk < row1; blk += 2048) {\n";
+  s += "    const int64_t base = blk + (int64_t)wave * 512;\n";
+  s += "    if (base >= row1) break;\n";
+  s += "    const int soff = (int)(base - row0);\n";
+  for (int i = 0; i < ns; ++i) {
+    if (!need_vals[i]) continue;
+    const int k = col_kind[slot_col[i]];
+    const std::string si = std::to_string(i);
+    s += "    uint64_t v" + si + "[8];\n";
+    s += "#pragma unroll\n    for (int j = 0; j < 8; ++j) {\n";
+    if (k == CK_I32) {
+      s += "      v" + si + "[j] = (uint64_t)__builtin_amdgcn_raw_buffer_load_b32(vr" + si +
+           ", lane * 4, (soff + 64 * j) * 4, 2);\n";
+    } else {
+      s += "      const auto w2 = __builtin_amdgcn_raw_buffer_load_b64(vr" + si + ", lane * 8, (soff + 64 * j) * 8, 2);\n";
+      s += "      v" + si + "[j] = ((uint64_t)w2[1] << 32) | w2[0];\n";
+    }
+    s += "    }\n";
+  }
+  for (int i = 0; i < ns; ++i)
+    s += "    const uint32_t vw" + std::to_string(i) + " = valid_words(vb" + std::to_string(i) + ", base, A.n_rows, lane);\n";
+  for (int h = 0; h < nh; ++h) s += "    int32_t qmin" + std::to_string(h) + " = 0;\n";
+  s += "#pragma unroll\n  for (int j = 0; j < 8; ++j) {\n";
+  s += "    const int64_t r = base + 64 * j;\n";
+  s += "    const uint64_t inr = mask64(nullptr, r, row1);\n";
+  for (int i = 0; i < ns; ++i) s += "    const uint64_t va" + std::to_string(i) + " = group_mask(vw" + std::to_string(i) + ", j) & inr;\n";
+  // the program: atoms and logic as scalar masks (SSA names, the operand stack resolved here)
+  std::vector<std::pair<std::string, std::string>> stack;
+  std::vector<std::pair<std::string, std::string>> roots(prog.n_roots > 0 ? prog.n_roots : 1);
+  int tmp = 0;
+  auto fresh = [&]() { return std::to_string(tmp++); };
+  for (int i = 0; i < prog.n_instr; ++i) {
+    const PredInstr& ins = prog.instr[i];
+    const std::string id = fresh();
+    const std::string T = "t" + id, N = "n" + id;
+    switch (ins.op) {
+      case PO_ATOM_CMP: {
+        const int a = slot_of(ins.col_a), b = ins.col_b >= 0 ? slot_of(ins.col_b) : -1;
+        const int ka = col_kind[ins.col_a], kb = b >= 0 ? col_kind[ins.col_b] : 0;
+        std::string wc;
+        if (ins.cmp == C_TRUE) wc = "~0ull";
+        else if (ins.cmp < C_LT || ins.cmp > C_NE) wc = "0ull";
+        else if (ins.ctype == CT_INT) {
+          const std::string y = b >= 0 ? as_int(b, kb) : "(int64_t)" + u64lit((uint64_t)ins.lit_i);
+          wc = "__builtin_amdgcn_ballot_w64(" + as_int(a, ka) + " " + cmp_op(ins.cmp) + " " + y + ")";
+        } else {
+          uint64_t lb;
+          std::memcpy(&lb, &ins.lit_d, 8);
+          const std::string y = b >= 0 ? as_dbl(b, kb) : "__longlong_as_double((long long)" + u64lit(lb) + ")";
+          wc = "__builtin_amdgcn_ballot_w64(spark_cmp(" + as_dbl(a, ka) + ", " + y + ") " + cmp_op(ins.cmp) + " 0)";
+        }
+        const std::string va = "va" + std::to_string(a), vb = b >= 0 ? "va" + std::to_string(b) : "~0ull";
+        const std::string nrt = ins.null_res == NR_TRUE ? "~0ull" : "0ull";
+        const std::string nrn = ins.null_res == NR_NULL ? "~0ull" : "0ull";
+        s += "    const uint64_t w" + id + " = " + wc + ";\n";
+        s += "    const uint64_t " + T + " = (" + va + " & " + vb + " & w" + id + ") | (~" + va + " & " + vb + " & " + nrt + ");\n";
+        s += "    const uint64_t " + N + " = ~" + vb + " | (~" + va + " & " + nrn + ");\n";
+        stack.push_back({T, N});
+        break;
+      }
+      case PO_ATOM_ISNULL:
+      case PO_ATOM_NOTNULL: {
+        const std::string va = "va" + std::to_string(slot_of(ins.col_a));
+        s += "    const uint64_t " + T + " = " + (ins.op == PO_ATOM_ISNULL ? "~" : "") + va + ";\n";
+        s += "    const uint64_t " + N + " = 0ull;\n";
+        stack.push_back({T, N});
+        break;
+      }
+      case PO_CONST:
+        s += "    const uint64_t " + T + " = " + (ins.null_res == NR_TRUE ? "~0ull" : "0ull") + ";\n";
+        s += "    const uint64_t " + N + " = " + (ins.null_res == NR_NULL ? "~0ull" : "0ull") + ";\n";
+        stack.push_back({T, N});
+        break;
+      case PO_AND:
+      case PO_OR: {
+        if (stack.size() < 2) return std::string();
+        const auto bb = stack.back();
+        stack.pop_back();
+        const auto aa = stack.back();
+        stack.pop_back();
+        const char* op = ins.op == PO_AND ? " & " : " | ";
+        const char* fop = ins.op == PO_AND ? " | " : " & ";
+        s += "    const uint64_t " + T + " = " + aa.first + op + bb.first + ";\n";
+        s += "    const uint64_t f" + id + " = (~" + aa.first + " & ~" + aa.second + ")" + fop + "(~" + bb.first + " & ~" +
+             bb.second + ");\n";
+        s += "    const uint64_t " + N + " = ~" + T + " & ~f" + id + ";\n";
+        stack.push_back({T, N});
+        break;
+      }
+      case PO_NOT: {
+        if (stack.empty()) return std::string();
+        const auto aa = stack.back();
+        stack.pop_back();
+        s += "    const uint64_t " + T + " = ~" + aa.first + " & ~" + aa.second + ";\n";
+        s += "    const uint64_t " + N + " = " + aa.second + ";\n";
+        stack.push_back({T, N});
+        break;
+      }
+      case PO_STORE:
+        if (stack.empty() || ins.slot < 0 || ins.slot >= (int)roots.size()) return std::string();
+        roots[ins.slot] = stack.back();
+        stack.pop_back();
+        break;
+      default:
+        return std::string();
+    }
+  }
+  for (int c = 0; c < prog.n_counters; ++c) {
+    const PredCounter pc = prog.counters[c];
+    if (pc.pred < 0 || pc.pred >= (int)roots.size() || pc.where >= (int)roots.size()) return std::string();
+    const std::string tw = pc.where < 0 ? "inr" : "(" + roots[pc.where].first + " & inr)";
+    s += "    ct" + std::to_string(c) + " += (uint64_t)__builtin_popcountll(" + roots[pc.pred].first + " & " + tw + ");\n";
+    s += "    cn" + std::to_string(c) + " += (uint64_t)__builtin_popcountll(~" + roots[pc.pred].second + " & " + tw + ");\n";
+  }
+  for (int b = 0; b < prog.n_bitmaps; ++b) {
+    const int rt = prog.bitmap_root[b];
+    if (rt < 0 || rt >= (int)roots.size()) return std::string();
+    s += "    if (r < row1 && lane == 0) A.where_bits[" + std::to_string(b) + "][r >> 6] = " + roots[rt].first + " & inr;\n";
+  }
+  // fused HLL tasks: XXH64 of the slot's raw value (doubleToLongBits for fp64: NaN canonical), exec-masked
+  // register max; the rare low-word rank redone exactly after the block
+  for (int h = 0; h < nh; ++h) {
+    const PredJitHll& e = hll[h];
+    const int k = col_kind[slot_col[e.slot]];
+    const std::string hs = std::to_string(h), vs = "v" + std::to_string(e.slot) + "[j]";
+    s += "    {\n";
+    s += "      const uint64_t sl = va" + std::to_string(e.slot) + " & inr;\n";
+    s += "      hc" + hs + " += (uint64_t)__builtin_popcountll(sl);\n";
+    if (k == CK_I32) {
+      s += "      const uint64_t hb = xxh64_int_head((uint32_t)" + vs + ");\n";
+    } else if (k == CK_F64) {
+      s += "      uint64_t raw = " + vs + ";\n";
+      s += "      if (__longlong_as_double((long long)raw) != __longlong_as_double((long long)raw)) raw = 0x7FF8000000000000ull;\n";
+      s += "      const uint64_t hb = xxh64_long_head(raw);\n";
+    } else {
+      s += "      const uint64_t hb = xxh64_long_head(" + vs + ");\n";
+    }
+    s += "      uint32_t addr; int32_t q; hll_key(hb, addr, q);\n";
+    s += "      qmin" + hs + " = q < qmin" + hs + " ? q : qmin" + hs + ";\n";
+    s += "      ds_max_masked(sl, (uint32_t)(uintptr_t)(regs + " + std::to_string(h * 512) + ") + addr, q);\n";
+    s += "    }\n";
+  }
+  s += "  }\n";  // j
+  for (int h = 0; h < nh; ++h) {
+    const PredJitHll& e = hll[h];
+    const int k = col_kind[slot_col[e.slot]];
+    const std::string hs = std::to_string(h), vs = "v" + std::to_string(e.slot) + "[j]";
+    s += "    if (__builtin_amdgcn_ballot_w64(qmin" + hs + " < 0) != 0) {\n";
+    s += "#pragma unroll\n      for (int j = 0; j < 8; ++j) {\n";
+    s += "        if (!lane_bit(group_mask(vw" + std::to_string(e.slot) + ", j) & mask64(nullptr, base + 64 * j, row1))) continue;\n";
+    if (k == CK_I32) {
+      s += "        hll_exact(regs + " + std::to_string(h * 512) + ", xxh64_int((uint32_t)" + vs + "));\n";
+    } else {
+      s += "        uint64_t raw = " + vs + ";\n";
+      if (k == CK_F64)
+        s += "        if (__longlong_as_double((long long)raw) != __longlong_as_double((long long)raw)) raw = 0x7FF8000000000000ull;\n";
+      s += "        hll_exact(regs + " + std::to_string(h * 512) + ", xxh64_long(raw));\n";
+    }
+    s += "      }\n    }\n";
+  }
+  s += "  }\n";  // blk
+  s += "  if (lane == 0) {\n";
+  for (int c = 0; c < prog.n_counters; ++c) {
+    const std::string cs = std::to_string(c);
+    s += "    atomicAdd(A.acc_t + " + cs + ", (unsigned long long)ct" + cs + ");\n";
+    s += "    atomicAdd(A.acc_nn + " + cs + ", (unsigned long long)cn" + cs + ");\n";
+  }
+  for (int h = 0; h < nh; ++h) s += "    atomicAdd(&hcnt[" + std::to_string(h) + "], (unsigned long long)hc" + std::to_string(h) + ");\n";
+  s += "  }\n";
+  if (nh > 0) {
+    s += "  asm volatile(\"s_waitcnt lgkmcnt(0)\" ::: \"memory\");\n";
+    s += "  __syncthreads();\n";
+    for (int h = 0; h < nh; ++h) {
+        // ColPartial (dq_device.h, 96 bytes): n mean m2 sum isum count nan_count fmin fmax pinf ninf pad
+      s += "  if (threadIdx.x == 0) {\n";
+      s += "    char* p = A.col_part + ((size_t)A.hll_task[" + std::to_string(h) + "] * " + std::to_string(kMaxWG) +
+           " + blockIdx.x) * 96;\n";
+      s += "    uint64_t* w = reinterpret_cast<uint64_t*>(p);\n";
+      s += "    w[0] = 0; w[1] = 0; w[2] = 0; w[3] = 0; w[4] = 0; w[5] = hcnt[" + std::to_string(h) + "]; w[6] = 0;\n";
+      s += "    w[7] = 0x7FF0000000000000ull; w[8] = 0xFFF0000000000000ull; w[9] = 0; w[10] = 0; w[11] = 0;\n";
+      s += "  }\n";
+      s += "  {\n    uint32_t* dst = A.hll_acc + ((size_t)A.hll_slot[" + std::to_string(h) + "] * " + std::to_string(kHllCopies) +
+           " + (blockIdx.x % " + std::to_string(kHllCopies) + ")) * 512;\n";
+      s += "    for (int i = threadIdx.x; i < 512; i += 256) {\n";
+      s += "      const uint32_t val = (uint32_t)(regs[" + std::to_string(h * 512) + " + i] + 1);\n";
+      s += "      if (val > __builtin_nontemporal_load(dst + i)) atomicMax(dst + i, val);\n";
+      s += "    }\n  }\n";
+    }
+  }
+  s += "}\n";
+  return s;
+}
+
+// compile (or find) the kernel of `src` for the current device
+hipFunction_t pred_jit_compile(const std::string& src, std::string& err) {
+  static std::mutex mu;
+  static std::map<std::pair<int, std::string>, hipFunction_t> cache;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) {
+    err = "hipGetDevice failed";
+    return nullptr;
+  }
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = cache.find({dev, src});
+  if (it != cache.end()) return it->second;
+  hiprtcProgram prog;
+  if (hiprtcCreateProgram(&prog, src.c_str(), "dq_pred_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
+    err = "hiprtcCreateProgram failed";
+    return nullptr;
+  }
+  const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
+  const hiprtcResult rc = hiprtcCompileProgram(prog, 3, opts);
+  if (rc != HIPRTC_SUCCESS) {
+    size_t n = 0;
+    hiprtcGetProgramLogSize(prog, &n);
+    std::string log(n, '\0');
+    if (n) hiprtcGetProgramLog(prog, &log[0]);
+    err = "hiprtc: " + log.substr(0, 2000);
+    hiprtcDestroyProgram(&prog);
+    return nullptr;
+  }
+  size_t n = 0;
+  hiprtcGetCodeSize(prog, &n);
+  std::vector<char> code(n);
+  hiprtcGetCode(prog, code.data());
+  hiprtcDestroyProgram(&prog);
+  hipModule_t mod;
+  if (hipModuleLoadData(&mod, code.data()) != hipSuccess) {
+    err = "hipModuleLoadData failed";
+    return nullptr;
+  }
+  hipFunction_t fn;
+  if (hipModuleGetFunction(&fn, mod, "dq_pred_jit") != hipSuccess) {
+    err = "hipModuleGetFunction failed";
+    return nullptr;
+  }
+  cache[{dev, src}] = fn;  // the module stays loaded for the process
+  return fn;
+}
+
+hipError_t pred_jit_launch(hipFunction_t fn, const PredJitArgs& a, int32_t nranges, hipStream_t st) {
+  PredJitArgs args = a;
+  void* params[] = {&args};
+  return hipModuleLaunchKernel(fn, (unsigned)nranges, 1, 1, kBlock, 1, 1, 0, st, params, nullptr);
+}
+
+}  // namespace dq

@@ -1,0 +1,40 @@
+// dq_pred_jit.h -- the predicate pass compiled per plan (dq_pred_jit.cpp).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "dq_device.h"
+
+namespace dq {
+
+// kernel argument block (layout shared with the generated source's dqj::Args)
+struct PredJitArgs {
+  const char* values[8];
+  const uint32_t* validity[8];
+  uint64_t* where_bits[8];
+  int64_t n_rows, rows_per_range;
+  unsigned long long* acc_t;
+  unsigned long long* acc_nn;
+  char* col_part;
+  uint32_t* hll_acc;
+  int32_t hll_task[8];  // fused HLL task h: column task (ColPartial row) and HLL accumulator slot
+  int32_t hll_slot[8];
+};
+
+// an HLL-only column task hashed by the predicate kernel: its program slot
+struct PredJitHll {
+  int32_t slot;
+};
+
+// col_kind[c]: CK_* of plan column c
+bool pred_jit_eligible(const PredProgram& prog, const int32_t* col_kind, int32_t ncols);
+std::string pred_jit_source(const PredProgram& prog, const int32_t* col_kind, std::vector<int32_t>& slot_col,
+                            const std::vector<PredJitHll>& hll);
+hipFunction_t pred_jit_compile(const std::string& src, std::string& err);
+hipError_t pred_jit_launch(hipFunction_t fn, const PredJitArgs& a, int32_t nranges, hipStream_t st);
+
+}  // namespace dq

@@ -71,6 +71,13 @@ class ScanPlan:
     def variant_bytes_per_row(self, variant: int) -> float:
         return L.lib.dq_plan_variant_bytes_per_row_x1000(self.handle, variant) / 1000.0
 
+    def pred_compiled(self):
+        """(True, "") when the predicate pass runs as the kernel compiled for this plan's program, else (False,
+        the reason the interpreter runs it) -- dq_plan_pred_compiled."""
+        buf = ctypes.create_string_buffer(2048)
+        on = L.lib.dq_plan_pred_compiled(self.handle, buf, len(buf))
+        return bool(on), buf.value.decode("utf-8", "replace")
+
     def kernel_bytes_per_row(self, kernel: int) -> float:
         """Algorithmic bytes per row of timing kernel `kernel` (0 pred, 2 pair, 16+v variant v; no UTF8 data)."""
         return L.lib.dq_plan_kernel_bytes_per_row_x1000(self.handle, kernel) / 1000.0

@@ -299,6 +299,11 @@ int64_t dq_plan_variant_bytes_per_row_x1000(const dq_plan* plan, int32_t variant
 /* The same per timing kernel id (0 = predicate pass: its atoms' columns, 2 = pair pass: its columns,
  * 16 + v = variant v); UTF8 data bytes excluded. */
 int64_t dq_plan_kernel_bytes_per_row_x1000(const dq_plan* plan, int32_t kernel);
+/* 1 when the plan's predicate pass runs as a kernel compiled for its program (the Compliance / where
+ * programs of numeric comparisons: whole-stage code generation as Spark does for the same expressions,
+ * hipRTC for gfx950), 0 when the interpreter runs it (or the plan has no predicates); note (optional,
+ * cap bytes incl. the terminator) receives the reason the interpreter runs. */
+int32_t dq_plan_pred_compiled(const dq_plan* plan, char* note, int32_t cap);
 
 /* Grouping analyzers (analyzers/GroupingAnalyzers.scala:44-82, 118-138): the frequencies
  * SELECT cols, COUNT(*) FROM data WHERE cols IS NOT NULL GROUP BY cols on the GPU (sort-based), and
