@@ -92,9 +92,12 @@ __device__ __forceinline__ uint64_t mask64(const uint32_t* bm, int64_t r, int64_
 // readlanes: scalar loads of every group's words, hoisted by the compiler, overflowed the scalar file.
 __device__ __forceinline__ uint32_t valid_words(const uint32_t* bm, int64_t base, int64_t n_rows, int lane) {
   if (!bm) return ~0u;
-  const __amdgpu_buffer_rsrc_t r =
-      __builtin_amdgcn_make_buffer_rsrc((void*)bm, (short)0, (int)(((n_rows + 31) >> 5) * 4), 0x00020000);
-  return __builtin_amdgcn_raw_buffer_load_b32(r, (lane & 15) * 4, (int)((base >> 5) * 4), 0);
+  // a global load with the word index clamped to the bitmap's last word (words past it belong to rows past
+  // n_rows, which `inr` masks): a pointer instead of a four-register descriptor per column
+  typedef const __attribute__((address_space(1))) uint32_t* gu32;
+  const uint32_t last = (uint32_t)(((n_rows + 31) >> 5) - 1);
+  const uint32_t w = (uint32_t)(base >> 5) + (uint32_t)(lane & 15);
+  return ((gu32)bm)[w < last ? w : last];
 }
 __device__ __forceinline__ uint64_t group_mask(uint32_t w, int j) {
   return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)w, 2 * j + 1) << 32) |
@@ -353,6 +356,8 @@ std::string pred_jit_source(const PredProgram& prog, const int32_t* col_kind, st
     if (rt < 0 || rt >= (int)roots.size()) return std::string();
     s += "    if (r < row1 && lane == 0) A.where_bits[" + std::to_string(b) + "][r >> 6] = " + roots[rt].first + " & inr;\n";
   }
+  // the group's predicate work (scalar masks) completes before its hashing starts
+  s += "    __builtin_amdgcn_sched_barrier(0);\n";
   // fused HLL tasks: XXH64 of the slot's raw value (doubleToLongBits for fp64: NaN canonical), exec-masked
   // register max; the rare low-word rank redone exactly after the block
   for (int h = 0; h < nh; ++h) {
