@@ -237,27 +237,30 @@ std::string pred_jit_source(const PredProgram& prog, const int32_t* col_kind, st
   }
   for (int c = 0; c < prog.n_counters; ++c) s += "  uint64_t ct" + std::to_string(c) + " = 0, cn" + std::to_string(c) + " = 0;\n";
   for (int h = 0; h < nh; ++h) s += "  uint64_t hc" + std::to_string(h) + " = 0;\n";
+  // values and validity words one block ahead, per row group: v[i][j] of the next block is loaded as soon as
+  // row group j of this block is done with it (same registers), so the next block's loads are in flight
+  // while this block is evaluated and hashed
+  auto load_vals = [&](int i, const std::string& soff, const std::string& j, const std::string& dst) {
+    const int k = col_kind[slot_col[i]];
+    const std::string si = std::to_string(i);
+    if (k == CK_I32)
+      return dst + " = (uint64_t)__builtin_amdgcn_raw_buffer_load_b32(vr" + si + ", lane * 4, (" + soff + " + 64 * " + j +
+             ") * 4, 2);\n";
+    return "{ const auto w2 = __builtin_amdgcn_raw_buffer_load_b64(vr" + si + ", lane * 8, (" + soff + " + 64 * " + j +
+           ") * 8, 2); " + dst + " = ((uint64_t)w2[1] << 32) | w2[0]; }\n";
+  };
+  for (int i = 0; i < ns; ++i) {
+    const std::string si = std::to_string(i);
+    if (need_vals[i]) {
+      s += "  uint64_t v" + si + "[8];\n";
+      s += "#pragma unroll\n  for (int j = 0; j < 8; ++j) " + load_vals(i, "wave * 512", "j", "v" + si + "[j]");
+    }
+    s += "  uint32_t vw" + si + " = valid_words(vb" + si + ", row0 + (int64_t)wave * 512, A.n_rows, lane), vwn" + si + ";\n";
+  }
   s += "  for (int64_t blk = row0; blk < row1; blk += 2048) {\n";
   s += "    const int64_t base = blk + (int64_t)wave * 512;\n";
   s += "    if (base >= row1) break;\n";
   s += "    const int soff = (int)(base - row0);\n";
-  for (int i = 0; i < ns; ++i) {
-    if (!need_vals[i]) continue;
-    const int k = col_kind[slot_col[i]];
-    const std::string si = std::to_string(i);
-    s += "    uint64_t v" + si + "[8];\n";
-    s += "#pragma unroll\n    for (int j = 0; j < 8; ++j) {\n";
-    if (k == CK_I32) {
-      s += "      v" + si + "[j] = (uint64_t)__builtin_amdgcn_raw_buffer_load_b32(vr" + si +
-           ", lane * 4, (soff + 64 * j) * 4, 2);\n";
-    } else {
-      s += "      const auto w2 = __builtin_amdgcn_raw_buffer_load_b64(vr" + si + ", lane * 8, (soff + 64 * j) * 8, 2);\n";
-      s += "      v" + si + "[j] = ((uint64_t)w2[1] << 32) | w2[0];\n";
-    }
-    s += "    }\n";
-  }
-  for (int i = 0; i < ns; ++i)
-    s += "    const uint32_t vw" + std::to_string(i) + " = valid_words(vb" + std::to_string(i) + ", base, A.n_rows, lane);\n";
   for (int h = 0; h < nh; ++h) s += "    int32_t qmin" + std::to_string(h) + " = 0;\n";
   s += "#pragma unroll\n  for (int j = 0; j < 8; ++j) {\n";
   s += "    const int64_t r = base + 64 * j;\n";
@@ -381,6 +384,14 @@ std::string pred_jit_source(const PredProgram& prog, const int32_t* col_kind, st
     s += "      ds_max_masked(sl, (uint32_t)(uintptr_t)(regs + " + std::to_string(h * 512) + ") + addr, q);\n";
     s += "    }\n";
   }
+  for (int i = 0; i < ns; ++i)
+    if (need_vals[i]) s += "    " + load_vals(i, "soff + 2048", "j", "v" + std::to_string(i) + "[j]");
+  // the next block's validity words right after row group 0 (loaded last, a whole block's loads would be
+  // in flight ahead of them when the next block needs them)
+  s += "    if (j == 0) {\n";
+  for (int i = 0; i < ns; ++i)
+    s += "      vwn" + std::to_string(i) + " = valid_words(vb" + std::to_string(i) + ", base + 2048, A.n_rows, lane);\n";
+  s += "    }\n";
   s += "  }\n";  // j
   for (int h = 0; h < nh; ++h) {
     const PredJitHll& e = hll[h];
@@ -389,17 +400,20 @@ std::string pred_jit_source(const PredProgram& prog, const int32_t* col_kind, st
     s += "    if (__builtin_amdgcn_ballot_w64(qmin" + hs + " < 0) != 0) {\n";
     s += "#pragma unroll\n      for (int j = 0; j < 8; ++j) {\n";
     s += "        if (!lane_bit(group_mask(vw" + std::to_string(e.slot) + ", j) & mask64(nullptr, base + 64 * j, row1))) continue;\n";
+    s += "        uint64_t cur;\n        " + load_vals(e.slot, "soff", "j", "cur");  // v[][j] holds the next block now
     if (k == CK_I32) {
-      s += "        hll_exact(regs + " + std::to_string(h * 512) + ", xxh64_int((uint32_t)" + vs + "));\n";
+      s += "        hll_exact(regs + " + std::to_string(h * 512) + ", xxh64_int((uint32_t)cur));\n";
     } else {
-      s += "        uint64_t raw = " + vs + ";\n";
+      s += "        uint64_t raw = cur;\n";
       if (k == CK_F64)
         s += "        if (__longlong_as_double((long long)raw) != __longlong_as_double((long long)raw)) raw = 0x7FF8000000000000ull;\n";
       s += "        hll_exact(regs + " + std::to_string(h * 512) + ", xxh64_long(raw));\n";
     }
     s += "      }\n    }\n";
   }
+  for (int i = 0; i < ns; ++i) s += "    vw" + std::to_string(i) + " = vwn" + std::to_string(i) + ";\n";
   s += "  }\n";  // blk
+  s += "  asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");  // the last prefetches land before exit\n";
   s += "  if (lane == 0) {\n";
   for (int c = 0; c < prog.n_counters; ++c) {
     const std::string cs = std::to_string(c);
