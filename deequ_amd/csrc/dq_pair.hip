@@ -124,9 +124,9 @@ __device__ double range_shift(const char* col, int kind, const uint32_t* vb, con
 
 // LDS ring of the fp64 path, per workgroup: kRing slots of one 64-row group -- the 8 columns (512 bytes each)
 // and the 18 selection words; 9 slots = 37 KB, 4 workgroups per CU
-constexpr int kRing = 9;
-constexpr int kSlotBytes = 8 * 512 + 128;
-constexpr int kSlotMaskWord = 8 * 128;  // dword index of the selection words in a slot
+constexpr int kRing = 4;
+constexpr int kSlotBytes = 8 * 1024 + 256;
+constexpr int kSlotMaskWord = 8 * 256;  // dword index of the selection words in a slot
 
 
 // per-lane sums of one wave task over its range
@@ -370,65 +370,66 @@ __device__ __forceinline__ bool pair_range(const PairWaveTask& T, const ScanCols
 
   const int64_t nfull = nr >> 6;
   if constexpr (RING) {
-    // ---- full groups through the workgroup's LDS ring (kRing slots, one 64-row group each): the two waves
-    // stage each group together, wave 0 the group's columns 0-3 and the where / column 0-3 selection words,
-    // wave 1 columns 4-7 and their selection words -- five DMA loads each (global_load_lds; lanes 0-31
-    // bring 16 bytes = 2 rows of a column, one lane per selection dword), kRing - 2 groups ahead of the
-    // fold, no VGPRs held.  One s_barrier per group: past it the partner's loads of group g have landed
-    // (each wave waits for its own first) and the partner has folded group g - 1, so the slot of group g - 2
-    // may be restaged.
+    // ---- full groups through the workgroup's LDS ring (kRing slots of two 64-row groups each): the two
+    // waves stage each slot together, wave 0 the slot's columns 0-3 and the where / column 0-3 selection
+    // words, wave 1 columns 4-7 and their selection words -- five DMA loads each (global_load_lds; every
+    // lane brings 16 bytes = 2 rows of a column, the 1 KB of a column's two groups in one instruction; one
+    // lane per selection dword, 4 per stream), kRing - 1 slots ahead of the fold, no VGPRs held.  One
+    // s_barrier per slot: past it the partner's loads of slot s have landed (each wave waits for its own
+    // first) and the partner has folded slot s - 1, whose ring slot is then restaged.
     static_assert(F64 && !CHECKED, "the ring path stages fp64 values");
-    constexpr int D = kRing - 2;
+    constexpr int D = kRing - 1;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)ring);
     const bool has_where = T.where >= 0;
-    // selection dwords of a slot: 0, 1 = where, 2 + 2 c, 3 + 2 c = column c.  Wave 0 stages dwords 0-9
-    // (lanes 0-9), wave 1 dwords 10-17 (lanes 0-7); wave w's position p is column p + w (mod 8).
+    // selection dwords of a slot: stream s (0 = where, 1 + c = column c) at 4 s .. 4 s + 3 (two words per
+    // group); wave 0 stages streams 0-4 (lanes 0-19), wave 1 streams 5-8 (lanes 0-15); wave w's position p
+    // is column p + w (mod 8).
     const uint32_t* mp;
     if (wave == 0) {
       mp = ww;
 #pragma unroll
       for (int c = 0; c < 4; ++c)
-        if (lane >> 1 == c + 1) mp = vw[c];
+        if (lane >> 2 == c + 1) mp = vw[c];
     } else {
       mp = vw[3];
 #pragma unroll
       for (int c = 1; c < 4; ++c)
-        if (lane >> 1 == c) mp = vw[3 + c];
+        if (lane >> 2 == c) mp = vw[3 + c];
     }
-    mp += lane & 1;
-    const uint64_t mexec = wave == 0 ? 0x3FFull : 0xFFull;
-    const uint32_t moff = 4096u + (wave == 0 ? 0u : 40u);
+    mp += lane & 3;
+    const uint64_t mexec = wave == 0 ? 0xFFFFFull : 0xFFFFull;
+    const uint32_t moff = (uint32_t)kSlotMaskWord * 4u + (wave == 0 ? 0u : 80u);
     // the four columns this wave stages: wave 0 positions 0-3, wave 1 positions 3-6 (= columns 4-7)
     const char* dp[4];
     const int p0 = wave == 0 ? 0 : 3;
 #pragma unroll
     for (int k = 0; k < 4; ++k) dp[k] = reinterpret_cast<const char*>(cols.values[T.cols[p0 + k]]) + row0 * 8;
-    const uint32_t dcol = wave == 0 ? 0u : 2048u;  // LDS byte offset of the first staged column
-    auto dma = [&](int64_t g, uint32_t slot) __attribute__((always_inline)) {
-      const uint32_t gc = (uint32_t)(g < nfull ? g : nfull - 1);
-      const uint32_t voff = gc * 512u + (uint32_t)lane * 16u;
+    const uint32_t dcol = wave == 0 ? 0u : 4096u;  // LDS byte offset of the first staged column
+    const int64_t npair = nfull >> 1;             // ring slots (two full groups each)
+    auto dma = [&](int64_t s, uint32_t slot) __attribute__((always_inline)) {
+      const uint32_t sc = (uint32_t)(s < npair ? s : npair - 1);
+      const uint32_t voff = sc * 1024u + (uint32_t)lane * 16u;
       const uint32_t d = lds0 + slot * (uint32_t)kSlotBytes + dcol;
       const uint32_t dm = lds0 + slot * (uint32_t)kSlotBytes + moff;
-      const uint32_t* ma = mp + 2 * gc;
+      const uint32_t* ma = mp + 4 * sc;
       uint32_t keep;
       uint64_t sv;
       asm volatile(
           "s_mov_b32 %[keep], m0\n\t"
           "s_mov_b64 %[sv], exec\n\t"
-          "s_mov_b32 exec_hi, 0\n\t"
           "s_mov_b32 m0, %[d]\n\t"
           "s_nop 0\n\t"
-          "global_load_lds_dwordx4 %[vo], %[b0]\n\t"
-          "s_add_u32 m0, %[d], 0x200\n\t"
-          "s_nop 0\n\t"
-          "global_load_lds_dwordx4 %[vo], %[b1]\n\t"
+          "global_load_lds_dwordx4 %[vo], %[b0] nt\n\t"
           "s_add_u32 m0, %[d], 0x400\n\t"
           "s_nop 0\n\t"
-          "global_load_lds_dwordx4 %[vo], %[b2]\n\t"
-          "s_add_u32 m0, %[d], 0x600\n\t"
+          "global_load_lds_dwordx4 %[vo], %[b1] nt\n\t"
+          "s_add_u32 m0, %[d], 0x800\n\t"
           "s_nop 0\n\t"
-          "global_load_lds_dwordx4 %[vo], %[b3]\n\t"
+          "global_load_lds_dwordx4 %[vo], %[b2] nt\n\t"
+          "s_add_u32 m0, %[d], 0xc00\n\t"
+          "s_nop 0\n\t"
+          "global_load_lds_dwordx4 %[vo], %[b3] nt\n\t"
           "s_mov_b64 exec, %[me]\n\t"
           "s_mov_b32 m0, %[dm]\n\t"
           "s_nop 0\n\t"
@@ -440,25 +441,19 @@ __device__ __forceinline__ bool pair_range(const PairWaveTask& T, const ScanCols
             [b2] "s"(dp[2]), [b3] "s"(dp[3]), [ma] "v"(ma)
           : "memory", "scc");
     };
-    // this wave's positions: ring column (p + wave) % 8; selection words: lanes 0, 1 of the first read =
-    // where, lanes 2 p, 2 p + 1 of the second = position p
+    // this wave's positions: ring column (p + wave) % 8; selection words of half h: lanes 0, 1 of the first
+    // read = where, lanes 2 p, 2 p + 1 of the second = position p
     const int64_t* xs0 = ring + lane;
     const uint32_t* ms0 = reinterpret_cast<const uint32_t*>(ring) + kSlotMaskWord;
-    const int mlw = lane & 1, mlc = lane < 16 ? 2 + ((2 * wave + lane) & 15) : 0;
-    auto one = [&](int64_t g, uint32_t slot) __attribute__((always_inline)) {
-      dma(g + D, slot + D < (uint32_t)kRing ? slot + D : slot + D - kRing);
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(5 * D) : "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      const int64_t* xs = xs0 + slot * (kSlotBytes / 8);
-      const uint32_t* ms = ms0 + slot * (kSlotBytes / 4);
+    const int mlw = lane & 1, mlc = lane < 16 ? 4 + 4 * (((lane >> 1) + wave) & 7) + (lane & 1) : 0;
+    auto half = [&](const int64_t* xs, const uint32_t* ms) __attribute__((always_inline)) {
       int64_t b[kPairPos];
       if (wave == 0) {
 #pragma unroll
-        for (int p = 0; p < kPairPos; ++p) b[p] = xs[p * 64];
+        for (int p = 0; p < kPairPos; ++p) b[p] = xs[p * 128];
       } else {
 #pragma unroll
-        for (int p = 0; p < kPairPos; ++p) b[p] = xs[((p + 1) % kPairPos) * 64];
+        for (int p = 0; p < kPairPos; ++p) b[p] = xs[((p + 1) % kPairPos) * 128];
       }
       const uint32_t mc = ms[mlc];
       auto word = [](uint32_t v, int i) {
@@ -474,12 +469,22 @@ __device__ __forceinline__ bool pair_range(const PairWaveTask& T, const ScanCols
       }
       if (active) fold_fast<true, MINMAX>(A, b, m, shift, kind);
     };
-    if (nfull > 0) {
+    auto one = [&](int64_t s, uint32_t slot) __attribute__((always_inline)) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(5 * (D - 1)) : "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      dma(s + D, slot == 0 ? (uint32_t)(kRing - 1) : slot - 1);
+      const int64_t* xs = xs0 + slot * (kSlotBytes / 8);
+      const uint32_t* ms = ms0 + slot * (kSlotBytes / 4);
+      half(xs, ms);
+      half(xs + 64, ms + 2);
+    };
+    if (npair > 0) {
 #pragma unroll
       for (int d = 0; d < D; ++d) dma(d, (uint32_t)d);
       uint32_t slot = 0;
-      for (int64_t g = 0; g < nfull; ++g) {
-        one(g, slot);
+      for (int64_t s = 0; s < npair; ++s) {
+        one(s, slot);
         slot = slot + 1 == kRing ? 0 : slot + 1;
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may outlive the workgroup (its LDS is reused)
@@ -493,6 +498,21 @@ __device__ __forceinline__ bool pair_range(const PairWaveTask& T, const ScanCols
       const int c = tp->cols[p];
       vw[p] = (cols.validity[c] ? cols.validity[c] : ones) + (row0 >> 5);
       vp[p] = reinterpret_cast<const char*>(cols.values[c]) + row0 * 8;
+    }
+    // an odd last full group (only at the end of the scan): values and masks loaded directly
+    for (int64_t g = 2 * npair; g < nfull; ++g) {
+      int64_t b[kPairPos];
+      uint64_t m[kPairPos];
+      const uint32_t off = (uint32_t)g * 8u;
+      const uint64_t wm = sword_at(ww, off);
+#pragma unroll
+      for (int p = 0; p < kPairPos; ++p) {
+        b[p] = *reinterpret_cast<const int64_t*>(vp[p] + ((uint32_t)g * 64u + (uint32_t)lane) * 8u);
+        const uint64_t mv = sword_at(vw[p], off) & wm;  // uniform, but the reloaded pointers look divergent
+        m[p] = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(mv >> 32)) << 32) |
+               (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)mv);
+      }
+      fold_fast<true, MINMAX>(A, b, m, shift, kind);
     }
   } else {
   // ---- full groups: values two groups ahead of the fold (three rotating buffers; two with Min / Max or
