@@ -32,8 +32,10 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md (HBM3E peak 8.0 TB/s)
 # FETCH_SIZE summary of this round's kernels (tools/profile_round.sh -> tools/summarize_prof.py):
 # per-dispatch HBM read bytes of each kernel at the default 125 M-row chunk, gfx950-corrected
-PMC_FILE = os.path.join(ROOT, "profiles", "r3b_pmc.json")
-CLOCK_FILE = os.path.join(ROOT, "profiles", "r3_clock.json")  # tools/clock_probe.sh: held clock per kernel
+PMC_FILE = os.path.join(ROOT, "profiles", "r3z_pmc.json")
+# tools/clock_probe.sh: held clock per kernel, one file per probe box (boxes hold 1.87-1.98 GHz under the same
+# kernels); the floor at the held clock takes the highest clock any probe saw (the conservative floor)
+CLOCK_FILES = [os.path.join(ROOT, "profiles", f) for f in ("r3_clock.json", "r3z_clock.json")]
 DEFAULT_CHUNK = 125_000_000  # 8 chunks per 1e9 rows; a UTF8 chunk's bytes (~2.0e9) stay < 2 GiB
 
 
@@ -383,16 +385,20 @@ def valu_bound(kernel, avg_ms):
            "source": os.path.relpath(PMC_FILE, ROOT)}
     # the clock the chip holds under this kernel (GRBM_GUI_ACTIVE / 8 XCDs / duration, committed probe): the
     # issue floor at that clock is what the launch can reach with its instruction count
-    try:
-        with open(CLOCK_FILE) as f:
-            clk = json.load(f).get("void " + kernel)
-    except (OSError, ValueError):
-        clk = None
-    if clk:
-        ghz = clk["effective_clock_GHz"]
+    clocks = {}
+    for path in CLOCK_FILES:
+        try:
+            with open(path) as f:
+                clk = json.load(f).get("void " + kernel)
+        except (OSError, ValueError):
+            clk = None
+        if clk:
+            clocks[os.path.relpath(path, ROOT)] = clk["effective_clock_GHz"]
+    if clocks:
+        ghz = max(clocks.values())
         held_ms = insts * VALU_CYCLES_PER_WAVE_INST / (1024 * ghz * 1e9) * 1e3
         out.update(held_clock_GHz=ghz, issue_floor_ms_at_held_clock=held_ms, frac_at_held_clock=held_ms / avg_ms,
-                   clock_source=os.path.relpath(CLOCK_FILE, ROOT))
+                   held_clock_by_probe=clocks)
     return out
 
 
