@@ -235,8 +235,10 @@ std::string pred_jit_source(const PredProgram& prog, const int32_t* col_kind, st
            " = __builtin_amdgcn_make_buffer_rsrc((void*)(A.values[" + std::to_string(i) + "] + row0 * " +
            std::to_string(sz) + "), (short)0, (int)((row1 - row0) * " + std::to_string(sz) + "), 0x00020000);\n";
   }
-  for (int c = 0; c < prog.n_counters; ++c) s += "  uint64_t ct" + std::to_string(c) + " = 0, cn" + std::to_string(c) + " = 0;\n";
-  for (int h = 0; h < nh; ++h) s += "  uint64_t hc" + std::to_string(h) + " = 0;\n";
+  // per-wave counters in 32 bits: a wave counts at most a quarter of its range's rows, and the planner's
+  // ranges (>= 64 per chunk, dq_plan.cpp size_ranges) keep that far below 2^32 for any chunk HBM can hold
+  for (int c = 0; c < prog.n_counters; ++c) s += "  uint32_t ct" + std::to_string(c) + " = 0, cn" + std::to_string(c) + " = 0;\n";
+  for (int h = 0; h < nh; ++h) s += "  uint32_t hc" + std::to_string(h) + " = 0;\n";
   // values and validity words one block ahead, per row group: v[i][j] of the next block is loaded as soon as
   // row group j of this block is done with it (same registers), so the next block's loads are in flight
   // while this block is evaluated and hashed
@@ -351,15 +353,23 @@ std::string pred_jit_source(const PredProgram& prog, const int32_t* col_kind, st
     const PredCounter pc = prog.counters[c];
     if (pc.pred < 0 || pc.pred >= (int)roots.size() || pc.where >= (int)roots.size()) return std::string();
     const std::string tw = pc.where < 0 ? "inr" : "(" + roots[pc.where].first + " & inr)";
-    s += "    ct" + std::to_string(c) + " += (uint64_t)__builtin_popcountll(" + roots[pc.pred].first + " & " + tw + ");\n";
-    s += "    cn" + std::to_string(c) + " += (uint64_t)__builtin_popcountll(~" + roots[pc.pred].second + " & " + tw + ");\n";
+    s += "    ct" + std::to_string(c) + " += (uint32_t)__builtin_popcountll(" + roots[pc.pred].first + " & " + tw + ");\n";
+    s += "    cn" + std::to_string(c) + " += (uint32_t)__builtin_popcountll(~" + roots[pc.pred].second + " & " + tw + ");\n";
   }
   for (int b = 0; b < prog.n_bitmaps; ++b) {
     const int rt = prog.bitmap_root[b];
     if (rt < 0 || rt >= (int)roots.size()) return std::string();
     s += "    if (r < row1 && lane == 0) A.where_bits[" + std::to_string(b) + "][r >> 6] = " + roots[rt].first + " & inr;\n";
   }
-  // the group's predicate work (scalar masks) completes before its hashing starts
+  // the group's counters are pinned here (left alone, LLVM sinks the popcount chains to the block's end
+  // and every ballot of the block stays live until then: SGPR spills), and the group's predicate work
+  // (scalar masks) completes before its hashing starts
+  if (prog.n_counters > 0) {
+    s += "    asm volatile(\"\" :";
+    for (int c = 0; c < prog.n_counters; ++c)
+      s += std::string(c ? "," : "") + " \"+s\"(ct" + std::to_string(c) + "), \"+s\"(cn" + std::to_string(c) + ")";
+    s += ");\n";
+  }
   s += "    __builtin_amdgcn_sched_barrier(0);\n";
   // fused HLL tasks: XXH64 of the slot's raw value (doubleToLongBits for fp64: NaN canonical), exec-masked
   // register max; the rare low-word rank redone exactly after the block
@@ -369,7 +379,8 @@ std::string pred_jit_source(const PredProgram& prog, const int32_t* col_kind, st
     const std::string hs = std::to_string(h), vs = "v" + std::to_string(e.slot) + "[j]";
     s += "    {\n";
     s += "      const uint64_t sl = va" + std::to_string(e.slot) + " & inr;\n";
-    s += "      hc" + hs + " += (uint64_t)__builtin_popcountll(sl);\n";
+    s += "      hc" + hs + " += (uint32_t)__builtin_popcountll(sl);\n";
+    s += "      asm volatile(\"\" : \"+s\"(hc" + hs + "));\n";
     if (k == CK_I32) {
       s += "      const uint64_t hb = xxh64_int_head((uint32_t)" + vs + ");\n";
     } else if (k == CK_F64) {
