@@ -118,7 +118,10 @@ def main():
     from deequ_amd.runner import ScanPlan
 
     if args.skip_headline:
-        out = {"configs": {cfg: run_config(cfg, args) for cfg in args.configs.split(",") if cfg}}
+        deferred_cpu = []
+        out = {"configs": {cfg: run_config(cfg, args, deferred_cpu) for cfg in args.configs.split(",") if cfg}}
+        for run in deferred_cpu:
+            run()
         print(json.dumps(out), flush=True)
         return
     n_total = args.rows
@@ -214,9 +217,15 @@ def main():
     }
     if rank == 0 and world == 1:
         out["state_io"] = state_io_timing(analyzers, persisted[0])
-        if args.cpu_sample > 0:
-            out["cpu_baseline"] = cpu_baseline(chunks[0], min(args.cpu_sample, chunks[0].num_rows), args.cpu_threads,
-                                               args.cpu_seconds)
+    # the CPU baselines run after every GPU measurement (their host copies are taken now): OpenMP's worker
+    # threads outlive a parallel region, and config steps timed after one showed 39-64 ms outliers among
+    # 22.5 ms C3 steps (none with the baseline off or run last)
+    deferred_cpu = []
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        n_cpu = min(args.cpu_sample, chunks[0].num_rows)
+        cols_cpu = _host_cols(chunks[0], n_cpu)
+        deferred_cpu.append(lambda: out.__setitem__("cpu_baseline", cpu_baseline(cols_cpu, n_cpu, args.cpu_threads,
+                                                                                 args.cpu_seconds)))
     plan.close()
     del chunks
     torch.cuda.empty_cache()
@@ -226,8 +235,10 @@ def main():
     if world == 1 and args.configs:
         out["configs"] = {}
         for cfg in [c for c in args.configs.split(",") if c]:
-            out["configs"][cfg] = run_config(cfg, args)
+            out["configs"][cfg] = run_config(cfg, args, deferred_cpu)
             torch.cuda.empty_cache()
+    for run in deferred_cpu:
+        run()
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -296,8 +307,9 @@ def config_setup(cfg, n, chunk):
     return tables, analyzers, desc
 
 
-def run_config(cfg, args) -> dict:
-    """One BASELINE config at its size on this GPU: rows/s, per-kernel roofline, HBM fraction of the step."""
+def run_config(cfg, args, deferred_cpu) -> dict:
+    """One BASELINE config at its size on this GPU: rows/s, per-kernel roofline, HBM fraction of the step.
+    Its CPU baseline (C1), if any, is appended to `deferred_cpu` and run after every GPU measurement."""
     import torch
 
     from deequ_amd.runner import ScanPlan
@@ -342,7 +354,9 @@ def run_config(cfg, args) -> dict:
                         "avg_launch_ms": dom["avg_ms"], "bytes_per_launch": dom["bytes_per_launch"]},
            "kernels": {k_: {kk: v[kk] for kk in ("launches", "avg_ms", "GBps")} for k_, v in kernels.items()}}
     if cfg == "c1" and args.cpu_sample > 0:
-        rec["cpu_baseline"] = cpu_baseline_c1(tables[0], args.cpu_threads, min(args.cpu_seconds, 5.0))
+        data_c1 = c1_host_data(tables[0])
+        deferred_cpu.append(lambda: rec.__setitem__("cpu_baseline", cpu_baseline_c1(data_c1, args.cpu_threads,
+                                                                                    min(args.cpu_seconds, 5.0))))
     plan.close()
     del tables
     return rec
@@ -552,11 +566,11 @@ def ingest_timing(args, analyzers) -> dict:
                     "2 slots; e2e = upload + fused scan + finish, copy of batch k+1 overlapping scan of k"}
 
 
-def cpu_baseline(table, n, threads, min_seconds=10.0):
-    """The C restatement (oracle/, "port") of the same profile scan on the host's CPU share."""
+def cpu_baseline(cols, n, threads, min_seconds=10.0):
+    """The C restatement (oracle/, "port") of the same profile scan on the host's CPU share; `cols` = the
+    host copy of the sample's columns (_host_cols)."""
     from oracle import dq_oracle_c as C
 
-    cols = _host_cols(table, n)
     share, how = host_cpu_share()
     threads = threads or share
     reps = 0
@@ -574,18 +588,24 @@ def cpu_baseline(table, n, threads, min_seconds=10.0):
                       f"threads = this host's CPU share ({how}), {dt:.1f} s"}
 
 
-def cpu_baseline_c1(table, threads, min_seconds):
+def c1_host_data(table):
+    """Host copies of the C1 columns its CPU path reads (the i64 columns, every validity bitmap)."""
+    n = table.num_rows
+    cols = [c for c in _host_cols(table, n) if c[0] == "i64"]
+    bitmaps = [c.validity[: (n + 7) // 8].cpu().numpy() for c in table.columns.values() if c.validity is not None]
+    return n, cols, bitmaps
+
+
+def cpu_baseline_c1(data, threads, min_seconds):
     """C1's CPU path: the oracle's C restatement of the Item-table analyzers (count / moments / min / max of
     id and numViews, validity counts of the strings) on the host's CPU share."""
     from oracle import dq_oracle_c as C
 
-    n = table.num_rows
+    n, cols, bitmaps = data
     share, how = host_cpu_share()
     threads = threads or share
     import numpy as np
 
-    cols = [c for c in _host_cols(table, n) if c[0] == "i64"]
-    bitmaps = [c.validity[: (n + 7) // 8].cpu().numpy() for c in table.columns.values() if c.validity is not None]
     reps = 0
     t0 = time.perf_counter()
     while True:
