@@ -180,8 +180,16 @@ bool pred_jit_eligible(const PredProgram& prog, const int32_t* col_kind, int32_t
 // The kernel source of `prog`; slot_col receives the program's distinct columns in slot order (the order of
 // PredJitArgs::values / validity); fused HLL task h hashes slot hll[h].slot (its task and accumulator come
 // in PredJitArgs::hll_task / hll_slot, so the source does not depend on task numbering).
+// 64-row groups per wave block (<= 8: valid_words loads 16 validity dwords per lane group).  8 groups: 117
+// VGPRs, 4 waves per SIMD, 0.870 ms per 125 M rows of C3; 4 groups (72 VGPRs, 7 waves) 0.871-0.904 ms, 2 groups
+// 0.899-0.923 ms (profiles/r3_pred_ab.txt, r3u)
+constexpr int kJitGroups = 8;
+
 std::string pred_jit_source(const PredProgram& prog, const int32_t* col_kind, std::vector<int32_t>& slot_col,
                             const std::vector<PredJitHll>& hll) {
+  // each wave takes blocks of kJitGroups 64-row groups (the workgroup's four waves 4x that many rows)
+  const std::string G = std::to_string(kJitGroups), WR = std::to_string(64 * kJitGroups),
+                    BR = std::to_string(256 * kJitGroups);
   slot_col.clear();
   auto slot_of = [&](int32_t c) {
     for (size_t i = 0; i < slot_col.size(); ++i)
@@ -254,17 +262,17 @@ std::string pred_jit_source(const PredProgram& prog, const int32_t* col_kind, st
   for (int i = 0; i < ns; ++i) {
     const std::string si = std::to_string(i);
     if (need_vals[i]) {
-      s += "  uint64_t v" + si + "[8];\n";
-      s += "#pragma unroll\n  for (int j = 0; j < 8; ++j) " + load_vals(i, "wave * 512", "j", "v" + si + "[j]");
+      s += "  uint64_t v" + si + "[" + G + "];\n";
+      s += "#pragma unroll\n  for (int j = 0; j < " + G + "; ++j) " + load_vals(i, "wave * " + WR, "j", "v" + si + "[j]");
     }
-    s += "  uint32_t vw" + si + " = valid_words(vb" + si + ", row0 + (int64_t)wave * 512, A.n_rows, lane), vwn" + si + ";\n";
+    s += "  uint32_t vw" + si + " = valid_words(vb" + si + ", row0 + (int64_t)wave * " + WR + ", A.n_rows, lane), vwn" + si + ";\n";
   }
-  s += "  for (int64_t blk = row0; blk < row1; blk += 2048) {\n";
-  s += "    const int64_t base = blk + (int64_t)wave * 512;\n";
+  s += "  for (int64_t blk = row0; blk < row1; blk += " + BR + ") {\n";
+  s += "    const int64_t base = blk + (int64_t)wave * " + WR + ";\n";
   s += "    if (base >= row1) break;\n";
   s += "    const int soff = (int)(base - row0);\n";
   for (int h = 0; h < nh; ++h) s += "    int32_t qmin" + std::to_string(h) + " = 0;\n";
-  s += "#pragma unroll\n  for (int j = 0; j < 8; ++j) {\n";
+  s += "#pragma unroll\n  for (int j = 0; j < " + G + "; ++j) {\n";
   s += "    const int64_t r = base + 64 * j;\n";
   s += "    const uint64_t inr = mask64(nullptr, r, row1);\n";
   for (int i = 0; i < ns; ++i) s += "    const uint64_t va" + std::to_string(i) + " = group_mask(vw" + std::to_string(i) + ", j) & inr;\n";
@@ -396,12 +404,12 @@ std::string pred_jit_source(const PredProgram& prog, const int32_t* col_kind, st
     s += "    }\n";
   }
   for (int i = 0; i < ns; ++i)
-    if (need_vals[i]) s += "    " + load_vals(i, "soff + 2048", "j", "v" + std::to_string(i) + "[j]");
+    if (need_vals[i]) s += "    " + load_vals(i, "soff + " + BR, "j", "v" + std::to_string(i) + "[j]");
   // the next block's validity words right after row group 0 (loaded last, a whole block's loads would be
   // in flight ahead of them when the next block needs them)
   s += "    if (j == 0) {\n";
   for (int i = 0; i < ns; ++i)
-    s += "      vwn" + std::to_string(i) + " = valid_words(vb" + std::to_string(i) + ", base + 2048, A.n_rows, lane);\n";
+    s += "      vwn" + std::to_string(i) + " = valid_words(vb" + std::to_string(i) + ", base + " + BR + ", A.n_rows, lane);\n";
   s += "    }\n";
   s += "  }\n";  // j
   for (int h = 0; h < nh; ++h) {
@@ -409,7 +417,7 @@ std::string pred_jit_source(const PredProgram& prog, const int32_t* col_kind, st
     const int k = col_kind[slot_col[e.slot]];
     const std::string hs = std::to_string(h), vs = "v" + std::to_string(e.slot) + "[j]";
     s += "    if (__builtin_amdgcn_ballot_w64(qmin" + hs + " < 0) != 0) {\n";
-    s += "#pragma unroll\n      for (int j = 0; j < 8; ++j) {\n";
+    s += "#pragma unroll\n      for (int j = 0; j < " + G + "; ++j) {\n";
     s += "        if (!lane_bit(group_mask(vw" + std::to_string(e.slot) + ", j) & mask64(nullptr, base + 64 * j, row1))) continue;\n";
     s += "        uint64_t cur;\n        " + load_vals(e.slot, "soff", "j", "cur");  // v[][j] holds the next block now
     if (k == CK_I32) {
