@@ -7,18 +7,19 @@
 // columns fused with their Mean and StdDev: every column is read from HBM once for all of that.
 //
 // Layout.  A workgroup task (PairWG, planned on the host) is one pair group (<= 8 columns, one `where`)
-// and two wave tasks; a workgroup is two waves and one row range, and the waves never synchronise.  Wave
-// w's position p holds the group's local column (p + w) % 8 and runs the fixed 14-slot pattern
-// kPairSlotA / kPairSlotB over its positions -- the two rotations of the pattern are the 28 pairs of 8
-// columns, each once -- plus the moments of its even positions.  Lane l takes row l of each 64-row group:
-// the 8 values come straight from HBM into VGPRs (two groups in flight ahead of the fold; the other wave
-// of the workgroup reads the same lines, an L1 / L2 hit), a position's selection (validity & where) is a
-// 64-bit SGPR mask read by a scalar load, and with z = x - shift zeroed outside the selection the pair
-// sums are exec-masked VALU updates grouped by position:
-//   exec = sel(a):  Sb += zb   Sbb += zb^2   Sab += za zb        exec = sel(b):  Sa += za   Saa += za^2
-// i.e. five fp64 VALU per pair and 64 rows, nothing for the counts: a pair's count (rows selected in both
-// columns) and a column's count are popcounts of bitmap words, taken at the end of the range by a
-// lane-per-word pass over the bitmaps (1/64 of the value bytes).
+// and two wave tasks; a workgroup is two waves and one row range.  Wave w's position p holds the group's
+// local column (p + w) % 8 and runs the fixed 14-slot pattern kPairSlotA / kPairSlotB over its positions --
+// the two rotations of the pattern are the 28 pairs of 8 columns, each once -- plus the moments of its even
+// positions.  Lane l takes row l of each 64-row group.  All-fp64, 16-byte aligned groups (RING) are staged
+// HBM -> LDS by global_load_lds DMA into a ring of kRing slots of two 64-row groups: each wave brings four
+// columns (one 1 KB instruction per column, all 64 lanes, nt policy) and its selection words, 3 slots ahead,
+// one s_barrier per slot; the selection masks come out of LDS by v_readlane.  Other groups load the values
+// into VGPRs two groups ahead and the masks by scalar loads.  Per pair and 64 rows the fold is five fp64
+// VALU under exec = sel(a) & sel(b) (the rows selected in both columns, nothing zeroed):
+//   Sa += za   Sb += zb   Sab += za zb   Saa += za^2   Sbb += zb^2        (z = x - shift)
+// and nothing for the counts: a pair's count (rows selected in both columns) and a column's count are
+// popcounts of bitmap words, taken at the end of the range by a lane-per-word pass over the bitmaps (1/64 of
+// the value bytes).
 //
 // Non-finite values.  The fold above assumes every selected value is finite.  A selected NaN / +-inf (or
 // a finite value whose square overflows) turns some active sum non-finite; the wave then flags its range
@@ -122,8 +123,9 @@ __device__ double range_shift(const char* col, int kind, const uint32_t* vb, con
   return 0.0;
 }
 
-// LDS ring of the fp64 path, per workgroup: kRing slots of one 64-row group -- the 8 columns (512 bytes each)
-// and the 18 selection words; 9 slots = 37 KB, 4 workgroups per CU
+// LDS ring of the fp64 path, per workgroup: kRing slots of two 64-row groups -- the 8 columns (1 KB each) and
+// the 36 selection words (4 per stream: where + 8 columns); 4 slots = 33 KB, 4 workgroups per CU (deeper rings
+// at 2-3 workgroups per CU measured slower: profiles/r3_pred_ab.txt, r3s)
 constexpr int kRing = 4;
 constexpr int kSlotBytes = 8 * 1024 + 256;
 constexpr int kSlotMaskWord = 8 * 256;  // dword index of the selection words in a slot
