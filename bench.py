@@ -56,6 +56,8 @@ def parse(argv=None):
     p.add_argument("--ingest-rows", type=int, default=62_500_000,
                    help="rows of the host-resident Arrow C5 batch for the ingestion leg (0 = skip)")
     p.add_argument("--ingest-reps", type=int, default=4, help="uploads + scans of that batch timed end to end")
+    p.add_argument("--no-plan-timing", dest="plan_timing", action="store_false",
+                   help="skip the fresh-process plan-creation timing (C3 / C5, cold and warm JIT cache)")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="process group for N > 1 (nccl = RCCL over xGMI; gloo: launcher tests with ranks sharing a GPU)")
     return p.parse_args(argv)
@@ -71,6 +73,54 @@ def launch_ranks(args) -> int:
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     return subprocess.call(cmd, env=env)
+
+
+# plan creation of C3 (whose predicate program becomes a kernel compiled with hipRTC) and C5 (no predicates), in a
+# fresh process: dq_plan_create's host time and its JIT part, for a first and a second plan of the process
+_PLAN_PROBE = r"""
+import json, sys, time
+sys.path.insert(0, %r)
+import torch
+from deequ_amd import synth
+from deequ_amd.runner import ScanPlan
+torch.cuda.set_device(0)
+out = {}
+for cfg, tab, an in (("c3", synth.c3_table, synth.c3_analyzers), ("c5", synth.c5_table, synth.profile_analyzers)):
+    t = tab(4096, seed=1)
+    torch.cuda.synchronize()
+    rec = {}
+    for k in ("first", "second"):
+        a = time.perf_counter()
+        plan = ScanPlan(an(t), t.schema)
+        wall = (time.perf_counter() - a) * 1e3
+        total, jit = plan.create_time()
+        rec[k] = {"wall_ms": round(wall, 3), "dq_plan_create_ms": round(total, 3), "pred_jit_ms": round(jit, 3),
+                  "pred_kernel": plan.pred_compiled()[1] if plan.pred_compiled()[0] else None}
+        plan.close()
+    out[cfg] = rec
+print(json.dumps(out))
+"""
+
+
+def plan_create_timing() -> dict:
+    """Plan-creation cost (deequ builds one plan per run, AnalysisRunner.scala:279-326): C3 / C5 plans created in
+    fresh processes, first with an empty code-object cache (the predicate kernel compiled by hipRTC), then with
+    the cache that run filled (loaded from disk); in each process a second plan hits the process cache.  Runs
+    before this process touches the GPU."""
+    import tempfile
+
+    out = {}
+    with tempfile.TemporaryDirectory(prefix="dq_jit_") as d:
+        env = dict(os.environ, DQ_JIT_CACHE_DIR=d)
+        for label in ("cold_cache", "warm_disk_cache"):
+            try:
+                r = subprocess.run([sys.executable, "-c", _PLAN_PROBE % ROOT], env=env, capture_output=True, text=True,
+                                   timeout=300)
+                out[label] = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else {
+                    "error": r.stderr[-500:]}
+            except (subprocess.TimeoutExpired, ValueError, IndexError) as e:
+                out[label] = {"error": str(e)}
+    return out
 
 
 def host_cpu_share() -> tuple:
@@ -100,10 +150,12 @@ def main():
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     if world_env != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} disagrees with WORLD_SIZE={world_env}")
+    rank = int(os.environ.get("RANK", "0"))
+    plan_ms = (plan_create_timing() if (rank == 0 and world_env == 1 and args.plan_timing and not args.skip_headline)
+               else None)
     import torch
     import torch.distributed as dist
 
-    rank = int(os.environ.get("RANK", "0"))
     world = world_env
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
@@ -214,6 +266,7 @@ def main():
         "append_ms_per_step": host_ms["append"] / args.steps,
         "roofline": roofline(dom_name, dom, traffic, kernels),
         "cpu_baseline": None,
+        "plan_create_ms": plan_ms,
     }
     if rank == 0 and world == 1:
         out["state_io"] = state_io_timing(analyzers, persisted[0])
@@ -251,7 +304,8 @@ def kernel_report(plan, chunks, n_total) -> dict:
 
     nch = len(chunks)
     out = {}
-    ids = [(0, "dq_pred_scan"), (2, "dq_pair_scan")] + [(16 + v, f"dq_column_scan<{nm}>") for v, nm in L.VARIANT_NAMES.items()]
+    pred_name = "dq_pred_jit" if plan.pred_compiled()[0] else "dq_pred_scan"  # the compiled kernel or the interpreter
+    ids = [(0, pred_name), (2, "dq_pair_scan")] + [(16 + v, f"dq_column_scan<{nm}>") for v, nm in L.VARIANT_NAMES.items()]
     for kid, name in ids:
         ms, nl = plan.kernel_time(kid)
         if not nl:
@@ -295,10 +349,7 @@ def config_setup(cfg, n, chunk):
                                                               dq.Minimum(c), dq.Maximum(c))]
         desc = "C2 8 x f64 (10% nulls): Size + Completeness/Mean/StdDev/Min/Max per column"
     elif cfg == "c3":
-        analyzers = [dq.Size()] + [dq.ApproxCountDistinct(c) for c in names]
-        analyzers += [dq.Compliance("p0", "i0 >= 0"),
-                      dq.Compliance("p1", "`i1` IS NULL OR (`i1` >= 10.0 AND `i1` <= 1000.0)"),
-                      dq.Compliance("p2", "i2 < i3"), dq.Compliance("p3", "COALESCE(i3, 0.0) >= 0")]
+        analyzers = synth.c3_analyzers(tables[0])
         desc = "C3 4 x i64 + 4 x utf8 (10% nulls): Size + ApproxCountDistinct x8 + Compliance x4"
     else:
         analyzers = [dq.Correlation(names[i], names[j]) for i in range(8) for j in range(i + 1, 8)]

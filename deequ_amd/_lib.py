@@ -8,7 +8,7 @@ from __future__ import annotations
 import ctypes
 import os
 
-ABI_VERSION = 2  # include/dqscan.h DQ_ABI_VERSION
+ABI_VERSION = 3  # include/dqscan.h DQ_ABI_VERSION
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DQ_LIB_PATH") or os.path.join(_HERE, "libdqscan.so")  # override: diagnostic A/B builds
@@ -76,6 +76,14 @@ class AnalyzerSpec(ctypes.Structure):
 class PredNode(ctypes.Structure):
     _fields_ = [("kind", ctypes.c_int32), ("a", ctypes.c_int32), ("b", ctypes.c_int32),
                 ("cmp", ctypes.c_int32), ("i64", ctypes.c_int64), ("f64", ctypes.c_double)]
+
+
+# dq_plan_options.pred_pass (enum dq_pred_pass)
+PRED_PASS = {"auto": 0, "interpreter": 1, "compiled": 2}
+
+
+class PlanOptions(ctypes.Structure):
+    _fields_ = [("struct_size", ctypes.c_int32), ("pred_pass", ctypes.c_int32), ("reserved", ctypes.c_int32 * 6)]
 
 
 class ColumnView(ctypes.Structure):
@@ -165,6 +173,14 @@ def _load():
     L.dq_plan_create_ex.restype = c.c_int32
     L.dq_plan_create_ex.argtypes = [P(AnalyzerSpec), c.c_int32, P(ColumnDesc), c.c_int32, P(PredNode), c.c_int32,
                                     P(c.c_char_p), c.c_int32, c.c_int32, P(c.c_void_p)]
+    L.dq_plan_create_opts.restype = c.c_int32
+    L.dq_plan_create_opts.argtypes = [P(AnalyzerSpec), c.c_int32, P(ColumnDesc), c.c_int32, P(PredNode), c.c_int32,
+                                      P(c.c_char_p), c.c_int32, P(PlanOptions), c.c_int32, P(c.c_void_p)]
+    L.dq_plan_explain.restype = c.c_int64
+    L.dq_plan_explain.argtypes = [P(AnalyzerSpec), c.c_int32, P(ColumnDesc), c.c_int32, P(PredNode), c.c_int32,
+                                  P(c.c_char_p), c.c_int32, P(PlanOptions), c.c_char_p, c.c_int64]
+    L.dq_plan_create_time.restype = c.c_int32
+    L.dq_plan_create_time.argtypes = [c.c_void_p, P(c.c_double), P(c.c_double)]
     L.dq_regex_info.restype = c.c_int32
     L.dq_regex_info.argtypes = [c.c_char_p, c.c_int32, P(c.c_int32), P(c.c_int32)]
     L.dq_pred_pool_create.restype = c.c_int32
@@ -258,7 +274,8 @@ lib = _load()
 
 # every symbol include/dqscan.h declares (checked by tests/test_boundary.py)
 EXPORTED = [
-    "dq_abi_version", "dq_last_error", "dq_plan_create", "dq_plan_create_ex", "dq_regex_info", "dq_regex_match_host",
+    "dq_abi_version", "dq_last_error", "dq_plan_create", "dq_plan_create_ex", "dq_plan_create_opts",
+    "dq_plan_create_time", "dq_plan_explain", "dq_regex_info", "dq_regex_match_host",
     "dq_pred_pool_create", "dq_pred_pool_add", "dq_pred_pool_add_regex", "dq_pred_pool_size", "dq_pred_pool_nodes",
     "dq_pred_pool_num_patterns", "dq_pred_pool_patterns", "dq_pred_pool_destroy",
     "dq_arrow_import", "dq_uploader_create", "dq_upload", "dq_upload_fence", "dq_upload_release", "dq_upload_sync",

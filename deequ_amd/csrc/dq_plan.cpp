@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -18,6 +19,7 @@
 #include <functional>
 #include <limits>
 #include <map>
+#include <memory>
 #include <string>
 #include <tuple>
 #include <vector>
@@ -442,7 +444,11 @@ struct dq_plan {
   std::vector<int32_t> pred_jit_cols;                   // its slots' plan columns
   std::vector<int32_t> pred_jit_hll_task, pred_jit_hll_slot;  // fused HLL tasks (post-sort index) / accumulators
   int32_t pred_fused_first = 0, pred_fused_count = 0;  // those tasks sort last (after the pair-fused ones)
-  std::string pred_jit_note;                            // why the interpreter runs (diagnostic)
+  std::string pred_jit_note;                            // why the interpreter runs, or the kernel's origin
+  int32_t pred_pass = DQ_PRED_PASS_AUTO;                // dq_plan_options.pred_pass
+  bool host_only = false;                               // dq_plan_explain: lower on the host, no device work
+  std::string pred_jit_src;                             // the generated kernel source (host_only plans)
+  double create_ms = 0.0, pred_jit_ms = 0.0;            // dq_plan_create_time
 
   // device memory
   ColTask* d_col_tasks = nullptr;
@@ -850,7 +856,7 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
   // the predicate program compiled into its own kernel when the generator takes it; HLL-only tasks (no
   // `where`) on its columns are hashed there (fused = 2) instead of re-reading the column in the column pass
   std::vector<int> pred_fused(p->col_tasks.size(), 0);
-  if (p->has_pred) {
+  if (p->has_pred && p->pred_pass != DQ_PRED_PASS_INTERPRETER) {
     std::vector<int32_t> kinds(ncols);
     for (int c = 0; c < ncols; ++c) kinds[c] = kind_of(p->schema[c].type);
     if (pred_jit_eligible(p->prog, kinds.data(), ncols)) {
@@ -868,8 +874,14 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
           }
       }
       const std::string src = pred_jit_source(p->prog, kinds.data(), slots, hll);
-      std::string err;
-      p->pred_jit = src.empty() ? nullptr : pred_jit_compile(src, err);
+      std::string note = "generator declined the program";
+      if (p->host_only) {
+        p->pred_jit_src = src;
+        note = src.empty() ? note : "host-only plan: kernel generated, not compiled";
+      } else if (!src.empty()) {
+        p->pred_jit = pred_jit_get(src, p->device, note, p->pred_jit_ms);
+      }
+      p->pred_jit_note = note;
       if (p->pred_jit) {
         p->pred_jit_cols = slots;
         p->pred_jit_hll_task = tasks;
@@ -877,12 +889,14 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
           pred_fused[t] = 2;
           p->pred_jit_hll_slot.push_back(p->col_tasks[t].hll_slot);
         }
-      } else {
-        p->pred_jit_note = src.empty() ? "generator declined the program" : err;
       }
     } else {
       p->pred_jit_note = "program not eligible (regex / string atoms or > 8 columns)";
     }
+    if (!p->pred_jit && !(p->host_only && !p->pred_jit_src.empty()) && p->pred_pass == DQ_PRED_PASS_COMPILED)
+      return set_error(DQ_E_UNSUPPORTED, "compiled predicate pass required: %s", p->pred_jit_note.c_str());
+  } else if (p->has_pred) {
+    p->pred_jit_note = "interpreter requested (DQ_PRED_PASS_INTERPRETER)";
   }
 
   // correlation pairs -> groups of <= kTileCols columns and one `where` (greedy), staged together
@@ -1025,6 +1039,8 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
   p->launches_per_scan = (p->has_pred ? 1 : 0) + (int32_t)p->groups.size() + (p->pair_wgs.empty() ? 0 : 1) +
                          ((p->col_tasks.size() + p->pair_tasks.size()) ? 1 : 0);
 
+  if (p->host_only) return DQ_OK;
+
   // device allocations
   const size_t nct = p->col_tasks.size(), npt = p->pair_tasks.size();
   if (dq_status s = dmalloc(&p->d_col_tasks, nct * sizeof(ColTask))) return s;
@@ -1075,7 +1091,26 @@ dq_status dq_plan_create(const dq_analyzer_spec* specs, int32_t n_specs, const d
 dq_status dq_plan_create_ex(const dq_analyzer_spec* specs, int32_t n_specs, const dq_column_desc* schema,
                             int32_t n_cols, const dq_pred_node* pred_pool, int32_t n_pred,
                             const char* const* patterns, int32_t n_patterns, int32_t device, dq_plan** out) {
+  return dq_plan_create_opts(specs, n_specs, schema, n_cols, pred_pool, n_pred, patterns, n_patterns, nullptr, device,
+                             out);
+}
+
+dq_status dq_plan_create_opts(const dq_analyzer_spec* specs, int32_t n_specs, const dq_column_desc* schema,
+                              int32_t n_cols, const dq_pred_node* pred_pool, int32_t n_pred,
+                              const char* const* patterns, int32_t n_patterns, const dq_plan_options* opts,
+                              int32_t device, dq_plan** out) {
+  const auto t0 = std::chrono::steady_clock::now();
   if (!out) return set_error(DQ_E_INVALID, "dq_plan_create: out is NULL");
+  // options: the fields the caller's struct_size covers, defaults past it
+  dq_plan_options o{};
+  o.struct_size = (int32_t)sizeof(dq_plan_options);
+  if (opts) {
+    if (opts->struct_size < (int32_t)(2 * sizeof(int32_t)))
+      return set_error(DQ_E_INVALID, "dq_plan_create: dq_plan_options.struct_size %d too small", opts->struct_size);
+    std::memcpy(&o, opts, std::min((size_t)opts->struct_size, sizeof(o)));
+  }
+  if (o.pred_pass < DQ_PRED_PASS_AUTO || o.pred_pass > DQ_PRED_PASS_COMPILED)
+    return set_error(DQ_E_INVALID, "dq_plan_create: unknown pred_pass %d", o.pred_pass);
   if (n_patterns < 0 || (n_patterns > 0 && !patterns)) return set_error(DQ_E_INVALID, "dq_plan_create: bad patterns");
   for (int32_t k = 0; k < n_patterns; ++k)
     if (!patterns[k]) return set_error(DQ_E_INVALID, "dq_plan_create: pattern %d is NULL", k);
@@ -1102,12 +1137,14 @@ dq_status dq_plan_create_ex(const dq_analyzer_spec* specs, int32_t n_specs, cons
     return set_error(DQ_E_HIP, "hipStreamCreate: %s", hipGetErrorString(e));
   }
   p->own_stream = true;
+  p->pred_pass = o.pred_pass;
   dq_status st = build_plan(p, pred_pool, n_pred);
   if (st != DQ_OK) {
     std::string msg = g_err;
     dq_plan_destroy(p);
     return set_error(st, "%s", msg.c_str());
   }
+  p->create_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   *out = p;
   return DQ_OK;
 }
@@ -1491,6 +1528,67 @@ int64_t dq_plan_variant_bytes_per_row_x1000(const dq_plan* p, int32_t variant) {
   return b;
 }
 int32_t dq_plan_num_launches(const dq_plan* p) { return p ? p->launches_per_scan : 0; }
+
+dq_status dq_plan_create_time(const dq_plan* p, double* total_ms, double* pred_jit_ms) {
+  if (!p) return set_error(DQ_E_INVALID, "dq_plan_create_time: plan is NULL");
+  if (total_ms) *total_ms = p->create_ms;
+  if (pred_jit_ms) *pred_jit_ms = p->pred_jit_ms;
+  return DQ_OK;
+}
+
+int64_t dq_plan_explain(const dq_analyzer_spec* specs, int32_t n_specs, const dq_column_desc* schema, int32_t n_cols,
+                        const dq_pred_node* pred_pool, int32_t n_pred, const char* const* patterns, int32_t n_patterns,
+                        const dq_plan_options* opts, char* out, int64_t cap) {
+  if (n_specs < 0 || (n_specs > 0 && !specs)) return set_error(DQ_E_INVALID, "dq_plan_explain: bad specs");
+  if (n_cols < 0 || n_cols > kMaxCols || (n_cols > 0 && !schema))
+    return set_error(DQ_E_INVALID, "dq_plan_explain: bad schema (at most %d columns)", kMaxCols);
+  if (n_pred < 0 || (n_pred > 0 && !pred_pool)) return set_error(DQ_E_INVALID, "dq_plan_explain: bad predicate pool");
+  if (n_patterns < 0 || (n_patterns > 0 && !patterns)) return set_error(DQ_E_INVALID, "dq_plan_explain: bad patterns");
+  for (int32_t k = 0; k < n_patterns; ++k)
+    if (!patterns[k]) return set_error(DQ_E_INVALID, "dq_plan_explain: pattern %d is NULL", k);
+  for (int32_t c = 0; c < n_cols; ++c)
+    if (schema[c].type < DQ_TYPE_F64 || schema[c].type > DQ_TYPE_LARGE_UTF8)
+      return set_error(DQ_E_TYPE, "dq_plan_explain: column %d has unknown type %d", c, schema[c].type);
+  if (cap < 0 || (cap > 0 && !out)) return set_error(DQ_E_INVALID, "dq_plan_explain: bad output buffer");
+  std::unique_ptr<dq_plan> holder(new dq_plan());
+  dq_plan& plan = *holder;
+  plan.host_only = true;
+  plan.schema.assign(schema, schema + n_cols);
+  plan.specs.assign(specs, specs + n_specs);
+  for (int32_t k = 0; k < n_patterns; ++k) plan.patterns.emplace_back(patterns[k]);
+  if (opts) {
+    if (opts->struct_size < (int32_t)(2 * sizeof(int32_t))) return set_error(DQ_E_INVALID, "dq_plan_explain: bad options");
+    if (opts->pred_pass < DQ_PRED_PASS_AUTO || opts->pred_pass > DQ_PRED_PASS_COMPILED)
+      return set_error(DQ_E_INVALID, "dq_plan_explain: unknown pred_pass %d", opts->pred_pass);
+    plan.pred_pass = opts->pred_pass;
+  }
+  if (dq_status st = build_plan(&plan, pred_pool, n_pred)) return st;
+  std::string t;
+  char line[256];
+  std::snprintf(line, sizeof line, "plan: %d analyzers, %d columns, %d launches per scan\n", n_specs, n_cols,
+                plan.launches_per_scan);
+  t += line;
+  for (const auto& g : plan.groups) {
+    std::snprintf(line, sizeof line, "column pass: variant %d, %d task(s)\n", g.variant, g.count);
+    t += line;
+  }
+  std::snprintf(line, sizeof line, "pair pass: %zu pair(s), %zu workgroup task(s)\n", plan.pair_tasks.size(),
+                plan.pair_wgs.size());
+  t += line;
+  if (plan.has_pred) {
+    std::snprintf(line, sizeof line, "predicate program: %d instructions, %d roots, %d counters, %d bitmaps\n",
+                  plan.prog.n_instr, plan.prog.n_roots, plan.prog.n_counters, plan.prog.n_bitmaps);
+    t += line;
+    t += "predicate pass: " + plan.pred_jit_note + "\n";
+    if (!plan.pred_jit_src.empty()) t += "--- generated kernel source ---\n" + plan.pred_jit_src;
+  }
+  if (cap > 0) {
+    const size_t n = std::min((size_t)cap - 1, t.size());
+    std::memcpy(out, t.data(), n);
+    out[n] = '\0';
+  }
+  return (int64_t)t.size() + 1;
+}
 
 int32_t dq_plan_pred_compiled(const dq_plan* p, char* note, int32_t cap) {
   if (note && cap > 0) {

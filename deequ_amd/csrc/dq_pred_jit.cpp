@@ -13,13 +13,21 @@
 //   * an HLL-only ApproxCountDistinct (no `where`) on a program column is hashed from the same registers
 //     (XXH64 seed 42, the column pass's formulation, dq_hash.h), so that column is read from HBM once.
 // The source is generated from the PredProgram the interpreter would run, compiled once per distinct source
-// and device (hipRTC, in-process cache; comgr keeps its own on-disk cache), and launched in place of
-// dq_pred_scan.  A program the generator does not take (regex atoms, strings, > 8 columns) or a failed
-// compile keeps the interpreter and the column pass's HLL tasks.
+// and device target (hipRTC for the device's gcnArchName; a process cache that also remembers failures, and a
+// persistent code-object cache keyed by generator revision, target, hipRTC version and source), and launched in
+// place of dq_pred_scan.  A program the generator does not take (regex atoms, strings, > 8 columns) or a failed
+// compile keeps the interpreter and the column pass's HLL tasks -- unless the plan asked for DQ_PRED_PASS_COMPILED
+// (dq_plan_create_opts), which then fails instead.
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <chrono>
 #include <cinttypes>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -250,14 +258,18 @@ std::string pred_jit_source(const PredProgram& prog, const int32_t* col_kind, st
   // values and validity words one block ahead, per row group: v[i][j] of the next block is loaded as soon as
   // row group j of this block is done with it (same registers), so the next block's loads are in flight
   // while this block is evaluated and hashed
+  // the whole row offset goes in voffset (lane + block row + 64 j; the compiler moves the 64 j part into the
+  // instruction's immediate offset): the descriptor's range check covers voffset + immediate, not soffset, so
+  // a prefetch past the range's last row -- the next block of the range's last block -- reads 0 instead of
+  // the bytes after the column
   auto load_vals = [&](int i, const std::string& soff, const std::string& j, const std::string& dst) {
     const int k = col_kind[slot_col[i]];
     const std::string si = std::to_string(i);
     if (k == CK_I32)
-      return dst + " = (uint64_t)__builtin_amdgcn_raw_buffer_load_b32(vr" + si + ", lane * 4, (" + soff + " + 64 * " + j +
-             ") * 4, 2);\n";
-    return "{ const auto w2 = __builtin_amdgcn_raw_buffer_load_b64(vr" + si + ", lane * 8, (" + soff + " + 64 * " + j +
-           ") * 8, 2); " + dst + " = ((uint64_t)w2[1] << 32) | w2[0]; }\n";
+      return dst + " = (uint64_t)__builtin_amdgcn_raw_buffer_load_b32(vr" + si + ", (lane + " + soff + " + 64 * " + j +
+             ") * 4, 0, 2);\n";
+    return "{ const auto w2 = __builtin_amdgcn_raw_buffer_load_b64(vr" + si + ", (lane + " + soff + " + 64 * " + j +
+           ") * 8, 0, 2); " + dst + " = ((uint64_t)w2[1] << 32) | w2[0]; }\n";
   };
   for (int i = 0; i < ns; ++i) {
     const std::string si = std::to_string(i);
@@ -465,24 +477,15 @@ std::string pred_jit_source(const PredProgram& prog, const int32_t* col_kind, st
   return s;
 }
 
-// compile (or find) the kernel of `src` for the current device
-hipFunction_t pred_jit_compile(const std::string& src, std::string& err) {
-  static std::mutex mu;
-  static std::map<std::pair<int, std::string>, hipFunction_t> cache;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) {
-    err = "hipGetDevice failed";
-    return nullptr;
-  }
-  std::lock_guard<std::mutex> lock(mu);
-  auto it = cache.find({dev, src});
-  if (it != cache.end()) return it->second;
+// hipRTC: the code object of `src` for `arch` (host only; no device needed)
+bool pred_jit_compile_code(const std::string& src, const std::string& arch, std::vector<char>& code, std::string& err) {
   hiprtcProgram prog;
   if (hiprtcCreateProgram(&prog, src.c_str(), "dq_pred_jit.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
     err = "hiprtcCreateProgram failed";
-    return nullptr;
+    return false;
   }
-  const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
+  const std::string arch_opt = "--offload-arch=" + arch;
+  const char* opts[] = {arch_opt.c_str(), "-O3", "-std=c++17"};
   const hiprtcResult rc = hiprtcCompileProgram(prog, 3, opts);
   if (rc != HIPRTC_SUCCESS) {
     size_t n = 0;
@@ -491,25 +494,148 @@ hipFunction_t pred_jit_compile(const std::string& src, std::string& err) {
     if (n) hiprtcGetProgramLog(prog, &log[0]);
     err = "hiprtc: " + log.substr(0, 2000);
     hiprtcDestroyProgram(&prog);
-    return nullptr;
+    return false;
   }
   size_t n = 0;
   hiprtcGetCodeSize(prog, &n);
-  std::vector<char> code(n);
+  code.assign(n, 0);
   hiprtcGetCode(prog, code.data());
   hiprtcDestroyProgram(&prog);
-  hipModule_t mod;
-  if (hipModuleLoadData(&mod, code.data()) != hipSuccess) {
-    err = "hipModuleLoadData failed";
-    return nullptr;
+  if (n == 0) {
+    err = "hiprtc returned no code";
+    return false;
+  }
+  return true;
+}
+
+namespace {
+
+// generated-source revision: part of the disk-cache key, so code objects of an older generator are not reused
+constexpr const char* kJitRevision = "dq_pred_jit r4";
+
+uint64_t fnv1a64(const std::string& s, uint64_t h) {
+  for (unsigned char c : s) h = (h ^ c) * 0x100000001B3ull;
+  return h;
+}
+
+// the persistent code-object cache directory: $DQ_JIT_CACHE_DIR ("off" disables it), else
+// $XDG_CACHE_HOME/deequ_amd/jit, else $HOME/.cache/deequ_amd/jit; "" when none is usable
+std::string cache_dir() {
+  const char* d = std::getenv("DQ_JIT_CACHE_DIR");
+  std::string dir;
+  if (d && *d) {
+    if (std::strcmp(d, "off") == 0) return std::string();
+    dir = d;
+  } else if (const char* x = std::getenv("XDG_CACHE_HOME"); x && *x) {
+    dir = std::string(x) + "/deequ_amd/jit";
+  } else if (const char* h = std::getenv("HOME"); h && *h) {
+    dir = std::string(h) + "/.cache/deequ_amd/jit";
+  } else {
+    return std::string();
+  }
+  // mkdir -p (0700: the cache holds code this user loads)
+  for (size_t i = 1; i <= dir.size(); ++i)
+    if (i == dir.size() || dir[i] == '/') {
+      const std::string part = dir.substr(0, i);
+      if (mkdir(part.c_str(), 0700) != 0 && errno != EEXIST) return std::string();
+    }
+  return dir;
+}
+
+bool read_file(const std::string& path, std::vector<char>& out) {
+  FILE* f = std::fopen(path.c_str(), "rb");
+  if (!f) return false;
+  std::fseek(f, 0, SEEK_END);
+  const long n = std::ftell(f);
+  std::fseek(f, 0, SEEK_SET);
+  bool ok = n > 4;
+  if (ok) {
+    out.resize((size_t)n);
+    ok = std::fread(out.data(), 1, (size_t)n, f) == (size_t)n;
+  }
+  std::fclose(f);
+  // an AMDGPU code object is an ELF file
+  return ok && out[0] == 0x7F && out[1] == 'E' && out[2] == 'L' && out[3] == 'F';
+}
+
+void write_file_atomic(const std::string& path, const std::vector<char>& code) {
+  const std::string tmp = path + ".tmp." + std::to_string((long)getpid());
+  FILE* f = std::fopen(tmp.c_str(), "wb");
+  if (!f) return;
+  const bool ok = std::fwrite(code.data(), 1, code.size(), f) == code.size();
+  if (std::fclose(f) == 0 && ok) {
+    if (std::rename(tmp.c_str(), path.c_str()) == 0) return;
+  }
+  std::remove(tmp.c_str());
+}
+
+struct JitEntry {
+  hipFunction_t fn = nullptr;
+  std::string err;  // why there is no function (failures are cached too: a failing compile is not retried)
+};
+
+}  // namespace
+
+// the kernel of `src` for `device`: the process cache (successes and failures), else the disk cache, else a
+// hipRTC compile for the device's own target (gcnArchName, e.g. gfx950:sramecc+:xnack-)
+hipFunction_t pred_jit_get(const std::string& src, int device, std::string& note, double& ms) {
+  static std::mutex mu;
+  static std::map<std::pair<int, std::string>, JitEntry> cache;
+  const auto t0 = std::chrono::steady_clock::now();
+  auto done = [&](hipFunction_t fn) {
+    ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return fn;
+  };
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = cache.find({device, src});
+  if (it != cache.end()) {
+    note = it->second.fn ? "process cache" : it->second.err;
+    return done(it->second.fn);
+  }
+  JitEntry& e = cache[{device, src}];
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
+    e.err = note = "hipGetDeviceProperties failed";
+    return done(nullptr);
+  }
+  const std::string arch = prop.gcnArchName;
+  int rv_major = 0, rv_minor = 0;
+  hiprtcVersion(&rv_major, &rv_minor);
+  const std::string key = std::string(kJitRevision) + "\n" + arch + "\nhiprtc " + std::to_string(rv_major) + "." +
+                          std::to_string(rv_minor) + "\n" + src;
+  char name[80];
+  std::snprintf(name, sizeof name, "%016" PRIx64 "%016" PRIx64 ".co", fnv1a64(key, 0xCBF29CE484222325ull),
+                fnv1a64(key, 0x84222325CBF29CE4ull));
+  const std::string dir = cache_dir();
+  std::vector<char> code;
+  std::string origin = "disk cache";
+  bool have = !dir.empty() && read_file(dir + "/" + name, code);
+  hipModule_t mod = nullptr;
+  if (have && hipModuleLoadData(&mod, code.data()) != hipSuccess) {
+    have = false;  // a stale or damaged file: compile again (and replace it)
+    mod = nullptr;
+  }
+  if (!have) {
+    origin = "hiprtc";
+    std::string err;
+    if (!pred_jit_compile_code(src, arch, code, err)) {
+      e.err = note = err;
+      return done(nullptr);
+    }
+    if (hipModuleLoadData(&mod, code.data()) != hipSuccess) {
+      e.err = note = "hipModuleLoadData failed";
+      return done(nullptr);
+    }
+    if (!dir.empty()) write_file_atomic(dir + "/" + name, code);
   }
   hipFunction_t fn;
   if (hipModuleGetFunction(&fn, mod, "dq_pred_jit") != hipSuccess) {
-    err = "hipModuleGetFunction failed";
-    return nullptr;
+    e.err = note = "hipModuleGetFunction failed";
+    return done(nullptr);
   }
-  cache[{dev, src}] = fn;  // the module stays loaded for the process
-  return fn;
+  e.fn = fn;  // the module stays loaded for the process
+  note = origin;
+  return done(fn);
 }
 
 hipError_t pred_jit_launch(hipFunction_t fn, const PredJitArgs& a, int32_t nranges, hipStream_t st) {

@@ -34,7 +34,11 @@ struct PredJitHll {
 bool pred_jit_eligible(const PredProgram& prog, const int32_t* col_kind, int32_t ncols);
 std::string pred_jit_source(const PredProgram& prog, const int32_t* col_kind, std::vector<int32_t>& slot_col,
                             const std::vector<PredJitHll>& hll);
-hipFunction_t pred_jit_compile(const std::string& src, std::string& err);
+// hipRTC compile of `src` for `arch` (host only)
+bool pred_jit_compile_code(const std::string& src, const std::string& arch, std::vector<char>& code, std::string& err);
+// the loaded kernel of `src` on `device` (process cache, disk cache, or compiled); note: its origin, or why there
+// is none; ms: host time spent
+hipFunction_t pred_jit_get(const std::string& src, int device, std::string& note, double& ms);
 hipError_t pred_jit_launch(hipFunction_t fn, const PredJitArgs& a, int32_t nranges, hipStream_t st);
 
 }  // namespace dq

@@ -31,9 +31,13 @@ def _chunks(data) -> List[Table]:
 
 
 class ScanPlan:
-    """One dq_plan: the fused scan of a set of analyzers over tables with a fixed schema."""
+    """One dq_plan: the fused scan of a set of analyzers over tables with a fixed schema.
 
-    def __init__(self, analyzers: Sequence[Analyzer], schema, device: Optional[int] = None):
+    pred_pass (dq_plan_options.pred_pass): "auto" runs the predicate program as the kernel compiled for it
+    when the generator takes it, else the interpreter; "interpreter" forces the interpreter; "compiled"
+    requires the compiled kernel (plan creation fails with DQError DQ_E_UNSUPPORTED instead of falling back)."""
+
+    def __init__(self, analyzers: Sequence[Analyzer], schema, device: Optional[int] = None, pred_pass: str = "auto"):
         import torch
 
         self.analyzers = list(analyzers)
@@ -52,8 +56,9 @@ class ScanPlan:
         handle = ctypes.c_void_p()
         pats, npats = b.pool.patterns_ctypes()
         self._pats = pats
-        L.check(L.lib.dq_plan_create_ex(specs, len(self.analyzers), sch, len(self.columns), pool, npred, pats, npats,
-                                        device, ctypes.byref(handle)))
+        opts = L.PlanOptions(ctypes.sizeof(L.PlanOptions), L.PRED_PASS[pred_pass])
+        L.check(L.lib.dq_plan_create_opts(specs, len(self.analyzers), sch, len(self.columns), pool, npred, pats, npats,
+                                          ctypes.byref(opts), device, ctypes.byref(handle)))
         self.handle = handle
         self.chunk = 0
         with torch.cuda.device(device):
@@ -72,11 +77,18 @@ class ScanPlan:
         return L.lib.dq_plan_variant_bytes_per_row_x1000(self.handle, variant) / 1000.0
 
     def pred_compiled(self):
-        """(True, "") when the predicate pass runs as the kernel compiled for this plan's program, else (False,
-        the reason the interpreter runs it) -- dq_plan_pred_compiled."""
+        """(True, origin of the code object: "hiprtc" / "disk cache" / "process cache") when the predicate pass
+        runs as the kernel compiled for this plan's program, else (False, the reason the interpreter runs it)
+        -- dq_plan_pred_compiled."""
         buf = ctypes.create_string_buffer(2048)
         on = L.lib.dq_plan_pred_compiled(self.handle, buf, len(buf))
         return bool(on), buf.value.decode("utf-8", "replace")
+
+    def create_time(self):
+        """(host ms dq_plan_create spent, of which ms obtaining the compiled predicate kernel)."""
+        total, jit = ctypes.c_double(), ctypes.c_double()
+        L.check(L.lib.dq_plan_create_time(self.handle, ctypes.byref(total), ctypes.byref(jit)))
+        return total.value, jit.value
 
     def kernel_bytes_per_row(self, kernel: int) -> float:
         """Algorithmic bytes per row of timing kernel `kernel` (0 pred, 2 pair, 16+v variant v; no UTF8 data)."""
@@ -117,10 +129,31 @@ class ScanPlan:
             pass
 
 
-def scan_results(data, analyzers: Sequence[Analyzer]) -> List[L.State]:
+def explain(analyzers: Sequence[Analyzer], schema, pred_pass: str = "auto") -> str:
+    """The plan dq_plan_create would build for these analyzers, lowered on the host only (dq_plan_explain: no
+    GPU): launches per scan, column-pass variants, the predicate program and the generated predicate kernel."""
+    b = PlanBuilder(schema)
+    specs = (L.AnalyzerSpec * max(1, len(analyzers)))()
+    for i, a in enumerate(analyzers):
+        op, ca, cb, pr, wr = a._lower(b)
+        specs[i].op, specs[i].col_a, specs[i].col_b, specs[i].pred_root, specs[i].where_root = op, ca, cb, pr, wr
+    sch = b.schema_ctypes()
+    pool, npred = b.pool.as_ctypes()
+    pats, npats = b.pool.patterns_ctypes()
+    opts = L.PlanOptions(ctypes.sizeof(L.PlanOptions), L.PRED_PASS[pred_pass])
+    args = (specs, len(analyzers), sch, len(b.columns), pool, npred, pats, npats, ctypes.byref(opts))
+    n = L.lib.dq_plan_explain(*args, None, 0)
+    if n < 0:
+        L.check(int(n))
+    buf = ctypes.create_string_buffer(int(n))
+    L.lib.dq_plan_explain(*args, buf, n)
+    return buf.value.decode("utf-8", "replace")
+
+
+def scan_results(data, analyzers: Sequence[Analyzer], pred_pass: str = "auto") -> List[L.State]:
     """Fused scan of all chunks -> raw aggregation-result slot sets, one per analyzer."""
     chunks = _chunks(data)
-    plan = ScanPlan(analyzers, chunks[0].schema)
+    plan = ScanPlan(analyzers, chunks[0].schema, pred_pass=pred_pass)
     try:
         for t in chunks:
             plan.scan(t)
@@ -129,8 +162,8 @@ def scan_results(data, analyzers: Sequence[Analyzer]) -> List[L.State]:
         plan.close()
 
 
-def scan_states(data, analyzers: Sequence[Analyzer]) -> Dict[Analyzer, Optional[State]]:
-    res = scan_results(data, analyzers)
+def scan_states(data, analyzers: Sequence[Analyzer], pred_pass: str = "auto") -> Dict[Analyzer, Optional[State]]:
+    res = scan_results(data, analyzers, pred_pass)
     return {a: a._from_result(r) for a, r in zip(analyzers, res)}
 
 

@@ -163,6 +163,16 @@ def profile_analyzers(table: Table):
     return out
 
 
+def c3_analyzers(table: Table):
+    """BASELINE config C3: Size + ApproxCountDistinct of every column + four Compliance predicates on i0..i3."""
+    from .analyzers import ApproxCountDistinct, Compliance, Size
+
+    out = [Size()] + [ApproxCountDistinct(c) for c in table.columns]
+    out += [Compliance("p0", "i0 >= 0"), Compliance("p1", "`i1` IS NULL OR (`i1` >= 10.0 AND `i1` <= 1000.0)"),
+            Compliance("p2", "i2 < i3"), Compliance("p3", "COALESCE(i3, 0.0) >= 0")]
+    return out
+
+
 def _device_i64_column(name, values, nullable=False) -> Column:
     """An int64 device column from a torch int64 tensor (padded as dqscan.h requires, no nulls)."""
     n = values.numel()

@@ -31,7 +31,8 @@
 extern "C" {
 #endif
 
-#define DQ_ABI_VERSION 2  /* 2: dq_state.reserved[0] = integral flag + Sum / Mean int64 partials; ingestion, pool and state-array entry points */
+#define DQ_ABI_VERSION 3  /* 2: dq_state.reserved[0] = integral flag + Sum / Mean int64 partials; ingestion, pool and state-array entry points;
+                             3: dq_plan_create_opts (predicate-pass mode), dq_plan_create_time, dq_plan_explain */
 
 typedef int32_t dq_status;
 #define DQ_OK 0
@@ -243,6 +244,24 @@ dq_status dq_plan_create(const dq_analyzer_spec* specs, int32_t n_specs, const d
 dq_status dq_plan_create_ex(const dq_analyzer_spec* specs, int32_t n_specs, const dq_column_desc* schema,
                             int32_t n_cols, const dq_pred_node* pred_pool, int32_t n_pred,
                             const char* const* patterns, int32_t n_patterns, int32_t device, dq_plan** out);
+/* How the predicate pass of a plan runs (dq_plan_options.pred_pass).  AUTO: the kernel generated and
+ * compiled for the plan's program when the generator takes it (numeric comparisons; Spark's whole-stage
+ * code generation of the same expressions), else -- or when the compile fails -- the interpreter, with
+ * the reason in dq_plan_pred_compiled's note.  INTERPRETER: always the interpreter (the reference
+ * implementation the compiled kernel is tested against).  COMPILED: the compiled kernel or
+ * DQ_E_UNSUPPORTED from dq_plan_create_opts (reason in dq_last_error) -- no silent fallback. */
+enum dq_pred_pass { DQ_PRED_PASS_AUTO = 0, DQ_PRED_PASS_INTERPRETER = 1, DQ_PRED_PASS_COMPILED = 2 };
+typedef struct dq_plan_options {
+  int32_t struct_size;  /* sizeof(dq_plan_options) as the caller was compiled (fields past it: defaults) */
+  int32_t pred_pass;    /* enum dq_pred_pass */
+  int32_t reserved[6];  /* 0 */
+} dq_plan_options;
+/* As dq_plan_create_ex with options (NULL = all defaults).  Replaces AnalysisRunner.runScanningAnalyzers'
+ * plan step (AnalysisRunner.scala:279-326): one plan per run, created before the first chunk. */
+dq_status dq_plan_create_opts(const dq_analyzer_spec* specs, int32_t n_specs, const dq_column_desc* schema,
+                              int32_t n_cols, const dq_pred_node* pred_pool, int32_t n_pred,
+                              const char* const* patterns, int32_t n_patterns, const dq_plan_options* opts,
+                              int32_t device, dq_plan** out);
 /* Compile a pattern without a GPU: DFA size (or the DQ_E_UNSUPPORTED reason in dq_last_error), and
  * the host walk of the same DFA over n values (UTF-8 bytes data[offsets[r] .. offsets[r + 1]))
  * for tests of the compiler; out[r] = 1 iff the value matches under `mode` (NULLs are the caller's). */
@@ -301,9 +320,21 @@ int64_t dq_plan_variant_bytes_per_row_x1000(const dq_plan* plan, int32_t variant
 int64_t dq_plan_kernel_bytes_per_row_x1000(const dq_plan* plan, int32_t kernel);
 /* 1 when the plan's predicate pass runs as a kernel compiled for its program (the Compliance / where
  * programs of numeric comparisons: whole-stage code generation as Spark does for the same expressions,
- * hipRTC for gfx950), 0 when the interpreter runs it (or the plan has no predicates); note (optional,
- * cap bytes incl. the terminator) receives the reason the interpreter runs. */
+ * hipRTC for the device's gfx950 target), 0 when the interpreter runs it (or the plan has no predicates);
+ * note (optional, cap bytes incl. the terminator) receives the reason the interpreter runs, or -- when
+ * compiled -- where the code object came from ("hiprtc", "disk cache", "process cache"). */
 int32_t dq_plan_pred_compiled(const dq_plan* plan, char* note, int32_t cap);
+/* EXPLAIN of the plan dq_plan_create_opts would build, on the host only (no device, no allocation, no
+ * compile): the launches per scan, the column-pass variants, the pair pass, the predicate program and -- when
+ * the predicate pass would be compiled -- the generated kernel source.  Writes at most cap bytes (incl. the
+ * terminator) to out and returns the full text's size incl. the terminator (call with cap 0 to size the
+ * buffer), or a negative dq_status (planning errors as dq_plan_create reports them). */
+int64_t dq_plan_explain(const dq_analyzer_spec* specs, int32_t n_specs, const dq_column_desc* schema, int32_t n_cols,
+                        const dq_pred_node* pred_pool, int32_t n_pred, const char* const* patterns, int32_t n_patterns,
+                        const dq_plan_options* opts, char* out, int64_t cap);
+/* Host wall time dq_plan_create* spent on the plan (ms), and the part of it spent obtaining the compiled
+ * predicate kernel (hipRTC compile, or a code-object cache lookup); 0 for the latter without one. */
+dq_status dq_plan_create_time(const dq_plan* plan, double* total_ms, double* pred_jit_ms);
 
 /* Grouping analyzers (analyzers/GroupingAnalyzers.scala:44-82, 118-138): the frequencies
  * SELECT cols, COUNT(*) FROM data WHERE cols IS NOT NULL GROUP BY cols on the GPU (sort-based), and

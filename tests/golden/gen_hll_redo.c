@@ -8,6 +8,7 @@
  *
  *   gen_hll_redo i64 <start> <count> <want>        int64 values start, start + 1, ...
  *   gen_hll_redo f64 <start> <count> <want>        finite doubles with bit patterns mix(k)
+ *   gen_hll_redo i32 <start> <count> <want>        int32 values (int32_t)k, k = start, start + 1, ... (hashInt)
  *   gen_hll_redo str <len> <start> <count> <want>  strings of <len> bytes from counter k
  * Prints one hit per line (the value, or the string as hex).
  */
@@ -36,7 +37,16 @@ static void make_str(uint64_t k, int len, uint8_t* out) {
 int main(int argc, char** argv) {
   if (argc < 5) return 2;
   int found = 0;
-  if (!strcmp(argv[1], "i64") || !strcmp(argv[1], "f64")) {
+  if (!strcmp(argv[1], "i32")) {
+    const uint64_t start = strtoull(argv[2], 0, 0), count = strtoull(argv[3], 0, 0);
+    const int want = atoi(argv[4]);
+    for (uint64_t k = start; k < start + count && found < want; ++k) {
+      if (redo(dqo_xxh64_int((int32_t)(uint32_t)k, 42))) {
+        printf("%d\n", (int32_t)(uint32_t)k);
+        ++found;
+      }
+    }
+  } else if (!strcmp(argv[1], "i64") || !strcmp(argv[1], "f64")) {
     const int is_f = argv[1][0] == 'f';
     const uint64_t start = strtoull(argv[2], 0, 0), count = strtoull(argv[3], 0, 0);
     const int want = atoi(argv[4]);

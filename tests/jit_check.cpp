@@ -1,9 +1,7 @@
 // jit_check.cpp -- host harness for tests/test_pred_jit_source.py: generates the compiled predicate pass's
 // source (deequ_amd/csrc/dq_pred_jit.cpp) for a few programs and compiles each with hipRTC for gfx950, as
 // dq_plan_create does -- without loading it (no GPU needed).  Usage: jit_check OUTDIR; prints one line per
-// program: "<name> <eligible> <compile rc> <code bytes>" and writes OUTDIR/<name>.co.
-#include <hip/hiprtc.h>
-
+// program: "<name> <eligible> <compile rc (0 ok)> <code bytes>" and writes OUTDIR/<name>.co.
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -69,27 +67,19 @@ int run(const char* outdir, const char* name, const PredProgram& prog, const int
   int rc = -1;
   size_t bytes = 0;
   if (!src.empty()) {
-    hiprtcProgram p;
-    hiprtcCreateProgram(&p, src.c_str(), "dq_pred_jit.hip", 0, nullptr, nullptr);
-    const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
-    rc = (int)hiprtcCompileProgram(p, 3, opts);
+    std::vector<char> code;
+    std::string err;
+    rc = pred_jit_compile_code(src, "gfx950", code, err) ? 0 : 1;
     if (rc != 0) {
-      size_t n = 0;
-      hiprtcGetProgramLogSize(p, &n);
-      std::string log(n, '\0');
-      hiprtcGetProgramLog(p, &log[0]);
-      std::fprintf(stderr, "%s: %s\n", name, log.substr(0, 2000).c_str());
+      std::fprintf(stderr, "%s: %s\n", name, err.c_str());
     } else {
-      hiprtcGetCodeSize(p, &bytes);
-      std::vector<char> code(bytes);
-      hiprtcGetCode(p, code.data());
+      bytes = code.size();
       const std::string path = std::string(outdir) + "/" + name + ".co";
       if (FILE* f = std::fopen(path.c_str(), "wb")) {
         std::fwrite(code.data(), 1, bytes, f);
         std::fclose(f);
       }
     }
-    hiprtcDestroyProgram(&p);
   }
   std::printf("%s %d %d %zu\n", name, eligible ? 1 : 0, rc, bytes);
   return 0;

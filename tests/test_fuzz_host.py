@@ -147,3 +147,86 @@ def test_arrow_import_fuzz(L, fmt, n, off, null_count, present, nbuf):
     assert rc in (L.DQ_OK, L.DQ_E_UNSUPPORTED, L.DQ_E_INVALID), rc
     if rc == L.DQ_OK:
         assert out.n_rows == n and 0 <= out.validity_bit < 8
+
+
+# ------------------------------------------------------------------------------------------------------
+# random predicate programs through the planner and the predicate-kernel generator (dq_plan_explain: host
+# only -- the plan is lowered and, for a numeric program, the compiled pass's kernel source generated from it,
+# the path dq_plan_create takes before hipRTC; Check.scala:670-871 builds the strings)
+# ------------------------------------------------------------------------------------------------------
+_COLS = [("a", "f64"), ("b", "i64"), ("c", "i32"), ("s", "utf8")]
+_NUM = ["a", "b", "c", "`a`", "`b`", "`c`"]
+_LITS = ["0", "1", "-3", "2.5", "-0.0", "1e3", "1.0e-2", "9223372036854775807", "-9223372036854775808",
+         "0.000000000000000000001", "NULL"]
+_OPS = [">", ">=", "<", "<=", "=", "==", "!=", "<>"]
+
+
+def _atom():
+    num = st.sampled_from(_NUM)
+    lit = st.sampled_from(_LITS)
+    return st.one_of(
+        st.builds(lambda x, o, y: f"{x} {o} {y}", num, st.sampled_from(_OPS), st.one_of(num, lit)),
+        st.builds(lambda x, o, y: f"{y} {o} {x}", num, st.sampled_from(_OPS), lit),
+        st.builds(lambda x, n: f"{x} IS {n}NULL", num, st.sampled_from(["", "NOT "])),
+        st.builds(lambda x, d, o, y: f"COALESCE({x}, {d}) {o} {y}", num, st.sampled_from(["0", "1.5", "-2"]),
+                  st.sampled_from(_OPS), lit),
+        st.sampled_from(["TRUE", "FALSE", "NULL", "1 < 2", "s = 'x'", "s IN ('a', 'b')", "s IS NULL"]))
+
+
+_PRED = st.recursive(_atom(), lambda e: st.one_of(
+    st.builds(lambda x, y: f"({x}) AND ({y})", e, e), st.builds(lambda x, y: f"({x}) OR ({y})", e, e),
+    st.builds(lambda x: f"NOT ({x})", e)), max_leaves=10)
+
+
+@SETTINGS
+@given(st.lists(_PRED, min_size=1, max_size=6), st.lists(st.booleans(), min_size=6, max_size=6),
+       st.sampled_from([0, 1, 2]))
+def test_pred_programs_through_planner_and_generator(L, preds, hll, pred_pass):
+    names = (ctypes.c_char_p * 4)(*[n.encode() for n, _ in _COLS])
+    tcode = {"f64": L.TYPE_F64, "i64": L.TYPE_I64, "i32": L.TYPE_I32, "utf8": L.TYPE_UTF8}
+    types = (ctypes.c_int32 * 4)(*[tcode[t] for _, t in _COLS])
+    h = ctypes.c_void_p()
+    assert L.lib.dq_pred_pool_create(names, types, 4, ctypes.byref(h)) == L.DQ_OK
+    try:
+        roots = []
+        for p in preds:
+            r = ctypes.c_int32(-1)
+            if L.lib.dq_pred_pool_add(h, p.encode(), ctypes.byref(r)) == L.DQ_OK:
+                roots.append((p, r.value))
+        if not roots:
+            return
+        specs = []
+        for i, (_, r) in enumerate(roots):
+            # Compliance of every accepted root; every second one also as a `where` of a Sum; fused-HLL
+            # candidates: ApproxCountDistinct without `where` on the numeric columns
+            specs.append((L.OP_COMPLIANCE, -1, -1, r, -1))
+            if i % 2:
+                specs.append((L.OP_SUM, 1, -1, -1, r))
+        for c in range(3):
+            if hll[c]:
+                specs.append((L.OP_APPROX_COUNT_DISTINCT, c, -1, -1, -1))
+        arr = (L.AnalyzerSpec * len(specs))(*[L.AnalyzerSpec(*x) for x in specs])
+        sch = (L.ColumnDesc * 4)(*[L.ColumnDesc(tcode[t], 1) for _, t in _COLS])
+        nodes = L.lib.dq_pred_pool_nodes(h)
+        npred = L.lib.dq_pred_pool_size(h)
+        npat = L.lib.dq_pred_pool_num_patterns(h)
+        pats = L.lib.dq_pred_pool_patterns(h)
+        opts = L.PlanOptions(ctypes.sizeof(L.PlanOptions), pred_pass)
+        args = (arr, len(specs), sch, 4, nodes, npred, pats, npat, ctypes.byref(opts))
+        n = L.lib.dq_plan_explain(*args, None, 0)
+        if n < 0:  # planning limits (counters, roots, nesting) or a required compile the program cannot have
+            assert n in (L.DQ_E_UNSUPPORTED, L.DQ_E_INVALID), (preds, n)
+            assert n == L.DQ_E_UNSUPPORTED or L.lib.dq_last_error()
+            return
+        buf = ctypes.create_string_buffer(int(n))
+        assert L.lib.dq_plan_explain(*args, buf, n) == n
+        text = buf.value.decode()
+        assert len(text) == n - 1 and text.startswith("plan: ")
+        uses_string = any("s " in p or "s=" in p for p, _ in roots)
+        if "--- generated kernel source ---" in text:
+            assert pred_pass != 1 and "dq_pred_jit" in text and "__global__" in text
+            assert not uses_string
+        elif pred_pass == 2:
+            raise AssertionError(("compiled pass required but no kernel generated", preds, text))
+    finally:
+        L.lib.dq_pred_pool_destroy(h)

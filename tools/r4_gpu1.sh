@@ -1,0 +1,8 @@
+#!/bin/bash
+# round-4 first GPU call: issue-rate probe, counter list, the compiled-predicate-pass parity tests
+cd "${GRAFT_REPO_ROOT:-$(pwd)}"; mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 120 ./tools/micro/issue_probe > gpurun_out/r4a_issue_probe.txt 2>&1 || exit $?
+timeout -k 10 60 rocprofv3 -L > gpurun_out/r4a_counters.txt 2>&1
+timeout -k 10 900 python -u -m pytest tests/test_pred_jit_gpu.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/r4a_pytest_jit.log 2>&1
+rc=$?; tail -5 gpurun_out/r4a_pytest_jit.log; exit $rc
