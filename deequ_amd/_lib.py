@@ -218,6 +218,9 @@ def _load():
     L.dq_approx_quantiles.restype = c.c_int32
     L.dq_approx_quantiles.argtypes = [c.c_int32, P(ColumnView), P(c.c_int64), c.c_int32, P(c.c_double), c.c_int32,
                                       c.c_double, c.c_int32, c.c_void_p, P(c.c_double), P(c.c_int64)]
+    L.dq_quantile_digest.restype = c.c_int32
+    L.dq_quantile_digest.argtypes = [c.c_int32, P(ColumnView), P(c.c_int64), c.c_int32, c.c_double, c.c_int32,
+                                     c.c_void_p, P(c.c_double), P(c.c_int64), c.c_int64, P(c.c_int64), P(c.c_int64)]
     L.dq_freq_top.restype = c.c_int32
     L.dq_freq_top.argtypes = [c.c_void_p, c.c_int32, P(c.c_uint64), P(c.c_int64), P(c.c_uint64), P(c.c_int32)]
     L.dq_freq_destroy.restype = None
@@ -281,7 +284,7 @@ EXPORTED = [
     "dq_arrow_import", "dq_uploader_create", "dq_upload", "dq_upload_fence", "dq_upload_release", "dq_upload_sync",
     "dq_uploader_destroy",
     "dq_plan_set_stream", "dq_freq_build", "dq_freq_merge", "dq_freq_summarize", "dq_freq_num_groups",
-    "dq_freq_export", "dq_freq_destroy", "dq_mutual_information", "dq_approx_quantiles", "dq_freq_top", "dq_scan", "dq_finish",
+    "dq_freq_export", "dq_freq_destroy", "dq_mutual_information", "dq_approx_quantiles", "dq_quantile_digest", "dq_freq_top", "dq_scan", "dq_finish",
     "dq_plan_reset", "dq_plan_destroy", "dq_plan_bytes_per_row_x1000", "dq_plan_num_launches",
     "dq_plan_enable_timing", "dq_plan_kernel_time", "dq_plan_variant_bytes_per_row_x1000",
     "dq_plan_kernel_bytes_per_row_x1000", "dq_plan_pred_compiled",

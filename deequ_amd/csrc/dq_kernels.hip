@@ -247,8 +247,10 @@ struct RangeBits {
 // ------------------------------------------------------------------------------------------
 
 // selected-row masks of the 8 lane groups [base + 64 j, + 64) of a wave's block (base a multiple of
-// 64; `full`: the whole block lies below row1).  All branches are wave-uniform.
-__device__ __forceinline__ void block_masks(const uint32_t* validity, const uint32_t* mask, int64_t base, int64_t row1,
+// 64; rem = row1 - base, <= 0 for a wave past the range's end; `full`: the whole block lies below row1).
+// All branches are wave-uniform, and every comparison is a 32-bit one on rem: the scalar unit has no 64-bit
+// ordered compare, so 64-bit row comparisons became VALU compares of SGPR pairs.
+__device__ __forceinline__ void block_masks(const uint32_t* validity, const uint32_t* mask, int64_t base, int32_t rem,
                                             bool full, uint64_t (&m)[8]) {
   const int64_t w0 = base >> 5;
   if (full) {
@@ -267,67 +269,90 @@ __device__ __forceinline__ void block_masks(const uint32_t* validity, const uint
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const int64_t r = base + 64 * j, w = w0 + 2 * j;
+    const int32_t left = rem - 64 * j;  // rows of group j below row1
+    const int64_t w = w0 + 2 * j;
     uint64_t x = 0;
-    if (r < row1) {
-      const bool two = r + 32 < row1;  // the second dword holds rows below row1
+    if (left > 0) {
+      const bool two = left > 32;  // the second dword holds rows below row1
       x = ~0ull;
       if (validity) x = ((uint64_t)(two ? ((const_u32s)validity)[w + 1] : 0u) << 32) | ((const_u32s)validity)[w];
       if (mask) x &= ((uint64_t)(two ? ((const_u32s)mask)[w + 1] : 0u) << 32) | ((const_u32s)mask)[w];
-      if (r + 64 > row1) x &= (1ull << (row1 - r)) - 1ull;
+      if (left < 64) x &= (1ull << left) - 1ull;
     }
     m[j] = x;
   }
 }
 
 
-// Per-lane streaming moments of a numeric column (lane l of a wave owns rows base + 64 j + l).  Values
-// are accumulated as shifted sums sd = sum(x - shift), sdd = sum((x - shift)^2), k under the selection
-// mask -- exec-masked updates, so an unselected row costs no VALU work -- and merged into the lane's
-// running (n, mean, m2) with Chan's formula (StandardDeviation.scala:37-44) every kChunkBlocks blocks:
-// one reciprocal per 64 values.  shift is the lane's running mean, so the shifted sums stay small;
-// a lane with nothing yet takes its first selected value.
-constexpr int kChunkBlocks = 8;
-
+// Moments of a numeric column (lane l of a wave owns rows base + 64 j + l) as shifted sums over the whole
+// workgroup range: sd = sum(x - shift), sdd = sum((x - shift)^2) per lane under the selection mask --
+// exec-masked updates, so an unselected row costs no VALU work -- with ONE shift for the range (wave-uniform,
+// in SGPRs): the mean of the range's first 64-row group holding finite selected values.  The selected-row
+// count is a popcount of the masks (scalar), so no lane keeps a count, and nothing is merged inside the loop;
+// at the range's end the wave's sums give (n, mean = shift + S1 / n, m2 = S2 - S1^2 / n), which merge across
+// waves / ranges / chunks with StandardDeviationState.sum's algebra (Chan, StandardDeviation.scala:37-44).
+// Accuracy: the range's first group is part of the range, so n (shift - mean)^2 <= (rows / 64) m2 for any
+// data and the cancellation in m2 costs at most ~1e-13 relative at 2^16-row ranges (the Correlation pass
+// uses the same shifts: tests/test_pair_lane.py drift test; full-scale C2 / C5 in tests/fullscale_parity.py).
 struct LaneMoments {
-  double shift, sd, sdd;
-  int32_t k;
+  double sd, sdd;
   int64_t is;  // wrapping int64 sum (integral kinds; Spark Sum on LongType)
 };
 
-// v_rcp_f64 + one Newton step: within an ulp of 1/a (a is a positive count; deterministic)
-__device__ __forceinline__ double rcp_nr(double a) {
-  const double r = __builtin_amdgcn_rcp(a);
-  return __builtin_fma(r, __builtin_fma(-a, r, 1.0), r);
+// this lane's value of row r of a range (buffer resource over the range's values; rows past it read 0)
+template <int KIND>
+__device__ __forceinline__ double range_value(__amdgpu_buffer_rsrc_t vr, int64_t rel) {
+  if constexpr (KIND == CK_I32) return (double)(int32_t)__builtin_amdgcn_raw_buffer_load_b32(vr, (int)(rel * 4), 0, 0);
+  const auto w2 = __builtin_amdgcn_raw_buffer_load_b64(vr, (int)(rel * 8), 0, 0);
+  if constexpr (KIND == CK_F64) return __builtin_bit_cast(double, ((uint64_t)w2[1] << 32) | w2[0]);
+  return __builtin_fma((double)(int32_t)w2[1], 4294967296.0, (double)w2[0]);
+}
+__device__ __forceinline__ double wave_uniform(double v) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b), hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ double wave_sum_f64(double v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+  return v;
+}
+__device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v = (int64_t)((uint64_t)v + (uint64_t)__shfl_xor(v, m));
+  return v;
 }
 
+// the range's shift: mean of its first 64-row group with finite selected values (0 if none); groups with no
+// selected row are skipped on their bitmap words alone
 template <int KIND>
-__device__ __forceinline__ void moments_flush(ColStats& s, LaneMoments& a) {
-  if (a.k != 0) {
-    const double kd = (double)a.k;
-    const double n2 = s.n + kd;
-    const double q = a.sd * rcp_nr(n2);
-    s.mean = a.shift + q;
-    s.m2 = s.m2 + __builtin_fma(-a.sd, q, a.sdd);
-    s.n = n2;
-    s.count += a.k;
-    if (KIND == CK_F64) s.sum += __builtin_fma(kd, a.shift, a.sd);
-    else s.isum = (int64_t)((uint64_t)s.isum + (uint64_t)a.is);
+__device__ double range_shift_of(__amdgpu_buffer_rsrc_t vr, const uint32_t* validity, const uint32_t* mask, int64_t row0,
+                                 int64_t row1, int lane) {
+  for (int64_t r = row0; r < row1; r += 64) {
+    uint64_t sel = ~0ull;
+    {
+      const int64_t w = r >> 5;
+      const bool two = r + 32 < row1;
+      if (validity) sel = ((uint64_t)(two ? ((const_u32s)validity)[w + 1] : 0u) << 32) | ((const_u32s)validity)[w];
+      if (mask) sel &= ((uint64_t)(two ? ((const_u32s)mask)[w + 1] : 0u) << 32) | ((const_u32s)mask)[w];
+      if (r + 64 > row1) sel &= (1ull << (row1 - r)) - 1ull;
+    }
+    if (sel == 0) continue;
+    const double x = range_value<KIND>(vr, r - row0 + lane);
+    const uint64_t fm = __builtin_amdgcn_ballot_w64(__builtin_isfinite(x)) & sel;
+    if (fm != 0) return wave_uniform(wave_sum_f64(lane_bit(fm) ? x : 0.0) / (double)__builtin_popcountll(fm));
   }
-  a.shift = s.mean;
-  a.sd = 0.0;
-  a.sdd = 0.0;
-  a.k = 0;
-  a.is = 0;
+  return 0.0;
 }
 
 // Exec-masked moment / min / max update of one value (inline asm so the accumulators are plain
 // read-write operands: a C++ `if` on a lane mask makes the compiler copy every accumulator into
 // its phi register before the branch).  exec &= ma for the moments, exec &= mb for min / max
 // (MINMAX_SEP: mb excludes NaN rows), then restored; the outer exec is respected (s_and_saveexec).
+// The shift is an SGPR pair (wave-uniform).
 template <bool INTEGRAL, bool MINMAX_SEP>
 __device__ __forceinline__ void masked_moments(LaneMoments& a, double& lo, double& hi, double x, uint64_t b,
-                                               uint64_t ma, uint64_t mb) {
+                                               double shift, uint64_t ma, uint64_t mb) {
   double d;
   uint64_t save;
   if constexpr (INTEGRAL) {
@@ -335,86 +360,54 @@ __device__ __forceinline__ void masked_moments(LaneMoments& a, double& lo, doubl
         "s_and_saveexec_b64 %[save], %[ma]\n\t"
         "v_add_f64 %[d], %[x], -%[sh]\n\t"
         "v_lshl_add_u64 %[is], %[b], 0, %[is]\n\t"
-        "v_add_u32 %[k], 1, %[k]\n\t"
-        "v_add_f64 %[sd], %[sd], %[d]\n\t"
-        "v_fma_f64 %[sdd], %[d], %[d], %[sdd]\n\t"
         "v_min_f64 %[lo], %[lo], %[x]\n\t"
         "v_max_f64 %[hi], %[hi], %[x]\n\t"
+        "v_add_f64 %[sd], %[sd], %[d]\n\t"
+        "v_fma_f64 %[sdd], %[d], %[d], %[sdd]\n\t"
         "s_mov_b64 exec, %[save]"
-        : [sd] "+v"(a.sd), [sdd] "+v"(a.sdd), [k] "+v"(a.k), [is] "+v"(a.is), [lo] "+v"(lo), [hi] "+v"(hi),
-          [d] "=&v"(d), [save] "=&s"(save)
-        : [x] "v"(x), [sh] "v"(a.shift), [b] "v"(b), [ma] "s"(ma)
+        : [sd] "+v"(a.sd), [sdd] "+v"(a.sdd), [is] "+v"(a.is), [lo] "+v"(lo), [hi] "+v"(hi), [d] "=&v"(d),
+          [save] "=&s"(save)
+        : [x] "v"(x), [sh] "s"(shift), [b] "v"(b), [ma] "s"(ma)
         : "scc");
   } else if constexpr (!MINMAX_SEP) {
     asm volatile(
         "s_and_saveexec_b64 %[save], %[ma]\n\t"
         "v_add_f64 %[d], %[x], -%[sh]\n\t"
-        "v_add_u32 %[k], 1, %[k]\n\t"
         "v_min_f64 %[lo], %[lo], %[x]\n\t"
         "v_max_f64 %[hi], %[hi], %[x]\n\t"
         "v_add_f64 %[sd], %[sd], %[d]\n\t"
         "v_fma_f64 %[sdd], %[d], %[d], %[sdd]\n\t"
         "s_mov_b64 exec, %[save]"
-        : [sd] "+v"(a.sd), [sdd] "+v"(a.sdd), [k] "+v"(a.k), [lo] "+v"(lo), [hi] "+v"(hi), [d] "=&v"(d),
-          [save] "=&s"(save)
-        : [x] "v"(x), [sh] "v"(a.shift), [ma] "s"(ma)
+        : [sd] "+v"(a.sd), [sdd] "+v"(a.sdd), [lo] "+v"(lo), [hi] "+v"(hi), [d] "=&v"(d), [save] "=&s"(save)
+        : [x] "v"(x), [sh] "s"(shift), [ma] "s"(ma)
         : "scc");
   } else {
     asm volatile(
         "s_and_saveexec_b64 %[save], %[ma]\n\t"
         "v_add_f64 %[d], %[x], -%[sh]\n\t"
-        "v_add_u32 %[k], 1, %[k]\n\t"
         "v_add_f64 %[sd], %[sd], %[d]\n\t"
         "v_fma_f64 %[sdd], %[d], %[d], %[sdd]\n\t"
         "s_and_b64 exec, %[save], %[mb]\n\t"
         "v_min_f64 %[lo], %[lo], %[x]\n\t"
         "v_max_f64 %[hi], %[hi], %[x]\n\t"
         "s_mov_b64 exec, %[save]"
-        : [sd] "+v"(a.sd), [sdd] "+v"(a.sdd), [k] "+v"(a.k), [lo] "+v"(lo), [hi] "+v"(hi), [d] "=&v"(d),
-          [save] "=&s"(save)
-        : [x] "v"(x), [sh] "v"(a.shift), [ma] "s"(ma), [mb] "s"(mb)
+        : [sd] "+v"(a.sd), [sdd] "+v"(a.sdd), [lo] "+v"(lo), [hi] "+v"(hi), [d] "=&v"(d), [save] "=&s"(save)
+        : [x] "v"(x), [sh] "s"(shift), [ma] "s"(ma), [mb] "s"(mb)
         : "scc");
   }
 }
 
-// One 512-row block of a wave: x[j] the lane's value of row group j as a double, bits[j] its raw
-// 64-bit pattern (i32: sign-extended), m[j] the selection masks, nanm[j] the selected NaN rows (F64).
-// NANS (the block holds a selected NaN or +-inf, rare): NaN rows hash as the canonical NaN
-// (doubleToLongBits) and stay out of min / max (Spark orders NaN above every value; the caller counts
-// them); +-inf rows (mm = m without them) stay out of the shifted moments -- x - shift would be inf - inf
-// for the rest of the lane -- and are counted by the caller: dq_finish adds them back into the sum
-// (Spark's sequential sum is then +-inf, or NaN with both signs) and the moments become NaN.
-template <int KIND, bool STATS, bool HLL, bool NANS>
+// One 512-row block of a wave: x[j] the lane's value of row group j as a double, bits[j] its raw 64-bit
+// pattern (i32: sign-extended), m[j] the selection masks (every selected value finite: a block with a
+// selected NaN / +-inf takes the caller's rolled path).
+template <int KIND, bool STATS, bool HLL>
 __device__ __forceinline__ void numeric_block(const double (&x)[8], const uint64_t (&bits)[8], const uint64_t (&m)[8],
-                                              const uint64_t (&mm)[8], const uint64_t (&nanm)[8], ColStats& s,
-                                              LaneMoments& a, int32_t* regs, int32_t& qmin, bool& started) {
-  if (STATS) {
-    // still-empty lanes take the block's first selected value as their shift (wave-uniform branch); once no
-    // lane is empty at a block's start the check is skipped for the rest of the range (`started`, uniform).
-    // Not for fp64: its loop is at the 6-wave register budget, and the flag spilled it (1.47 -> 2.16 ms).
-    if (KIND == CK_F64 || !started) {
-      if (__builtin_amdgcn_ballot_w64(s.n == 0.0 && a.k == 0) != 0) {
-        double first = a.shift;
-#pragma unroll
-        for (int j = 7; j >= 0; --j) first = lane_bit(mm[j]) ? x[j] : first;
-        if (s.n == 0.0 && a.k == 0) a.shift = first;
-      } else {
-        started = true;
-      }
-    }
-  }
+                                              double shift, ColStats& s, LaneMoments& a, int32_t* regs, int32_t& qmin) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    if (STATS) masked_moments<KIND != CK_F64, NANS>(a, s.fmin, s.fmax, x[j], bits[j], mm[j], m[j] & ~nanm[j]);
+    if (STATS) masked_moments<KIND != CK_F64, false>(a, s.fmin, s.fmax, x[j], bits[j], shift, m[j], m[j]);
     if (HLL) {
-      HllKey key;
-      if (KIND == CK_I32) {
-        key = hll_key_int((uint32_t)bits[j]);
-      } else {
-        uint64_t b = bits[j];
-        if (NANS) b = lane_bit(nanm[j]) ? 0x7FF8000000000000ull : b;
-        key = hll_key_long(b);
-      }
+      const HllKey key = KIND == CK_I32 ? hll_key_int((uint32_t)bits[j]) : hll_key_long(bits[j]);
       qmin = min(qmin, key.q);
       if (lane_bit(m[j])) atomicMax(reinterpret_cast<int32_t*>(reinterpret_cast<char*>(regs) + key.addr), key.q);
     }
@@ -425,11 +418,7 @@ __device__ __forceinline__ void numeric_block(const double (&x)[8], const uint64
     if (__builtin_amdgcn_ballot_w64(qmin < 0) != 0) {
 #pragma unroll 1
       for (int j = 0; j < 8; ++j) {
-        if (lane_bit(m[j])) {
-          uint64_t b = bits[j];
-          if (KIND == CK_F64 && x[j] != x[j]) b = 0x7FF8000000000000ull;
-          hll_update(regs, KIND == CK_I32 ? xxh64_int((uint32_t)b) : xxh64_long(b));
-        }
+        if (lane_bit(m[j])) hll_update(regs, KIND == CK_I32 ? xxh64_int((uint32_t)bits[j]) : xxh64_long(bits[j]));
       }
       qmin = 0;
     }
@@ -446,70 +435,70 @@ __device__ void numeric_range(const void* values, const uint32_t* validity, cons
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const T* v = reinterpret_cast<const T*>(values);
-  // values of [row0, row1) through a bounds-checked buffer resource: lane offset in one VGPR, the
-  // row-group offset in an SGPR, and rows past row1 read 0 (they are masked out) -- no address math
-  // per row.  dq_scan bounds a chunk to < 2^31 rows, so a range is < 2^31 bytes.
+  // values of [row0, row1) through a bounds-checked buffer resource: the row offset in voffset (lane + block
+  // row; the row group's 64 j folds into the instruction's immediate offset) -- the descriptor's range check
+  // covers voffset + immediate, so rows past row1 read 0 (they are masked out) and nothing past the column is
+  // touched.  dq_scan bounds a chunk to < 2^31 rows, so a range is < 2^31 bytes.
   const __amdgpu_buffer_rsrc_t vr = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<T*>(v + row0), (short)0, (int)((row1 - row0) * (int64_t)sizeof(T)), 0x00020000);
   // counts of selected NaN / +inf / -inf values, kept by lane 0 in VGPRs (as wave-uniform SGPR
   // counters they pushed the loop's SGPR pressure into spills)
   int64_t nan_v = 0, pinf_v = 0, ninf_v = 0;
-  int64_t cnt_w = 0;  // wave-uniform count of selected rows (HLL-only variant)
-  LaneMoments a{0.0, 0.0, 0.0, 0, 0};
+  int64_t cnt_w = 0;  // wave-uniform count of the rows in the moments (STATS) / selected rows (HLL only)
+  LaneMoments a{0.0, 0.0, 0};
+  const double shift = STATS ? range_shift_of<KIND>(vr, validity, mask, row0, row1, lane) : 0.0;
   int32_t qmin = 0;
-  bool started = false;  // every lane has its moments shift (wave-uniform)
-  int nb = 0;
-  // (the block's loads software-pipelined one block ahead measured slower: 107 VGPRs for f64 stats+HLL,
-  // 4 waves per SIMD instead of 5, 1.51 -> 1.59 ms per 125 M rows x 8 columns)
-  for (int64_t blk = row0; blk < row1; blk += kRowsPerIter, ++nb) {
-    const int64_t base = blk + (int64_t)wave * 512;
-    const bool full = blk + kRowsPerIter <= row1;
+  const int32_t nr = (int32_t)(row1 - row0);  // range-relative rows: 32-bit (scalar) loop control and compares
+  for (int32_t rb = 0; rb < nr; rb += kRowsPerIter) {
+    const int64_t base = row0 + rb + wave * 512;
+    const int32_t rem = nr - rb - wave * 512;  // rows of the range from this wave's block on
+    const bool full = rb + kRowsPerIter <= nr;
     uint64_t bits[8], m[8];
     double x[8];
+    const int32_t vo = (rb + wave * 512 + lane) * (int32_t)sizeof(T);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int soff = (int)((base - row0 + j * 64) * (int64_t)sizeof(T));
       if constexpr (sizeof(T) == 8) {
-        const auto w2 = __builtin_amdgcn_raw_buffer_load_b64(vr, lane * 8, soff, 2 /* nt */);
+        const auto w2 = __builtin_amdgcn_raw_buffer_load_b64(vr, vo + j * 512, 0, 2 /* nt */);
         bits[j] = ((uint64_t)w2[1] << 32) | w2[0];
         if (KIND == CK_F64) x[j] = __builtin_bit_cast(double, bits[j]);
         else x[j] = __builtin_fma((double)(int32_t)w2[1], 4294967296.0, (double)w2[0]);  // exact int64 -> double
       } else {
-        const int32_t w = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(vr, lane * 4, soff, 2 /* nt */);
+        const int32_t w = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(vr, vo + j * 256, 0, 2 /* nt */);
         bits[j] = (uint64_t)(int64_t)w;
         x[j] = (double)w;
       }
     }
-    block_masks(validity, mask, base, row1, full, m);
+    block_masks(validity, mask, base, rem, full, m);
     // one v_cmp_class per value (NaN or +-inf); only their OR stays live on the common path (keeping
     // the 8 masks for the rare path spilled SGPRs into v_writelane / v_readlane on every block)
     uint64_t nf_any = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       if (KIND == CK_F64) nf_any |= __builtin_amdgcn_ballot_w64(!__builtin_isfinite(x[j])) & m[j];
-      if (!STATS) cnt_w += __builtin_popcountll(m[j]);
     }
     if (KIND == CK_F64 && nf_any != 0) {
       // rare: a selected NaN / +-inf in the block.  One row group at a time, the values re-read (L2) and
       // the selection rebuilt per group: a rolled loop whose state is one group's, so this path does not
-      // raise the register count of the common one (an unrolled 8-group copy took it from 66 to 91 VGPRs,
-      // 7 -> 5 waves per SIMD).  NaN rows hash as the canonical NaN (doubleToLongBits) and stay out of
-      // min / max (Spark orders NaN above every value); +-inf rows stay out of the shifted moments (x - shift
-      // would be inf - inf for the rest of the lane) and are counted: dq_finish adds them back into the sum
-      // (Spark's sequential sum is then +-inf, or NaN with both signs) and the moments become NaN.
+      // raise the register count of the common one.  NaN rows hash as the canonical NaN
+      // (doubleToLongBits) and stay out of min / max (Spark orders NaN above every value) but enter the
+      // moments (which become NaN, as Spark's); +-inf rows stay out of the shifted moments and are counted:
+      // dq_finish adds them back into the sum (Spark's sequential sum is then +-inf, or NaN with both
+      // signs) and the moments become NaN.
 #pragma unroll 1
       for (int j = 0; j < 8; ++j) {
+        const int32_t left = rem - 64 * j;
+        if (left <= 0) break;
         const int64_t r = base + 64 * j;
-        if (r >= row1) break;
         uint64_t mj = ~0ull;
         {
           const int64_t w = r >> 5;
-          const bool two = r + 32 < row1;
+          const bool two = left > 32;
           if (validity) mj = ((uint64_t)(two ? ((const_u32s)validity)[w + 1] : 0u) << 32) | ((const_u32s)validity)[w];
           if (mask) mj &= ((uint64_t)(two ? ((const_u32s)mask)[w + 1] : 0u) << 32) | ((const_u32s)mask)[w];
-          if (r + 64 > row1) mj &= (1ull << (row1 - r)) - 1ull;
+          if (left < 64) mj &= (1ull << left) - 1ull;
         }
-        const auto w2 = __builtin_amdgcn_raw_buffer_load_b64(vr, lane * 8, (int)((r - row0) * 8), 2 /* nt */);
+        const auto w2 = __builtin_amdgcn_raw_buffer_load_b64(vr, vo + j * 512, 0, 2 /* nt */);
         uint64_t b = ((uint64_t)w2[1] << 32) | w2[0];
         const double xv = __builtin_bit_cast(double, b);
         const uint64_t nf = __builtin_amdgcn_ballot_w64(!__builtin_isfinite(xv)) & mj;
@@ -522,8 +511,10 @@ __device__ void numeric_range(const void* values, const uint32_t* validity, cons
         }
         if (STATS) {
           const uint64_t mm = mj & ~inf;
-          if (s.n == 0.0 && a.k == 0 && lane_bit(mm)) a.shift = xv;  // a still-empty lane's first value
-          masked_moments<false, true>(a, s.fmin, s.fmax, xv, b, mm, mj & ~nanm);
+          cnt_w += __builtin_popcountll(mm);
+          masked_moments<false, true>(a, s.fmin, s.fmax, xv, b, shift, mm, mj & ~nanm);
+        } else {
+          cnt_w += __builtin_popcountll(mj);
         }
         if (HLL) {
           if (lane_bit(nanm)) b = 0x7FF8000000000000ull;
@@ -535,18 +526,32 @@ __device__ void numeric_range(const void* values, const uint32_t* validity, cons
         }
       }
     } else {
-      const uint64_t nanm[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      numeric_block<KIND, STATS, HLL, false>(x, bits, m, m, nanm, s, a, regs, qmin, started);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) cnt_w += __builtin_popcountll(m[j]);
+      numeric_block<KIND, STATS, HLL>(x, bits, m, shift, s, a, regs, qmin);
     }
-    if (STATS && (nb % kChunkBlocks) == kChunkBlocks - 1) moments_flush<KIND>(s, a);
   }
-  if (STATS) moments_flush<KIND>(s, a);
-  if (!STATS && lane == 0) s.count += cnt_w;
+  if (STATS) {
+    // the wave's moments from its lanes' shifted sums (fixed butterfly order: deterministic); lane 0 holds
+    // them, the other lanes only min / max (n = 0: neutral in stats_merge)
+    const double S1 = wave_sum_f64(a.sd), S2 = wave_sum_f64(a.sdd);
+    const int64_t is = KIND == CK_F64 ? 0 : wave_sum_i64(a.is);
+    if (lane == 0 && cnt_w > 0) {
+      const double n = (double)cnt_w, q = S1 / n;
+      s.n = n;
+      s.mean = shift + q;
+      const double m2 = __builtin_fma(-S1, q, S2);
+      s.m2 = m2 < 0.0 ? 0.0 : m2;  // rounding can leave a constant column's m2 at -ulp; a NaN stays NaN
+      if (KIND == CK_F64) s.sum = __builtin_fma(n, shift, S1);
+      else s.isum = is;
+    }
+  }
+  if (lane == 0) s.count += cnt_w;
   if (KIND == CK_F64 && lane == 0) {
     s.nan_count += nan_v;
     s.pinf += pinf_v;
     s.ninf += ninf_v;
-    if (STATS) s.count += pinf_v + ninf_v;  // the moments' k counted only the finite / NaN rows
+    if (STATS) s.count += pinf_v + ninf_v;  // the moments counted only the finite / NaN rows
   }
 }
 
@@ -680,21 +685,25 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
   // conditional one makes the wait counts of both paths merge).
   constexpr int kOffRing = 4;
   OffT ra[kOffRing], rb[kOffRing];  // offsets o0, o1 of rows j .. j + 3 (slot = row & 3)
-  auto load_offsets = [&](int64_t blk, int j) {
-    const int soff = (int)((blk + (int64_t)wave * 512 - row0 + j * 64) * W);
+  // the row offset of a load in voffset (the block's lane row in a VGPR, set once per block; the row group's
+  // 64 j W bytes in the instruction's immediate offset): the descriptor's range check covers voffset +
+  // immediate, so the next block's prefetch past the range's last row reads 0 -- nothing past the offsets
+  auto lane_off = [&](int64_t blk) -> int32_t { return (int32_t)((blk + (int64_t)wave * 512 - row0 + lane) * W); };
+  auto load_offsets = [&](int32_t vo, int j) {
     const int q = j & (kOffRing - 1);
     if constexpr (W == 4) {
-      ra[q] = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(orsrc, lane * 4, soff, 0);
-      rb[q] = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(orsrc, lane * 4 + 4, soff, 0);
+      ra[q] = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(orsrc, vo + j * 256, 0, 0);
+      rb[q] = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(orsrc, vo + j * 256 + 4, 0, 0);
     } else {
-      const auto a0 = __builtin_amdgcn_raw_buffer_load_b64(orsrc, lane * 8, soff, 0);
-      const auto a1 = __builtin_amdgcn_raw_buffer_load_b64(orsrc, lane * 8 + 8, soff, 0);
+      const auto a0 = __builtin_amdgcn_raw_buffer_load_b64(orsrc, vo + j * 512, 0, 0);
+      const auto a1 = __builtin_amdgcn_raw_buffer_load_b64(orsrc, vo + j * 512 + 8, 0, 0);
       ra[q] = (int64_t)(((uint64_t)a0[1] << 32) | a0[0]);
       rb[q] = (int64_t)(((uint64_t)a1[1] << 32) | a1[0]);
     }
   };
+  int32_t vo_cur = lane_off(row0);
 #pragma unroll
-  for (int j = 0; j < kOffRing; ++j) load_offsets(row0, j);
+  for (int j = 0; j < kOffRing; ++j) load_offsets(vo_cur, j);
   // o0 rel. to the window (low 2 bits = the string's byte alignment) and len of the row in slot j & 3
   auto rel_of = [&](int j) -> uint32_t {
     const int q = j & (kOffRing - 1);
@@ -740,11 +749,23 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
     }
     qtail = rest;
   };
-  for (int64_t blk = row0; blk < row1; blk += kRowsPerIter) {
-    const int64_t base = blk + (int64_t)wave * 512;
-    const bool full = blk + kRowsPerIter <= row1;
+  const int32_t nr = (int32_t)(row1 - row0);  // range-relative rows: 32-bit (scalar) loop control and compares
+  for (int32_t rb = 0; rb < nr; rb += kRowsPerIter) {
+    const int64_t blk = row0 + rb;
+    const int64_t base = blk + wave * 512;
+    const int32_t rem = nr - rb - wave * 512;  // rows of the range from this wave's block on
+    const bool full = rb + kRowsPerIter <= nr;
+    const int32_t vo_next = lane_off(blk + kRowsPerIter);
     uint64_t m[8];  // selected rows that take the fast path (SGPR budget: the rare path reloads the masks)
-    block_masks(validity, mask, base, row1, full, m);
+    block_masks(validity, mask, base, rem, full, m);
+    // every 32-byte window of the block lies inside the chunk's bytes iff its last row's does (offsets only
+    // grow): then no row needs the per-row window compare (all but a chunk's last blocks)
+    bool wins_in;
+    {
+      const int32_t last = rem > 512 ? 511 : rem - 1;  // the block's last row below row1 (rel. to base)
+      const int64_t o_last = last >= 0 ? (int64_t)offsets[base + last] : 0;  // uniform: a scalar load
+      wins_in = win >= 0 && (int32_t)(o_last - lo) <= win3;
+    }
     uint64_t slow = 0;  // OR of the selected rows that need the general hash
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -752,8 +773,12 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
         cnt_w += __builtin_popcountll(m[j]);
         // the compares' own masks (llvm.amdgcn.icmp; signedness from the predicate) ANDed in SGPRs: a
         // ballot of the combined bool materialises it in a VGPR and compares again (2 VALU per row)
-        const uint64_t fastm = __builtin_amdgcn_uicmp(len_of(j), 28u, 37 /* ICMP_ULE */) &
-                               __builtin_amdgcn_uicmp(rel_of(j), (uint32_t)win3, 41 /* ICMP_SLE: signed */);
+        uint64_t fastm = __builtin_amdgcn_uicmp(len_of(j), 28u, 37 /* ICMP_ULE */);
+        if (!wins_in) {  // a uniform branch: the compare (in asm, so it is not hoisted) runs only here
+          uint64_t wm;
+          asm volatile("v_cmp_le_i32_e64 %0, %1, %2" : "=s"(wm) : "v"(rel_of(j)), "s"(win3));
+          fastm &= wm;
+        }
         slow |= m[j] & ~fastm;
         m[j] &= fastm;
       }
@@ -781,7 +806,9 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
         const uint64_t h2 = xxh64_stripes<2>(wv, len_of(j), d4p);
         const uint64_t dm = m[j] & __builtin_amdgcn_ballot_w64(len_of(j) >= 24u);  // needs the third round
         if (dm != 0) {
-          const uint32_t pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(dm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dm, qtail));
+          // position = qtail + the lane's rank among the pushing lanes (qtail joins the scalar LDS base: no
+          // v_mov of it into the mbcnt)
+          const uint32_t pos = qtail + __builtin_amdgcn_mbcnt_hi((uint32_t)(dm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dm, 0u));
           if (lane_bit(dm)) {
             dq[0 * kDefCap + pos] = (uint32_t)h2;
             dq[1 * kDefCap + pos] = (uint32_t)(h2 >> 32);
@@ -798,8 +825,8 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
         if (qtail >= 64u) drain_full();
       }
       // row j + 4 into the slot row j frees (of the next block for j >= 4)
-      if (j + kOffRing < 8) load_offsets(blk, j + kOffRing);
-      else load_offsets(blk + kRowsPerIter, j + kOffRing - 8);
+      if (j + kOffRing < 8) load_offsets(vo_cur, j + kOffRing);
+      else load_offsets(vo_next, j + kOffRing - 8);
 #pragma unroll
       for (int q = 0; q + 1 < kStrAhead; ++q) {
         win_a[q] = win_a[q + 1];
@@ -808,11 +835,12 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
       win_a[kStrAhead - 1] = an;
       win_c[kStrAhead - 1] = cn;
     }
+    vo_cur = vo_next;
     // rare: long / window-crossing strings, or a rank that needs the hash's low word (2^-23).  The
     // HLL update is idempotent, so the block's selected rows are simply redone; DataType counts only
     // the rows the fast path skipped.
     if ((slow | __builtin_amdgcn_ballot_w64(qmin < 0)) != 0) {
-      block_masks(validity, mask, base, row1, full, m);
+      block_masks(validity, mask, base, rem, full, m);
 #pragma unroll 1
       for (int j = 0; j < 8; ++j) {
         if (lane_bit(m[j])) {

@@ -882,7 +882,7 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
         p->pred_jit = pred_jit_get(src, p->device, note, p->pred_jit_ms);
       }
       p->pred_jit_note = note;
-      if (p->pred_jit) {
+      if (p->pred_jit || (p->host_only && !p->pred_jit_src.empty())) {  // (explain: as the compiled plan would)
         p->pred_jit_cols = slots;
         p->pred_jit_hll_task = tasks;
         for (int32_t t : tasks) {
@@ -891,7 +891,8 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
         }
       }
     } else {
-      p->pred_jit_note = "program not eligible (regex / string atoms or > 8 columns)";
+      p->pred_jit_note = "program not eligible (regex / string atoms, > 8 columns, or > 16 counters / 8 where "
+                         "bitmaps / 96 instructions)";
     }
     if (!p->pred_jit && !(p->host_only && !p->pred_jit_src.empty()) && p->pred_pass == DQ_PRED_PASS_COMPILED)
       return set_error(DQ_E_UNSUPPORTED, "compiled predicate pass required: %s", p->pred_jit_note.c_str());

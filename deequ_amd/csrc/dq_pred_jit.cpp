@@ -165,8 +165,15 @@ const char* cmp_op(int c) {
 
 }  // namespace
 
+// Size limits of a program the generator takes: every counter pair is pinned in SGPRs per row group (two per
+// counter) next to the atoms' 64-bit masks; past ~24 counters LLVM's register allocation fails (after up to a
+// minute of hipRTC time: 26 counters 9 s, 29 counters 70 s, measured in this container), so larger programs --
+// a VerificationSuite with many Compliance checks -- stay on the interpreter, whose cost grows per atom anyway.
+constexpr int kJitMaxCounters = 16, kJitMaxBitmaps = 8, kJitMaxInstr = 96;
+
 bool pred_jit_eligible(const PredProgram& prog, const int32_t* col_kind, int32_t ncols) {
   if (prog.regex_words > 0 || prog.n_loads == 0) return false;
+  if (prog.n_counters > kJitMaxCounters || prog.n_bitmaps > kJitMaxBitmaps || prog.n_instr > kJitMaxInstr) return false;
   std::vector<int32_t> cols;
   for (int i = 0; i < prog.n_instr; ++i) {
     const PredInstr& ins = prog.instr[i];

@@ -20,6 +20,7 @@
 // bound, no sort, no scratch the size of the column.  Chunks and row shards add their histograms, so
 // the same select runs over any number of chunks (and across ranks with one all-reduce per pass).
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cmath>
@@ -278,6 +279,42 @@ double key_to_double(int32_t type, uint64_t key) {
   return (double)(int64_t)(key ^ 0x8000000000000000ull);
 }
 
+// The order keys of a chunk's non-null values appended to keys[*cursor ...] (order free: they are sorted next);
+// one 64-bit atomic per wave.
+template <int TYPE>
+__global__ __launch_bounds__(kQBlock) void dq_digest_keys(const void* __restrict__ values,
+                                                          const uint32_t* __restrict__ validity, int64_t n,
+                                                          unsigned long long* __restrict__ keys,
+                                                          unsigned long long* __restrict__ cursor) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t r0 = (int64_t)blockIdx.x * kQBlock; r0 < n; r0 += (int64_t)gridDim.x * kQBlock) {
+    const int64_t r = r0 + threadIdx.x;
+    bool ok = r < n;
+    uint64_t raw = 0;
+    if (ok) {
+      if (validity) ok = (validity[r >> 5] >> (r & 31)) & 1u;
+      if constexpr (TYPE == DQ_TYPE_I32) raw = (uint32_t)reinterpret_cast<const int32_t*>(values)[r];
+      else raw = reinterpret_cast<const uint64_t*>(values)[r];
+    }
+    const uint64_t b = __builtin_amdgcn_ballot_w64(ok);
+    if (b == 0) continue;
+    const int first = __builtin_ctzll(b);
+    unsigned long long base = 0;
+    if (lane == first) base = atomicAdd(cursor, (unsigned long long)__builtin_popcountll(b));
+    base = __shfl(base, first);
+    if (ok) keys[base + __builtin_popcountll(b & ((1ull << lane) - 1ull))] = order_key<TYPE>(raw);
+  }
+}
+
+// out[i] = the sorted key at 1-based rank 1 + i * s (the last sample at rank n)
+__global__ void dq_digest_gather(const unsigned long long* __restrict__ sorted, int64_t n, int64_t s, int64_t m,
+                                 unsigned long long* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  const int64_t rank = i == m - 1 ? n : 1 + i * s;
+  out[i] = sorted[rank - 1];
+}
+
 }  // namespace
 }  // namespace dq
 
@@ -448,6 +485,83 @@ dq_status dq_approx_quantiles(int32_t type, const dq_column_view* cols, const in
     }
   }
   for (int q = 0; q < n_q; ++q) out[q] = key_to_double(type, sel.prefix[q]);
+  return DQ_OK;
+}
+
+dq_status dq_quantile_digest(int32_t type, const dq_column_view* cols, const int64_t* chunk_rows, int32_t n_chunks,
+                             double relative_error, int32_t device, void* hip_stream, double* values, int64_t* ranks,
+                             int64_t cap, int64_t* n_samples, int64_t* count) {
+  if (!cols || !chunk_rows || !n_samples || !count || n_chunks < 0 || cap < 0 || (cap > 0 && (!values || !ranks)))
+    return set_error(DQ_E_INVALID, "dq_quantile_digest: NULL argument");
+  if (type != DQ_TYPE_F64 && type != DQ_TYPE_I64 && type != DQ_TYPE_I32)
+    return set_error(DQ_E_TYPE, "dq_quantile_digest: column type %d is not numeric", type);
+  if (!(relative_error >= 0.0 && relative_error <= 1.0))
+    return set_error(DQ_E_INVALID,
+                     "Relative error parameter must be in the closed interval [0, 1]. Currently, the value is: %g!",
+                     relative_error);
+  int64_t total = 0;
+  for (int c = 0; c < n_chunks; ++c) {
+    if (chunk_rows[c] < 0 || chunk_rows[c] > ((int64_t)1 << 40))
+      return set_error(DQ_E_INVALID, "dq_quantile_digest: chunk %d has %lld rows", c, (long long)chunk_rows[c]);
+    if (chunk_rows[c] > 0 && !cols[c].values)
+      return set_error(DQ_E_INVALID, "dq_quantile_digest: chunk %d has no values", c);
+    if (cols[c].reserved != 0) return set_error(DQ_E_INVALID, "dq_quantile_digest: reserved field must be 0");
+    total += chunk_rows[c];
+  }
+  *n_samples = 0;
+  *count = 0;
+  QHIP(hipSetDevice(device));
+  hipStream_t stream = reinterpret_cast<hipStream_t>(hip_stream);
+  if (total == 0) return DQ_OK;
+  // every non-null value's order key, compacted (one pass over the column), then one radix sort of the keys
+  DevHist keys, sorted, cursor, tmp;
+  QHIP(hipMalloc(&keys.p, (size_t)total * 8));
+  QHIP(hipMalloc(&sorted.p, (size_t)total * 8));
+  QHIP(hipMalloc(&cursor.p, 8));
+  QHIP(hipMemsetAsync(cursor.p, 0, 8, stream));
+  for (int c = 0; c < n_chunks; ++c) {
+    const int64_t rows = chunk_rows[c];
+    if (rows == 0) continue;
+    const auto* val = reinterpret_cast<const uint32_t*>(cols[c].validity);
+    const int grid = (int)std::min<int64_t>(8192, (rows + kQBlock - 1) / kQBlock);
+    if (type == DQ_TYPE_F64)
+      hipLaunchKernelGGL(dq_digest_keys<DQ_TYPE_F64>, dim3(grid), dim3(kQBlock), 0, stream, cols[c].values, val, rows,
+                         keys.p, cursor.p);
+    else if (type == DQ_TYPE_I64)
+      hipLaunchKernelGGL(dq_digest_keys<DQ_TYPE_I64>, dim3(grid), dim3(kQBlock), 0, stream, cols[c].values, val, rows,
+                         keys.p, cursor.p);
+    else
+      hipLaunchKernelGGL(dq_digest_keys<DQ_TYPE_I32>, dim3(grid), dim3(kQBlock), 0, stream, cols[c].values, val, rows,
+                         keys.p, cursor.p);
+    QHIP(hipGetLastError());
+  }
+  unsigned long long n_ull = 0;
+  QHIP(hipMemcpyAsync(&n_ull, cursor.p, 8, hipMemcpyDeviceToHost, stream));
+  QHIP(hipStreamSynchronize(stream));
+  const int64_t n = (int64_t)n_ull;
+  *count = n;
+  if (n == 0) return DQ_OK;  // all values NULL: no digest
+  // the digest's sample ranks (deequ_amd/quantiles.py digest_ranks): 1, 1 + s, ..., n, s = max(1, floor(2 e n))
+  const int64_t s = std::max<int64_t>(1, (int64_t)std::floor(2.0 * relative_error * (double)n));
+  const int64_t m = (n - 1) / s + 1 + ((n - 1) % s != 0 ? 1 : 0);
+  *n_samples = m;
+  if (m > cap) return set_error(DQ_E_INVALID, "dq_quantile_digest: %lld samples, room for %lld", (long long)m, (long long)cap);
+  // (hipCUB's item count is an int here, as in the grouping pass)
+  if (n > (int64_t)0x7FFFFFFF)
+    return set_error(DQ_E_UNSUPPORTED, "dq_quantile_digest: %lld values (at most 2^31 - 1)", (long long)n);
+  size_t tb = 0;
+  QHIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, keys.p, sorted.p, (int)n, 0, 64, stream));
+  QHIP(hipMalloc(&tmp.p, std::max<size_t>(tb, 8)));
+  QHIP(hipcub::DeviceRadixSort::SortKeys(tmp.p, tb, keys.p, sorted.p, (int)n, 0, 64, stream));
+  hipLaunchKernelGGL(dq_digest_gather, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, stream, sorted.p, n, s, m, keys.p);
+  QHIP(hipGetLastError());
+  std::vector<unsigned long long> got((size_t)m);
+  QHIP(hipMemcpyAsync(got.data(), keys.p, (size_t)m * 8, hipMemcpyDeviceToHost, stream));
+  QHIP(hipStreamSynchronize(stream));
+  for (int64_t i = 0; i < m; ++i) {
+    values[i] = key_to_double(type, got[(size_t)i]);
+    ranks[i] = i == m - 1 ? n : 1 + i * s;
+  }
   return DQ_OK;
 }
 

@@ -226,29 +226,58 @@ def digest_ranks(n: int, relativeError: float) -> List[int]:
     return ranks
 
 
-MAX_DIGEST_SAMPLES = 4096  # order statistics the state may hold (8 per device select call)
+# samples the state may hold: relativeError e keeps about 1 / (2 e) + 2 of them (52 at e = 0.01); e = 0 keeps
+# every value, as Spark's GK summary does.  Past this, the Python digest (a list of samples) would not fit.
+MAX_DIGEST_SAMPLES = 1 << 20
 
 
 def device_digest(data, column: str, relativeError: float) -> PercentileDigest:
-    """The column's digest from exact order statistics (dq_approx_quantiles at each sample rank); an empty
-    digest (count 0) when every value is NULL."""
+    """The column's digest from exact order statistics: dq_quantile_digest sorts the column's non-null values
+    once on the device and returns the values at every sample rank (one pass, whatever the number of
+    samples); an empty digest (count 0) when every value is NULL."""
     rel = spark_relative_error(relativeError)
-    select = _rank_select(data, column)
-    n, _ = select([0.5])
+    n, ranks, values = _digest_samples(data, column, rel)
     if n == 0:
         return PercentileDigest(QuantileSummaries(QuantileSummaries.defaultCompressThreshold, rel))
-    ranks = digest_ranks(n, rel)
-    if len(ranks) > MAX_DIGEST_SAMPLES:
-        raise UnsupportedOnGpuPathException(
-            f"a relativeError of {relativeError} over {n} values needs {len(ranks)} samples in the quantile state")
-    values: List[float] = []
-    for lo in range(0, len(ranks), 8):  # DQ_MAX_QUANTILES per call; rank r as quantile (r - 0.5) / n
-        values.extend(select([(r - 0.5) / n for r in ranks[lo:lo + 8]])[1])
+    assert ranks == digest_ranks(n, rel)[:len(ranks)] and ranks[-1] == n
     sampled, prev = [], 0
     for r, v in zip(ranks, values):
         sampled.append((v, r - prev, 0))
         prev = r
     return PercentileDigest(QuantileSummaries(QuantileSummaries.defaultCompressThreshold, rel, sampled, n))
+
+
+def _digest_samples(data, column: str, rel: float):
+    """(n, sample ranks, sample values) of the column through dq_quantile_digest."""
+    import torch
+
+    from .runner import _chunks
+
+    chunks = _chunks(data)
+    schema = {name: dt for name, dt, _ in chunks[0].schema}
+    views = (L.ColumnView * max(1, len(chunks)))()
+    rows = (ctypes.c_int64 * max(1, len(chunks)))()
+    total = 0
+    for k, t in enumerate(chunks):
+        rows[k] = t.num_rows
+        views[k] = t.columns[column].view()
+        total += t.num_rows
+    # the sample count for n <= total values: (n - 1) / s + 2 at most, s = max(1, floor(2 rel n)), which peaks
+    # near n = 1 / rel (s = 1 below it)
+    cap = total + 1 if rel == 0.0 else min(total + 1, int(1.0 / rel) + 4)
+    cap = min(cap, MAX_DIGEST_SAMPLES)
+    vals = (ctypes.c_double * max(1, cap))()
+    rks = (ctypes.c_int64 * max(1, cap))()
+    m, cnt = ctypes.c_int64(), ctypes.c_int64()
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    rc = L.lib.dq_quantile_digest(_TYPES[schema[column]], views, rows, len(chunks), rel, torch.cuda.current_device(),
+                                  stream, vals, rks, cap, ctypes.byref(m), ctypes.byref(cnt))
+    if rc == L.DQ_E_INVALID and m.value > cap:
+        raise UnsupportedOnGpuPathException(
+            f"a relativeError of {rel} over {cnt.value} values needs {m.value} samples in the quantile state "
+            f"(at most {MAX_DIGEST_SAMPLES} on the GPU path)")
+    L.check(rc)
+    return cnt.value, list(rks[:m.value]), list(vals[:m.value])
 
 
 def _rank_select(data, column: str):

@@ -32,7 +32,7 @@ extern "C" {
 #endif
 
 #define DQ_ABI_VERSION 3  /* 2: dq_state.reserved[0] = integral flag + Sum / Mean int64 partials; ingestion, pool and state-array entry points;
-                             3: dq_plan_create_opts (predicate-pass mode), dq_plan_create_time, dq_plan_explain */
+                             3: dq_plan_create_opts (predicate-pass mode), dq_plan_create_time, dq_plan_explain, dq_quantile_digest */
 
 typedef int32_t dq_status;
 #define DQ_OK 0
@@ -372,6 +372,15 @@ void dq_freq_destroy(dq_freq_table* t);
 dq_status dq_approx_quantiles(int32_t type, const dq_column_view* cols, const int64_t* chunk_rows, int32_t n_chunks,
                               const double* quantiles, int32_t n_q, double relative_error, int32_t device,
                               void* hip_stream, double* out, int64_t* count);
+/* ApproxQuantileState's digest (ApproxQuantile.scala:28-35, 69-80) in one pass: every non-null value's order
+ * key compacted, radix-sorted once (Double.compare order: NaN largest, -0.0 < 0.0), and the values at the
+ * 1-based ranks 1, 1 + s, 1 + 2 s, ..., n with s = max(1, floor(2 relative_error n)) -- the samples of a
+ * QuantileSummaries with exact ranks (g = rank gaps, delta = 0; deequ_amd/quantiles.py).  *count = n
+ * (0: every value NULL, no samples); *n_samples = the number of samples; DQ_E_INVALID when it exceeds cap
+ * (call again with a larger buffer; relative_error 0 samples every value). */
+dq_status dq_quantile_digest(int32_t type, const dq_column_view* cols, const int64_t* chunk_rows, int32_t n_chunks,
+                             double relative_error, int32_t device, void* hip_stream, double* values, int64_t* ranks,
+                             int64_t cap, int64_t* n_samples, int64_t* count);
 /* Histogram (analyzers/Histogram.scala:33-99): the n largest groups by count (ties in key order):
  * key, count and -- for a table built from data with hashed keys (strings) -- one representative row
  * id (chunk << 40 | row) whose value the caller renders; ~0 when not available (merged tables). */

@@ -1,12 +1,15 @@
-"""The Correlation pass fused with the column moments (deequ_amd/csrc/dq_pair.hip): the matrix-core Gram
-kernel (default) and the lane-per-row kernel (DQ_PAIR_KERNEL=lane).
+"""The Correlation pass fused with the column moments (deequ_amd/csrc/dq_pair.hip): the VALU co-moment pass
+(dq_pair_scan: per <= 8-column pair group two waves, a 14-slot pattern whose two rotations are the 28 pairs,
+fp64 groups staged HBM -> LDS by global_load_lds in a ring of two-group slots) and its checked re-run of
+non-finite ranges (dq_pair_redo).
 
 Correlation co-moments (Correlation.scala:37-52) and the Mean / StandardDeviation / Sum / Minimum /
 Maximum states of the same columns are computed in ONE read of each column.  Checked against the C
-oracle (Spark partition order) and against the LDS-tile kernel (DQ_PAIR_KERNEL=tile) on: nulls, `where`
-filters, f64 / i64 / i32 columns, NaN / +-inf values, pairs in both orientations, ragged sizes around
-the 64 / 128-row blocks, and a complete 8-column pair set (C4's 28 correlations) plus pairs on columns
-without moments.
+oracle (Spark partition order) on: nulls, `where` filters, f64 / i64 / i32 columns (the mixed-kind groups
+take the register-staged fold), NaN / +-inf values, pairs in both orientations, ragged sizes around the
+64-row groups and the two-group ring slots, columns drifting far from their first values (the per-range
+shift), a complete 8-column pair set (C4's 28 correlations, bitwise deterministic across runs) plus pairs
+on columns without moments.
 """
 from __future__ import annotations
 

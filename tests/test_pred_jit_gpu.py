@@ -115,6 +115,26 @@ def test_c3_plan_runs_the_compiled_pass(dq):
         assert c[a] == i[a] or (c[a] is None and i[a] is None), (a, c[a], i[a])
 
 
+def test_large_program_stays_on_the_interpreter(dq):
+    """A program of more than 16 counters (29 Compliance predicates) is not compiled -- LLVM's register
+    allocation of the pinned counters fails past ~24 after up to a minute of hipRTC time -- and runs on the
+    interpreter, equal to the oracle; DQ_PRED_PASS_COMPILED refuses it."""
+    from deequ_amd._lib import DQ_E_UNSUPPORTED, DQError
+    from deequ_amd.runner import ScanPlan, scan_states
+
+    t, ocols = _abc_table(dq, 4097, 9)
+    an = [dq.Compliance(f"r{i}", p) for i, p in enumerate(PREDICATES)]
+    plan = ScanPlan(an, t.schema)
+    ok, note = plan.pred_compiled()
+    assert not ok and "16 counters" in note, note
+    assert plan.create_time()[1] == 0.0
+    plan.close()
+    with pytest.raises(DQError) as e:
+        ScanPlan(an, t.schema, pred_pass="compiled")
+    assert e.value.status == DQ_E_UNSUPPORTED
+    _check_vs_oracle(dq, scan_states(t, an), an, ocols, 4097)
+
+
 def test_compiled_requires_eligible_program(dq):
     """DQ_PRED_PASS_COMPILED on a program with a string atom fails plan creation (no silent interpreter)."""
     from deequ_amd._lib import DQ_E_UNSUPPORTED, DQError
@@ -163,14 +183,17 @@ def test_predicates_compiled_equals_interpreter_and_oracle(dq, n):
     """Every PREDICATES / WHERES program of the parity suite in one plan: compiled == interpreter == oracle,
     with NaN / +-inf / -0.0 in the fp64 column."""
     t, ocols = _abc_table(dq, n, 100 + n)
-    an = [dq.Compliance(f"r{i}", p) for i, p in enumerate(PREDICATES)]
+    wheres = []
     for w in WHERES:
-        an += [dq.Size(w), dq.Compliance("w", "a < b", w), dq.ApproxCountDistinct("a", w),
-               dq.ApproxCountDistinct("b", w), dq.Completeness("c", w)]
-    c, i, _, _ = _both_passes(dq, t, an)
-    for a in an:
-        assert c[a] == i[a] or (c[a] is None and i[a] is None), (a, c[a], i[a])
-    _check_vs_oracle(dq, c, an, ocols, n)
+        wheres += [dq.Size(w), dq.Compliance("w", "a < b", w), dq.ApproxCountDistinct("a", w),
+                   dq.ApproxCountDistinct("b", w), dq.Completeness("c", w)]
+    # plans of <= 16 counters (the compiled pass's limit; larger programs stay on the interpreter)
+    preds = [dq.Compliance(f"r{i}", p) for i, p in enumerate(PREDICATES)]
+    for an in (preds[:12], preds[12:24], preds[24:], wheres[:15], wheres[15:]):
+        c, i, _, _ = _both_passes(dq, t, an)
+        for a in an:
+            assert c[a] == i[a] or (c[a] is None and i[a] is None), (a, c[a], i[a])
+        _check_vs_oracle(dq, c, an, ocols, n)
 
 
 @pytest.mark.parametrize("n", [1, 513, 4099, 300_007])

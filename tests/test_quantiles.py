@@ -223,11 +223,30 @@ def test_gpu_digest_matches_exact_ranks(dq, dtype):
     valid = rng.random(n) >= 0.1
     cuts = [0, 50_000, 50_000, 99_999, n]
     parts = [dq.Table([column_from_numpy("x", dtype, v[a:b], valid[a:b])]) for a, b in zip(cuts, cuts[1:])]
-    for err in (0.01, 0.1, 0.5):
+    for err in (0.0, 1e-5, 0.001, 0.01, 0.1, 0.5):  # 0: every value sampled (one sort answers all ranks)
         got = device_digest(parts, "x", err).quantileSummaries
         cnt, want = O.gk_digest_exact(v, valid, err)
         assert got.count == cnt and len(got.sampled) == len(want)
         assert all(_same(a[0], b[0]) and a[1:] == b[1:] for a, b in zip(got.sampled, want)), (dtype, err)
+
+
+@pytest.mark.gpu
+def test_gpu_digest_sample_limit(dq, monkeypatch):
+    """relativeError 0 keeps every value (as Spark's GK does); past MAX_DIGEST_SAMPLES the GPU path refuses
+    with UnsupportedOnGpuPathException (the analyzer goes to the Spark fallback) instead of building a digest
+    the host cannot hold."""
+    from deequ_amd import quantiles as Q
+    from deequ_amd.metrics import UnsupportedOnGpuPathException
+    from deequ_amd.table import column_from_numpy
+
+    x = np.random.default_rng(3).normal(size=5000)
+    t = dq.Table([column_from_numpy("x", "f64", x, np.ones(len(x), bool))])
+    got = Q.device_digest(t, "x", 0.0).quantileSummaries
+    assert got.count == len(x) and [s[0] for s in got.sampled] == sorted(x.tolist())
+    monkeypatch.setattr(Q, "MAX_DIGEST_SAMPLES", 4096)
+    with pytest.raises(UnsupportedOnGpuPathException):
+        Q.device_digest(t, "x", 0.0)
+    assert len(Q.device_digest(t, "x", 0.001).quantileSummaries.sampled) == 501
 
 
 @pytest.mark.gpu

@@ -12,7 +12,7 @@ fi
 i=0
 for lib in "$@"; do
   i=$((i+1)); name=$(basename $lib .so)_$i
-  DQ_LIB_PATH=$lib timeout -k 10 300 python bench.py --configs= --cpu-sample 0 --ingest-rows 0 --steps ${STEPS:-8} > gpurun_out/${TAG}_$name.json 2> gpurun_out/${TAG}_$name.err || { echo "bench $name failed"; tail -5 gpurun_out/${TAG}_$name.err; exit 3; }
+  DQ_LIB_PATH=$lib timeout -k 10 300 python bench.py --configs= --cpu-sample 0 --ingest-rows 0 --no-plan-timing --steps ${STEPS:-8} > gpurun_out/${TAG}_$name.json 2> gpurun_out/${TAG}_$name.err || { echo "bench $name failed"; tail -5 gpurun_out/${TAG}_$name.err; exit 3; }
   python3 -c "
 import json
 d=json.loads(open('gpurun_out/${TAG}_$name.json').read().strip().splitlines()[-1])

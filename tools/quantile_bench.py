@@ -45,6 +45,20 @@ def main():
         gbs = (8 + 1 / 8) * n / (ms * 1e-3) / 1e9
         print(f"quantiles={len(qs)} rows={n:.3g} ms={ms:.3f} rows/s={n / (ms * 1e-3):.4g} "
               f"column-read-equivalent GB/s={gbs:.0f} first={r[0]:.6g}", flush=True)
+    # ApproxQuantileState's digest: one compaction + radix sort + gather for all 1 / (2 e) + 2 sample ranks
+    from deequ_amd.quantiles import device_digest
+
+    if n <= (1 << 31) - 1:
+        for err in (0.01, 0.001):
+            device_digest(t, "x", err)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(a.reps):
+                d = device_digest(t, "x", err)
+            torch.cuda.synchronize()
+            ms = (time.perf_counter() - t0) / a.reps * 1e3
+            print(f"digest relativeError={err} samples={len(d.quantileSummaries.sampled)} rows={n:.3g} ms={ms:.3f} "
+                  f"rows/s={n / (ms * 1e-3):.4g}", flush=True)
 
 
 if __name__ == "__main__":
