@@ -83,17 +83,10 @@ __device__ __forceinline__ void ds_max_masked(uint64_t m, uint32_t addr, int32_t
   asm volatile("s_and_saveexec_b64 %0, %1\n\tds_max_i32 %2, %3\n\ts_mov_b64 exec, %0"
                : "=&s"(save) : "s"(m), "v"(addr), "v"(q) : "memory", "scc");
 }
-// bits of rows [r, r + 64) of a bitmap (scalar loads), clipped to rows below row1; all ones without one
-__device__ __forceinline__ uint64_t mask64(const uint32_t* bm, int64_t r, int64_t row1) {
-  if (r >= row1) return 0;
-  uint64_t x = ~0ull;
-  if (bm) {
-    const int64_t w = r >> 5;
-    const bool two = r + 32 < row1;
-    x = ((uint64_t)(two ? ((dq_const_u32s)bm)[w + 1] : 0u) << 32) | ((dq_const_u32s)bm)[w];
-  }
-  if (r + 64 > row1) x &= (1ull << (row1 - r)) - 1ull;
-  return x;
+// rows [r, r + 64) of the range below its end, from left = rows of the range from r on (32-bit: the scalar unit
+// has no 64-bit ordered compare, so 64-bit row comparisons became VALU compares of SGPR pairs)
+__device__ __forceinline__ uint64_t rows_mask(int32_t left) {
+  return left >= 64 ? ~0ull : (left <= 0 ? 0ull : (1ull << left) - 1ull);
 }
 // validity words of a block (lanes 0..15: rows base + 32 l .. + 31) through a bounds-checked descriptor over
 // the chunk's bitmap (past it: 0); all ones without a bitmap.  The 64-bit mask of row group j is then two
@@ -286,14 +279,17 @@ std::string pred_jit_source(const PredProgram& prog, const int32_t* col_kind, st
     }
     s += "  uint32_t vw" + si + " = valid_words(vb" + si + ", row0 + (int64_t)wave * " + WR + ", A.n_rows, lane), vwn" + si + ";\n";
   }
-  s += "  for (int64_t blk = row0; blk < row1; blk += " + BR + ") {\n";
-  s += "    const int64_t base = blk + (int64_t)wave * " + WR + ";\n";
-  s += "    if (base >= row1) break;\n";
-  s += "    const int soff = (int)(base - row0);\n";
+  // range-relative rows in 32 bits (scalar loop control and compares)
+  s += "  const int32_t nrr = (int32_t)(row1 - row0);\n";
+  s += "  for (int32_t rbk = 0; rbk < nrr; rbk += " + BR + ") {\n";
+  s += "    const int soff = rbk + wave * " + WR + ";\n";
+  s += "    if (soff >= nrr) break;\n";
+  s += "    const int64_t base = row0 + soff;\n";
+  s += "    const int32_t rem = nrr - soff;\n";
   for (int h = 0; h < nh; ++h) s += "    int32_t qmin" + std::to_string(h) + " = 0;\n";
   s += "#pragma unroll\n  for (int j = 0; j < " + G + "; ++j) {\n";
   s += "    const int64_t r = base + 64 * j;\n";
-  s += "    const uint64_t inr = mask64(nullptr, r, row1);\n";
+  s += "    const uint64_t inr = rows_mask(rem - 64 * j);\n";
   for (int i = 0; i < ns; ++i) s += "    const uint64_t va" + std::to_string(i) + " = group_mask(vw" + std::to_string(i) + ", j) & inr;\n";
   // the program: atoms and logic as scalar masks (SSA names, the operand stack resolved here)
   std::vector<std::pair<std::string, std::string>> stack;
@@ -386,7 +382,7 @@ std::string pred_jit_source(const PredProgram& prog, const int32_t* col_kind, st
   for (int b = 0; b < prog.n_bitmaps; ++b) {
     const int rt = prog.bitmap_root[b];
     if (rt < 0 || rt >= (int)roots.size()) return std::string();
-    s += "    if (r < row1 && lane == 0) A.where_bits[" + std::to_string(b) + "][r >> 6] = " + roots[rt].first + " & inr;\n";
+    s += "    if (rem - 64 * j > 0 && lane == 0) A.where_bits[" + std::to_string(b) + "][r >> 6] = " + roots[rt].first + " & inr;\n";
   }
   // the group's counters are pinned here (left alone, LLVM sinks the popcount chains to the block's end
   // and every ballot of the block stays live until then: SGPR spills), and the group's predicate work
@@ -437,7 +433,7 @@ std::string pred_jit_source(const PredProgram& prog, const int32_t* col_kind, st
     const std::string hs = std::to_string(h), vs = "v" + std::to_string(e.slot) + "[j]";
     s += "    if (__builtin_amdgcn_ballot_w64(qmin" + hs + " < 0) != 0) {\n";
     s += "#pragma unroll\n      for (int j = 0; j < " + G + "; ++j) {\n";
-    s += "        if (!lane_bit(group_mask(vw" + std::to_string(e.slot) + ", j) & mask64(nullptr, base + 64 * j, row1))) continue;\n";
+    s += "        if (!lane_bit(group_mask(vw" + std::to_string(e.slot) + ", j) & rows_mask(rem - 64 * j))) continue;\n";
     s += "        uint64_t cur;\n        " + load_vals(e.slot, "soff", "j", "cur");  // v[][j] holds the next block now
     if (k == CK_I32) {
       s += "        hll_exact(regs + " + std::to_string(h * 512) + ", xxh64_int((uint32_t)cur));\n";
@@ -518,7 +514,7 @@ bool pred_jit_compile_code(const std::string& src, const std::string& arch, std:
 namespace {
 
 // generated-source revision: part of the disk-cache key, so code objects of an older generator are not reused
-constexpr const char* kJitRevision = "dq_pred_jit r4";
+constexpr const char* kJitRevision = "dq_pred_jit r4b";
 
 uint64_t fnv1a64(const std::string& s, uint64_t h) {
   for (unsigned char c : s) h = (h ^ c) * 0x100000001B3ull;
