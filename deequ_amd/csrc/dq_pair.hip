@@ -129,6 +129,12 @@ __device__ double range_shift(const char* col, int kind, const uint32_t* vb, con
 constexpr int kRing = 4;
 constexpr int kSlotBytes = 8 * 1024 + 256;
 constexpr int kSlotMaskWord = 8 * 256;  // dword index of the selection words in a slot
+// the fp64 ring without Min / Max reads each slot into registers one slot ahead (round 4); 0 = the round-3
+// loop (kept for A/B builds: -DDQ_PAIR_PIPE=0)
+#ifndef DQ_PAIR_PIPE
+#define DQ_PAIR_PIPE 1
+#endif
+constexpr bool kPairPipe = DQ_PAIR_PIPE;
 
 
 // per-lane sums of one wave task over its range
@@ -443,6 +449,97 @@ __device__ __forceinline__ bool pair_range(const PairWaveTask& T, const ScanCols
             [b2] "s"(dp[2]), [b3] "s"(dp[3]), [ma] "v"(ma)
           : "memory", "scc");
     };
+    if constexpr (kPairPipe && !MINMAX) {
+      // ---- pipelined ring (round 4): a slot's values and selection words are read into registers one slot
+      // ahead, so the LDS latency hides behind the second half of the previous slot's fold, and the barrier
+      // sits between the two halves.  Iteration s: fold group 0 of slot s; wait until this wave's slot s
+      // registers and its own DMA of slot s + 1 have landed; s_barrier (past it the partner holds slot s in
+      // registers and its DMA of slot s + 1 has landed); DMA slot s + kRing into slot s's ring position; read
+      // slot s + 1; fold group 1 of slot s.  Branch-free addressing: position p reads ring column
+      // (p + wave) % 8, i.e. positions 0-6 at xa + 128 p and position 7 at xb.
+      const int64_t* xa = ring + lane + wave * 128;
+      const int64_t* xb = ring + lane + (wave == 0 ? 7 * 128 : 0);
+      // selection dwords of both groups in one read: lanes 0-15 the stream of position lane / 2, lanes 16
+      // and 17 the where stream (dword 2 further on = the slot's second group)
+      const uint32_t* mq = reinterpret_cast<const uint32_t*>(ring) + kSlotMaskWord +
+                           (lane < 16 ? 4 + 4 * (((lane >> 1) + wave) & 7) + (lane & 1) : (lane & 1));
+      struct SlotRegs {
+        int64_t v[2][kPairPos];
+        uint32_t m[2];
+      };
+      auto rd = [&](SlotRegs& R, uint32_t slot) __attribute__((always_inline)) {
+        const int64_t* a = xa + slot * (uint32_t)(kSlotBytes / 8);
+        const int64_t* b = xb + slot * (uint32_t)(kSlotBytes / 8);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+#pragma unroll
+          for (int p = 0; p < kPairPos - 1; ++p) R.v[h][p] = a[p * 128 + 64 * h];
+          R.v[h][kPairPos - 1] = b[64 * h];
+        }
+        const uint32_t* q = mq + slot * (uint32_t)(kSlotBytes / 4);
+        R.m[0] = q[0];
+        R.m[1] = q[2];
+      };
+      auto fold_group = [&](const int64_t (&v)[kPairPos], uint32_t mv) __attribute__((always_inline)) {
+        auto word = [](uint32_t x, int i) {
+          return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(x, i + 1) << 32) |
+                 (uint32_t)__builtin_amdgcn_readlane(x, i);
+        };
+        uint64_t m[kPairPos];
+#pragma unroll
+        for (int p = 0; p < kPairPos; ++p) m[p] = word(mv, 2 * p);
+        if (has_where) {
+          const uint64_t wm = word(mv, 16);
+#pragma unroll
+          for (int p = 0; p < kPairPos; ++p) m[p] &= wm;
+        }
+        if (active) fold_fast<true, false>(A, v, m, shift, kind);
+      };
+      // this wave's own DMA of slot t landed, with `after` slots issued after it (uniform; 5 loads per slot)
+      static_assert(kRing == 4, "the waits below count up to three slots after the awaited one");
+      auto wait_slot = [](int32_t after) __attribute__((always_inline)) {
+        if (after >= 3) asm volatile("s_waitcnt vmcnt(15) lgkmcnt(0)" ::: "memory");
+        else if (after == 2) asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)" ::: "memory");
+        else if (after == 1) asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      };
+      // one ring slot: R holds slot s (its reads issued), N receives slot s + 1.  Slots past the range's
+      // last are never staged (no wasted loads; the waits count what was issued).  32-bit slot numbers: the
+      // scalar unit has no 64-bit ordered compare.
+      const int32_t ns = (int32_t)npair;
+      auto iter = [&](SlotRegs& R, SlotRegs& N, int32_t s, uint32_t slot) __attribute__((always_inline)) {
+        fold_group(R.v[0], R.m[0]);
+        if (s + 1 < ns) {
+          // issued after slot s + 1: slots s + 2 .. min(s + kRing - 1, ns - 1)
+          const int32_t last = s + kRing - 1 < ns - 1 ? s + kRing - 1 : ns - 1;
+          wait_slot(last - (s + 1));
+          __builtin_amdgcn_s_barrier();
+          asm volatile("" ::: "memory");
+          if (s + kRing < ns) dma(s + kRing, slot);
+          rd(N, (slot + 1) & (kRing - 1));
+        }
+        fold_group(R.v[1], R.m[1]);
+      };
+      if (ns > 0) {
+#pragma unroll
+        for (int d = 0; d < kRing; ++d)
+          if (d < ns) dma(d, (uint32_t)d);
+        wait_slot((ns < kRing ? ns : kRing) - 1);
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        SlotRegs R0, R1;
+        rd(R0, 0u);
+        uint32_t slot = 0;
+        int32_t s = 0;
+        for (; s + 2 <= ns; s += 2) {
+          iter(R0, R1, s, slot);
+          iter(R1, R0, s + 1, slot + 1);
+          slot = (slot + 2) & (kRing - 1);
+        }
+        if (s < ns) iter(R0, R1, s, slot);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may outlive the workgroup (its LDS is reused)
+      }
+    } else {
     // this wave's positions: ring column (p + wave) % 8; selection words of half h: lanes 0, 1 of the first
     // read = where, lanes 2 p, 2 p + 1 of the second = position p
     const int64_t* xs0 = ring + lane;
@@ -490,6 +587,7 @@ __device__ __forceinline__ bool pair_range(const PairWaveTask& T, const ScanCols
         slot = slot + 1 == kRing ? 0 : slot + 1;
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may outlive the workgroup (its LDS is reused)
+    }
     }
     if (!active) return true;
     // the column pointers again for the tail and the counts (reloaded, not held in SGPRs through the loop)

@@ -1205,8 +1205,9 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
   }
   ScanBitmaps bm{};
   for (int b = 0; b < kMaxWhere; ++b) bm.where_bits[b] = p->d_where_bits[b];
-  // all-ones bitmap standing in for a missing validity / where bitmap in the pair pass
-  if (!p->pair_wgs.empty() && words + 1 > p->ones_cap_words) {
+  // all-ones bitmap standing in for a missing validity / where bitmap in the pair pass and the compiled
+  // predicate pass
+  if ((!p->pair_wgs.empty() || p->pred_jit) && words + 1 > p->ones_cap_words) {
     HIP_TRY(hipStreamSynchronize(p->stream));
     if (p->d_ones) (void)hipFree(p->d_ones);
     p->d_ones = nullptr;
@@ -1279,7 +1280,8 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
             PredJitArgs a{};
             for (size_t i = 0; i < p->pred_jit_cols.size(); ++i) {
               a.values[i] = reinterpret_cast<const char*>(sc.values[p->pred_jit_cols[i]]);
-              a.validity[i] = sc.validity[p->pred_jit_cols[i]];
+              const uint32_t* vb = sc.validity[p->pred_jit_cols[i]];
+              a.validity[i] = vb ? vb : reinterpret_cast<const uint32_t*>(p->d_ones);
             }
             for (int b = 0; b < kMaxWhere && b < 8; ++b) a.where_bits[b] = bm.where_bits[b];
             a.n_rows = n_rows;

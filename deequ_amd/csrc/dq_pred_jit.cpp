@@ -88,11 +88,11 @@ __device__ __forceinline__ void ds_max_masked(uint64_t m, uint32_t addr, int32_t
 __device__ __forceinline__ uint64_t rows_mask(int32_t left) {
   return left >= 64 ? ~0ull : (left <= 0 ? 0ull : (1ull << left) - 1ull);
 }
-// validity words of a block (lanes 0..15: rows base + 32 l .. + 31) through a bounds-checked descriptor over
-// the chunk's bitmap (past it: 0); all ones without a bitmap.  The 64-bit mask of row group j is then two
-// readlanes: scalar loads of every group's words, hoisted by the compiler, overflowed the scalar file.
+// validity words of a block (lanes 0..15: rows base + 32 l .. + 31).  A column without a bitmap gets the plan's
+// all-ones bitmap (dq_plan.cpp), so the load is unconditional: no branch around it for the waitcnt pass to
+// merge.  The 64-bit mask of row group j is then two readlanes: scalar loads of every group's words, hoisted
+// by the compiler, overflowed the scalar file.
 __device__ __forceinline__ uint32_t valid_words(const uint32_t* bm, int64_t base, int64_t n_rows, int lane) {
-  if (!bm) return ~0u;
   // a global load with the word index clamped to the bitmap's last word (words past it belong to rows past
   // n_rows, which `inr` masks): a pointer instead of a four-register descriptor per column
   typedef const __attribute__((address_space(1))) uint32_t* gu32;
@@ -271,14 +271,24 @@ std::string pred_jit_source(const PredProgram& prog, const int32_t* col_kind, st
     return "{ const auto w2 = __builtin_amdgcn_raw_buffer_load_b64(vr" + si + ", (lane + " + soff + " + 64 * " + j +
            ") * 8, 0, 2); " + dst + " = ((uint64_t)w2[1] << 32) | w2[0]; }\n";
   };
+  // the first block's loads in the loop's own issue order (row group by row group, each column's values, the
+  // validity words after row group 0): the waitcnt pass merges the states the loop header is entered with, and
+  // with a different prologue order it had settled on vmcnt(0) at every block's start (the whole next block
+  // waited for before its first row group instead of each row group's own loads)
   for (int i = 0; i < ns; ++i) {
     const std::string si = std::to_string(i);
-    if (need_vals[i]) {
-      s += "  uint64_t v" + si + "[" + G + "];\n";
-      s += "#pragma unroll\n  for (int j = 0; j < " + G + "; ++j) " + load_vals(i, "wave * " + WR, "j", "v" + si + "[j]");
-    }
-    s += "  uint32_t vw" + si + " = valid_words(vb" + si + ", row0 + (int64_t)wave * " + WR + ", A.n_rows, lane), vwn" + si + ";\n";
+    if (need_vals[i]) s += "  uint64_t v" + si + "[" + G + "];\n";
+    s += "  uint32_t vw" + si + ", vwn" + si + ";\n";
   }
+  s += "#pragma unroll\n  for (int j = 0; j < " + G + "; ++j) {\n";
+  for (int i = 0; i < ns; ++i)
+    if (need_vals[i]) s += "    " + load_vals(i, "wave * " + WR, "j", "v" + std::to_string(i) + "[j]");
+  s += "    if (j == 0) {\n";
+  for (int i = 0; i < ns; ++i)
+    s += "      vw" + std::to_string(i) + " = valid_words(vb" + std::to_string(i) + ", row0 + (int64_t)wave * " + WR +
+         ", A.n_rows, lane);\n";
+  // (the machine scheduler would otherwise issue them column by column)
+  s += "    }\n    __builtin_amdgcn_sched_barrier(0);\n  }\n";
   // range-relative rows in 32 bits (scalar loop control and compares)
   s += "  const int32_t nrr = (int32_t)(row1 - row0);\n";
   s += "  for (int32_t rbk = 0; rbk < nrr; rbk += " + BR + ") {\n";
@@ -514,7 +524,7 @@ bool pred_jit_compile_code(const std::string& src, const std::string& arch, std:
 namespace {
 
 // generated-source revision: part of the disk-cache key, so code objects of an older generator are not reused
-constexpr const char* kJitRevision = "dq_pred_jit r4b";
+constexpr const char* kJitRevision = "dq_pred_jit r4c";
 
 uint64_t fnv1a64(const std::string& s, uint64_t h) {
   for (unsigned char c : s) h = (h ^ c) * 0x100000001B3ull;
