@@ -3,6 +3,7 @@
 # the loop-ordered prologue, pipelined Correlation ring), unaligned-LDS probe, the LDS-staged UTF8 variant's
 # string tests, then A/B lines: C5 (r3 base / in-tree / staged UTF8), C4 (r3 base / in-tree), C3 (r4c
 # predicate JIT / in-tree).  Summary lines in gpurun_out/r4f_summary.txt.
+set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"; mkdir -p gpurun_out
 export TMPDIR=/tmp
 S=gpurun_out/r4f_summary.txt
