@@ -9,5 +9,5 @@ mkdir -p build_variants/$NAME
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result "$@" \
   -c deequ_amd/csrc/${SRC:-dq_kernels}.hip -o build_variants/$NAME/${SRC:-dq_kernels}.o
 OBJS=$(ls deequ_amd/build/*.o | grep -v ${SRC:-dq_kernels}.o)
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o build_variants/lib$NAME.so build_variants/$NAME/${SRC:-dq_kernels}.o $OBJS
-echo build_variants/lib$NAME.so
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o build_variants/lib$NAME.so build_variants/$NAME/${SRC:-dq_kernels}.o $OBJS -lhiprtc
+python3 -c "import ctypes; ctypes.CDLL(\"build_variants/lib$NAME.so\")" && echo build_variants/lib$NAME.so
