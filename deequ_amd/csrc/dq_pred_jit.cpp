@@ -191,7 +191,10 @@ bool pred_jit_eligible(const PredProgram& prog, const int32_t* col_kind, int32_t
 // 64-row groups per wave block (<= 8: valid_words loads 16 validity dwords per lane group).  8 groups: 117
 // VGPRs, 4 waves per SIMD, 0.870 ms per 125 M rows of C3; 4 groups (72 VGPRs, 7 waves) 0.871-0.904 ms, 2 groups
 // 0.899-0.923 ms (profiles/r3_pred_ab.txt, r3u)
-constexpr int kJitGroups = 8;
+#ifndef DQ_JIT_GROUPS
+#define DQ_JIT_GROUPS 8
+#endif
+constexpr int kJitGroups = DQ_JIT_GROUPS;  // (A/B builds: -DDQ_JIT_GROUPS=4)
 
 std::string pred_jit_source(const PredProgram& prog, const int32_t* col_kind, std::vector<int32_t>& slot_col,
                             const std::vector<PredJitHll>& hll) {
@@ -405,27 +408,35 @@ std::string pred_jit_source(const PredProgram& prog, const int32_t* col_kind, st
   }
   s += "    __builtin_amdgcn_sched_barrier(0);\n";
   // fused HLL tasks: XXH64 of the slot's raw value (doubleToLongBits for fp64: NaN canonical), exec-masked
-  // register max; the rare low-word rank redone exactly after the block
+  // register max; the rare low-word rank redone exactly after the block.  All the group's hashes first (one
+  // basic block: the scheduler interleaves the independent chains, each a dependent sequence of 64-bit
+  // multiplies), then the register updates (each exec-masked ds_max ends a basic block).
   for (int h = 0; h < nh; ++h) {
     const PredJitHll& e = hll[h];
     const int k = col_kind[slot_col[e.slot]];
     const std::string hs = std::to_string(h), vs = "v" + std::to_string(e.slot) + "[j]";
+    if (k == CK_I32) {
+      s += "    const uint64_t hb" + hs + " = xxh64_int_head((uint32_t)" + vs + ");\n";
+    } else if (k == CK_F64) {
+      s += "    uint64_t raw" + hs + " = " + vs + ";\n";
+      s += "    if (__longlong_as_double((long long)raw" + hs + ") != __longlong_as_double((long long)raw" + hs +
+           ")) raw" + hs + " = 0x7FF8000000000000ull;\n";
+      s += "    const uint64_t hb" + hs + " = xxh64_long_head(raw" + hs + ");\n";
+    } else {
+      s += "    const uint64_t hb" + hs + " = xxh64_long_head(" + vs + ");\n";
+    }
+    s += "    uint32_t addr" + hs + "; int32_t q" + hs + "; hll_key(hb" + hs + ", addr" + hs + ", q" + hs + ");\n";
+  }
+  for (int h = 0; h < nh; ++h) {
+    const PredJitHll& e = hll[h];
+    const std::string hs = std::to_string(h);
     s += "    {\n";
     s += "      const uint64_t sl = va" + std::to_string(e.slot) + " & inr;\n";
     s += "      hc" + hs + " += (uint32_t)__builtin_popcountll(sl);\n";
     s += "      asm volatile(\"\" : \"+s\"(hc" + hs + "));\n";
-    if (k == CK_I32) {
-      s += "      const uint64_t hb = xxh64_int_head((uint32_t)" + vs + ");\n";
-    } else if (k == CK_F64) {
-      s += "      uint64_t raw = " + vs + ";\n";
-      s += "      if (__longlong_as_double((long long)raw) != __longlong_as_double((long long)raw)) raw = 0x7FF8000000000000ull;\n";
-      s += "      const uint64_t hb = xxh64_long_head(raw);\n";
-    } else {
-      s += "      const uint64_t hb = xxh64_long_head(" + vs + ");\n";
-    }
-    s += "      uint32_t addr; int32_t q; hll_key(hb, addr, q);\n";
-    s += "      qmin" + hs + " = q < qmin" + hs + " ? q : qmin" + hs + ";\n";
-    s += "      ds_max_masked(sl, (uint32_t)(uintptr_t)(regs + " + std::to_string(h * 512) + ") + addr, q);\n";
+    s += "      qmin" + hs + " = q" + hs + " < qmin" + hs + " ? q" + hs + " : qmin" + hs + ";\n";
+    s += "      ds_max_masked(sl, (uint32_t)(uintptr_t)(regs + " + std::to_string(h * 512) + ") + addr" + hs + ", q" + hs +
+         ");\n";
     s += "    }\n";
   }
   for (int i = 0; i < ns; ++i)
@@ -524,7 +535,7 @@ bool pred_jit_compile_code(const std::string& src, const std::string& arch, std:
 namespace {
 
 // generated-source revision: part of the disk-cache key, so code objects of an older generator are not reused
-constexpr const char* kJitRevision = "dq_pred_jit r4c";
+constexpr const char* kJitRevision = "dq_pred_jit r4d";
 
 uint64_t fnv1a64(const std::string& s, uint64_t h) {
   for (unsigned char c : s) h = (h ^ c) * 0x100000001B3ull;
