@@ -915,168 +915,6 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
   if constexpr (DT) dtc.flush(s);
 }
 
-#ifndef DQ_STR_LDS
-#define DQ_STR_LDS 0
-#endif
-// UTF8 HLL pass with each row group's string bytes staged through LDS (DQ_STR_LDS=1; int32 offsets, HLL only).
-// Per 64-row group the wave loads the 2 KB of string bytes from the group's first string on -- 16 aligned
-// bytes per lane and load, two loads, coalesced, through a descriptor over [first string & ~15, end of the
-// chunk's bytes) so past the end the range check fills zeros -- two groups ahead into registers, writes them
-// to its own 2 KB LDS slot when the group comes up, and each lane reads its string's 32-byte window from the
-// slot at the string's own byte offset (unaligned ds_read_b128: the gfx950 DS unit takes byte addresses in
-// unaligned mode).  The 7 v_alignbyte per string and the window address arithmetic of utf8_range disappear,
-// and the global loads are 16-byte aligned and contiguous instead of one 32-byte window per lane.  Strings
-// longer than 28 bytes, or whose window leaves the slot (a group spanning more than 2 KB), take the general
-// path after the block as in utf8_range.
-constexpr int kStgBytes = 2048;
-constexpr int kStgAhead = 2;  // groups of string bytes in flight ahead of the one being hashed
-
-template <bool HLL_>
-__device__ void utf8_range_staged(const uint8_t* data, const int32_t* offsets, const uint32_t* validity,
-                                  const uint32_t* mask, int64_t row0, int64_t row1, int64_t n_rows, ColStats& s,
-                                  int32_t* regs, const uint64_t* p5, uint32_t* dq, uint8_t* stg) {
-  static_assert(HLL_, "the staged pass hashes only");
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (row0 >= row1) return;
-  const int64_t span = (int64_t)offsets[n_rows];  // the chunk's string bytes (< 2 GiB for int32 offsets)
-  const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<int32_t*>(offsets + row0), (short)0, (int)((row1 - row0 + 1) * 4), 0x00020000);
-  int64_t cnt_w = 0;
-  int32_t qmin = 0;
-  const auto bp = [p5](uint32_t b) { return p5[b]; };
-  constexpr int kOffRing = 4;
-  int32_t ra[kOffRing], rbv[kOffRing];  // offsets o0, o1 of groups j .. j + 3 (slot = group & 3)
-  auto lane_off = [&](int64_t blk) -> int32_t { return (int32_t)((blk + (int64_t)wave * 512 - row0 + lane) * 4); };
-  auto load_offsets = [&](int32_t vo, int j) {
-    const int q = j & (kOffRing - 1);
-    ra[q] = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(orsrc, vo + j * 256, 0, 0);
-    rbv[q] = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(orsrc, vo + j * 256 + 4, 0, 0);
-  };
-  // a group's bytes: [a, a + 2 KB) with a = its first string's offset & ~15 (lane 0's o0, uniform)
-  u32x4 sa[kStgAhead], sc[kStgAhead];
-  uint32_t sbase[kStgAhead];
-  auto load_group = [&](int q, int jo) __attribute__((always_inline)) {
-    const uint32_t a = (uint32_t)__builtin_amdgcn_readfirstlane(ra[jo & 3]) & ~15u;
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(data + a), (short)0,
-                                                                        (int)(span - (int64_t)a), 0x00020000);
-    sa[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, 0, 2 /* nt */);
-    sc[q] = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16 + 1024, 0, 2 /* nt */);
-    sbase[q] = a;
-  };
-  int32_t vo_cur = lane_off(row0);
-#pragma unroll
-  for (int j = 0; j < kOffRing; ++j) load_offsets(vo_cur, j);
-#pragma unroll
-  for (int q = 0; q < kStgAhead; ++q) load_group(q, q);
-  u32x4* const slot = reinterpret_cast<u32x4*>(stg);
-  uint32_t qtail = 0;
-  auto drain = [&](uint32_t n) __attribute__((always_inline)) {
-    if ((uint32_t)lane < n) {
-      const uint64_t h = ((uint64_t)dq[1 * kDefCap + lane] << 32) | dq[0 * kDefCap + lane];
-      const uint64_t k1 = ((uint64_t)dq[3 * kDefCap + lane] << 32) | dq[2 * kDefCap + lane];
-      const uint64_t b = xxh64_tail_head(xxh64_stripe_round(h, k1), (uint64_t)dq[4 * kDefCap + lane],
-                                         dq[5 * kDefCap + lane], bp);
-      const HllKey key = hll_key_from_fmix(b);
-      if (key.q >= 0) atomicMax(reinterpret_cast<int32_t*>(reinterpret_cast<char*>(regs) + key.addr), key.q);
-      else hll_update(regs, fmix_tail(b));
-    }
-  };
-  auto drain_full = [&]() __attribute__((always_inline)) {
-    drain(64u);
-    const uint32_t rest = qtail - 64u;
-    if ((uint32_t)lane < rest) {
-      uint32_t v[kDefFields];
-#pragma unroll
-      for (int f = 0; f < kDefFields; ++f) v[f] = dq[f * kDefCap + 64 + lane];
-#pragma unroll
-      for (int f = 0; f < kDefFields; ++f) dq[f * kDefCap + lane] = v[f];
-    }
-    qtail = rest;
-  };
-  const int32_t nr = (int32_t)(row1 - row0);
-  for (int32_t rb = 0; rb < nr; rb += kRowsPerIter) {
-    const int64_t blk = row0 + rb;
-    const int64_t base = blk + wave * 512;
-    const int32_t rem = nr - rb - wave * 512;
-    const bool full = rb + kRowsPerIter <= nr;
-    const int32_t vo_next = lane_off(blk + kRowsPerIter);
-    uint64_t m[8];
-    block_masks(validity, mask, base, rem, full, m);
-    uint64_t slow = 0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      // this group's bytes into the wave's slot, then every lane's window out of it (one wave's LDS
-      // operations run in order: the previous group's reads are done before these writes land)
-      slot[lane] = sa[0];
-      slot[64 + lane] = sc[0];
-      const int32_t o0 = ra[j & 3];
-      const uint32_t len = (uint32_t)(rbv[j & 3] - o0);
-      // the string's LDS address: o0 - (staged base - slot address), one VALU for the address and, compared
-      // with the slot's last window start, for the capacity check
-      const uint32_t slot_lds = (uint32_t)(uintptr_t)stg;
-      const uint32_t addr = (uint32_t)o0 - (sbase[0] - slot_lds);
-      const uint8_t __attribute__((address_space(3)))* wp = (const uint8_t __attribute__((address_space(3)))*)(uintptr_t)addr;
-      u32x4 wa, wc;
-      __builtin_memcpy(&wa, (const void*)wp, 16);
-      __builtin_memcpy(&wc, (const void*)(wp + 16), 16);
-      {
-        cnt_w += __builtin_popcountll(m[j]);
-        // fast: at most 28 bytes and the 32-byte window inside the slot
-        const uint64_t fastm = __builtin_amdgcn_uicmp(len, 28u, 37 /* ICMP_ULE */) &
-                               __builtin_amdgcn_uicmp(addr, slot_lds + (uint32_t)(kStgBytes - 32), 37 /* ICMP_ULE */);
-        slow |= m[j] & ~fastm;
-        m[j] &= fastm;
-      }
-      // group + 2's bytes (of the next block for j >= 6; its offsets are in the ring), then group + 4's offsets
-#pragma unroll
-      for (int q = 0; q + 1 < kStgAhead; ++q) {
-        sa[q] = sa[q + 1];
-        sc[q] = sc[q + 1];
-        sbase[q] = sbase[q + 1];
-      }
-      load_group(kStgAhead - 1, j + kStgAhead);
-      if (j + kOffRing < 8) load_offsets(vo_cur, j + kOffRing);
-      else load_offsets(vo_next, j + kOffRing - 8);
-      const uint32_t wv[8] = {wa.x, wa.y, wa.z, wa.w, wc.x, wc.y, wc.z, wc.w};
-      uint64_t d4p;
-      const uint64_t h2 = xxh64_stripes<2>(wv, len, d4p);
-      const uint64_t dm = m[j] & __builtin_amdgcn_ballot_w64(len >= 24u);
-      if (dm != 0) {
-        const uint32_t pos = qtail + __builtin_amdgcn_mbcnt_hi((uint32_t)(dm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dm, 0u));
-        if (lane_bit(dm)) {
-          dq[0 * kDefCap + pos] = (uint32_t)h2;
-          dq[1 * kDefCap + pos] = (uint32_t)(h2 >> 32);
-          dq[2 * kDefCap + pos] = (uint32_t)d4p;
-          dq[3 * kDefCap + pos] = (uint32_t)(d4p >> 32);
-          dq[4 * kDefCap + pos] = wv[6];
-          dq[5 * kDefCap + pos] = len;
-        }
-        qtail += (uint32_t)__builtin_popcountll(dm);
-      }
-      const HllKey key = hll_key_from_fmix(xxh64_tail_head(h2, d4p, len, bp));
-      qmin = min(qmin, key.q);
-      if (lane_bit(m[j] & ~dm)) atomicMax(reinterpret_cast<int32_t*>(reinterpret_cast<char*>(regs) + key.addr), key.q);
-      if (qtail >= 64u) drain_full();
-    }
-    vo_cur = vo_next;
-    if ((slow | __builtin_amdgcn_ballot_w64(qmin < 0)) != 0) {
-      block_masks(validity, mask, base, rem, full, m);
-#pragma unroll 1
-      for (int j = 0; j < 8; ++j) {
-        if (lane_bit(m[j])) {
-          const int64_t row = base + j * 64 + lane;
-          const int64_t o0 = (int64_t)offsets[row], o1 = (int64_t)offsets[row + 1];
-          hll_update(regs, xxh64_bytes(data, o0, o1 - o0));
-        }
-      }
-      qmin = 0;
-    }
-  }
-  if (qtail != 0) drain(qtail);
-  if (lane == 0) s.count += cnt_w;
-}
-
 // DataType of a double column: Spark casts the value to a string with Double.toString, which is
 // plain decimal (matches FRACTIONAL) iff the value is finite and zero or 1e-3 <= |x| < 1e7, and
 // otherwise "NaN", "Infinity" or computerized scientific notation ("1.0E7": a STRING).  Counts the
@@ -1125,7 +963,7 @@ __device__ void run_numeric(const ColTask& t, const ScanCols& cols, const ScanBi
 template <int V>
 __device__ __forceinline__ void run_variant(const ColTask& t, const ScanCols& cols, const uint32_t* mask, int64_t row0,
                                             int64_t row1, int64_t n_rows, ColStats& s, int32_t* regs,
-                                            const uint64_t* p5, uint32_t* dq, uint8_t* stg) {
+                                            const uint64_t* p5, uint32_t* dq) {
   const void* v = cols.values[t.col];
   const uint32_t* val = cols.validity[t.col];
   if constexpr (V == CV_VALIDITY) validity_range(val, mask, row0, row1, s);
@@ -1139,9 +977,6 @@ __device__ __forceinline__ void run_variant(const ColTask& t, const ScanCols& co
   else if constexpr (V == CV_I32_SH) numeric_range<CK_I32, true, true>(v, val, mask, row0, row1, s, regs);
   else if constexpr (V == CV_I32_H) numeric_range<CK_I32, false, true>(v, val, mask, row0, row1, s, regs);
   else if constexpr (V == CV_F64_D) f64_dtype_range(reinterpret_cast<const double*>(v), val, mask, row0, row1, s);
-  else if constexpr (V == CV_UTF8_H && DQ_STR_LDS)
-    utf8_range_staged<true>(reinterpret_cast<const uint8_t*>(v), reinterpret_cast<const int32_t*>(cols.offsets[t.col]),
-                            val, mask, row0, row1, n_rows, s, regs, p5, dq, stg);
   else if constexpr (V == CV_UTF8_H || V == CV_UTF8_D || V == CV_UTF8_HD)
     utf8_range<int32_t, V != CV_UTF8_D, V != CV_UTF8_H>(
         reinterpret_cast<const uint8_t*>(v), reinterpret_cast<const int32_t*>(cols.offsets[t.col]), val, mask, row0,
@@ -1178,8 +1013,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kMinWave
   __shared__ int32_t regs[kHll ? 512 : 1];  // q = pw - 1, -1 = empty (see hll_q_exact)
   __shared__ uint64_t p5[kStr ? 256 : 1];   // b * P5 for the byte rounds of the string hash
   __shared__ uint32_t dfq[kStr ? kWaves * kDefFields * kDefCap : 1];  // deferred 24..28-byte strings
-  constexpr bool kStg = V == CV_UTF8_H && DQ_STR_LDS;
-  __shared__ __attribute__((aligned(16))) uint8_t stg[kStg ? kWaves * kStgBytes : 16];  // staged string bytes
   __shared__ ColStats red[kWaves];
   const int32_t ti = blockIdx.x % ntasks;
   const int32_t range = blockIdx.x / ntasks;
@@ -1196,8 +1029,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kMinWave
   stats_init(s);
   const uint32_t* mask = t.where >= 0 ? reinterpret_cast<const uint32_t*>(bm.where_bits[t.where]) : nullptr;
   run_variant<V>(t, cols, mask, row0, row1, n_rows, s, regs, p5,
-                 dfq + (kStr ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * kDefFields * kDefCap : 0),
-                 stg + (kStg ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * kStgBytes : 0));
+                 dfq + (kStr ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * kDefFields * kDefCap : 0));
   block_reduce_store(s, partials + (size_t)(part_base + ti) * kMaxWG + range, red);
   if constexpr (kHll) {
     // registers only grow: merge into the plan accumulator with device-scope atomicMax, skipping
