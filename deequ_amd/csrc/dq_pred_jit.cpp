@@ -195,6 +195,11 @@ bool pred_jit_eligible(const PredProgram& prog, const int32_t* col_kind, int32_t
 #define DQ_JIT_GROUPS 8
 #endif
 constexpr int kJitGroups = DQ_JIT_GROUPS;  // (A/B builds: -DDQ_JIT_GROUPS=4)
+// what may cross the barrier between a row group's predicate work and its hashing (sched_barrier mask; A/B
+// builds: 2 = VALU may cross)
+#ifndef DQ_JIT_SCHED_MASK
+#define DQ_JIT_SCHED_MASK 0
+#endif
 
 std::string pred_jit_source(const PredProgram& prog, const int32_t* col_kind, std::vector<int32_t>& slot_col,
                             const std::vector<PredJitHll>& hll) {
@@ -406,7 +411,7 @@ std::string pred_jit_source(const PredProgram& prog, const int32_t* col_kind, st
       s += std::string(c ? "," : "") + " \"+s\"(ct" + std::to_string(c) + "), \"+s\"(cn" + std::to_string(c) + ")";
     s += ");\n";
   }
-  s += "    __builtin_amdgcn_sched_barrier(0);\n";
+  s += "    __builtin_amdgcn_sched_barrier(" + std::to_string(DQ_JIT_SCHED_MASK) + ");\n";
   // fused HLL tasks: XXH64 of the slot's raw value (doubleToLongBits for fp64: NaN canonical), exec-masked
   // register max; the rare low-word rank redone exactly after the block.  All the group's hashes first (one
   // basic block: the scheduler interleaves the independent chains, each a dependent sequence of 64-bit
