@@ -196,9 +196,9 @@ bool pred_jit_eligible(const PredProgram& prog, const int32_t* col_kind, int32_t
 #endif
 constexpr int kJitGroups = DQ_JIT_GROUPS;  // (A/B builds: -DDQ_JIT_GROUPS=4)
 // what may cross the barrier between a row group's predicate work and its hashing (sched_barrier mask; A/B
-// builds: 2 = VALU may cross)
+// builds: 0 = nothing crosses; 2 = VALU may cross: 0.838-0.847 vs 0.856-0.869 ms per 125 M rows of C3, r4i)
 #ifndef DQ_JIT_SCHED_MASK
-#define DQ_JIT_SCHED_MASK 0
+#define DQ_JIT_SCHED_MASK 2
 #endif
 
 std::string pred_jit_source(const PredProgram& prog, const int32_t* col_kind, std::vector<int32_t>& slot_col,
@@ -540,7 +540,7 @@ bool pred_jit_compile_code(const std::string& src, const std::string& arch, std:
 namespace {
 
 // generated-source revision: part of the disk-cache key, so code objects of an older generator are not reused
-constexpr const char* kJitRevision = "dq_pred_jit r4d";
+constexpr const char* kJitRevision = "dq_pred_jit r4e";
 
 uint64_t fnv1a64(const std::string& s, uint64_t h) {
   for (unsigned char c : s) h = (h ^ c) * 0x100000001B3ull;
