@@ -38,4 +38,14 @@ def test_generated_kernels_compile(tmp_path):
         vgprs = int(re.search(r"\.vgpr_count:\s+(\d+)", notes).group(1))
         assert scratch == 0, f"{name}: the generated kernel uses scratch ({scratch} bytes)"
         assert vgprs <= 128, f"{name}: {vgprs} VGPRs (< 4 waves per SIMD)"
+    # the next block's loads stay in flight through the block: C3's kernel waits for a row group's own loads
+    # with a good part of the next block still in flight (vmcnt >= 10 of its 36 loads per block), or drains everything
+    # (vmcnt(0): the rare exact-rank redo, the exit) -- the shallow waits (vmcnt(6), (7), (8)) are what a
+    # prologue issued out of the loop's order left at every block's start (the waitcnt pass merges the loop
+    # header's entry states; round 4)
+    objdump = os.path.join(os.path.dirname(READELF), "llvm-objdump")
+    dis = subprocess.run([objdump, "-d", "--mcpu=gfx950", str(tmp_path / "c3.co")], capture_output=True, text=True,
+                         check=True).stdout
+    waits = [int(x) for x in re.findall(r"s_waitcnt vmcnt\((\d+)\)", dis)]
+    assert waits and not [w for w in waits if 0 < w < 10], sorted(set(waits))
     shutil.rmtree(tmp_path, ignore_errors=True)
