@@ -1,0 +1,12 @@
+#!/bin/bash
+# round-4 GPU call 11 (final evidence, part 2): full GPU suite, smoke(), then bench.py with default arguments.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(pwd)}"; mkdir -p gpurun_out
+export TMPDIR=/tmp
+S=gpurun_out/r4z_summary.txt
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --durations=12 --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/r4z_pytest.log 2>&1
+rc=$?; tail -2 gpurun_out/r4z_pytest.log | tee $S; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/r4z_smoke.txt 2>&1
+rc=$?; tail -2 gpurun_out/r4z_smoke.txt | tee -a $S; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 700 python -u bench.py > gpurun_out/r4z_bench.json 2> gpurun_out/r4z_bench.err
+rc=$?; tail -c 600 gpurun_out/r4z_bench.json | tee -a $S; [ $rc -eq 0 ] || { tail -5 gpurun_out/r4z_bench.err; exit $rc; }
