@@ -279,13 +279,60 @@ double key_to_double(int32_t type, uint64_t key) {
   return (double)(int64_t)(key ^ 0x8000000000000000ull);
 }
 
-// The order keys of a chunk's non-null values appended to keys[*cursor ...] (order free: they are sorted next);
-// one 64-bit atomic per wave.
+// ---- the digest's multi-rank select (dq_quantile_digest): every sample rank of the digest in two passes over
+// the column.  Splitters from an evenly spaced sample of the keys cut the key range into kDBuckets buckets of
+// about equal population; pass 1 counts each bucket's keys, the host finds the bucket of every sample rank,
+// pass 2 compacts the keys of those buckets only (about m / kDBuckets of the column for m samples) and one
+// radix sort of that small set gives every sample rank's exact key.  A skewed column (one value in most
+// rows) only makes a target bucket larger: the sort then covers it, still exactly.
+constexpr int kDBuckets = 2048;              // buckets (kDBuckets - 1 splitters, a branchless 11-step search)
+constexpr int kDSample = 16384;              // keys sampled for the splitters
+
+// the key of row i * n / m of a chunk (i < m), and whether the row is non-null
 template <int TYPE>
-__global__ __launch_bounds__(kQBlock) void dq_digest_keys(const void* __restrict__ values,
+__global__ __launch_bounds__(kQBlock) void dq_digest_sample(const void* __restrict__ values,
+                                                            const uint32_t* __restrict__ validity, int64_t n, int64_t m,
+                                                            unsigned long long* __restrict__ keys,
+                                                            unsigned char* __restrict__ ok) {
+  const int64_t i = (int64_t)blockIdx.x * kQBlock + threadIdx.x;
+  if (i >= m) return;
+  const int64_t r = i * (n / m) + (i * (n % m)) / m;  // floor(i n / m) without 128-bit products (m <= 16384)
+  uint64_t raw;
+  if constexpr (TYPE == DQ_TYPE_I32) raw = (uint32_t)reinterpret_cast<const int32_t*>(values)[r];
+  else raw = reinterpret_cast<const uint64_t*>(values)[r];
+  keys[i] = order_key<TYPE>(raw);
+  ok[i] = validity ? (unsigned char)((validity[r >> 5] >> (r & 31)) & 1u) : (unsigned char)1;
+}
+
+// bucket of a key: the number of splitters <= key (spl: kDBuckets - 1 sorted keys in LDS)
+__device__ __forceinline__ uint32_t digest_bucket(const unsigned long long* spl, uint64_t key) {
+  uint32_t pos = 0;
+#pragma unroll
+  for (uint32_t step = kDBuckets / 2; step >= 1; step >>= 1)
+    if (spl[pos + step - 1] <= key) pos += step;
+  return pos;
+}
+
+// Pass over a chunk: COUNT -- per-bucket key counts into counts[kDBuckets]; else the keys of the flagged
+// buckets appended to cand[*cursor ...] (order free: sorted next; one 64-bit atomic per wave).
+template <int TYPE, bool COUNT>
+__global__ __launch_bounds__(kQBlock) void dq_digest_pass(const void* __restrict__ values,
                                                           const uint32_t* __restrict__ validity, int64_t n,
-                                                          unsigned long long* __restrict__ keys,
+                                                          const unsigned long long* __restrict__ splitters,
+                                                          unsigned long long* __restrict__ counts,
+                                                          const unsigned char* __restrict__ target,
+                                                          unsigned long long* __restrict__ cand,
                                                           unsigned long long* __restrict__ cursor) {
+  __shared__ unsigned long long spl[kDBuckets - 1];
+  __shared__ uint32_t hist[COUNT ? kDBuckets : 1];
+  __shared__ unsigned char tgt[COUNT ? 1 : kDBuckets];
+  for (int i = threadIdx.x; i < kDBuckets - 1; i += kQBlock) spl[i] = splitters[i];
+  if constexpr (COUNT) {
+    for (int i = threadIdx.x; i < kDBuckets; i += kQBlock) hist[i] = 0;
+  } else {
+    for (int i = threadIdx.x; i < kDBuckets; i += kQBlock) tgt[i] = target[i];
+  }
+  __syncthreads();
   const int lane = threadIdx.x & 63;
   for (int64_t r0 = (int64_t)blockIdx.x * kQBlock; r0 < n; r0 += (int64_t)gridDim.x * kQBlock) {
     const int64_t r = r0 + threadIdx.x;
@@ -293,26 +340,36 @@ __global__ __launch_bounds__(kQBlock) void dq_digest_keys(const void* __restrict
     uint64_t raw = 0;
     if (ok) {
       if (validity) ok = (validity[r >> 5] >> (r & 31)) & 1u;
-      if constexpr (TYPE == DQ_TYPE_I32) raw = (uint32_t)reinterpret_cast<const int32_t*>(values)[r];
-      else raw = reinterpret_cast<const uint64_t*>(values)[r];
+      if constexpr (TYPE == DQ_TYPE_I32) raw = (uint32_t)__builtin_nontemporal_load(reinterpret_cast<const int32_t*>(values) + r);
+      else raw = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(values) + r);
     }
-    const uint64_t b = __builtin_amdgcn_ballot_w64(ok);
-    if (b == 0) continue;
-    const int first = __builtin_ctzll(b);
-    unsigned long long base = 0;
-    if (lane == first) base = atomicAdd(cursor, (unsigned long long)__builtin_popcountll(b));
-    base = __shfl(base, first);
-    if (ok) keys[base + __builtin_popcountll(b & ((1ull << lane) - 1ull))] = order_key<TYPE>(raw);
+    const uint64_t key = order_key<TYPE>(raw);
+    const uint32_t bk = digest_bucket(spl, key);
+    if constexpr (COUNT) {
+      if (ok) atomicAdd(&hist[bk], 1u);
+    } else {
+      const bool take = ok && tgt[bk];
+      const uint64_t bal = __builtin_amdgcn_ballot_w64(take);
+      if (bal == 0) continue;
+      const int first = __builtin_ctzll(bal);
+      unsigned long long base = 0;
+      if (lane == first) base = atomicAdd(cursor, (unsigned long long)__builtin_popcountll(bal));
+      base = __shfl(base, first);
+      if (take) cand[base + __builtin_popcountll(bal & ((1ull << lane) - 1ull))] = key;
+    }
+  }
+  if constexpr (COUNT) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < kDBuckets; i += kQBlock)
+      if (hist[i]) atomicAdd(&counts[i], (unsigned long long)hist[i]);
   }
 }
 
-// out[i] = the sorted key at 1-based rank 1 + i * s (the last sample at rank n)
-__global__ void dq_digest_gather(const unsigned long long* __restrict__ sorted, int64_t n, int64_t s, int64_t m,
-                                 unsigned long long* __restrict__ out) {
+// out[i] = sorted[idx[i]]
+__global__ void dq_digest_gather(const unsigned long long* __restrict__ sorted, const long long* __restrict__ idx,
+                                 int64_t m, unsigned long long* __restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= m) return;
-  const int64_t rank = i == m - 1 ? n : 1 + i * s;
-  out[i] = sorted[rank - 1];
+  if (i < m) out[i] = sorted[idx[i]];
 }
 
 }  // namespace
@@ -513,32 +570,69 @@ dq_status dq_quantile_digest(int32_t type, const dq_column_view* cols, const int
   QHIP(hipSetDevice(device));
   hipStream_t stream = reinterpret_cast<hipStream_t>(hip_stream);
   if (total == 0) return DQ_OK;
-  // every non-null value's order key, compacted (one pass over the column), then one radix sort of the keys
-  DevHist keys, sorted, cursor, tmp;
-  QHIP(hipMalloc(&keys.p, (size_t)total * 8));
-  QHIP(hipMalloc(&sorted.p, (size_t)total * 8));
-  QHIP(hipMalloc(&cursor.p, 8));
-  QHIP(hipMemsetAsync(cursor.p, 0, 8, stream));
+  auto for_chunks = [&](auto&& launch) -> dq_status {
+    for (int c = 0; c < n_chunks; ++c) {
+      const int64_t rows = chunk_rows[c];
+      if (rows == 0) continue;
+      const int grid = (int)std::min<int64_t>(4096, (rows + kQBlock - 1) / kQBlock);
+      auto go = [&](auto kern) { launch(kern, grid, c, rows); };
+      if (type == DQ_TYPE_F64) go(std::integral_constant<int, DQ_TYPE_F64>{});
+      else if (type == DQ_TYPE_I64) go(std::integral_constant<int, DQ_TYPE_I64>{});
+      else go(std::integral_constant<int, DQ_TYPE_I32>{});
+      QHIP(hipGetLastError());
+    }
+    return DQ_OK;
+  };
+  // 1. splitters from an evenly spaced sample of every chunk's rows (nulls dropped on the host)
+  std::vector<int64_t> s_off((size_t)n_chunks + 1, 0);
   for (int c = 0; c < n_chunks; ++c) {
-    const int64_t rows = chunk_rows[c];
-    if (rows == 0) continue;
-    const auto* val = reinterpret_cast<const uint32_t*>(cols[c].validity);
-    const int grid = (int)std::min<int64_t>(8192, (rows + kQBlock - 1) / kQBlock);
-    if (type == DQ_TYPE_F64)
-      hipLaunchKernelGGL(dq_digest_keys<DQ_TYPE_F64>, dim3(grid), dim3(kQBlock), 0, stream, cols[c].values, val, rows,
-                         keys.p, cursor.p);
-    else if (type == DQ_TYPE_I64)
-      hipLaunchKernelGGL(dq_digest_keys<DQ_TYPE_I64>, dim3(grid), dim3(kQBlock), 0, stream, cols[c].values, val, rows,
-                         keys.p, cursor.p);
-    else
-      hipLaunchKernelGGL(dq_digest_keys<DQ_TYPE_I32>, dim3(grid), dim3(kQBlock), 0, stream, cols[c].values, val, rows,
-                         keys.p, cursor.p);
-    QHIP(hipGetLastError());
+    const int64_t want = chunk_rows[c] == 0 ? 0 : std::max<int64_t>(1, (int64_t)((double)kDSample * chunk_rows[c] / total));
+    s_off[(size_t)c + 1] = s_off[(size_t)c] + std::min<int64_t>(want, chunk_rows[c]);
   }
-  unsigned long long n_ull = 0;
-  QHIP(hipMemcpyAsync(&n_ull, cursor.p, 8, hipMemcpyDeviceToHost, stream));
+  const int64_t ns_all = s_off[(size_t)n_chunks];
+  DevHist d_sample, d_ok, d_spl, d_counts, d_target, d_cursor, d_cand, d_sorted, d_tmp, d_idx;
+  QHIP(hipMalloc(&d_sample.p, (size_t)ns_all * 8));
+  QHIP(hipMalloc(&d_ok.p, (size_t)ns_all));
+  if (dq_status st = for_chunks([&](auto tk, int grid, int c, int64_t rows) {
+        (void)grid;
+        const int64_t mc = s_off[(size_t)c + 1] - s_off[(size_t)c];
+        hipLaunchKernelGGL((dq_digest_sample<decltype(tk)::value>), dim3((unsigned)((mc + kQBlock - 1) / kQBlock)),
+                           dim3(kQBlock), 0, stream, cols[c].values, reinterpret_cast<const uint32_t*>(cols[c].validity),
+                           rows, mc, d_sample.p + s_off[(size_t)c],
+                           reinterpret_cast<unsigned char*>(d_ok.p) + s_off[(size_t)c]);
+      }))
+    return st;
+  std::vector<unsigned long long> samp((size_t)ns_all);
+  std::vector<unsigned char> sok((size_t)ns_all);
+  QHIP(hipMemcpyAsync(samp.data(), d_sample.p, (size_t)ns_all * 8, hipMemcpyDeviceToHost, stream));
+  QHIP(hipMemcpyAsync(sok.data(), d_ok.p, (size_t)ns_all, hipMemcpyDeviceToHost, stream));
   QHIP(hipStreamSynchronize(stream));
-  const int64_t n = (int64_t)n_ull;
+  size_t nv = 0;
+  for (size_t i = 0; i < samp.size(); ++i)
+    if (sok[i]) samp[nv++] = samp[i];
+  samp.resize(nv);
+  std::sort(samp.begin(), samp.end());
+  std::vector<unsigned long long> spl(kDBuckets - 1, ~0ull);  // no sample: one bucket holds every key
+  for (int k = 1; k < kDBuckets && nv > 0; ++k) spl[(size_t)k - 1] = samp[(size_t)k * nv / kDBuckets];
+  QHIP(hipMalloc(&d_spl.p, (size_t)(kDBuckets - 1) * 8));
+  QHIP(hipMalloc(&d_counts.p, (size_t)kDBuckets * 8));
+  QHIP(hipMalloc(&d_target.p, (size_t)kDBuckets));
+  QHIP(hipMalloc(&d_cursor.p, 8));
+  QHIP(hipMemcpyAsync(d_spl.p, spl.data(), (size_t)(kDBuckets - 1) * 8, hipMemcpyHostToDevice, stream));
+  QHIP(hipMemsetAsync(d_counts.p, 0, (size_t)kDBuckets * 8, stream));
+  QHIP(hipMemsetAsync(d_cursor.p, 0, 8, stream));
+  // 2. per-bucket counts
+  if (dq_status st = for_chunks([&](auto tk, int grid, int c, int64_t rows) {
+        hipLaunchKernelGGL((dq_digest_pass<decltype(tk)::value, true>), dim3(grid), dim3(kQBlock), 0, stream,
+                           cols[c].values, reinterpret_cast<const uint32_t*>(cols[c].validity), rows, d_spl.p,
+                           d_counts.p, nullptr, nullptr, nullptr);
+      }))
+    return st;
+  std::vector<unsigned long long> cnt((size_t)kDBuckets);
+  QHIP(hipMemcpyAsync(cnt.data(), d_counts.p, (size_t)kDBuckets * 8, hipMemcpyDeviceToHost, stream));
+  QHIP(hipStreamSynchronize(stream));
+  int64_t n = 0;
+  for (unsigned long long x : cnt) n += (int64_t)x;
   *count = n;
   if (n == 0) return DQ_OK;  // all values NULL: no digest
   // the digest's sample ranks (deequ_amd/quantiles.py digest_ranks): 1, 1 + s, ..., n, s = max(1, floor(2 e n))
@@ -546,21 +640,55 @@ dq_status dq_quantile_digest(int32_t type, const dq_column_view* cols, const int
   const int64_t m = (n - 1) / s + 1 + ((n - 1) % s != 0 ? 1 : 0);
   *n_samples = m;
   if (m > cap) return set_error(DQ_E_INVALID, "dq_quantile_digest: %lld samples, room for %lld", (long long)m, (long long)cap);
+  // 3. the bucket of every sample rank; the flagged buckets' keys are the candidates, in bucket (= key) order
+  std::vector<int64_t> before((size_t)kDBuckets + 1, 0);
+  for (int b = 0; b < kDBuckets; ++b) before[(size_t)b + 1] = before[(size_t)b] + (int64_t)cnt[(size_t)b];
+  std::vector<unsigned char> tgt((size_t)kDBuckets, 0);
+  std::vector<int64_t> rank((size_t)m);
+  std::vector<int> rb((size_t)m);
+  for (int64_t i = 0, b = 0; i < m; ++i) {
+    rank[(size_t)i] = i == m - 1 ? n : 1 + i * s;
+    while (before[(size_t)b + 1] < rank[(size_t)i]) ++b;  // ranks ascend: bucket b holds ranks (before[b], before[b + 1]]
+    rb[(size_t)i] = (int)b;
+    tgt[(size_t)b] = 1;
+  }
+  std::vector<int64_t> cand_before((size_t)kDBuckets + 1, 0);
+  for (int b = 0; b < kDBuckets; ++b)
+    cand_before[(size_t)b + 1] = cand_before[(size_t)b] + (tgt[(size_t)b] ? (int64_t)cnt[(size_t)b] : 0);
+  const int64_t nc = cand_before[(size_t)kDBuckets];
   // (hipCUB's item count is an int here, as in the grouping pass)
-  if (n > (int64_t)0x7FFFFFFF)
-    return set_error(DQ_E_UNSUPPORTED, "dq_quantile_digest: %lld values (at most 2^31 - 1)", (long long)n);
+  if (nc > (int64_t)0x7FFFFFFF)
+    return set_error(DQ_E_UNSUPPORTED, "dq_quantile_digest: %lld candidate values (at most 2^31 - 1)", (long long)nc);
+  QHIP(hipMemcpyAsync(d_target.p, tgt.data(), (size_t)kDBuckets, hipMemcpyHostToDevice, stream));
+  QHIP(hipMalloc(&d_cand.p, (size_t)nc * 8));
+  QHIP(hipMalloc(&d_sorted.p, (size_t)nc * 8));
+  if (dq_status st = for_chunks([&](auto tk, int grid, int c, int64_t rows) {
+        hipLaunchKernelGGL((dq_digest_pass<decltype(tk)::value, false>), dim3(grid), dim3(kQBlock), 0, stream,
+                           cols[c].values, reinterpret_cast<const uint32_t*>(cols[c].validity), rows, d_spl.p, nullptr,
+                           reinterpret_cast<const unsigned char*>(d_target.p), d_cand.p, d_cursor.p);
+      }))
+    return st;
   size_t tb = 0;
-  QHIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, keys.p, sorted.p, (int)n, 0, 64, stream));
-  QHIP(hipMalloc(&tmp.p, std::max<size_t>(tb, 8)));
-  QHIP(hipcub::DeviceRadixSort::SortKeys(tmp.p, tb, keys.p, sorted.p, (int)n, 0, 64, stream));
-  hipLaunchKernelGGL(dq_digest_gather, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, stream, sorted.p, n, s, m, keys.p);
+  QHIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, d_cand.p, d_sorted.p, (int)nc, 0, 64, stream));
+  QHIP(hipMalloc(&d_tmp.p, std::max<size_t>(tb, 8)));
+  QHIP(hipcub::DeviceRadixSort::SortKeys(d_tmp.p, tb, d_cand.p, d_sorted.p, (int)nc, 0, 64, stream));
+  // 4. sample i = the sorted candidate at (its rank within its bucket) + (candidates of the flagged buckets before)
+  std::vector<long long> idx((size_t)m);
+  for (int64_t i = 0; i < m; ++i) {
+    const int b = rb[(size_t)i];
+    idx[(size_t)i] = (long long)(rank[(size_t)i] - 1 - before[(size_t)b] + cand_before[(size_t)b]);
+  }
+  QHIP(hipMalloc(&d_idx.p, (size_t)m * 8));
+  QHIP(hipMemcpyAsync(d_idx.p, idx.data(), (size_t)m * 8, hipMemcpyHostToDevice, stream));
+  hipLaunchKernelGGL(dq_digest_gather, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, stream, d_sorted.p,
+                     reinterpret_cast<const long long*>(d_idx.p), m, d_cand.p);
   QHIP(hipGetLastError());
   std::vector<unsigned long long> got((size_t)m);
-  QHIP(hipMemcpyAsync(got.data(), keys.p, (size_t)m * 8, hipMemcpyDeviceToHost, stream));
+  QHIP(hipMemcpyAsync(got.data(), d_cand.p, (size_t)m * 8, hipMemcpyDeviceToHost, stream));
   QHIP(hipStreamSynchronize(stream));
   for (int64_t i = 0; i < m; ++i) {
     values[i] = key_to_double(type, got[(size_t)i]);
-    ranks[i] = i == m - 1 ? n : 1 + i * s;
+    ranks[i] = rank[(size_t)i];
   }
   return DQ_OK;
 }

@@ -45,7 +45,8 @@ def main():
         gbs = (8 + 1 / 8) * n / (ms * 1e-3) / 1e9
         print(f"quantiles={len(qs)} rows={n:.3g} ms={ms:.3f} rows/s={n / (ms * 1e-3):.4g} "
               f"column-read-equivalent GB/s={gbs:.0f} first={r[0]:.6g}", flush=True)
-    # ApproxQuantileState's digest: one compaction + radix sort + gather for all 1 / (2 e) + 2 sample ranks
+    # ApproxQuantileState's digest: every 1 / (2 e) + 2 sample ranks in two passes (bucket counts against sampled
+    # splitters, then the flagged buckets' keys compacted and sorted)
     from deequ_amd.quantiles import device_digest
 
     if n <= (1 << 31) - 1:

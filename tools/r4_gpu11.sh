@@ -1,5 +1,6 @@
 #!/bin/bash
-# round-4 GPU call 11 (final evidence, part 2): full GPU suite, smoke(), then bench.py with default arguments.
+# round-4 GPU call 11 (final evidence, part 2): full GPU suite, smoke(), the quantile / digest timing at 1e8 rows, then
+# bench.py with default arguments.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"; mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -8,5 +9,7 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --durations=12 --timeou
 rc=$?; tail -2 gpurun_out/r4z_pytest.log | tee $S; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/r4z_smoke.txt 2>&1
 rc=$?; tail -2 gpurun_out/r4z_smoke.txt | tee -a $S; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u tools/quantile_bench.py --rows 1e8 > gpurun_out/r4z_quantile_bench.txt 2>&1
+rc=$?; tail -5 gpurun_out/r4z_quantile_bench.txt | tee -a $S; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 700 python -u bench.py > gpurun_out/r4z_bench.json 2> gpurun_out/r4z_bench.err
 rc=$?; tail -c 600 gpurun_out/r4z_bench.json | tee -a $S; [ $rc -eq 0 ] || { tail -5 gpurun_out/r4z_bench.err; exit $rc; }
