@@ -372,9 +372,10 @@ void dq_freq_destroy(dq_freq_table* t);
 dq_status dq_approx_quantiles(int32_t type, const dq_column_view* cols, const int64_t* chunk_rows, int32_t n_chunks,
                               const double* quantiles, int32_t n_q, double relative_error, int32_t device,
                               void* hip_stream, double* out, int64_t* count);
-/* ApproxQuantileState's digest (ApproxQuantile.scala:28-35, 69-80) in one pass: every non-null value's order
- * key compacted, radix-sorted once (Double.compare order: NaN largest, -0.0 < 0.0), and the values at the
- * 1-based ranks 1, 1 + s, 1 + 2 s, ..., n with s = max(1, floor(2 relative_error n)) -- the samples of a
+/* ApproxQuantileState's digest (ApproxQuantile.scala:28-35, 69-80), every sample rank in two passes over the
+ * column: the order keys (Double.compare order: NaN largest, -0.0 < 0.0) counted per bucket against splitters
+ * from an evenly spaced sample, then only the buckets holding a sample rank compacted and radix-sorted; the
+ * values at the 1-based ranks 1, 1 + s, 1 + 2 s, ..., n with s = max(1, floor(2 relative_error n)) -- the samples of a
  * QuantileSummaries with exact ranks (g = rank gaps, delta = 0; deequ_amd/quantiles.py).  *count = n
  * (0: every value NULL, no samples); *n_samples = the number of samples; DQ_E_INVALID when it exceeds cap
  * (call again with a larger buffer; relative_error 0 samples every value). */
