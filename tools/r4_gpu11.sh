@@ -13,3 +13,5 @@ timeout -k 10 300 python -u tools/quantile_bench.py --rows 1e8 > gpurun_out/r4z_
 rc=$?; tail -5 gpurun_out/r4z_quantile_bench.txt | tee -a $S; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 700 python -u bench.py > gpurun_out/r4z_bench.json 2> gpurun_out/r4z_bench.err
 rc=$?; tail -c 600 gpurun_out/r4z_bench.json | tee -a $S; [ $rc -eq 0 ] || { tail -5 gpurun_out/r4z_bench.err; exit $rc; }
+# diagnostic: the Correlation ring without its per-slot barrier (libnobar, results wrong) vs the in-tree pass on C4
+CFG=c4 SKIP_TESTS=1 TAG=r4j4 bash tools/ab_c3.sh deequ_amd/libdqscan.so build_variants/libnobar.so deequ_amd/libdqscan.so build_variants/libnobar.so | tee gpurun_out/r4j_summary.txt
