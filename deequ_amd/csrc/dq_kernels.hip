@@ -695,14 +695,6 @@ constexpr int kStrAhead = DQ_STR_AHEAD;  // string windows in flight ahead of th
 constexpr uint32_t kDefCap = 128;  // < 64 left after a drain + <= 64 pushed per row group
 constexpr int kDefFields = 6;      // h lo, h hi, w4, w5, w6, len
 
-// A/B switches of the UTF8 pass (diagnostic builds, tools/build_variant.sh): round-3 forms of the offsets loads
-// (row offset in soffset) and of the window check (a compare on every row instead of a per-range branch)
-#ifndef DQ_UTF8_SOFF
-#define DQ_UTF8_SOFF 0
-#endif
-#ifndef DQ_UTF8_WCHK
-#define DQ_UTF8_WCHK 0
-#endif
 template <typename OffT, bool HLL, bool DT>
 __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint32_t* validity,
                            const uint32_t* mask, int64_t row0, int64_t row1, int64_t n_rows, ColStats& s,
@@ -738,13 +730,11 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
   // 64 j W bytes in the instruction's immediate offset): the descriptor's range check covers voffset +
   // immediate, so the next block's prefetch past the range's last row reads 0 -- nothing past the offsets
   auto lane_off = [&](int64_t blk) -> int32_t { return (int32_t)((blk + (int64_t)wave * 512 - row0 + lane) * W); };
-  auto load_offsets = [&](int32_t vo, int j, int64_t blk) {
+  // (round 4 A/B, profiles/r4_ab.txt r4g: the round-3 form with the row offset in soffset measured 1.916-1.919 vs
+  // 1.902-1.907 ms per 125 M rows x 4)
+  auto load_offsets = [&](int32_t vo, int j) {
     const int q = j & (kOffRing - 1);
-    if constexpr (W == 4 && DQ_UTF8_SOFF) {  // A/B: round-3 form, row offset in soffset
-      const int soff = (int)((blk + (int64_t)wave * 512 - row0 + j * 64) * W);
-      ra[q] = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(orsrc, lane * 4, soff, 0);
-      rb[q] = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(orsrc, lane * 4 + 4, soff, 0);
-    } else if constexpr (W == 4) {
+    if constexpr (W == 4) {
       ra[q] = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(orsrc, vo + j * 256, 0, 0);
       rb[q] = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(orsrc, vo + j * 256 + 4, 0, 0);
     } else {
@@ -756,7 +746,7 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
   };
   int32_t vo_cur = lane_off(row0);
 #pragma unroll
-  for (int j = 0; j < kOffRing; ++j) load_offsets(vo_cur, j, row0);
+  for (int j = 0; j < kOffRing; ++j) load_offsets(vo_cur, j);
   // o0 rel. to the window (low 2 bits = the string's byte alignment) and len of the row in slot j & 3
   auto rel_of = [&](int j) -> uint32_t {
     const int q = j & (kOffRing - 1);
@@ -824,9 +814,8 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
         // the compares' own masks (llvm.amdgcn.icmp; signedness from the predicate) ANDed in SGPRs: a
         // ballot of the combined bool materialises it in a VGPR and compares again (2 VALU per row)
         uint64_t fastm = __builtin_amdgcn_uicmp(len_of(j), 28u, 37 /* ICMP_ULE */);
-        if constexpr (DQ_UTF8_WCHK) {  // A/B: round-3 form, the window compare on every row, no branch
-          fastm &= __builtin_amdgcn_uicmp(rel_of(j), (uint32_t)win3, 41 /* ICMP_SLE: signed */);
-        } else if (!wins_in) {  // a uniform branch (the chunk's last range): the compare, in asm so it is not hoisted
+        // (the round-3 compare on every row, no branch: 1.911-1.915 vs 1.902-1.907 ms, r4g)
+        if (!wins_in) {  // a uniform branch (the chunk's last range): the compare, in asm so it is not hoisted
           uint64_t wm;
           asm volatile("v_cmp_le_i32_e64 %0, %1, %2" : "=s"(wm) : "v"(rel_of(j)), "s"(win3));
           fastm &= wm;
@@ -877,8 +866,8 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
         if (qtail >= 64u) drain_full();
       }
       // row j + 4 into the slot row j frees (of the next block for j >= 4)
-      if (j + kOffRing < 8) load_offsets(vo_cur, j + kOffRing, blk);
-      else load_offsets(vo_next, j + kOffRing - 8, blk + kRowsPerIter);
+      if (j + kOffRing < 8) load_offsets(vo_cur, j + kOffRing);
+      else load_offsets(vo_next, j + kOffRing - 8);
 #pragma unroll
       for (int q = 0; q + 1 < kStrAhead; ++q) {
         win_a[q] = win_a[q + 1];
