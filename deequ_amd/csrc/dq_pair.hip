@@ -129,28 +129,8 @@ __device__ double range_shift(const char* col, int kind, const uint32_t* vb, con
 constexpr int kRing = 4;
 constexpr int kSlotBytes = 8 * 1024 + 256;
 constexpr int kSlotMaskWord = 8 * 256;  // dword index of the selection words in a slot
-constexpr uint32_t kSlotSeqByte = kSlotMaskWord * 4 + 192;  // DQ_PAIR_FLAGS: the waves' sequence words of a slot
 // the fp64 ring without Min / Max reads each slot into registers one slot ahead (round 4); 0 = the round-3
 // loop (kept for A/B builds: -DDQ_PAIR_PIPE=0)
-// A/B (-DDQ_PAIR_FLAGS=1): the pipelined ring's per-slot s_barrier replaced by LDS flags -- each wave's DMA of
-// a slot ends with a sequence word (from kSlotSeq) landing after its data, each wave publishes the slots it
-// has consumed, and a wave waits only for the partner state it needs (that slot's data, or the ring
-// position it restages), so the two waves may drift a slot apart
-#ifndef DQ_PAIR_FLAGS
-#define DQ_PAIR_FLAGS 0
-#endif
-struct SlotSeq {
-  uint32_t v[4096];
-  constexpr SlotSeq() : v() {
-    for (int i = 0; i < 4096; ++i) v[i] = (uint32_t)i + 1;
-  }
-};
-__device__ const SlotSeq kSlotSeq = SlotSeq();
-// diagnostic only (results wrong): the pipelined ring without its per-slot barrier, each wave waiting for its
-// own loads alone -- the time the waves' lock-step costs (-DDQ_PAIR_NOBAR=1)
-#ifndef DQ_PAIR_NOBAR
-#define DQ_PAIR_NOBAR 0
-#endif
 #ifndef DQ_PAIR_PIPE
 #define DQ_PAIR_PIPE 1
 #endif
@@ -468,27 +448,6 @@ __device__ __forceinline__ bool pair_range(const PairWaveTask& T, const ScanCols
           : [vo] "v"(voff), [d] "s"(d), [dm] "s"(dm), [me] "s"(mexec), [b0] "s"(dp[0]), [b1] "s"(dp[1]),
             [b2] "s"(dp[2]), [b3] "s"(dp[3]), [ma] "v"(ma)
           : "memory", "scc");
-      if constexpr (DQ_PAIR_FLAGS) {
-        // the slot's sequence word, by lane 0, after the data: the partner polls it (loads return in order)
-        const uint64_t sqa = (uint64_t)(uintptr_t)&kSlotSeq.v[sc & 4095u];
-        const uint32_t* sq = (const uint32_t*)(uintptr_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(
-                                                               (uint32_t)(sqa >> 32)) << 32) |
-                                                           (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)sqa));
-        const uint32_t dsq = __builtin_amdgcn_readfirstlane(lds0 + slot * (uint32_t)kSlotBytes + kSlotSeqByte +
-                                                            (uint32_t)wave * 4u);
-        asm volatile(
-            "s_mov_b32 %[keep], m0\n\t"
-            "s_mov_b64 %[sv], exec\n\t"
-            "s_mov_b64 exec, 1\n\t"
-            "s_mov_b32 m0, %[d]\n\t"
-            "s_nop 0\n\t"
-            "global_load_lds_dword %[z], %[b]\n\t"
-            "s_mov_b64 exec, %[sv]\n\t"
-            "s_mov_b32 m0, %[keep]"
-            : [keep] "=&s"(keep), [sv] "=&s"(sv)
-            : [z] "v"(0u), [d] "s"(dsq), [b] "s"(sq)
-            : "memory", "scc");
-      }
     };
     if constexpr (kPairPipe && !MINMAX) {
       // ---- pipelined ring (round 4): a slot's values and selection words are read into registers one slot
@@ -496,7 +455,8 @@ __device__ __forceinline__ bool pair_range(const PairWaveTask& T, const ScanCols
       // sits between the two halves.  Iteration s: fold group 0 of slot s; wait until this wave's slot s
       // registers and its own DMA of slot s + 1 have landed; s_barrier (past it the partner holds slot s in
       // registers and its DMA of slot s + 1 has landed); DMA slot s + kRing into slot s's ring position; read
-      // slot s + 1; fold group 1 of slot s.  Branch-free addressing: position p reads ring column
+      // slot s + 1; fold group 1 of slot s.  (The barrier is not what limits the pass: a diagnostic build
+      // without it -- results wrong -- ran 1.554-1.556 vs 1.535-1.536 ms per 125 M rows, r4j.)  Branch-free addressing: position p reads ring column
       // (p + wave) % 8, i.e. positions 0-6 at xa + 128 p and position 7 at xb.
       const int64_t* xa = ring + lane + wave * 128;
       const int64_t* xb = ring + lane + (wave == 0 ? 7 * 128 : 0);
@@ -554,100 +514,14 @@ __device__ __forceinline__ bool pair_range(const PairWaveTask& T, const ScanCols
           // issued after slot s + 1: slots s + 2 .. min(s + kRing - 1, ns - 1)
           const int32_t last = s + kRing - 1 < ns - 1 ? s + kRing - 1 : ns - 1;
           wait_slot(last - (s + 1));
-          if constexpr (!DQ_PAIR_NOBAR) __builtin_amdgcn_s_barrier();
+          __builtin_amdgcn_s_barrier();
           asm volatile("" ::: "memory");
           if (s + kRing < ns) dma(s + kRing, slot);
           rd(N, (slot + 1) & (kRing - 1));
         }
         fold_group(R.v[1], R.m[1]);
       };
-      if constexpr (DQ_PAIR_FLAGS) {
-        // LDS flags instead of the barrier: slot s's data is in when the partner's sequence word for it reads
-        // kSlotSeq[s] (this wave's own by vmcnt); ring position p is restaged with slot s + kRing - 1 once
-        // both waves consumed slot s - 1 (cons[w] = slots consumed).  DMA kRing - 1 slots ahead.
-        const uint32_t cons0 = lds0 + (uint32_t)(kRing * kSlotBytes);
-        auto lds_read = [](uint32_t addr) __attribute__((always_inline)) {
-          uint32_t v;
-          asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr) : "memory");
-          return (uint32_t)__builtin_amdgcn_readfirstlane(v);
-        };
-        auto lds_write = [](uint32_t addr, uint32_t v) __attribute__((always_inline)) {
-          asm volatile("ds_write_b32 %0, %1" ::"v"(addr), "v"(v) : "memory");
-        };
-        // every poll is bounded (a lost flag must not hang the GPU): past ~2^20 sleeps the wave stops waiting
-        // for good and flags its range for the checked re-run (dq_pair_redo, which reads HBM directly)
-        bool lost = false;
-        auto wait_data = [&](int32_t t, uint32_t pos) __attribute__((always_inline)) {
-          const uint32_t a = lds0 + pos * (uint32_t)kSlotBytes + kSlotSeqByte + (uint32_t)(wave ^ 1) * 4u;
-          const uint32_t want = kSlotSeq.v[(uint32_t)t & 4095u];
-          for (int32_t it = 0; !lost && lds_read(a) != want; ++it) {
-            if (it > (1 << 20)) lost = true;
-            __builtin_amdgcn_s_sleep(1);
-          }
-        };
-        auto wait_consumed = [&](int32_t t) __attribute__((always_inline)) {  // partner consumed slots < t
-          for (int32_t it = 0; !lost && (int32_t)lds_read(cons0 + (uint32_t)(wave ^ 1) * 4u) < t; ++it) {
-            if (it > (1 << 20)) lost = true;
-            __builtin_amdgcn_s_sleep(1);
-          }
-        };
-        // own loads of slot t landed, `after` slots issued after it (6 loads per slot)
-        auto wait_own = [](int32_t after) __attribute__((always_inline)) {
-          if (after >= 2) asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)" ::: "memory");
-          else if (after == 1) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
-          else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        };
-        constexpr int32_t D = kRing - 1;
-        auto fiter = [&](SlotRegs& R, SlotRegs& N, int32_t s, uint32_t slot) __attribute__((always_inline)) {
-          fold_group(R.v[0], R.m[0]);
-          if (s + 1 < ns) {
-            // issued after slot s + 1: slots s + 2 .. min(s + D - 1, ns - 1)
-            const int32_t last = s + D - 1 < ns - 1 ? s + D - 1 : ns - 1;
-            wait_own(last - (s + 1));           // R(s) in registers too (lgkmcnt)
-            lds_write(cons0 + (uint32_t)wave * 4u, (uint32_t)(s + 1));
-            if (s + D < ns) {                   // slot s + D into the position of slot s - 1
-              wait_consumed(s);
-              dma(s + D, (slot + D) & (kRing - 1));
-            }
-            wait_data(s + 1, (slot + 1) & (kRing - 1));
-            rd(N, (slot + 1) & (kRing - 1));
-          }
-          fold_group(R.v[1], R.m[1]);
-        };
-        if (ns > 0) {
-          if (lane == 0) {
-            lds_write(cons0 + (uint32_t)wave * 4u, 0u);
-#pragma unroll
-            for (int p = 0; p < kRing; ++p) lds_write(lds0 + (uint32_t)(p * kSlotBytes) + kSlotSeqByte + (uint32_t)wave * 4u, 0u);
-          }
-          __builtin_amdgcn_s_barrier();  // both waves' flags cleared before any DMA can set one
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          __builtin_amdgcn_s_barrier();
-#pragma unroll
-          for (int d = 0; d < D; ++d)
-            if (d < ns) dma(d, (uint32_t)d);
-          wait_own((ns < D ? ns : D) - 1);
-          wait_data(0, 0u);
-          SlotRegs R0, R1;
-          rd(R0, 0u);
-          uint32_t slot = 0;
-          int32_t s = 0;
-          for (; s + 2 <= ns; s += 2) {
-            fiter(R0, R1, s, slot);
-            fiter(R1, R0, s + 1, slot + 1);
-            slot = (slot + 2) & (kRing - 1);
-          }
-          if (s < ns) fiter(R0, R1, s, slot);
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          if (lost) {  // every active sum non-finite -> the range goes to the checked re-run
-            const double nan = __builtin_bit_cast(double, 0x7FF8000000000000ull);
-#pragma unroll
-            for (int q = 0; q < kPairSlots; ++q) A.s[q][0] = nan;
-#pragma unroll
-            for (int k = 0; k < kPairMoments; ++k) A.sd[k] = nan;
-          }
-        }
-      } else if (ns > 0) {
+      if (ns > 0) {
 #pragma unroll
         for (int d = 0; d < kRing; ++d)
           if (d < ns) dma(d, (uint32_t)d);
@@ -921,7 +795,7 @@ __global__ __launch_bounds__(64 * kPairWaves) __attribute__((amdgpu_waves_per_eu
   const uint32_t* where = T.where >= 0 ? reinterpret_cast<const uint32_t*>(bm.where_bits[T.where]) : ones;
   int64_t* ring = nullptr;
   if constexpr (RING) {
-    __shared__ __attribute__((aligned(16))) int64_t ring_lds[kRing * kSlotBytes / 8 + (DQ_PAIR_FLAGS ? 2 : 0)];
+    __shared__ __attribute__((aligned(16))) int64_t ring_lds[kRing * kSlotBytes / 8];
     ring = ring_lds;
   }
   const bool done = pair_range<false, F64, MINMAX, RING>(T, cols, where, ones, row0, row1, range, pair_part,

@@ -269,6 +269,33 @@ struct DevHist {
   }
 };
 
+// stream-ordered scratch (hipMallocAsync from the device's default pool, kept between calls: the digest's
+// temporaries cost no hipMalloc / hipFree round trips after the first call)
+struct StreamTmp {
+  void* p = nullptr;
+  hipStream_t s = nullptr;
+  StreamTmp() = default;
+  StreamTmp(const StreamTmp&) = delete;
+  ~StreamTmp() {
+    if (p) (void)hipFreeAsync(p, s);
+  }
+  hipError_t alloc(size_t bytes, hipStream_t st) {
+    s = st;
+    return hipMallocAsync(&p, std::max<size_t>(bytes, 16), st);
+  }
+};
+hipError_t keep_pool(int device) {
+  static int kept = -1;
+  if (kept == device) return hipSuccess;
+  hipMemPool_t pool;
+  hipError_t e = hipDeviceGetDefaultMemPool(&pool, device);
+  if (e != hipSuccess) return e;
+  uint64_t keep = ~0ull;  // retain freed blocks for the next call
+  e = hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+  if (e == hipSuccess) kept = device;
+  return e;
+}
+
 double key_to_double(int32_t type, uint64_t key) {
   if (type == DQ_TYPE_F64) {
     const uint64_t b = (key >> 63) ? (key & 0x7FFFFFFFFFFFFFFFull) : ~key;
@@ -590,16 +617,27 @@ dq_status dq_quantile_digest(int32_t type, const dq_column_view* cols, const int
     s_off[(size_t)c + 1] = s_off[(size_t)c] + std::min<int64_t>(want, chunk_rows[c]);
   }
   const int64_t ns_all = s_off[(size_t)n_chunks];
-  DevHist d_sample, d_ok, d_spl, d_counts, d_target, d_cursor, d_cand, d_sorted, d_tmp, d_idx;
-  QHIP(hipMalloc(&d_sample.p, (size_t)ns_all * 8));
-  QHIP(hipMalloc(&d_ok.p, (size_t)ns_all));
+  // one scratch block: sample keys | splitters | counts | cursor | sample flags | bucket flags
+  QHIP(keep_pool(device));
+  StreamTmp small;
+  const size_t o_spl = (size_t)ns_all * 8, o_cnt = o_spl + (size_t)(kDBuckets - 1) * 8, o_cur = o_cnt + (size_t)kDBuckets * 8,
+               o_ok = o_cur + 8, o_tgt = o_ok + (size_t)ns_all;
+  QHIP(small.alloc(o_tgt + kDBuckets, stream));
+  char* const sb = static_cast<char*>(small.p);
+  struct {
+    unsigned long long* p;
+  } d_sample{reinterpret_cast<unsigned long long*>(sb)}, d_spl{reinterpret_cast<unsigned long long*>(sb + o_spl)},
+      d_counts{reinterpret_cast<unsigned long long*>(sb + o_cnt)},
+      d_cursor{reinterpret_cast<unsigned long long*>(sb + o_cur)};
+  struct {
+    unsigned char* p;
+  } d_ok{reinterpret_cast<unsigned char*>(sb + o_ok)}, d_target{reinterpret_cast<unsigned char*>(sb + o_tgt)};
   if (dq_status st = for_chunks([&](auto tk, int grid, int c, int64_t rows) {
         (void)grid;
         const int64_t mc = s_off[(size_t)c + 1] - s_off[(size_t)c];
         hipLaunchKernelGGL((dq_digest_sample<decltype(tk)::value>), dim3((unsigned)((mc + kQBlock - 1) / kQBlock)),
                            dim3(kQBlock), 0, stream, cols[c].values, reinterpret_cast<const uint32_t*>(cols[c].validity),
-                           rows, mc, d_sample.p + s_off[(size_t)c],
-                           reinterpret_cast<unsigned char*>(d_ok.p) + s_off[(size_t)c]);
+                           rows, mc, d_sample.p + s_off[(size_t)c], d_ok.p + s_off[(size_t)c]);
       }))
     return st;
   std::vector<unsigned long long> samp((size_t)ns_all);
@@ -614,10 +652,6 @@ dq_status dq_quantile_digest(int32_t type, const dq_column_view* cols, const int
   std::sort(samp.begin(), samp.end());
   std::vector<unsigned long long> spl(kDBuckets - 1, ~0ull);  // no sample: one bucket holds every key
   for (int k = 1; k < kDBuckets && nv > 0; ++k) spl[(size_t)k - 1] = samp[(size_t)k * nv / kDBuckets];
-  QHIP(hipMalloc(&d_spl.p, (size_t)(kDBuckets - 1) * 8));
-  QHIP(hipMalloc(&d_counts.p, (size_t)kDBuckets * 8));
-  QHIP(hipMalloc(&d_target.p, (size_t)kDBuckets));
-  QHIP(hipMalloc(&d_cursor.p, 8));
   QHIP(hipMemcpyAsync(d_spl.p, spl.data(), (size_t)(kDBuckets - 1) * 8, hipMemcpyHostToDevice, stream));
   QHIP(hipMemsetAsync(d_counts.p, 0, (size_t)kDBuckets * 8, stream));
   QHIP(hipMemsetAsync(d_cursor.p, 0, 8, stream));
@@ -660,31 +694,35 @@ dq_status dq_quantile_digest(int32_t type, const dq_column_view* cols, const int
   if (nc > (int64_t)0x7FFFFFFF)
     return set_error(DQ_E_UNSUPPORTED, "dq_quantile_digest: %lld candidate values (at most 2^31 - 1)", (long long)nc);
   QHIP(hipMemcpyAsync(d_target.p, tgt.data(), (size_t)kDBuckets, hipMemcpyHostToDevice, stream));
-  QHIP(hipMalloc(&d_cand.p, (size_t)nc * 8));
-  QHIP(hipMalloc(&d_sorted.p, (size_t)nc * 8));
+  // second scratch block: candidates | sorted candidates | sample indices | radix-sort temp
+  size_t tb = 0;
+  QHIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
+                                         (int)nc, 0, 64, stream));
+  StreamTmp big;
+  const size_t o_sorted = (size_t)nc * 8, o_idx = o_sorted + (size_t)nc * 8, o_tmp = (o_idx + (size_t)m * 8 + 255) & ~(size_t)255;
+  QHIP(big.alloc(o_tmp + tb, stream));
+  char* const bb = static_cast<char*>(big.p);
+  unsigned long long* const cand = reinterpret_cast<unsigned long long*>(bb);
+  unsigned long long* const sorted = reinterpret_cast<unsigned long long*>(bb + o_sorted);
+  long long* const d_idx = reinterpret_cast<long long*>(bb + o_idx);
   if (dq_status st = for_chunks([&](auto tk, int grid, int c, int64_t rows) {
         hipLaunchKernelGGL((dq_digest_pass<decltype(tk)::value, false>), dim3(grid), dim3(kQBlock), 0, stream,
                            cols[c].values, reinterpret_cast<const uint32_t*>(cols[c].validity), rows, d_spl.p, nullptr,
-                           reinterpret_cast<const unsigned char*>(d_target.p), d_cand.p, d_cursor.p);
+                           d_target.p, cand, d_cursor.p);
       }))
     return st;
-  size_t tb = 0;
-  QHIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, d_cand.p, d_sorted.p, (int)nc, 0, 64, stream));
-  QHIP(hipMalloc(&d_tmp.p, std::max<size_t>(tb, 8)));
-  QHIP(hipcub::DeviceRadixSort::SortKeys(d_tmp.p, tb, d_cand.p, d_sorted.p, (int)nc, 0, 64, stream));
+  QHIP(hipcub::DeviceRadixSort::SortKeys(bb + o_tmp, tb, cand, sorted, (int)nc, 0, 64, stream));
   // 4. sample i = the sorted candidate at (its rank within its bucket) + (candidates of the flagged buckets before)
   std::vector<long long> idx((size_t)m);
   for (int64_t i = 0; i < m; ++i) {
     const int b = rb[(size_t)i];
     idx[(size_t)i] = (long long)(rank[(size_t)i] - 1 - before[(size_t)b] + cand_before[(size_t)b]);
   }
-  QHIP(hipMalloc(&d_idx.p, (size_t)m * 8));
-  QHIP(hipMemcpyAsync(d_idx.p, idx.data(), (size_t)m * 8, hipMemcpyHostToDevice, stream));
-  hipLaunchKernelGGL(dq_digest_gather, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, stream, d_sorted.p,
-                     reinterpret_cast<const long long*>(d_idx.p), m, d_cand.p);
+  QHIP(hipMemcpyAsync(d_idx, idx.data(), (size_t)m * 8, hipMemcpyHostToDevice, stream));
+  hipLaunchKernelGGL(dq_digest_gather, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, stream, sorted, d_idx, m, cand);
   QHIP(hipGetLastError());
   std::vector<unsigned long long> got((size_t)m);
-  QHIP(hipMemcpyAsync(got.data(), d_cand.p, (size_t)m * 8, hipMemcpyDeviceToHost, stream));
+  QHIP(hipMemcpyAsync(got.data(), cand, (size_t)m * 8, hipMemcpyDeviceToHost, stream));
   QHIP(hipStreamSynchronize(stream));
   for (int64_t i = 0; i < m; ++i) {
     values[i] = key_to_double(type, got[(size_t)i]);
