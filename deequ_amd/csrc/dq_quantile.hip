@@ -314,6 +314,7 @@ double key_to_double(int32_t type, uint64_t key) {
 // rows) only makes a target bucket larger: the sort then covers it, still exactly.
 constexpr int kDBuckets = 2048;              // buckets (kDBuckets - 1 splitters, a branchless 11-step search)
 constexpr int kDSample = 16384;              // keys sampled for the splitters
+constexpr int kDStage = 2048;                // candidate keys staged per workgroup before a flush
 
 // the key of row i * n / m of a chunk (i < m), and whether the row is non-null
 template <int TYPE>
@@ -341,7 +342,9 @@ __device__ __forceinline__ uint32_t digest_bucket(const unsigned long long* spl,
 }
 
 // Pass over a chunk: COUNT -- per-bucket key counts into counts[kDBuckets]; else the keys of the flagged
-// buckets appended to cand[*cursor ...] (order free: sorted next; one 64-bit atomic per wave).
+// buckets appended to cand[*cursor ...] (order free: sorted next), staged in the workgroup's LDS and flushed
+// with one global atomic per kDStage - kQBlock keys (one cursor for the whole launch: a per-wave global atomic
+// on it ran 17 ms per 1e8 rows, r4l)
 template <int TYPE, bool COUNT>
 __global__ __launch_bounds__(kQBlock) void dq_digest_pass(const void* __restrict__ values,
                                                           const uint32_t* __restrict__ validity, int64_t n,
@@ -353,6 +356,10 @@ __global__ __launch_bounds__(kQBlock) void dq_digest_pass(const void* __restrict
   __shared__ unsigned long long spl[kDBuckets - 1];
   __shared__ uint32_t hist[COUNT ? kDBuckets : 1];
   __shared__ unsigned char tgt[COUNT ? 1 : kDBuckets];
+  __shared__ unsigned long long stage[COUNT ? 1 : kDStage];
+  __shared__ uint32_t st_n;
+  __shared__ unsigned long long st_base;
+  if (threadIdx.x == 0) st_n = 0;
   for (int i = threadIdx.x; i < kDBuckets - 1; i += kQBlock) spl[i] = splitters[i];
   if constexpr (COUNT) {
     for (int i = threadIdx.x; i < kDBuckets; i += kQBlock) hist[i] = 0;
@@ -375,20 +382,41 @@ __global__ __launch_bounds__(kQBlock) void dq_digest_pass(const void* __restrict
     if constexpr (COUNT) {
       if (ok) atomicAdd(&hist[bk], 1u);
     } else {
+      // (every thread of the workgroup runs the same iterations: the flush below is workgroup-uniform)
       const bool take = ok && tgt[bk];
       const uint64_t bal = __builtin_amdgcn_ballot_w64(take);
-      if (bal == 0) continue;
-      const int first = __builtin_ctzll(bal);
-      unsigned long long base = 0;
-      if (lane == first) base = atomicAdd(cursor, (unsigned long long)__builtin_popcountll(bal));
-      base = __shfl(base, first);
-      if (take) cand[base + __builtin_popcountll(bal & ((1ull << lane) - 1ull))] = key;
+      if (bal != 0) {
+        const int first = __builtin_ctzll(bal);
+        uint32_t pos = 0;
+        if (lane == first) pos = atomicAdd(&st_n, (uint32_t)__builtin_popcountll(bal));
+        pos = __shfl(pos, first);  // < kDStage - kQBlock + kQBlock - 64: fits (flushed below otherwise)
+        if (take) stage[pos + __builtin_popcountll(bal & ((1ull << lane) - 1ull))] = key;
+      }
+      __syncthreads();
+      const uint32_t staged = st_n;
+      if (staged > (uint32_t)(kDStage - kQBlock)) {
+        if (threadIdx.x == 0) st_base = atomicAdd(cursor, (unsigned long long)staged);
+        __syncthreads();
+        const unsigned long long b = st_base;
+        for (uint32_t i = threadIdx.x; i < staged; i += kQBlock) cand[b + i] = stage[i];
+        __syncthreads();
+        if (threadIdx.x == 0) st_n = 0;
+        __syncthreads();
+      }
     }
   }
+  __syncthreads();
   if constexpr (COUNT) {
-    __syncthreads();
     for (int i = threadIdx.x; i < kDBuckets; i += kQBlock)
       if (hist[i]) atomicAdd(&counts[i], (unsigned long long)hist[i]);
+  } else {
+    const uint32_t staged = st_n;
+    if (staged > 0) {
+      if (threadIdx.x == 0) st_base = atomicAdd(cursor, (unsigned long long)staged);
+      __syncthreads();
+      const unsigned long long b = st_base;
+      for (uint32_t i = threadIdx.x; i < staged; i += kQBlock) cand[b + i] = stage[i];
+    }
   }
 }
 
