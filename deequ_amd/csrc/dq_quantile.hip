@@ -314,7 +314,7 @@ double key_to_double(int32_t type, uint64_t key) {
 // rows) only makes a target bucket larger: the sort then covers it, still exactly.
 constexpr int kDBuckets = 2048;              // buckets (kDBuckets - 1 splitters, a branchless 11-step search)
 constexpr int kDSample = 16384;              // keys sampled for the splitters
-constexpr int kDStage = 2048;                // candidate keys staged per workgroup before a flush
+constexpr int kDStage = 2048;                // candidate keys staged per workgroup (flushed past kDStage - 1024)
 
 // the key of row i * n / m of a chunk (i < m), and whether the row is non-null
 template <int TYPE>
@@ -332,13 +332,19 @@ __global__ __launch_bounds__(kQBlock) void dq_digest_sample(const void* __restri
   ok[i] = validity ? (unsigned char)((validity[r >> 5] >> (r & 31)) & 1u) : (unsigned char)1;
 }
 
-// bucket of a key: the number of splitters <= key (spl: kDBuckets - 1 sorted keys in LDS)
-__device__ __forceinline__ uint32_t digest_bucket(const unsigned long long* spl, uint64_t key) {
-  uint32_t pos = 0;
+constexpr int kDRows = 4;                    // rows per thread and iteration (independent searches in flight)
+
+// buckets of kDRows keys: the number of splitters <= key (spl: kDBuckets - 1 sorted keys in LDS), the searches
+// interleaved step by step (each is a chain of 11 dependent LDS reads)
+__device__ __forceinline__ void digest_buckets(const unsigned long long* spl, const uint64_t (&key)[kDRows],
+                                               uint32_t (&pos)[kDRows]) {
+#pragma unroll
+  for (int u = 0; u < kDRows; ++u) pos[u] = 0;
 #pragma unroll
   for (uint32_t step = kDBuckets / 2; step >= 1; step >>= 1)
-    if (spl[pos + step - 1] <= key) pos += step;
-  return pos;
+#pragma unroll
+    for (int u = 0; u < kDRows; ++u)
+      if (spl[pos[u] + step - 1] <= key[u]) pos[u] += step;
 }
 
 // Pass over a chunk: COUNT -- per-bucket key counts into counts[kDBuckets]; else the keys of the flagged
@@ -368,33 +374,45 @@ __global__ __launch_bounds__(kQBlock) void dq_digest_pass(const void* __restrict
   }
   __syncthreads();
   const int lane = threadIdx.x & 63;
-  for (int64_t r0 = (int64_t)blockIdx.x * kQBlock; r0 < n; r0 += (int64_t)gridDim.x * kQBlock) {
-    const int64_t r = r0 + threadIdx.x;
-    bool ok = r < n;
-    uint64_t raw = 0;
-    if (ok) {
-      if (validity) ok = (validity[r >> 5] >> (r & 31)) & 1u;
-      if constexpr (TYPE == DQ_TYPE_I32) raw = (uint32_t)__builtin_nontemporal_load(reinterpret_cast<const int32_t*>(values) + r);
-      else raw = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(values) + r);
+  constexpr int kIter = kQBlock * kDRows;  // rows per workgroup and iteration
+  for (int64_t r0 = (int64_t)blockIdx.x * kIter; r0 < n; r0 += (int64_t)gridDim.x * kIter) {
+    bool ok[kDRows];
+    uint64_t key[kDRows];
+#pragma unroll
+    for (int u = 0; u < kDRows; ++u) {
+      const int64_t r = r0 + u * kQBlock + threadIdx.x;
+      ok[u] = r < n;
+      uint64_t raw = 0;
+      if (ok[u]) {
+        if (validity) ok[u] = (validity[r >> 5] >> (r & 31)) & 1u;
+        if constexpr (TYPE == DQ_TYPE_I32) raw = (uint32_t)__builtin_nontemporal_load(reinterpret_cast<const int32_t*>(values) + r);
+        else raw = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(values) + r);
+      }
+      key[u] = order_key<TYPE>(raw);
     }
-    const uint64_t key = order_key<TYPE>(raw);
-    const uint32_t bk = digest_bucket(spl, key);
+    uint32_t bk[kDRows];
+    digest_buckets(spl, key, bk);
     if constexpr (COUNT) {
-      if (ok) atomicAdd(&hist[bk], 1u);
+#pragma unroll
+      for (int u = 0; u < kDRows; ++u)
+        if (ok[u]) atomicAdd(&hist[bk[u]], 1u);
     } else {
       // (every thread of the workgroup runs the same iterations: the flush below is workgroup-uniform)
-      const bool take = ok && tgt[bk];
-      const uint64_t bal = __builtin_amdgcn_ballot_w64(take);
-      if (bal != 0) {
-        const int first = __builtin_ctzll(bal);
-        uint32_t pos = 0;
-        if (lane == first) pos = atomicAdd(&st_n, (uint32_t)__builtin_popcountll(bal));
-        pos = __shfl(pos, first);  // < kDStage - kQBlock + kQBlock - 64: fits (flushed below otherwise)
-        if (take) stage[pos + __builtin_popcountll(bal & ((1ull << lane) - 1ull))] = key;
+#pragma unroll
+      for (int u = 0; u < kDRows; ++u) {
+        const bool take = ok[u] && tgt[bk[u]];
+        const uint64_t bal = __builtin_amdgcn_ballot_w64(take);
+        if (bal != 0) {
+          const int first = __builtin_ctzll(bal);
+          uint32_t pos = 0;
+          if (lane == first) pos = atomicAdd(&st_n, (uint32_t)__builtin_popcountll(bal));
+          pos = __shfl(pos, first);  // <= kDStage - kIter before this iteration: fits
+          if (take) stage[pos + __builtin_popcountll(bal & ((1ull << lane) - 1ull))] = key[u];
+        }
       }
       __syncthreads();
       const uint32_t staged = st_n;
-      if (staged > (uint32_t)(kDStage - kQBlock)) {
+      if (staged > (uint32_t)(kDStage - kIter)) {
         if (threadIdx.x == 0) st_base = atomicAdd(cursor, (unsigned long long)staged);
         __syncthreads();
         const unsigned long long b = st_base;
@@ -629,7 +647,7 @@ dq_status dq_quantile_digest(int32_t type, const dq_column_view* cols, const int
     for (int c = 0; c < n_chunks; ++c) {
       const int64_t rows = chunk_rows[c];
       if (rows == 0) continue;
-      const int grid = (int)std::min<int64_t>(4096, (rows + kQBlock - 1) / kQBlock);
+      const int grid = (int)std::min<int64_t>(4096, (rows + kQBlock * kDRows - 1) / (kQBlock * kDRows));
       auto go = [&](auto kern) { launch(kern, grid, c, rows); };
       if (type == DQ_TYPE_F64) go(std::integral_constant<int, DQ_TYPE_F64>{});
       else if (type == DQ_TYPE_I64) go(std::integral_constant<int, DQ_TYPE_I64>{});
