@@ -197,12 +197,6 @@ bool pred_jit_eligible(const PredProgram& prog, const int32_t* col_kind, int32_t
 constexpr int kJitGroups = DQ_JIT_GROUPS;  // (A/B builds: -DDQ_JIT_GROUPS=4)
 // what may cross the barrier between a row group's predicate work and its hashing (sched_barrier mask; A/B
 // builds: 0 = nothing crosses; 2 = VALU may cross: 0.838-0.847 vs 0.856-0.869 ms per 125 M rows of C3, r4i)
-// A/B (-DDQ_JIT_PIPE=1): the row-group loop software-pipelined (group j + 1's predicate work beside group j's
-// hashing)
-#ifndef DQ_JIT_PIPE
-#define DQ_JIT_PIPE 0
-#endif
-constexpr bool kJitPipe = DQ_JIT_PIPE;
 #ifndef DQ_JIT_SCHED_MASK
 #define DQ_JIT_SCHED_MASK 2
 #endif
@@ -420,21 +414,9 @@ std::string pred_jit_source(const PredProgram& prog, const int32_t* col_kind, st
   }
   const std::string pt = s.substr(pt0);
   s.resize(pt0);
-  if (kJitPipe) {
-    // software-pipelined: row group j + 1's predicate work (scalar mask logic) and row group j's hashing (VALU)
-    // in one basic block, so the scheduler interleaves the two; the groups' selection masks carried in va_s
-    for (int i = 0; i < ns; ++i) s += "    uint64_t va_s" + std::to_string(i) + "[" + G + "];\n";
-    s += "    auto pred_group = [&](const int j) __attribute__((always_inline)) {\n" + pt;
-    for (int i = 0; i < ns; ++i) s += "    va_s" + std::to_string(i) + "[j] = va" + std::to_string(i) + ";\n";
-    s += "    };\n";
-    s += "#pragma unroll\n  for (int j = 0; j < " + G + "; ++j) {\n";
-    s += "    if (j == 0) pred_group(0);\n";
-    s += "    if (j + 1 < " + G + ") pred_group(j + 1);\n";
-    s += "    const int64_t r = base + 64 * j;\n";
-    s += "    const uint64_t inr = rows_mask(rem - 64 * j);\n";
-    for (int i = 0; i < ns; ++i) s += "    const uint64_t va" + std::to_string(i) + " = va_s" + std::to_string(i) + "[j];\n";
-    s += "    (void)r;\n";
-  } else {
+  // (round 4: row group j + 1's predicate work emitted beside row group j's hashing, software-pipelined,
+  // measured no different: 0.827-0.868 vs 0.829-0.852 ms per 125 M rows of C3, r4m)
+  {
     s += "#pragma unroll\n  for (int j = 0; j < " + G + "; ++j) {\n" + pt;
     s += "    __builtin_amdgcn_sched_barrier(" + std::to_string(DQ_JIT_SCHED_MASK) + ");\n";
   }
