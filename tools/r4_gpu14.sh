@@ -14,3 +14,5 @@ rc=$?; tail -5 gpurun_out/r4n_quantile_bench.txt | tee -a $S; [ $rc -eq 0 ] || e
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r4n_qprof -o q --output-format csv -- python3 tools/quantile_bench.py --rows 1e8 --reps 2 > gpurun_out/r4n_qprof.log 2>&1 || { tail -5 gpurun_out/r4n_qprof.log; exit 5; }
 timeout -k 10 700 python -u bench.py > gpurun_out/r4n_bench.json 2> gpurun_out/r4n_bench.err
 rc=$?; tail -c 400 gpurun_out/r4n_bench.json | tee -a $S; [ $rc -eq 0 ] || { tail -5 gpurun_out/r4n_bench.err; exit $rc; }
+# C2 (8 x f64 moments, the stats-only column pass) against the round-3 kernels
+CFG=c2 SKIP_TESTS=1 TAG=r4n2 bash tools/ab_c3.sh build_variants/libbase.so deequ_amd/libdqscan.so build_variants/libbase.so deequ_amd/libdqscan.so | tee -a $S
