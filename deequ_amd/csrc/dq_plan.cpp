@@ -27,6 +27,11 @@
 #include "dq_device.h"
 #include "dq_internal.h"
 #include "dq_pred_jit.h"
+
+// predicate-pass workgroups per chunk (A/B builds: -DDQ_PRED_WGS=...)
+#ifndef DQ_PRED_WGS
+#define DQ_PRED_WGS 2048
+#endif
 #include "dq_regex.h"
 
 namespace dq {
@@ -1260,7 +1265,7 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
   }
   // predicate pass: ~2048 workgroups of whole 2048-row iterations (HBM-bound; counters leave by atomics;
   // 1024-16384 workgroups measured within 2 % on C3)
-  int32_t nr_pred = (int32_t)std::min<int64_t>(2048, ceil_div(n_rows, kRowsPerIter));
+  int32_t nr_pred = (int32_t)std::min<int64_t>(DQ_PRED_WGS, ceil_div(n_rows, kRowsPerIter));
   int64_t rpr_pred = ceil_div(ceil_div(n_rows, nr_pred), kRowsPerIter) * kRowsPerIter;
   nr_pred = (int32_t)ceil_div(n_rows, rpr_pred);
 
