@@ -23,6 +23,7 @@ constexpr int kTargetWGs = 8192;            // column/pair launch: aim for ~32 w
 constexpr int kMaxCols = 64;
 constexpr int kMaxWhere = 8;
 constexpr int kHllCopies = 8;             // accumulator copies per HLL column (spreads the merge atomics)
+constexpr int kPredAccCopies = 16;        // predicate-counter accumulator copies (compiled pass: one per blockIdx % 16)
 constexpr int kMaxRoots = 32;
 constexpr int kMaxCounters = 32;
 constexpr int kMaxInstr = 96;

@@ -546,7 +546,7 @@ static dq_status reset_acc(dq_plan* p) {
   HIP_TRY(launch_init_acc(p->d_col_acc, (int32_t)p->col_tasks.size(), p->d_pair_acc, (int32_t)p->pair_tasks.size(),
                           p->stream));
   if (p->n_hll) HIP_TRY(hipMemsetAsync(p->d_hll_acc, 0, (size_t)p->n_hll * kHllCopies * 512 * sizeof(uint32_t), p->stream));
-  if (p->has_pred) HIP_TRY(hipMemsetAsync(p->d_pred_acc, 0, sizeof(PredPartial), p->stream));
+  if (p->has_pred) HIP_TRY(hipMemsetAsync(p->d_pred_acc, 0, kPredAccCopies * sizeof(PredPartial), p->stream));
   p->total_rows = 0;
   p->next_chunk = 0;
   return DQ_OK;
@@ -1063,7 +1063,8 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
   if (dq_status s = dmalloc(&p->d_col_acc, nct * sizeof(ColPartial))) return s;
   if (dq_status s = dmalloc(&p->d_hll_acc, (size_t)p->n_hll * kHllCopies * 512 * sizeof(uint32_t))) return s;
   if (dq_status s = dmalloc(&p->d_pair_acc, npt * sizeof(CorrPartial))) return s;
-  if (dq_status s = dmalloc(&p->d_pred_acc, sizeof(PredPartial))) return s;
+  // (kPredAccCopies copies: the compiled predicate pass spreads its counter atomics over them; the host adds them)
+  if (dq_status s = dmalloc(&p->d_pred_acc, kPredAccCopies * sizeof(PredPartial))) return s;
   if (nct) HIP_TRY(hipMemcpyAsync(p->d_col_tasks, p->col_tasks.data(), nct * sizeof(ColTask), hipMemcpyHostToDevice, p->stream));
   if (npt) HIP_TRY(hipMemcpyAsync(p->d_pair_tasks, p->pair_tasks.data(), npt * sizeof(PairTask), hipMemcpyHostToDevice, p->stream));
   if (p->regex_blob.size() > (size_t)kMaxRegexWords)
@@ -1352,8 +1353,16 @@ dq_status dq_finish(dq_plan* p, dq_state* out) {
   if (!hll.empty())
     HIP_TRY(hipMemcpyAsync(hll.data(), p->d_hll_acc, hll.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, p->stream));
   if (!pair.empty()) HIP_TRY(hipMemcpyAsync(pair.data(), p->d_pair_acc, pair.size() * sizeof(CorrPartial), hipMemcpyDeviceToHost, p->stream));
-  if (p->has_pred) HIP_TRY(hipMemcpyAsync(&pred, p->d_pred_acc, sizeof(PredPartial), hipMemcpyDeviceToHost, p->stream));
+  std::vector<PredPartial> pred_copies(p->has_pred ? kPredAccCopies : 0);
+  if (p->has_pred)
+    HIP_TRY(hipMemcpyAsync(pred_copies.data(), p->d_pred_acc, kPredAccCopies * sizeof(PredPartial), hipMemcpyDeviceToHost,
+                           p->stream));
   HIP_TRY(hipStreamSynchronize(p->stream));
+  for (const PredPartial& c : pred_copies)  // integer sums: the order of the copies does not matter
+    for (int k = 0; k < kMaxCounters; ++k) {
+      pred.t[k] += c.t[k];
+      pred.nn[k] += c.nn[k];
+    }
   // timed launches of this scan -> counters, their events back to the pool (no hipEventCreate in later scans)
   if (dq_status s = resolve_timing(p)) return s;
 

@@ -241,11 +241,14 @@ std::string pred_jit_source(const PredProgram& prog, const int32_t* col_kind, st
   s += "  using namespace dq; using namespace dqj;\n";
   s += "  __shared__ int32_t regs[" + std::to_string(nh > 0 ? nh * 512 : 1) + "];\n";
   s += "  __shared__ unsigned long long hcnt[" + std::to_string(nh > 0 ? nh : 1) + "];\n";
+  s += "  __shared__ unsigned long long cacc[" + std::to_string(prog.n_counters > 0 ? 2 * prog.n_counters : 1) + "];\n";
+  if (prog.n_counters > 0)
+    s += "  if (threadIdx.x < " + std::to_string(2 * prog.n_counters) + ") cacc[threadIdx.x] = 0;\n";
   if (nh > 0) {
     s += "  for (int i = threadIdx.x; i < " + std::to_string(nh * 512) + "; i += 256) regs[i] = -1;\n";
     s += "  if (threadIdx.x < " + std::to_string(nh) + ") hcnt[threadIdx.x] = 0;\n";
-    s += "  __syncthreads();\n";
   }
+  s += "  __syncthreads();\n";
   s += "  const int lane = threadIdx.x & 63;\n";
   s += "  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n";
   s += "  const int64_t row0 = (int64_t)blockIdx.x * A.rows_per_range;\n";
@@ -482,17 +485,28 @@ std::string pred_jit_source(const PredProgram& prog, const int32_t* col_kind, st
   for (int i = 0; i < ns; ++i) s += "    vw" + std::to_string(i) + " = vwn" + std::to_string(i) + ";\n";
   s += "  }\n";  // blk
   s += "  asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");  // the last prefetches land before exit\n";
+  // the workgroup's counters summed in LDS, then one global atomic per counter into one of kPredAccCopies
+  // accumulator copies (blockIdx % copies; the host adds the copies): per-wave atomics on the same eight
+  // addresses had serialized at the end of the launch (2048 -> 8192 workgroups: 0.84 -> 1.67 ms, r4o)
   s += "  if (lane == 0) {\n";
   for (int c = 0; c < prog.n_counters; ++c) {
     const std::string cs = std::to_string(c);
-    s += "    atomicAdd(A.acc_t + " + cs + ", (unsigned long long)ct" + cs + ");\n";
-    s += "    atomicAdd(A.acc_nn + " + cs + ", (unsigned long long)cn" + cs + ");\n";
+    s += "    atomicAdd(&cacc[" + std::to_string(2 * c) + "], (unsigned long long)ct" + cs + ");\n";
+    s += "    atomicAdd(&cacc[" + std::to_string(2 * c + 1) + "], (unsigned long long)cn" + cs + ");\n";
   }
   for (int h = 0; h < nh; ++h) s += "    atomicAdd(&hcnt[" + std::to_string(h) + "], (unsigned long long)hc" + std::to_string(h) + ");\n";
   s += "  }\n";
+  s += "  asm volatile(\"s_waitcnt lgkmcnt(0)\" ::: \"memory\");\n";
+  s += "  __syncthreads();\n";
+  if (prog.n_counters > 0) {
+    s += "  if (threadIdx.x < " + std::to_string(2 * prog.n_counters) + ") {\n";
+    s += "    const int c = threadIdx.x >> 1;\n";
+    s += "    unsigned long long* dst = ((threadIdx.x & 1) ? A.acc_nn : A.acc_t) + (size_t)(blockIdx.x % " +
+         std::to_string(kPredAccCopies) + ") * " + std::to_string(sizeof(PredPartial) / 8) + " + c;\n";
+    s += "    atomicAdd(dst, cacc[threadIdx.x]);\n";
+    s += "  }\n";
+  }
   if (nh > 0) {
-    s += "  asm volatile(\"s_waitcnt lgkmcnt(0)\" ::: \"memory\");\n";
-    s += "  __syncthreads();\n";
     for (int h = 0; h < nh; ++h) {
         // ColPartial (dq_device.h, 96 bytes): n mean m2 sum isum count nan_count fmin fmax pinf ninf pad
       s += "  if (threadIdx.x == 0) {\n";
@@ -548,7 +562,7 @@ bool pred_jit_compile_code(const std::string& src, const std::string& arch, std:
 namespace {
 
 // generated-source revision: part of the disk-cache key, so code objects of an older generator are not reused
-constexpr const char* kJitRevision = "dq_pred_jit r4e";
+constexpr const char* kJitRevision = "dq_pred_jit r4f";
 
 uint64_t fnv1a64(const std::string& s, uint64_t h) {
   for (unsigned char c : s) h = (h ^ c) * 0x100000001B3ull;
