@@ -1422,7 +1422,7 @@ __device__ __forceinline__ void pred_block_out(const PredScratch& S, const PredC
   }
 }
 
-// Workgroup partials -> accumulator (integer atomics: order-free); waits for every wave's counters.
+// Workgroup partials -> accumulator copy (integer atomics: order-free); waits for every wave's counters.
 __device__ __forceinline__ void pred_counters_out(const uint32_t* pred_lds, int wave_words, const PredProgram& prog,
                                                   PredPartial* acc) {
   __syncthreads();
@@ -1436,8 +1436,11 @@ __device__ __forceinline__ void pred_counters_out(const uint32_t* pred_lds, int 
         t += W.ct[c * 16 + l];
         nn += W.cn[c * 16 + l];
       }
-    atomicAdd(reinterpret_cast<unsigned long long*>(&acc->t[c]), (unsigned long long)t);
-    atomicAdd(reinterpret_cast<unsigned long long*>(&acc->nn[c]), (unsigned long long)nn);
+    // one of kPredAccCopies accumulator copies per workgroup (the host adds them): every workgroup's atomics
+    // on the same addresses serialize at the end of the launch
+    PredPartial* a = acc + (blockIdx.x % kPredAccCopies);
+    atomicAdd(reinterpret_cast<unsigned long long*>(&a->t[c]), (unsigned long long)t);
+    atomicAdd(reinterpret_cast<unsigned long long*>(&a->nn[c]), (unsigned long long)nn);
   }
 }
 
