@@ -314,6 +314,8 @@ double key_to_double(int32_t type, uint64_t key) {
 // rows) only makes a target bucket larger: the sort then covers it, still exactly.
 constexpr int kDBuckets = 2048;              // buckets (kDBuckets - 1 splitters, a branchless 11-step search)
 constexpr int kDSample = 16384;              // keys sampled for the splitters
+constexpr int kDCountCopies = 8;             // bucket-count copies (blockIdx % 8; the host adds them): a skewed
+                                             // column's hot bucket gets every workgroup's atomic at the launch's end
 constexpr int kDStage = 2048;                // candidate keys staged per workgroup (flushed past kDStage - 1024)
 
 // the key of row i * n / m of a chunk (i < m), and whether the row is non-null
@@ -347,7 +349,7 @@ __device__ __forceinline__ void digest_buckets(const unsigned long long* spl, co
       if (spl[pos[u] + step - 1] <= key[u]) pos[u] += step;
 }
 
-// Pass over a chunk: COUNT -- per-bucket key counts into counts[kDBuckets]; else the keys of the flagged
+// Pass over a chunk: COUNT -- per-bucket key counts into counts[kDCountCopies][kDBuckets]; else the keys of the flagged
 // buckets appended to cand[*cursor ...] (order free: sorted next), staged in the workgroup's LDS and flushed
 // with one global atomic per kDStage - kQBlock keys (one cursor for the whole launch: a per-wave global atomic
 // on it ran 17 ms per 1e8 rows, r4l)
@@ -426,7 +428,7 @@ __global__ __launch_bounds__(kQBlock) void dq_digest_pass(const void* __restrict
   __syncthreads();
   if constexpr (COUNT) {
     for (int i = threadIdx.x; i < kDBuckets; i += kQBlock)
-      if (hist[i]) atomicAdd(&counts[i], (unsigned long long)hist[i]);
+      if (hist[i]) atomicAdd(&counts[(blockIdx.x % kDCountCopies) * kDBuckets + i], (unsigned long long)hist[i]);
   } else {
     const uint32_t staged = st_n;
     if (staged > 0) {
@@ -666,7 +668,8 @@ dq_status dq_quantile_digest(int32_t type, const dq_column_view* cols, const int
   // one scratch block: sample keys | splitters | counts | cursor | sample flags | bucket flags
   QHIP(keep_pool(device));
   StreamTmp small;
-  const size_t o_spl = (size_t)ns_all * 8, o_cnt = o_spl + (size_t)(kDBuckets - 1) * 8, o_cur = o_cnt + (size_t)kDBuckets * 8,
+  const size_t o_spl = (size_t)ns_all * 8, o_cnt = o_spl + (size_t)(kDBuckets - 1) * 8,
+               o_cur = o_cnt + (size_t)kDCountCopies * kDBuckets * 8,
                o_ok = o_cur + 8, o_tgt = o_ok + (size_t)ns_all;
   QHIP(small.alloc(o_tgt + kDBuckets, stream));
   char* const sb = static_cast<char*>(small.p);
@@ -699,7 +702,7 @@ dq_status dq_quantile_digest(int32_t type, const dq_column_view* cols, const int
   std::vector<unsigned long long> spl(kDBuckets - 1, ~0ull);  // no sample: one bucket holds every key
   for (int k = 1; k < kDBuckets && nv > 0; ++k) spl[(size_t)k - 1] = samp[(size_t)k * nv / kDBuckets];
   QHIP(hipMemcpyAsync(d_spl.p, spl.data(), (size_t)(kDBuckets - 1) * 8, hipMemcpyHostToDevice, stream));
-  QHIP(hipMemsetAsync(d_counts.p, 0, (size_t)kDBuckets * 8, stream));
+  QHIP(hipMemsetAsync(d_counts.p, 0, (size_t)kDCountCopies * kDBuckets * 8, stream));
   QHIP(hipMemsetAsync(d_cursor.p, 0, 8, stream));
   // 2. per-bucket counts
   if (dq_status st = for_chunks([&](auto tk, int grid, int c, int64_t rows) {
@@ -708,9 +711,10 @@ dq_status dq_quantile_digest(int32_t type, const dq_column_view* cols, const int
                            d_counts.p, nullptr, nullptr, nullptr);
       }))
     return st;
-  std::vector<unsigned long long> cnt((size_t)kDBuckets);
-  QHIP(hipMemcpyAsync(cnt.data(), d_counts.p, (size_t)kDBuckets * 8, hipMemcpyDeviceToHost, stream));
+  std::vector<unsigned long long> cnt_copies((size_t)kDCountCopies * kDBuckets), cnt((size_t)kDBuckets, 0);
+  QHIP(hipMemcpyAsync(cnt_copies.data(), d_counts.p, cnt_copies.size() * 8, hipMemcpyDeviceToHost, stream));
   QHIP(hipStreamSynchronize(stream));
+  for (size_t i = 0; i < cnt_copies.size(); ++i) cnt[i % kDBuckets] += cnt_copies[i];
   int64_t n = 0;
   for (unsigned long long x : cnt) n += (int64_t)x;
   *count = n;
