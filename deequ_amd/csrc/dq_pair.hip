@@ -135,6 +135,9 @@ constexpr int kSlotMaskWord = 8 * 256;  // dword index of the selection words in
 #define DQ_PAIR_PIPE 1
 #endif
 constexpr bool kPairPipe = DQ_PAIR_PIPE;
+// (round 4, r4s: raising the wave's issue priority (s_setprio 2) from the slot hand-off until its DMA and LDS
+// reads of the next slot are issued measured 1.535-1.540 vs 1.527-1.534 ms per 125 M rows; for the fold of a
+// slot's first group instead 1.553-1.567 -- removed)
 
 
 // per-lane sums of one wave task over its range

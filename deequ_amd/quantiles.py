@@ -232,9 +232,10 @@ MAX_DIGEST_SAMPLES = 1 << 20
 
 
 def device_digest(data, column: str, relativeError: float) -> PercentileDigest:
-    """The column's digest from exact order statistics: dq_quantile_digest sorts the column's non-null values
-    once on the device and returns the values at every sample rank (one pass, whatever the number of
-    samples); an empty digest (count 0) when every value is NULL."""
+    """The column's digest from exact order statistics: dq_quantile_digest answers every sample rank in two
+    passes over the column's non-null values on the device (per-bucket counts against sampled splitters, then
+    the keys of the buckets that hold a sample rank compacted and sorted), whatever the number of samples; an
+    empty digest (count 0) when every value is NULL."""
     rel = spark_relative_error(relativeError)
     n, ranks, values = _digest_samples(data, column, rel)
     if n == 0:
