@@ -240,6 +240,30 @@ def test_gpu_digest_matches_exact_ranks(dq, dtype):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 2, 63, 513, 2049, 16_385, 16_387])
+def test_gpu_digest_small_and_ragged(dq, n):
+    """Sizes around the digest's sample (16 K rows) and bucket (2048) counts, one chunk and split into three
+    (the last one ragged), with nulls: every sample rank equals the exact order statistic."""
+    from deequ_amd.quantiles import device_digest
+    from deequ_amd.table import column_from_numpy
+
+    rng = np.random.default_rng(n)
+    for dtype in ("f64", "i64"):
+        v = _f64_data(rng, n) if dtype == "f64" else rng.integers(-50, 50, n, dtype=np.int64)
+        valid = rng.random(n) >= 0.1
+        valid[0] = True
+        cuts = [0, n // 3, n - n // 5, n]
+        whole = dq.Table([column_from_numpy("x", dtype, v, valid)])
+        parts = [dq.Table([column_from_numpy("x", dtype, v[a:b], valid[a:b])]) for a, b in zip(cuts, cuts[1:])]
+        for err in (0.0, 0.001, 0.01, 0.3):
+            cnt, want = O.gk_digest_exact(v, valid, err)
+            for data in (whole, parts):
+                got = device_digest(data, "x", err).quantileSummaries
+                assert got.count == cnt and len(got.sampled) == len(want), (dtype, n, err)
+                assert all(_same(a[0], b[0]) and a[1:] == b[1:] for a, b in zip(got.sampled, want)), (dtype, n, err)
+
+
+@pytest.mark.gpu
 def test_gpu_digest_sample_limit(dq, monkeypatch):
     """relativeError 0 keeps every value (as Spark's GK does); past MAX_DIGEST_SAMPLES the GPU path refuses
     with UnsupportedOnGpuPathException (the analyzer goes to the Spark fallback) instead of building a digest
