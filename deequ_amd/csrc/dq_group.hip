@@ -93,14 +93,18 @@ __device__ uint64_t tuple_hash(const GroupCols& g, int64_t r, uint64_t seed = kS
       const uint8_t* p;
       int64_t len;
       str_of(g, c, r, p, len);
+      // little-endian words by (unaligned) 8- / 4-byte loads -- the same k as assembling the bytes one by one
+      typedef uint64_t u64u __attribute__((aligned(1)));
+      typedef uint32_t u32u __attribute__((aligned(1)));
       int64_t i = 0;
-      for (; i + 8 <= len; i += 8) {
-        uint64_t k = 0;
-        for (int b = 0; b < 8; ++b) k |= (uint64_t)p[i + b] << (8 * b);
-        h = mix8(h, k);
-      }
+      for (; i + 8 <= len; i += 8) h = mix8(h, *reinterpret_cast<const u64u*>(p + i));
       uint64_t k = 0;
-      for (int b = 0; i + b < len; ++b) k |= (uint64_t)p[i + b] << (8 * b);
+      int b = 0;
+      if (i + 4 <= len) {
+        k = *reinterpret_cast<const u32u*>(p + i);
+        b = 4;
+      }
+      for (; i + b < len; ++b) k |= (uint64_t)p[i + b] << (8 * b);
       h = mix8(h, k ^ ((uint64_t)len << 56) ^ 0xA5);
     } else {
       h = mix8(h, value_bits(g, c, r));
