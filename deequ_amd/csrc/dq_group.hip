@@ -152,12 +152,16 @@ __device__ bool tuple_equal(const GroupCols* chunks, uint64_t ra, uint64_t rb) {
 // output array: 3.0 ms per 1e8 rows and select, r4g2.)
 constexpr int kCompactPer = 8;                        // rows per thread and tile
 constexpr int kCompactRows = 256 * kCompactPer;
+// cursor[0]: the append cursor; cursor[1] / cursor[2]: AND / OR of every appended key (their XOR has the bits in
+// which the keys differ: the radix sort skips the common high bits)
 __global__ __launch_bounds__(256) void group_compact(GroupCols g, int64_t n, int32_t hashed, int64_t chunk,
                                                      uint64_t* __restrict__ out_keys, uint64_t* __restrict__ out_rows,
                                                      unsigned long long* __restrict__ cursor) {
   __shared__ uint32_t wave_n[4];
   __shared__ unsigned long long tile_base;
+  __shared__ unsigned long long wave_and[4], wave_or[4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint64_t k_and = ~0ull, k_or = 0;
   for (int64_t t0 = (int64_t)blockIdx.x * kCompactRows; t0 < n; t0 += (int64_t)gridDim.x * kCompactRows) {
     uint64_t key[kCompactPer];
     uint64_t bal[kCompactPer];
@@ -167,6 +171,10 @@ __global__ __launch_bounds__(256) void group_compact(GroupCols g, int64_t n, int
       const int64_t r = t0 + u * 256 + threadIdx.x;
       const bool v = r < n && row_valid(g, r);
       key[u] = v ? (hashed ? tuple_key(g, r) : value_bits(g, 0, r)) : 0;
+      if (v) {
+        k_and &= key[u];
+        k_or |= key[u];
+      }
       bal[u] = __builtin_amdgcn_ballot_w64(v);
       cnt += (uint32_t)__builtin_popcountll(bal[u]);
     }
@@ -192,6 +200,22 @@ __global__ __launch_bounds__(256) void group_compact(GroupCols g, int64_t n, int
       pos += (unsigned long long)__builtin_popcountll(bal[u]);
     }
     __syncthreads();  // wave_n / tile_base are rewritten by the next tile
+  }
+  // the workgroup's AND / OR: lanes, then waves, then one atomic pair
+  for (int d = 32; d >= 1; d >>= 1) {
+    k_and &= __shfl_xor(k_and, d);
+    k_or |= __shfl_xor(k_or, d);
+  }
+  if (lane == 0) {
+    wave_and[wave] = k_and;
+    wave_or[wave] = k_or;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint64_t a = wave_and[0] & wave_and[1] & wave_and[2] & wave_and[3];
+    const uint64_t o = wave_or[0] | wave_or[1] | wave_or[2] | wave_or[3];
+    if (a != ~0ull) atomicAnd(&cursor[1], (unsigned long long)a);
+    if (o != 0) atomicOr(&cursor[2], (unsigned long long)o);
   }
 }
 
@@ -519,13 +543,14 @@ static dq_status freq_build_impl(const int32_t* types, int32_t n_cols, const dq_
   std::lock_guard<std::mutex> lock(g_arena_mu);
   const int D = device;
   DevBuf sel_keys(D, 2), sel_rows(D, 4), nsel(D, 5), tmp(D, 6), sorted_keys(D, 7), sorted_rows(D, 8), d_chunks(D, 9);
-  if (dq_status s = nsel.alloc(8)) return s;
+  if (dq_status s = nsel.alloc(24)) return s;
   if (dq_status s = sel_keys.alloc(std::max<int64_t>(1, total) * 8)) return s;
   if (t->hashed) {
     if (dq_status s = sel_rows.alloc(std::max<int64_t>(1, total) * 8)) return s;
   }
   int64_t nv = 0;
-  GHIP(hipMemsetAsync(nsel.p, 0, 8, t->stream));
+  const unsigned long long cur0[3] = {0ull, ~0ull, 0ull};  // count, AND, OR of the appended keys
+  GHIP(hipMemcpyAsync(nsel.p, cur0, sizeof(cur0), hipMemcpyHostToDevice, t->stream));
   for (int k = 0; k < n_chunks; ++k) {
     const int64_t n = chunk_rows[k];
     if (n == 0) continue;
@@ -535,8 +560,14 @@ static dq_status freq_build_impl(const int32_t* types, int32_t n_cols, const dq_
                        nsel.as<unsigned long long>());
     GHIP(hipGetLastError());
   }
-  GHIP(hipMemcpyAsync(&nv, nsel.p, 8, hipMemcpyDeviceToHost, t->stream));
+  unsigned long long cur[3];
+  GHIP(hipMemcpyAsync(cur, nsel.p, sizeof(cur), hipMemcpyDeviceToHost, t->stream));
   GHIP(hipStreamSynchronize(t->stream));
+  nv = (int64_t)cur[0];
+  // the keys agree above their highest differing bit: sorting bits [0, end_bit) gives the same order as all 64
+  // (small-range integer columns: 2 digit passes instead of 6)
+  const uint64_t differ = nv > 0 ? (uint64_t)(cur[1] ^ cur[2]) : 0ull;
+  const int end_bit = differ ? 64 - __builtin_clzll(differ) : 1;
   t->n_values = nv;
   if (dq_status s = sorted_keys.alloc(std::max<int64_t>(1, nv) * 8)) return s;
   if (nv > 0) {
@@ -544,11 +575,11 @@ static dq_status freq_build_impl(const int32_t* types, int32_t n_cols, const dq_
     if (t->hashed) {
       if (dq_status s = sorted_rows.alloc(nv * 8)) return s;
       GHIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, sel_keys.as<uint64_t>(), sorted_keys.as<uint64_t>(),
-                                              sel_rows.as<uint64_t>(), sorted_rows.as<uint64_t>(), (int)nv, 0, 64,
+                                              sel_rows.as<uint64_t>(), sorted_rows.as<uint64_t>(), (int)nv, 0, end_bit,
                                               t->stream));
       if (dq_status s = tmp.alloc(tb)) return s;
       GHIP(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, sel_keys.as<uint64_t>(), sorted_keys.as<uint64_t>(),
-                                              sel_rows.as<uint64_t>(), sorted_rows.as<uint64_t>(), (int)nv, 0, 64,
+                                              sel_rows.as<uint64_t>(), sorted_rows.as<uint64_t>(), (int)nv, 0, end_bit,
                                               t->stream));
       // exact check of equal-hash neighbours
       if (dq_status s = d_chunks.alloc(gcs.size() * sizeof(GroupCols))) return s;
@@ -563,10 +594,10 @@ static dq_status freq_build_impl(const int32_t* types, int32_t n_cols, const dq_
       if (coll) return set_error(DQ_E_UNSUPPORTED, "dq_freq_build: 64-bit tuple-hash collision between distinct values");
     } else {
       GHIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, sel_keys.as<uint64_t>(), sorted_keys.as<uint64_t>(),
-                                             (int)nv, 0, 64, t->stream));
+                                             (int)nv, 0, end_bit, t->stream));
       if (dq_status s = tmp.alloc(tb)) return s;
       GHIP(hipcub::DeviceRadixSort::SortKeys(tmp.p, tb, sel_keys.as<uint64_t>(), sorted_keys.as<uint64_t>(), (int)nv,
-                                             0, 64, t->stream));
+                                             0, end_bit, t->stream));
     }
   }
   if (mi) return mi_from_joint(t, sorted_keys.as<uint64_t>(), sorted_rows.as<uint64_t>(), nv, d_chunks.as<GroupCols>(), *mi);
