@@ -738,12 +738,26 @@ dq_status dq_freq_merge(const dq_freq_table* a, const dq_freq_table* b, dq_freq_
   GHIP(hipMalloc(&t->d_counts, std::max<int64_t>(1, n) * 8));
   if (t->hashed) GHIP(hipMalloc(&t->d_keys2, std::max<int64_t>(1, n) * 8));
   if (n > 0 && !t->hashed) {
+    // both tables' keys are sorted: every key lies between the smaller first and the larger last key, and so
+    // shares their common high bits -- the sort covers only the bits below (same order as all 64)
+    uint64_t ends[4] = {~0ull, 0ull, ~0ull, 0ull};
+    if (a->n_groups > 0) {
+      GHIP(hipMemcpyAsync(&ends[0], a->d_keys, 8, hipMemcpyDeviceToHost, t->stream));
+      GHIP(hipMemcpyAsync(&ends[1], a->d_keys + (a->n_groups - 1), 8, hipMemcpyDeviceToHost, t->stream));
+    }
+    if (b->n_groups > 0) {
+      GHIP(hipMemcpyAsync(&ends[2], b->d_keys, 8, hipMemcpyDeviceToHost, t->stream));
+      GHIP(hipMemcpyAsync(&ends[3], b->d_keys + (b->n_groups - 1), 8, hipMemcpyDeviceToHost, t->stream));
+    }
+    GHIP(hipStreamSynchronize(t->stream));
+    const uint64_t lo = std::min(ends[0], ends[2]), hi = std::max(ends[1], ends[3]);
+    const int end_bit = (lo ^ hi) ? 64 - __builtin_clzll(lo ^ hi) : 1;
     size_t tb = 0;
     GHIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k_in.as<uint64_t>(), k_s.as<uint64_t>(), c_in.as<int64_t>(),
-                                            c_s.as<int64_t>(), (int)n, 0, 64, t->stream));
+                                            c_s.as<int64_t>(), (int)n, 0, end_bit, t->stream));
     if (dq_status s = tmp.alloc(tb)) return s;
     GHIP(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, k_in.as<uint64_t>(), k_s.as<uint64_t>(), c_in.as<int64_t>(),
-                                            c_s.as<int64_t>(), (int)n, 0, 64, t->stream));
+                                            c_s.as<int64_t>(), (int)n, 0, end_bit, t->stream));
     tb = 0;
     GHIP(hipcub::DeviceReduce::ReduceByKey(nullptr, tb, k_s.as<uint64_t>(), t->d_keys, c_s.as<int64_t>(), t->d_counts,
                                            nruns.as<int64_t>(), hipcub::Sum(), (int)n, t->stream));
