@@ -114,10 +114,7 @@ __device__ uint64_t tuple_hash(const GroupCols& g, int64_t r, uint64_t seed = kS
 }
 __device__ uint64_t tuple_key(const GroupCols& g, int64_t r) { return tuple_hash(g, r) & g.key_mask; }
 
-__device__ bool tuple_equal(const GroupCols* chunks, uint64_t ra, uint64_t rb) {
-  const GroupCols& ga = chunks[ra >> kRowBits];
-  const GroupCols& gb = chunks[rb >> kRowBits];
-  const int64_t a = (int64_t)(ra & ((1ull << kRowBits) - 1)), b = (int64_t)(rb & ((1ull << kRowBits) - 1));
+__device__ __forceinline__ bool tuple_equal_rows(const GroupCols& ga, const GroupCols& gb, int64_t a, int64_t b) {
   for (int c = 0; c < ga.n_cols; ++c) {
     if (ga.type[c] == DQ_TYPE_UTF8 || ga.type[c] == DQ_TYPE_LARGE_UTF8) {
       const uint8_t *pa, *pb;
@@ -143,6 +140,10 @@ __device__ bool tuple_equal(const GroupCols* chunks, uint64_t ra, uint64_t rb) {
     }
   }
   return true;
+}
+__device__ bool tuple_equal(const GroupCols* chunks, uint64_t ra, uint64_t rb) {
+  return tuple_equal_rows(chunks[ra >> kRowBits], chunks[rb >> kRowBits], (int64_t)(ra & ((1ull << kRowBits) - 1)),
+                          (int64_t)(rb & ((1ull << kRowBits) - 1)));
 }
 
 // The non-null rows' keys (and, hashed, their row ids) of a chunk appended to out_keys / out_rows at the launch-wide
@@ -219,11 +220,19 @@ __global__ __launch_bounds__(256) void group_compact(GroupCols g, int64_t n, int
   }
 }
 
-// neighbours with equal hash keys must hold equal tuples
+// neighbours with equal hash keys must hold equal tuples.  ONE: a single chunk, whose column descriptor comes in the
+// kernel arguments (scalar loads) instead of from a per-row lookup in global memory -- one dependent load fewer
+// per compared pair
+template <bool ONE>
 __global__ void verify_runs(const uint64_t* __restrict__ keys, const uint64_t* __restrict__ rows, int64_t n,
-                            const GroupCols* __restrict__ chunks, int32_t* __restrict__ collision) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x + 1; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    if (keys[i] == keys[i - 1] && !tuple_equal(chunks, rows[i], rows[i - 1])) atomicOr(collision, 1);
+                            const GroupCols* __restrict__ chunks, GroupCols g0, int32_t* __restrict__ collision) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x + 1; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (keys[i] != keys[i - 1]) continue;
+    const bool eq = ONE ? tuple_equal_rows(g0, g0, (int64_t)(rows[i] & ((1ull << kRowBits) - 1)),
+                                           (int64_t)(rows[i - 1] & ((1ull << kRowBits) - 1)))
+                        : tuple_equal(chunks, rows[i], rows[i - 1]);
+    if (!eq) atomicOr(collision, 1);
+  }
 }
 
 constexpr int kSumBlocks = 1024;
@@ -585,8 +594,12 @@ static dq_status freq_build_impl(const int32_t* types, int32_t n_cols, const dq_
       if (dq_status s = d_chunks.alloc(gcs.size() * sizeof(GroupCols))) return s;
       GHIP(hipMemcpyAsync(d_chunks.p, gcs.data(), gcs.size() * sizeof(GroupCols), hipMemcpyHostToDevice, t->stream));
       GHIP(hipMemsetAsync(nsel.p, 0, 8, t->stream));
-      hipLaunchKernelGGL(verify_runs, dim3(grid_for(nv)), dim3(256), 0, t->stream, sorted_keys.as<uint64_t>(),
-                         sorted_rows.as<uint64_t>(), nv, d_chunks.as<GroupCols>(), nsel.as<int32_t>());
+      if (gcs.size() == 1)
+        hipLaunchKernelGGL(verify_runs<true>, dim3(grid_for(nv)), dim3(256), 0, t->stream, sorted_keys.as<uint64_t>(),
+                           sorted_rows.as<uint64_t>(), nv, d_chunks.as<GroupCols>(), gcs[0], nsel.as<int32_t>());
+      else
+        hipLaunchKernelGGL(verify_runs<false>, dim3(grid_for(nv)), dim3(256), 0, t->stream, sorted_keys.as<uint64_t>(),
+                           sorted_rows.as<uint64_t>(), nv, d_chunks.as<GroupCols>(), gcs[0], nsel.as<int32_t>());
       GHIP(hipGetLastError());
       int32_t coll = 0;
       GHIP(hipMemcpyAsync(&coll, nsel.p, 4, hipMemcpyDeviceToHost, t->stream));
