@@ -38,6 +38,7 @@ constexpr int kQBins = 2048;  // 11-bit digits
 constexpr int kQUnroll = 4;   // 16-byte vectors in flight per thread
 constexpr int kQPasses = 6;
 constexpr int kQStage = 256;  // APPEND: candidate keys staged in LDS per quantile and workgroup
+constexpr int kQAndOrCopies = 16;  // pass 0's AND / OR of the keys: copies the workgroups spread over
 constexpr int kQShift[kQPasses] = {53, 42, 31, 20, 9, 0};
 constexpr int kQWidth[kQPasses] = {11, 11, 11, 11, 11, 9};
 
@@ -88,7 +89,8 @@ template <int TYPE, int V, bool APPEND>
 __global__ __launch_bounds__(kQBlock) void dq_quantile_hist(const void* __restrict__ values,
                                                             const uint32_t* __restrict__ validity, int64_t n,
                                                             int32_t shift, uint32_t dmask, int32_t nq, QSelect sel,
-                                                            unsigned long long* __restrict__ hist) {
+                                                            unsigned long long* __restrict__ hist,
+                                                            unsigned long long* __restrict__ andor) {
   using T = typename std::conditional<TYPE == DQ_TYPE_I32, uint32_t, uint64_t>::type;
   // LDS: nq x kQBins digit counts; APPEND: + nq x kQStage staged keys + nq reserved / nq staged counts
   extern __shared__ uint32_t lds_hist[];
@@ -99,6 +101,7 @@ __global__ __launch_bounds__(kQBlock) void dq_quantile_hist(const void* __restri
   if (APPEND && threadIdx.x < 2 * nq) st_res[threadIdx.x] = 0;
   __syncthreads();
   const T* v = reinterpret_cast<const T*>(values);
+  uint64_t k_and = ~0ull, k_or = 0;  // andor != nullptr (pass 0): AND / OR of the non-null keys
   const int64_t nvec = (n + V - 1) / V;
   const int64_t stride = (int64_t)gridDim.x * kQBlock;
   for (int64_t v0 = (int64_t)blockIdx.x * kQBlock + threadIdx.x; v0 - threadIdx.x < nvec; v0 += stride * kQUnroll) {
@@ -141,6 +144,16 @@ __global__ __launch_bounds__(kQBlock) void dq_quantile_hist(const void* __restri
         dig[u * V + e] = (uint32_t)(key[u * V + e] >> shift) & dmask;
       }
     if constexpr (!APPEND) {
+      if (andor) {
+#pragma unroll
+        for (int u = 0; u < kQUnroll; ++u)
+#pragma unroll
+          for (int e = 0; e < V; ++e)
+            if ((vw[u] >> e) & 1u) {
+              k_and &= key[u * V + e];
+              k_or |= key[u * V + e];
+            }
+      }
       for (int q = 0; q < nq; ++q) {
         const uint64_t pm = sel.pmask[q], pf = sel.prefix[q];
         uint32_t* hq = lds_hist + q * kQBins;
@@ -217,6 +230,30 @@ __global__ __launch_bounds__(kQBlock) void dq_quantile_hist(const void* __restri
   __syncthreads();
   for (int i = threadIdx.x; i < nq * kQBins; i += kQBlock)
     if (lds_hist[i]) atomicAdd(&hist[i], (unsigned long long)lds_hist[i]);
+  if (!APPEND && andor) {
+    // the keys agree on every bit where AND == OR: the host skips the later passes whose digit lies there.  Lanes,
+    // then waves (LDS), then one atomic pair per workgroup into one of kQAndOrCopies copies (blockIdx % copies; the
+    // host combines them): every wave's atomics on one pair of addresses had serialized (+0.3 ms per launch)
+    __shared__ unsigned long long w_and[kQBlock / 64], w_or[kQBlock / 64];
+    for (int d = 32; d >= 1; d >>= 1) {
+      k_and &= __shfl_xor(k_and, d);
+      k_or |= __shfl_xor(k_or, d);
+    }
+    if ((threadIdx.x & 63) == 0) {
+      w_and[threadIdx.x >> 6] = k_and;
+      w_or[threadIdx.x >> 6] = k_or;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int w = 1; w < kQBlock / 64; ++w) {
+        k_and &= w_and[w];
+        k_or |= w_or[w];
+      }
+      unsigned long long* const c = andor + 2 * (blockIdx.x % kQAndOrCopies);
+      if (k_and != ~0ull) atomicAnd(&c[0], (unsigned long long)k_and);
+      if (k_or != 0) atomicOr(&c[1], (unsigned long long)k_or);
+    }
+  }
   if constexpr (APPEND) {
     __shared__ unsigned long long flush_base[DQ_MAX_QUANTILES];
     if (threadIdx.x < nq && st_ok[threadIdx.x] > 0)
@@ -248,13 +285,14 @@ __global__ __launch_bounds__(kQBlock) void dq_quantile_cand_hist(const unsigned 
 
 template <int TYPE, int V>
 void launch_hist(bool append, int grid, size_t lds, hipStream_t st, const void* values, const uint32_t* val,
-                 int64_t rows, int shift, uint32_t dmask, int nq, const QSelect& sel, unsigned long long* hist) {
+                 int64_t rows, int shift, uint32_t dmask, int nq, const QSelect& sel, unsigned long long* hist,
+                 unsigned long long* andor) {
   if (append)
     hipLaunchKernelGGL((dq_quantile_hist<TYPE, V, true>), dim3(grid), dim3(kQBlock), lds, st, values, val, rows, shift,
-                       dmask, nq, sel, hist);
+                       dmask, nq, sel, hist, nullptr);
   else
     hipLaunchKernelGGL((dq_quantile_hist<TYPE, V, false>), dim3(grid), dim3(kQBlock), lds, st, values, val, rows,
-                       shift, dmask, nq, sel, hist);
+                       shift, dmask, nq, sel, hist, andor);
 }
 
 #define QHIP(x)                                                                             \
@@ -589,7 +627,30 @@ dq_status dq_approx_quantiles(int32_t type, const dq_column_view* cols, const in
   bool compacted = false;
   std::vector<int64_t> remaining(n_q, 0), cand_off(n_q, 0), cand_len(n_q, 0);
   std::vector<int> hrow(n_q);  // histogram row of quantile q in this pass
+  // pass 0 also leaves the AND / OR of the non-null keys: a later pass whose digit bits are equal in every key
+  // (a small-range integer column's high digits) is skipped -- its digit is known and no rank moves
+  DevHist andor_buf;
+  QHIP(hipMalloc(&andor_buf.p, 16 * kQAndOrCopies));
+  unsigned long long* const d_andor = andor_buf.p;
+  unsigned long long andor0[2 * kQAndOrCopies];
+  for (int i = 0; i < kQAndOrCopies; ++i) {
+    andor0[2 * i] = ~0ull;
+    andor0[2 * i + 1] = 0ull;
+  }
+  QHIP(hipMemcpyAsync(d_andor, andor0, sizeof(andor0), hipMemcpyHostToDevice, stream));
+  uint64_t same_bits = 0;  // bits equal in every non-null key (known after pass 0)
+  uint64_t or_bits = 0;
   for (int pass = 0; pass < kQPasses; ++pass) {
+    if (pass > 0) {
+      const uint64_t dm = ((1ull << kQWidth[pass]) - 1ull) << kQShift[pass];
+      if ((same_bits & dm) == dm) {
+        for (int q = 0; q < n_q; ++q) {
+          sel.prefix[q] |= or_bits & dm;
+          sel.pmask[q] |= dm;
+        }
+        continue;
+      }
+    }
     QHIP(hipMemsetAsync(dh.p, 0, hist_bytes, stream));
     for (int q = 0; q < n_q; ++q) hrow[q] = q;
     const uint32_t dmask32 = (1u << kQWidth[pass]) - 1u;
@@ -653,15 +714,16 @@ dq_status dq_approx_quantiles(int32_t type, const dq_column_view* cols, const in
         const int grid = (int)std::min<int64_t>(4096, (rows + per_block - 1) / per_block);
         const void* vals = cols[c].values;
         const int sh = kQShift[pass];
+        unsigned long long* const ao_p = pass == 0 ? d_andor : nullptr;
         if (type == DQ_TYPE_F64) {
-          if (aligned) launch_hist<DQ_TYPE_F64, 2>(append, grid, lds, stream, vals, val, rows, sh, dmask32, nu, usel, dh.p);
-          else launch_hist<DQ_TYPE_F64, 1>(append, grid, lds, stream, vals, val, rows, sh, dmask32, nu, usel, dh.p);
+          if (aligned) launch_hist<DQ_TYPE_F64, 2>(append, grid, lds, stream, vals, val, rows, sh, dmask32, nu, usel, dh.p, ao_p);
+          else launch_hist<DQ_TYPE_F64, 1>(append, grid, lds, stream, vals, val, rows, sh, dmask32, nu, usel, dh.p, ao_p);
         } else if (type == DQ_TYPE_I64) {
-          if (aligned) launch_hist<DQ_TYPE_I64, 2>(append, grid, lds, stream, vals, val, rows, sh, dmask32, nu, usel, dh.p);
-          else launch_hist<DQ_TYPE_I64, 1>(append, grid, lds, stream, vals, val, rows, sh, dmask32, nu, usel, dh.p);
+          if (aligned) launch_hist<DQ_TYPE_I64, 2>(append, grid, lds, stream, vals, val, rows, sh, dmask32, nu, usel, dh.p, ao_p);
+          else launch_hist<DQ_TYPE_I64, 1>(append, grid, lds, stream, vals, val, rows, sh, dmask32, nu, usel, dh.p, ao_p);
         } else {
-          if (aligned) launch_hist<DQ_TYPE_I32, 4>(append, grid, lds, stream, vals, val, rows, sh, dmask32, nu, usel, dh.p);
-          else launch_hist<DQ_TYPE_I32, 1>(append, grid, lds, stream, vals, val, rows, sh, dmask32, nu, usel, dh.p);
+          if (aligned) launch_hist<DQ_TYPE_I32, 4>(append, grid, lds, stream, vals, val, rows, sh, dmask32, nu, usel, dh.p, ao_p);
+          else launch_hist<DQ_TYPE_I32, 1>(append, grid, lds, stream, vals, val, rows, sh, dmask32, nu, usel, dh.p, ao_p);
         }
         QHIP(hipGetLastError());
       }
@@ -679,6 +741,16 @@ dq_status dq_approx_quantiles(int32_t type, const dq_column_view* cols, const in
     QHIP(hipMemcpyAsync(h.data(), dh.p, hist_bytes, hipMemcpyDeviceToHost, stream));
     QHIP(hipStreamSynchronize(stream));
     if (pass == 0) {
+      unsigned long long ao[2 * kQAndOrCopies];
+      QHIP(hipMemcpyAsync(ao, d_andor, sizeof(ao), hipMemcpyDeviceToHost, stream));
+      QHIP(hipStreamSynchronize(stream));
+      uint64_t k_and = ~0ull;
+      or_bits = 0;
+      for (int i = 0; i < kQAndOrCopies; ++i) {
+        k_and &= ao[2 * i];
+        or_bits |= ao[2 * i + 1];
+      }
+      same_bits = ~(k_and ^ or_bits);
       for (int b = 0; b < kQBins; ++b) n += (int64_t)h[b];  // every non-null row matches the empty prefix (row 0)
       *count = n;
       if (n == 0) return DQ_OK;  // all values NULL: no digest (fromAggregationResult -> None)

@@ -120,6 +120,39 @@ def O_str(q):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("case", ["i64_small", "i32_small", "i64_const", "f64_one_binade", "f64_const", "i64_two"])
+def test_gpu_quantiles_skip_equal_digits(dq, case):
+    """Columns whose keys agree on whole digits (small-range integers, one binade, a constant): the select skips
+    the passes over those digits (known from pass 0's AND / OR of the keys) and still answers every rank exactly,
+    over several chunks with nulls."""
+    from deequ_amd.table import column_from_numpy
+
+    rng = np.random.default_rng(len(case))
+    n = 250_003
+    dtype = case.split("_")[0]
+    if case == "i64_small":
+        v = rng.integers(0, 1000, n, dtype=np.int64)
+    elif case == "i32_small":
+        v = rng.integers(0, 70_000, n, dtype=np.int64).astype(np.int32)
+    elif case == "i64_const":
+        v = np.full(n, -7, dtype=np.int64)
+    elif case == "i64_two":
+        v = rng.choice(np.array([1 << 40, (1 << 40) + 3], dtype=np.int64), n)
+    elif case == "f64_one_binade":
+        v = 1.0 + rng.random(n)
+    else:
+        v = np.full(n, 2.5)
+    valid = rng.random(n) >= 0.1
+    cuts = [0, 7, 100_000, n]
+    parts = [dq.Table([column_from_numpy("x", dtype, v[a:b], valid[a:b])]) for a, b in zip(cuts, cuts[1:])]
+    for err in (0.0, 0.01):
+        want = O.approx_quantiles_exact(v, valid, QS, err)
+        got = dq.ApproxQuantiles("x", QS, err).calculate(parts).value.get()
+        for q, w in zip(QS, want):
+            assert _same(got[O_str(q)], w), (case, err, q, got[O_str(q)], w)
+
+
+@pytest.mark.gpu
 def test_gpu_quantiles_chunks_nulls_and_reference_bands(dq):
     from deequ_amd.table import column_from_numpy
 

@@ -26,13 +26,17 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=float, default=1e9)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--int-range", type=int, default=0, help="an i64 column uniform in [0, R) instead of the f64 one")
     a = ap.parse_args()
     n = int(a.rows)
     g = torch.Generator(device="cuda").manual_seed(7)
-    vals = torch.randn(n, device="cuda", dtype=torch.float64, generator=g) * 1e3
+    if a.int_range:
+        vals = torch.randint(0, a.int_range, (n,), device="cuda", dtype=torch.int64, generator=g)
+    else:
+        vals = torch.randn(n, device="cuda", dtype=torch.float64, generator=g) * 1e3
     valid = torch.randint(0, 256, ((n + 31) // 32 * 4,), device="cuda", dtype=torch.uint8, generator=g)
     valid |= 0xEF  # ~1/8 nulls
-    col = Column("x", "f64", n, vals.view(torch.uint8), valid, None, nullable=True)
+    col = Column("x", "i64" if a.int_range else "f64", n, vals.view(torch.uint8), valid, None, nullable=True)
     t = dq.Table([col])
     for qs in ([0.5], [0.25, 0.5, 0.75], [0.01, 0.1, 0.25, 0.5, 0.75, 0.9, 0.99, 0.999]):
         device_quantiles(t, "x", qs, 0.01)  # warm-up
