@@ -359,6 +359,7 @@ constexpr int kDCountCopies = 8;             // bucket-count copies (blockIdx % 
                                              // column's hot bucket gets every workgroup's atomic at the launch's end
 constexpr int kDStage = 2048;                // candidate keys staged per workgroup (flushed past kDStage - 1024)
 constexpr int kDCells = 2048;                // cells of the splitters' lookup table (DigestCells)
+constexpr int kDAndOrCopies = 16;            // the candidates' AND / OR: copies the workgroups spread over
 
 // the key of row i * n / m of a chunk (i < m), and whether the row is non-null
 template <int TYPE>
@@ -463,6 +464,7 @@ __global__ __launch_bounds__(kQBlock) void dq_digest_pass(const void* __restrict
   }
   __syncthreads();
   const int lane = threadIdx.x & 63;
+  uint64_t c_and = ~0ull, c_or = 0;  // !COUNT: AND / OR of the thread's candidate keys
   constexpr int kIter = kQBlock * kDRows;  // rows per workgroup and iteration
   // the next iteration's values and validity words are loaded before this iteration's searches (in flight
   // behind them): per 1e8 rows the count pass 0.49 -> 0.23 ms, the compaction pass 0.63 -> 0.35 ms (r4y)
@@ -506,6 +508,10 @@ __global__ __launch_bounds__(kQBlock) void dq_digest_pass(const void* __restrict
 #pragma unroll
       for (int u = 0; u < kDRows; ++u) {
         const bool take = ok[u] && tgt[bk[u]];
+        if (take) {
+          c_and &= key[u];
+          c_or |= key[u];
+        }
         const uint64_t bal = __builtin_amdgcn_ballot_w64(take);
         if (bal != 0) {
           const int first = __builtin_ctzll(bal);
@@ -539,6 +545,27 @@ __global__ __launch_bounds__(kQBlock) void dq_digest_pass(const void* __restrict
       __syncthreads();
       const unsigned long long b = st_base;
       for (uint32_t i = threadIdx.x; i < staged; i += kQBlock) cand[b + i] = stage[i];
+    }
+    // the candidates' AND / OR (lanes, waves, then one pair per workgroup into copy blockIdx % kDAndOrCopies of
+    // cursor[1 ..]): the sort skips the high bits every candidate shares
+    __shared__ unsigned long long w_and[kQBlock / 64], w_or[kQBlock / 64];
+    for (int d = 32; d >= 1; d >>= 1) {
+      c_and &= __shfl_xor(c_and, d);
+      c_or |= __shfl_xor(c_or, d);
+    }
+    if (lane == 0) {
+      w_and[threadIdx.x >> 6] = c_and;
+      w_or[threadIdx.x >> 6] = c_or;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int w = 1; w < kQBlock / 64; ++w) {
+        c_and &= w_and[w];
+        c_or |= w_or[w];
+      }
+      unsigned long long* const c = cursor + 1 + 2 * (blockIdx.x % kDAndOrCopies);
+      if (c_and != ~0ull) atomicAnd(&c[0], (unsigned long long)c_and);
+      if (c_or != 0) atomicOr(&c[1], (unsigned long long)c_or);
     }
   }
 }
@@ -834,7 +861,8 @@ dq_status dq_quantile_digest(int32_t type, const dq_column_view* cols, const int
   QHIP(keep_pool(device));
   StreamTmp small;
   const size_t o_spl = (size_t)ns_all * 8, o_cnt = o_spl + (size_t)(kDBuckets - 1) * 8,
-               o_cur = o_cnt + (size_t)kDCountCopies * kDBuckets * 8, o_first = o_cur + 8,
+               o_cur = o_cnt + (size_t)kDCountCopies * kDBuckets * 8,
+               o_first = o_cur + 8 + (size_t)kDAndOrCopies * 16,
                o_ok = o_first + ((size_t)(kDCells + 1) * 2 + 7) / 8 * 8, o_tgt = o_ok + (size_t)ns_all;
   QHIP(small.alloc(o_tgt + kDBuckets, stream));
   char* const sb = static_cast<char*>(small.p);
@@ -872,7 +900,16 @@ dq_status dq_quantile_digest(int32_t type, const dq_column_view* cols, const int
   const DigestCells C = digest_cells(type, spl, first);
   QHIP(hipMemcpyAsync(d_first, first.data(), first.size() * 2, hipMemcpyHostToDevice, stream));
   QHIP(hipMemsetAsync(d_counts.p, 0, (size_t)kDCountCopies * kDBuckets * 8, stream));
-  QHIP(hipMemsetAsync(d_cursor.p, 0, 8, stream));
+  {
+    unsigned long long cur0[1 + 2 * kDAndOrCopies];  // cursor, then (AND, OR) copies
+    cur0[0] = 0;
+    for (int i = 0; i < kDAndOrCopies; ++i) {
+      cur0[1 + 2 * i] = ~0ull;
+      cur0[2 + 2 * i] = 0ull;
+    }
+    QHIP(hipMemcpyAsync(d_cursor.p, cur0, sizeof(cur0), hipMemcpyHostToDevice, stream));
+    QHIP(hipStreamSynchronize(stream));  // cur0 is a stack array
+  }
   // 2. per-bucket counts
   if (dq_status st = for_chunks([&](auto tk, int grid, int c, int64_t rows) {
         hipLaunchKernelGGL((dq_digest_pass<decltype(tk)::value, true>), dim3(grid), dim3(kQBlock), 0, stream,
@@ -930,7 +967,17 @@ dq_status dq_quantile_digest(int32_t type, const dq_column_view* cols, const int
                            C, nullptr, d_target.p, cand, d_cursor.p);
       }))
     return st;
-  QHIP(hipcub::DeviceRadixSort::SortKeys(bb + o_tmp, tb, cand, sorted, (int)nc, 0, 64, stream));
+  // the candidates agree above their highest differing bit: sorting the bits below gives the full order
+  unsigned long long cur[1 + 2 * kDAndOrCopies];
+  QHIP(hipMemcpyAsync(cur, d_cursor.p, sizeof(cur), hipMemcpyDeviceToHost, stream));
+  QHIP(hipStreamSynchronize(stream));
+  uint64_t c_and = ~0ull, c_or = 0;
+  for (int i = 0; i < kDAndOrCopies; ++i) {
+    c_and &= cur[1 + 2 * i];
+    c_or |= cur[2 + 2 * i];
+  }
+  const int end_bit = (c_and ^ c_or) ? 64 - __builtin_clzll(c_and ^ c_or) : 1;
+  QHIP(hipcub::DeviceRadixSort::SortKeys(bb + o_tmp, tb, cand, sorted, (int)nc, 0, end_bit, stream));
   // 4. sample i = the sorted candidate at (its rank within its bucket) + (candidates of the flagged buckets before)
   std::vector<long long> idx((size_t)m);
   for (int64_t i = 0; i < m; ++i) {
