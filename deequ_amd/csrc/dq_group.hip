@@ -155,23 +155,61 @@ constexpr int kCompactPer = 8;                        // rows per thread and til
 constexpr int kCompactRows = 256 * kCompactPer;
 // cursor[0]: the append cursor; cursor[1] / cursor[2]: AND / OR of every appended key (their XOR has the bits in
 // which the keys differ: the radix sort skips the common high bits)
-__global__ __launch_bounds__(256) void group_compact(GroupCols g, int64_t n, int32_t hashed, int64_t chunk,
+// HASHED: keys are tuple hashes (any columns); else one numeric column whose value bits are the keys -- its next
+// tile's values and validity words are loaded before this tile's work (in flight behind it)
+template <bool HASHED>
+__global__ __launch_bounds__(256) void group_compact(GroupCols g, int64_t n, int64_t chunk,
                                                      uint64_t* __restrict__ out_keys, uint64_t* __restrict__ out_rows,
                                                      unsigned long long* __restrict__ cursor) {
   __shared__ uint32_t wave_n[4];
   __shared__ unsigned long long tile_base;
   __shared__ unsigned long long wave_and[4], wave_or[4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const bool hashed = HASHED;
   uint64_t k_and = ~0ull, k_or = 0;
-  for (int64_t t0 = (int64_t)blockIdx.x * kCompactRows; t0 < n; t0 += (int64_t)gridDim.x * kCompactRows) {
+  const int64_t tstride = (int64_t)gridDim.x * kCompactRows;
+  uint64_t nval[HASHED ? 1 : kCompactPer];
+  uint32_t nvw[HASHED ? 1 : kCompactPer];
+  auto fetch = [&](int64_t t0) __attribute__((always_inline)) {
+    if constexpr (!HASHED) {
+#pragma unroll
+      for (int u = 0; u < kCompactPer; ++u) {
+        const int64_t r = t0 + u * 256 + threadIdx.x;
+        nval[u] = 0;
+        nvw[u] = 0;
+        if (r < n) {
+          nval[u] = value_bits(g, 0, r);
+          nvw[u] = g.validity[0] ? g.validity[0][r >> 5] : 0xFFFFFFFFu;
+        }
+      }
+    }
+  };
+  fetch((int64_t)blockIdx.x * kCompactRows);
+  for (int64_t t0 = (int64_t)blockIdx.x * kCompactRows; t0 < n; t0 += tstride) {
     uint64_t key[kCompactPer];
     uint64_t bal[kCompactPer];
     uint32_t cnt = 0;
+    uint64_t cval[HASHED ? 1 : kCompactPer];
+    uint32_t cvw[HASHED ? 1 : kCompactPer];
+    if constexpr (!HASHED) {
+#pragma unroll
+      for (int u = 0; u < kCompactPer; ++u) {
+        cval[u] = nval[u];
+        cvw[u] = nvw[u];
+      }
+      if (t0 + tstride < n) fetch(t0 + tstride);
+    }
 #pragma unroll
     for (int u = 0; u < kCompactPer; ++u) {
       const int64_t r = t0 + u * 256 + threadIdx.x;
-      const bool v = r < n && row_valid(g, r);
-      key[u] = v ? (hashed ? tuple_key(g, r) : value_bits(g, 0, r)) : 0;
+      bool v;
+      if constexpr (HASHED) {
+        v = r < n && row_valid(g, r);
+        key[u] = v ? tuple_key(g, r) : 0;
+      } else {
+        v = r < n && ((cvw[u] >> (r & 31)) & 1u);
+        key[u] = v ? cval[u] : 0;
+      }
       if (v) {
         k_and &= key[u];
         k_or |= key[u];
@@ -564,9 +602,12 @@ static dq_status freq_build_impl(const int32_t* types, int32_t n_cols, const dq_
     const int64_t n = chunk_rows[k];
     if (n == 0) continue;
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(2048, (n + kCompactRows - 1) / kCompactRows));
-    hipLaunchKernelGGL(group_compact, dim3(grid), dim3(256), 0, t->stream, gcs[k], n, t->hashed, (int64_t)k,
-                       sel_keys.as<uint64_t>(), t->hashed ? sel_rows.as<uint64_t>() : nullptr,
-                       nsel.as<unsigned long long>());
+    if (t->hashed)
+      hipLaunchKernelGGL(group_compact<true>, dim3(grid), dim3(256), 0, t->stream, gcs[k], n, (int64_t)k,
+                         sel_keys.as<uint64_t>(), sel_rows.as<uint64_t>(), nsel.as<unsigned long long>());
+    else
+      hipLaunchKernelGGL(group_compact<false>, dim3(grid), dim3(256), 0, t->stream, gcs[k], n, (int64_t)k,
+                         sel_keys.as<uint64_t>(), nullptr, nsel.as<unsigned long long>());
     GHIP(hipGetLastError());
   }
   unsigned long long cur[3];
