@@ -95,7 +95,10 @@ for cfg, tab, an in (("c3", synth.c3_table, synth.c3_analyzers), ("c5", synth.c5
         plan = ScanPlan(an(t), t.schema)
         wall = (time.perf_counter() - a) * 1e3
         total, jit = plan.create_time()
+        plan.pred_wait()
+        ready = (time.perf_counter() - a) * 1e3
         rec[k] = {"wall_ms": round(wall, 3), "dq_plan_create_ms": round(total, 3), "pred_jit_ms": round(jit, 3),
+                  "pred_kernel_ready_ms": round(ready, 3),
                   "pred_kernel": plan.pred_compiled()[1] if plan.pred_compiled()[0] else None}
         plan.close()
     out[cfg] = rec
@@ -370,6 +373,10 @@ def run_config(cfg, args, deferred_cpu) -> dict:
     tables, analyzers, desc = config_setup(cfg, n, DEFAULT_CHUNK)
     torch.cuda.synchronize()
     plan = ScanPlan(analyzers, tables[0].schema)
+    # the steady state: a predicate kernel compiling in the background (AUTO) is waited for before the warm-up
+    a = time.perf_counter()
+    pred_compiled = plan.pred_wait()
+    pred_wait_ms = (time.perf_counter() - a) * 1e3
     str_bytes = sum(c.data_bytes for t in tables for c in t.columns.values() if c.dtype in ("utf8", "large_utf8"))
 
     def step():
@@ -405,6 +412,9 @@ def run_config(cfg, args, deferred_cpu) -> dict:
            "roofline": {"kernel": dom_name, "achieved": dom["GBps"], "frac": dom["GBps"] / HBM_PEAK_GBS,
                         "avg_launch_ms": dom["avg_ms"], "bytes_per_launch": dom["bytes_per_launch"]},
            "kernels": {k_: {kk: v[kk] for kk in ("launches", "avg_ms", "GBps")} for k_, v in kernels.items()}}
+    if plan.pred_compiled()[1] != "no predicates":
+        rec["pred_pass"] = {"compiled": pred_compiled, "note": plan.pred_compiled()[1],
+                            "waited_ms_before_warmup": round(pred_wait_ms, 3)}
     if cfg == "c1" and args.cpu_sample > 0:
         data_c1 = c1_host_data(tables[0])
         deferred_cpu.append(lambda: rec.__setitem__("cpu_baseline", cpu_baseline_c1(data_c1, args.cpu_threads,
@@ -414,14 +424,42 @@ def run_config(cfg, args, deferred_cpu) -> dict:
     return rec
 
 
+def _sha256(path):
+    import hashlib
+
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for blk in iter(lambda: f.read(1 << 20), b""):
+            h.update(blk)
+    return h.hexdigest()
+
+
+_PMC_CACHE = {}
+
+
+def pmc_file():
+    """The committed PMC summary (FETCH_SIZE + SQ passes, tools/profile_round.sh) -- used only when it was taken
+    from THIS library build (its recorded libdqscan.so sha256 equals the loaded library's), so a stale file
+    cannot feed the line."""
+    if "d" not in _PMC_CACHE:
+        from deequ_amd import _lib as L
+
+        d = None
+        try:
+            with open(PMC_FILE) as f:
+                d = json.load(f)
+            if d.get("library_sha256") != _sha256(L.LIB_PATH):
+                d = None
+        except (OSError, ValueError):
+            d = None
+        _PMC_CACHE["d"] = d
+    return _PMC_CACHE["d"]
+
+
 def pmc_record(kernel):
-    """The committed PMC pass record of `kernel` (FETCH_SIZE bytes, SQ instruction counts per launch), or None."""
-    try:
-        with open(PMC_FILE) as f:
-            recs = json.load(f)["kernels"]
-    except (OSError, ValueError, KeyError):
-        return None
-    for r in recs:
+    """The PMC pass record of `kernel` (FETCH_SIZE bytes, SQ instruction counts per launch), or None."""
+    d = pmc_file()
+    for r in (d or {}).get("kernels", []):
         if r["kernel"] == kernel:
             return r
     return None
@@ -448,7 +486,8 @@ def valu_bound(kernel, avg_ms):
     floor_ms = insts * VALU_CYCLES_PER_WAVE_INST / (1024 * 2.4e9) * 1e3
     out = {"valu_insts_per_launch": insts, "issue_floor_ms": floor_ms, "frac_of_launch": floor_ms / avg_ms,
            "model": "4 SIMD cycles per wave64 VALU instruction, 1024 SIMDs x 2.4 GHz (nominal peak clock)",
-           "source": os.path.relpath(PMC_FILE, ROOT)}
+           "source": os.path.relpath(PMC_FILE, ROOT), "pmc_commit": pmc_file().get("commit"),
+           "pmc_library_sha256": pmc_file().get("library_sha256")}
     # the clock the chip holds under this kernel (GRBM_GUI_ACTIVE / 8 XCDs / duration, committed probe): the
     # issue floor at that clock is what the launch can reach with its instruction count
     clocks = {}
@@ -469,23 +508,19 @@ def valu_bound(kernel, avg_ms):
 
 
 def roofline(dom_name, dom, traffic, kernels) -> dict:
-    """The dominant kernel against the bound that binds it.  Both floors per launch: HBM = algorithmic
-    bytes / 8 TB/s; VALU issue = wave64 VALU instructions (committed SQ pass) x 4 cycles / (1024 SIMDs x
-    2.4 GHz).  The larger floor is the roofline (`bound`); `achieved` / `peak` / `frac` are in its unit
-    (GB/s, or wave-instructions per second for VALU), the other bound is reported beside it."""
-    hbm = {"achieved": dom["GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": dom["GBps"] / HBM_PEAK_GBS,
-           "floor_ms": dom["bytes_per_launch"] / (HBM_PEAK_GBS * 1e9) * 1e3}
+    """The dominant kernel against the HBM roofline: `achieved` = its algorithmic bytes per launch
+    (§8d per-row bytes x the rows of one launch + its UTF8 payload) / its hipEvent-timed average launch, `frac`
+    = achieved / 8 TB/s.  The HLL kernels are limited by VALU issue before HBM: `valu_issue` gives that floor
+    (wave64 VALU instructions of the committed SQ pass of the same library build x 4 cycles / 1024 SIMDs, at the
+    nominal 2.4 GHz and at the clock the chip held) and the fraction of the launch it accounts for."""
     valu = valu_bound(dom["pmc_name"], dom["avg_ms"])
-    out = {"kernel": dom_name, "bytes_per_launch": dom["bytes_per_launch"], "avg_launch_ms": dom["avg_ms"],
-           "launches": dom["launches"], "traffic": traffic,
-           "traffic_source": os.path.relpath(PMC_FILE, ROOT) if traffic is not None else None}
-    if valu is not None and valu["issue_floor_ms"] > hbm["floor_ms"]:
-        peak = 1024 * 2.4e9 / VALU_CYCLES_PER_WAVE_INST
-        out.update(bound="valu", achieved=valu["valu_insts_per_launch"] / (dom["avg_ms"] / 1e3), peak=peak,
-                   unit="wave64 VALU instructions/s", frac=valu["frac_of_launch"], valu_issue=valu, hbm=hbm)
-    else:
-        out.update(bound="hbm", achieved=hbm["achieved"], peak=hbm["peak"], unit="GB/s", frac=hbm["frac"],
-                   valu_issue=valu, hbm=hbm)
+    out = {"kernel": dom_name, "bound": "hbm", "achieved": dom["GBps"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": dom["GBps"] / HBM_PEAK_GBS, "traffic": traffic,
+           "traffic_source": os.path.relpath(PMC_FILE, ROOT) if traffic is not None else None,
+           "bytes_per_launch": dom["bytes_per_launch"], "avg_launch_ms": dom["avg_ms"], "launches": dom["launches"],
+           "hbm_floor_ms": dom["bytes_per_launch"] / (HBM_PEAK_GBS * 1e9) * 1e3, "valu_issue": valu,
+           "limiter": ("valu_issue" if valu is not None and valu.get("frac_at_held_clock", valu["frac_of_launch"]) >
+                       dom["GBps"] / HBM_PEAK_GBS else "hbm")}
     out["kernels"] = kernels
     return out
 

@@ -8,7 +8,7 @@ from __future__ import annotations
 import ctypes
 import os
 
-ABI_VERSION = 3  # include/dqscan.h DQ_ABI_VERSION
+ABI_VERSION = 4  # include/dqscan.h DQ_ABI_VERSION
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DQ_LIB_PATH") or os.path.join(_HERE, "libdqscan.so")  # override: diagnostic A/B builds
@@ -249,6 +249,8 @@ def _load():
     L.dq_plan_kernel_bytes_per_row_x1000.argtypes = [c.c_void_p, c.c_int32]
     L.dq_plan_pred_compiled.restype = c.c_int32
     L.dq_plan_pred_compiled.argtypes = [c.c_void_p, c.c_char_p, c.c_int32]
+    L.dq_plan_pred_wait.restype = c.c_int32
+    L.dq_plan_pred_wait.argtypes = [c.c_void_p, c.c_int32]
     L.dq_state_merge.restype = c.c_int32
     L.dq_state_merge.argtypes = [P(State), P(State), P(State)]
     L.dq_state_combine.restype = c.c_int32
@@ -287,7 +289,7 @@ EXPORTED = [
     "dq_freq_export", "dq_freq_destroy", "dq_mutual_information", "dq_approx_quantiles", "dq_quantile_digest", "dq_freq_top", "dq_scan", "dq_finish",
     "dq_plan_reset", "dq_plan_destroy", "dq_plan_bytes_per_row_x1000", "dq_plan_num_launches",
     "dq_plan_enable_timing", "dq_plan_kernel_time", "dq_plan_variant_bytes_per_row_x1000",
-    "dq_plan_kernel_bytes_per_row_x1000", "dq_plan_pred_compiled",
+    "dq_plan_kernel_bytes_per_row_x1000", "dq_plan_pred_compiled", "dq_plan_pred_wait",
     "dq_state_merge", "dq_state_combine", "dq_state_merge_n", "dq_state_combine_n", "dq_state_is_defined", "dq_state_metric", "dq_hll_estimate",
     "dq_state_to_bytes", "dq_state_from_bytes", "dq_state_identifier",
 ]

@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <iterator>
 #include <limits>
 #include <map>
 #include <memory>
@@ -53,6 +54,10 @@ hipError_t launch_finalize(int32_t ncol, int32_t nranges_col, const ColPartial* 
 hipError_t launch_init_acc(ColPartial* col_acc, int32_t ncol, CorrPartial* pair_acc, int32_t npair, hipStream_t st);
 
 static thread_local char g_err[1024] = "";
+// set with the error when a plan exceeds a fixed per-plan capacity (columns, predicates, counters, `where`
+// bitmaps, column tasks, program length, regex LDS): dq_plan_create then splits the analyzers over several
+// plans instead of failing (a spec that exceeds a capacity alone is a routing error, DQ_E_UNSUPPORTED)
+static thread_local bool g_capacity = false;
 
 dq_status set_error(dq_status code, const char* fmt, ...) {
   va_list ap;
@@ -60,6 +65,15 @@ dq_status set_error(dq_status code, const char* fmt, ...) {
   std::vsnprintf(g_err, sizeof(g_err), fmt, ap);
   va_end(ap);
   return code;
+}
+
+static dq_status cap_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  std::vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  g_capacity = true;
+  return DQ_E_UNSUPPORTED;
 }
 
 #define HIP_TRY(expr)                                                                              \
@@ -433,6 +447,7 @@ struct dq_plan {
   std::vector<ColTask> col_tasks;        // sorted by variant
   struct Group { int32_t variant, first, count; };
   std::vector<Group> groups;              // one column-scan launch per variant group
+  std::vector<Group> pred_fused_groups;   // the predicate kernel's HLL tasks as column-pass launches (interpreter)
   std::vector<PairTask> pair_tasks;      // sorted by pair group
   std::vector<PairWG> pair_wgs;          // Correlation pass workgroup tasks (dq_pair.hip), moments fused
   int32_t n_fused = 0;                    // column tasks computed by the pair pass (sorted last)
@@ -446,12 +461,14 @@ struct dq_plan {
   bool has_pred = false;
   // the predicate pass compiled for this program (dq_pred_jit.cpp), or null: the interpreter runs it
   hipFunction_t pred_jit = nullptr;
+  PredJitRef pred_jit_ref;                              // its compile, while it runs in the background (AUTO)
   std::vector<int32_t> pred_jit_cols;                   // its slots' plan columns
   std::vector<int32_t> pred_jit_hll_task, pred_jit_hll_slot;  // fused HLL tasks (post-sort index) / accumulators
   int32_t pred_fused_first = 0, pred_fused_count = 0;  // those tasks sort last (after the pair-fused ones)
   std::string pred_jit_note;                            // why the interpreter runs, or the kernel's origin
   int32_t pred_pass = DQ_PRED_PASS_AUTO;                // dq_plan_options.pred_pass
   bool host_only = false;                               // dq_plan_explain: lower on the host, no device work
+  bool probe = false;                                   // host-only capacity check: stop after the program
   std::string pred_jit_src;                             // the generated kernel source (host_only plans)
   double create_ms = 0.0, pred_jit_ms = 0.0;            // dq_plan_create_time
 
@@ -487,6 +504,13 @@ struct dq_plan {
   int64_t bytes_per_row_x1000 = 0;
   int64_t pred_bytes_x1000 = 0, pair_bytes_x1000 = 0;
   int32_t launches_per_scan = 0;
+
+  // composite plan: an analyzer set over one plan's capacity runs as several fused plans ("parts") over
+  // disjoint spec subsets, each reading only its own columns; dq_scan runs every part on every chunk (in
+  // part order, on this plan's stream) and dq_finish scatters their states back to the caller's spec order
+  std::vector<dq_plan*> parts;
+  std::vector<std::vector<int32_t>> part_specs;  // this plan's spec index of each part spec
+  std::vector<std::vector<int32_t>> part_cols;   // this plan's column of each part column
 };
 
 static dq_status take_event(dq_plan* p, hipEvent_t* e) {
@@ -649,7 +673,7 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
     std::string key = canon(pool, n_pred, node);
     auto it = root_slot.find(key);
     if (it != root_slot.end()) { slot = it->second; return DQ_OK; }
-    if ((int32_t)root_slot.size() >= kMaxRoots) return set_error(DQ_E_UNSUPPORTED, "more than %d distinct predicates", kMaxRoots);
+    if ((int32_t)root_slot.size() >= kMaxRoots) return cap_error("more than %d distinct predicates", kMaxRoots);
     low.out.clear();
     if (dq_status s = low.lower(node, 0)) return s;
     slot = (int32_t)root_slot.size();
@@ -661,7 +685,7 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
     std::string key = "notnull:" + std::to_string(col);
     auto it = root_slot.find(key);
     if (it != root_slot.end()) { slot = it->second; return DQ_OK; }
-    if ((int32_t)root_slot.size() >= kMaxRoots) return set_error(DQ_E_UNSUPPORTED, "more than %d distinct predicates", kMaxRoots);
+    if ((int32_t)root_slot.size() >= kMaxRoots) return cap_error("more than %d distinct predicates", kMaxRoots);
     PredInstr ins{};
     ins.op = PO_ATOM_NOTNULL; ins.col_a = col; ins.col_b = -1;
     slot = (int32_t)root_slot.size();
@@ -673,7 +697,7 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
     auto key = std::make_pair(pred, where);
     auto it = counter_of.find(key);
     if (it != counter_of.end()) { c = it->second; return DQ_OK; }
-    if ((int32_t)counter_of.size() >= kMaxCounters) return set_error(DQ_E_UNSUPPORTED, "more than %d predicate counters", kMaxCounters);
+    if ((int32_t)counter_of.size() >= kMaxCounters) return cap_error("more than %d predicate counters", kMaxCounters);
     c = (int32_t)counter_of.size();
     counter_of[key] = c;
     return DQ_OK;
@@ -682,7 +706,7 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
     if (where_slot < 0) { b = -1; return DQ_OK; }
     auto it = bitmap_of.find(where_slot);
     if (it != bitmap_of.end()) { b = it->second; return DQ_OK; }
-    if ((int32_t)bitmap_of.size() >= kMaxWhere) return set_error(DQ_E_UNSUPPORTED, "more than %d distinct where filters on value analyzers", kMaxWhere);
+    if ((int32_t)bitmap_of.size() >= kMaxWhere) return cap_error("more than %d distinct where filters on value analyzers", kMaxWhere);
     b = (int32_t)bitmap_of.size();
     bitmap_of[where_slot] = b;
     return DQ_OK;
@@ -692,7 +716,7 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
     auto key = std::make_tuple(col, bm, dtype && p->schema[col].type == DQ_TYPE_F64 ? 1 : 0);
     auto it = col_task_of.find(key);
     if (it == col_task_of.end()) {
-      if ((int32_t)p->col_tasks.size() >= 256) return set_error(DQ_E_UNSUPPORTED, "too many column tasks");
+      if ((int32_t)p->col_tasks.size() >= kMaxColTasks) return cap_error("more than %d column tasks", kMaxColTasks);
       t = (int32_t)p->col_tasks.size();
       col_task_of[key] = t;
       ColTask ct{};
@@ -836,7 +860,7 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
       st.op = PO_STORE; st.slot = (int32_t)r; st.col_a = st.col_b = -1;
       code.push_back(st);
     }
-    if ((int32_t)code.size() > kMaxInstr) return set_error(DQ_E_UNSUPPORTED, "predicate program too long (%zu)", code.size());
+    if ((int32_t)code.size() > kMaxInstr) return cap_error("predicate program too long (%zu instructions, at most %d)", code.size(), kMaxInstr);
     int depth = 0, max_depth = 0;
     for (const PredInstr& ins : code) {
       depth += (ins.op == PO_AND || ins.op == PO_OR || ins.op == PO_STORE) ? -1 : (ins.op == PO_NOT ? 0 : 1);
@@ -857,6 +881,10 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
     prog.n_bitmaps = (int32_t)bitmap_of.size();
     for (auto& kv : bitmap_of) prog.bitmap_root[kv.second] = kv.first;
   }
+  if (p->regex_blob.size() > (size_t)kMaxRegexWords)
+    return cap_error("compiled patterns need %zu KB (LDS budget %d KB)", p->regex_blob.size() * 2 / 1024,
+                     kMaxRegexWords * 2 / 1024);
+  if (p->probe) return DQ_OK;  // capacity probe (dq_plan_create's split): every capacity check is above
 
   // the predicate program compiled into its own kernel when the generator takes it; HLL-only tasks (no
   // `where`) on its columns are hashed there (fused = 2) instead of re-reading the column in the column pass
@@ -884,10 +912,17 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
         p->pred_jit_src = src;
         note = src.empty() ? note : "host-only plan: kernel generated, not compiled";
       } else if (!src.empty()) {
-        p->pred_jit = pred_jit_get(src, p->device, note, p->pred_jit_ms);
+        // AUTO: hipRTC on a background thread (a cold compile takes ~0.3 s); the scan starts on the interpreter
+        // and switches to the compiled kernel between chunks once it is ready (dq_scan).  COMPILED: wait for it.
+        const bool bg = p->pred_pass == DQ_PRED_PASS_AUTO;
+        p->pred_jit_ref = pred_jit_request(src, p->device, bg, p->pred_jit_ms);
+        p->pred_jit = pred_jit_poll(p->pred_jit_ref, bg ? 0 : -1, note);
+        if (p->pred_jit || !pred_jit_pending(p->pred_jit_ref)) p->pred_jit_ref.reset();
       }
       p->pred_jit_note = note;
-      if (p->pred_jit || (p->host_only && !p->pred_jit_src.empty())) {  // (explain: as the compiled plan would)
+      // the fused arrangement (HLL tasks in the predicate kernel) whenever the kernel exists or is on its way;
+      // until it is there, dq_scan runs those tasks in the column pass (pred_fused_groups)
+      if (p->pred_jit || p->pred_jit_ref || (p->host_only && !p->pred_jit_src.empty())) {  // (explain: as compiled)
         p->pred_jit_cols = slots;
         p->pred_jit_hll_task = tasks;
         for (int32_t t : tasks) {
@@ -993,6 +1028,11 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
         p->groups.push_back({p->col_tasks[k].variant, k, 0});
       p->groups.back().count++;
     }
+    for (int32_t k = p->pred_fused_first; k < (int32_t)p->col_tasks.size(); ++k) {
+      if (p->pred_fused_groups.empty() || p->pred_fused_groups.back().variant != p->col_tasks[k].variant)
+        p->pred_fused_groups.push_back({p->col_tasks[k].variant, k, 0});
+      p->pred_fused_groups.back().count++;
+    }
     p->n_fused = (int32_t)std::count_if(fused.begin(), fused.end(), [](int f) { return f != 0; });
   }
 
@@ -1067,9 +1107,6 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
   if (dq_status s = dmalloc(&p->d_pred_acc, kPredAccCopies * sizeof(PredPartial))) return s;
   if (nct) HIP_TRY(hipMemcpyAsync(p->d_col_tasks, p->col_tasks.data(), nct * sizeof(ColTask), hipMemcpyHostToDevice, p->stream));
   if (npt) HIP_TRY(hipMemcpyAsync(p->d_pair_tasks, p->pair_tasks.data(), npt * sizeof(PairTask), hipMemcpyHostToDevice, p->stream));
-  if (p->regex_blob.size() > (size_t)kMaxRegexWords)
-    return set_error(DQ_E_UNSUPPORTED, "compiled patterns need %zu KB (LDS budget %d KB)",
-                     p->regex_blob.size() * 2 / 1024, kMaxRegexWords * 2 / 1024);
   if (!p->regex_blob.empty()) {
     if (dq_status s = dmalloc(&p->d_regex, p->regex_blob.size() * sizeof(uint16_t))) return s;
     HIP_TRY(hipMemcpyAsync(p->d_regex, p->regex_blob.data(), p->regex_blob.size() * sizeof(uint16_t),
@@ -1083,7 +1120,192 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
   return DQ_OK;
 }
 
+
+// ------------------------------------------------------------------------------------------
+// Splitting an analyzer set over one plan's capacity (composite plans)
+// ------------------------------------------------------------------------------------------
+// The reference fuses any number of scan-shareable analyzers into one data.agg
+// (AnalysisRunner.scala:293-303).  One plan here has fixed capacities (kMaxCols columns, kMaxRoots distinct
+// predicates, kMaxCounters counters, kMaxWhere `where` bitmaps, kMaxColTasks column tasks, kMaxInstr program
+// instructions, kMaxRegexWords of DFAs); an analyzer set over any of them is planned as several fused plans
+// over disjoint spec subsets.  Every part is one fused pass over the same chunks, merged in chunk order, so
+// each analyzer's state is exactly the one a single plan would produce (the states of different analyzers
+// are independent); a column shared by two parts is read once per part.
+
+static void pred_columns(const dq_pred_node* pool, int32_t n_pred, int32_t idx, std::vector<int32_t>& cols,
+                         int depth = 0) {
+  if (idx < 0 || idx >= n_pred || depth > 64) return;
+  const dq_pred_node& n = pool[idx];
+  switch (n.kind) {
+    case DQ_PRED_COLUMN: cols.push_back(n.a); return;
+    case DQ_PRED_CMP: case DQ_PRED_AND: case DQ_PRED_OR: case DQ_PRED_COALESCE:
+      pred_columns(pool, n_pred, n.a, cols, depth + 1);
+      pred_columns(pool, n_pred, n.b, cols, depth + 1);
+      return;
+    case DQ_PRED_NOT: case DQ_PRED_IS_NULL: case DQ_PRED_IS_NOT_NULL: case DQ_PRED_REGEX:
+      pred_columns(pool, n_pred, n.a, cols, depth + 1);
+      return;
+    default: return;
+  }
+}
+
+// the schema columns a spec reads (sorted, unique; out-of-range indices are left to the part's own planning)
+static std::vector<int32_t> spec_columns(const dq_analyzer_spec& s, const dq_pred_node* pool, int32_t n_pred,
+                                         int32_t ncols) {
+  std::vector<int32_t> c;
+  if (s.op == DQ_OP_CORRELATION) { c.push_back(s.col_a); c.push_back(s.col_b); }
+  else if (s.op != DQ_OP_SIZE && s.op != DQ_OP_COMPLIANCE) c.push_back(s.col_a);
+  pred_columns(pool, n_pred, s.pred_root, c);
+  pred_columns(pool, n_pred, s.where_root, c);
+  c.erase(std::remove_if(c.begin(), c.end(), [&](int32_t x) { return x < 0 || x >= ncols; }), c.end());
+  std::sort(c.begin(), c.end());
+  c.erase(std::unique(c.begin(), c.end()), c.end());
+  return c;
+}
+
+// one part's inputs: its specs and predicate pool with columns renumbered into its own schema
+struct PartInput {
+  std::vector<dq_analyzer_spec> specs;
+  std::vector<dq_column_desc> schema;
+  std::vector<dq_pred_node> pool;
+};
+
+static void make_part_input(const std::vector<dq_analyzer_spec>& specs, const std::vector<dq_column_desc>& schema,
+                            const dq_pred_node* pool, int32_t n_pred, const std::vector<int32_t>& spec_idx,
+                            const std::vector<int32_t>& cols, PartInput& in) {
+  const int32_t ncols = (int32_t)schema.size();
+  std::vector<int32_t> local(ncols, -1);
+  in.schema.clear();
+  for (size_t j = 0; j < cols.size(); ++j) {
+    local[cols[j]] = (int32_t)j;
+    in.schema.push_back(schema[cols[j]]);
+  }
+  auto map = [&](int32_t c) { return c >= 0 && c < ncols ? local[c] : -1; };
+  in.specs.clear();
+  for (int32_t i : spec_idx) {
+    dq_analyzer_spec sp = specs[i];
+    if (sp.col_a >= 0) sp.col_a = map(sp.col_a);
+    if (sp.col_b >= 0) sp.col_b = map(sp.col_b);
+    in.specs.push_back(sp);
+  }
+  in.pool.assign(pool, pool + n_pred);
+  for (dq_pred_node& n : in.pool)
+    if (n.kind == DQ_PRED_COLUMN) n.a = map(n.a);  // a column outside the part is not reachable from its roots
+}
+
+// host-only planning of one part (capacity probe, or the plan dq_plan_explain describes)
+static dq_status plan_part_host(const dq_plan& parent, const dq_pred_node* pool, int32_t n_pred,
+                                const std::vector<int32_t>& spec_idx, const std::vector<int32_t>& cols, bool probe,
+                                dq_plan& q) {
+  PartInput in;
+  make_part_input(parent.specs, parent.schema, pool, n_pred, spec_idx, cols, in);
+  q.host_only = true;
+  q.probe = probe;
+  q.schema = in.schema;
+  q.specs = in.specs;
+  q.patterns = parent.patterns;
+  q.pred_pass = parent.pred_pass;
+  g_capacity = false;
+  return build_plan(&q, in.pool.data(), (int32_t)in.pool.size());
+}
+
+// Greedy split: specs in order of their lowest column (a column's analyzers -- ColumnProfiler emits them per
+// column -- land in one part, so each column is read by as few parts as possible), each part grown while it
+// fits.  Specs without predicates or `where` only add column tasks (at most one each); the others are checked
+// by a host-only probe of the grown part.  A spec that does not fit a part by itself is an error (its own
+// status: DQ_E_UNSUPPORTED routes it to the fallback set, DQ_E_INVALID / DQ_E_TYPE are spec errors).
+static dq_status partition_specs(const dq_plan& parent, const dq_pred_node* pool, int32_t n_pred,
+                                 std::vector<std::vector<int32_t>>& part_specs,
+                                 std::vector<std::vector<int32_t>>& part_cols) {
+  const int32_t ns = (int32_t)parent.specs.size(), ncols = (int32_t)parent.schema.size();
+  std::vector<std::vector<int32_t>> sc(ns);
+  std::vector<int32_t> order(ns);
+  for (int32_t i = 0; i < ns; ++i) {
+    sc[i] = spec_columns(parent.specs[i], pool, n_pred, ncols);
+    order[i] = i;
+  }
+  std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
+    return (sc[a].empty() ? -1 : sc[a][0]) < (sc[b].empty() ? -1 : sc[b][0]);
+  });
+  std::vector<int32_t> cur, cur_cols;
+  int32_t cur_tasks = 0;
+  auto probe = [&](const std::vector<int32_t>& idx, const std::vector<int32_t>& cols) {
+    std::unique_ptr<dq_plan> q(new dq_plan());
+    return plan_part_host(parent, pool, n_pred, idx, cols, true, *q);
+  };
+  auto start = [&](int32_t i) -> dq_status {
+    if ((int32_t)sc[i].size() > kMaxCols)
+      return set_error(DQ_E_UNSUPPORTED, "spec %d reads %zu columns (one plan reads at most %d)", i, sc[i].size(), kMaxCols);
+    cur.assign(1, i);
+    cur_cols = sc[i];
+    cur_tasks = 1;
+    if (dq_status st = probe(cur, cur_cols)) {
+      std::string msg = g_err;
+      return set_error(st, "spec %d: %s", i, msg.c_str());
+    }
+    return DQ_OK;
+  };
+  auto close = [&] {
+    if (cur.empty()) return;
+    part_specs.push_back(cur);
+    part_cols.push_back(cur_cols);
+    cur.clear();
+    cur_cols.clear();
+  };
+  for (int32_t i : order) {
+    if (cur.empty()) {
+      if (dq_status st = start(i)) return st;
+      continue;
+    }
+    std::vector<int32_t> u;
+    std::set_union(cur_cols.begin(), cur_cols.end(), sc[i].begin(), sc[i].end(), std::back_inserter(u));
+    bool fits = (int32_t)u.size() <= kMaxCols;
+    const dq_analyzer_spec& s = parent.specs[i];
+    if (fits && (s.pred_root >= 0 || s.where_root >= 0 || cur_tasks + 1 > kMaxColTasks)) {
+      std::vector<int32_t> trial(cur);
+      trial.push_back(i);
+      dq_status st = probe(trial, u);
+      if (st != DQ_OK && !g_capacity) {
+        std::string msg = g_err;
+        return set_error(st, "spec %d: %s", i, msg.c_str());
+      }
+      fits = st == DQ_OK;
+    }
+    if (fits) {
+      cur.push_back(i);
+      cur_cols.swap(u);
+      ++cur_tasks;
+    } else {
+      close();
+      if (dq_status st = start(i)) return st;
+    }
+  }
+  close();
+  return DQ_OK;
+}
+
 static int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// dq_plan_explain's description of one (host-only) plan
+static std::string explain_text(const dq_plan& plan) {
+  std::string t;
+  char line[256];
+  for (const auto& g : plan.groups) {
+    std::snprintf(line, sizeof line, "column pass: variant %d, %d task(s)\n", g.variant, g.count);
+    t += line;
+  }
+  std::snprintf(line, sizeof line, "pair pass: %zu pair(s), %zu workgroup task(s)\n", plan.pair_tasks.size(),
+                plan.pair_wgs.size());
+  t += line;
+  if (plan.has_pred) {
+    std::snprintf(line, sizeof line, "predicate program: %d instructions, %d roots, %d counters, %d bitmaps\n",
+                  plan.prog.n_instr, plan.prog.n_roots, plan.prog.n_counters, plan.prog.n_bitmaps);
+    t += line;
+    t += "predicate pass: " + plan.pred_jit_note + "\n";
+    if (!plan.pred_jit_src.empty()) t += "--- generated kernel source ---\n" + plan.pred_jit_src;
+  }
+  return t;
+}
 
 extern "C" {
 
@@ -1100,6 +1322,36 @@ dq_status dq_plan_create_ex(const dq_analyzer_spec* specs, int32_t n_specs, cons
                             const char* const* patterns, int32_t n_patterns, int32_t device, dq_plan** out) {
   return dq_plan_create_opts(specs, n_specs, schema, n_cols, pred_pool, n_pred, patterns, n_patterns, nullptr, device,
                              out);
+}
+
+// one plan over the whole spec set (the capacity flag tells dq_plan_create_opts to split instead)
+static dq_status create_single(const std::vector<dq_analyzer_spec>& specs, const std::vector<dq_column_desc>& schema,
+                               const dq_pred_node* pred_pool, int32_t n_pred, const std::vector<std::string>& patterns,
+                               int32_t pred_pass, int32_t device, dq_plan** out) {
+  g_capacity = false;
+  if ((int32_t)schema.size() > kMaxCols) return cap_error("more than %d columns in one plan", kMaxCols);
+  dq_plan* p = new dq_plan();
+  p->device = device;
+  p->schema = schema;
+  p->specs = specs;
+  p->patterns = patterns;
+  hipError_t e = hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete p;
+    return set_error(DQ_E_HIP, "hipStreamCreate: %s", hipGetErrorString(e));
+  }
+  p->own_stream = true;
+  p->pred_pass = pred_pass;
+  dq_status st = build_plan(p, pred_pool, n_pred);
+  if (st != DQ_OK) {
+    const bool cap = g_capacity;
+    std::string msg = g_err;
+    dq_plan_destroy(p);
+    g_capacity = cap;
+    return set_error(st, "%s", msg.c_str());
+  }
+  *out = p;
+  return DQ_OK;
 }
 
 dq_status dq_plan_create_opts(const dq_analyzer_spec* specs, int32_t n_specs, const dq_column_desc* schema,
@@ -1123,8 +1375,8 @@ dq_status dq_plan_create_opts(const dq_analyzer_spec* specs, int32_t n_specs, co
     if (!patterns[k]) return set_error(DQ_E_INVALID, "dq_plan_create: pattern %d is NULL", k);
   *out = nullptr;
   if (n_specs < 0 || (n_specs > 0 && !specs)) return set_error(DQ_E_INVALID, "dq_plan_create: bad specs");
-  if (n_cols < 0 || n_cols > kMaxCols || (n_cols > 0 && !schema))
-    return set_error(DQ_E_INVALID, "dq_plan_create: bad schema (at most %d columns)", kMaxCols);
+  if (n_cols < 0 || n_cols > kMaxSchemaCols || (n_cols > 0 && !schema))
+    return set_error(DQ_E_INVALID, "dq_plan_create: bad schema (at most %d columns)", kMaxSchemaCols);
   if (n_pred < 0 || (n_pred > 0 && !pred_pool)) return set_error(DQ_E_INVALID, "dq_plan_create: bad predicate pool");
   for (int32_t c = 0; c < n_cols; ++c)
     if (schema[c].type < DQ_TYPE_F64 || schema[c].type > DQ_TYPE_LARGE_UTF8)
@@ -1133,23 +1385,53 @@ dq_status dq_plan_create_opts(const dq_analyzer_spec* specs, int32_t n_specs, co
   HIP_TRY(hipGetDeviceCount(&ndev));
   if (device < 0 || device >= ndev) return set_error(DQ_E_INVALID, "dq_plan_create: device %d of %d", device, ndev);
   HIP_TRY(hipSetDevice(device));
-  dq_plan* p = new dq_plan();
-  p->device = device;
-  p->schema.assign(schema, schema + n_cols);
-  p->specs.assign(specs, specs + n_specs);
-  for (int32_t k = 0; k < n_patterns; ++k) p->patterns.emplace_back(patterns[k]);
-  hipError_t e = hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking);
-  if (e != hipSuccess) {
-    delete p;
-    return set_error(DQ_E_HIP, "hipStreamCreate: %s", hipGetErrorString(e));
-  }
-  p->own_stream = true;
-  p->pred_pass = o.pred_pass;
-  dq_status st = build_plan(p, pred_pool, n_pred);
+  const std::vector<dq_analyzer_spec> vspecs(specs, specs + n_specs);
+  const std::vector<dq_column_desc> vschema(schema, schema + n_cols);
+  std::vector<std::string> vpat;
+  for (int32_t k = 0; k < n_patterns; ++k) vpat.emplace_back(patterns[k]);
+  dq_plan* p = nullptr;
+  dq_status st = create_single(vspecs, vschema, pred_pool, n_pred, vpat, o.pred_pass, device, &p);
+  if (st != DQ_OK && !g_capacity) return st;
   if (st != DQ_OK) {
-    std::string msg = g_err;
-    dq_plan_destroy(p);
-    return set_error(st, "%s", msg.c_str());
+    // over one plan's capacity: several fused plans on this plan's stream
+    p = new dq_plan();
+    p->device = device;
+    p->schema = vschema;
+    p->specs = vspecs;
+    p->patterns = vpat;
+    p->pred_pass = o.pred_pass;
+    hipError_t e = hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+      delete p;
+      return set_error(DQ_E_HIP, "hipStreamCreate: %s", hipGetErrorString(e));
+    }
+    p->own_stream = true;
+    st = partition_specs(*p, pred_pool, n_pred, p->part_specs, p->part_cols);
+    for (size_t k = 0; st == DQ_OK && k < p->part_specs.size(); ++k) {
+      PartInput in;
+      make_part_input(vspecs, vschema, pred_pool, n_pred, p->part_specs[k], p->part_cols[k], in);
+      dq_plan* part = nullptr;
+      st = create_single(in.specs, in.schema, in.pool.data(), (int32_t)in.pool.size(), vpat, o.pred_pass, device, &part);
+      if (st == DQ_OK) {
+        p->parts.push_back(part);
+        st = dq_plan_set_stream(part, p->stream);
+      } else {
+        std::string msg = g_err;
+        st = set_error(st, "part %zu of %zu: %s", k, p->part_specs.size(), msg.c_str());
+      }
+    }
+    if (st != DQ_OK) {
+      std::string msg = g_err;
+      dq_plan_destroy(p);
+      return set_error(st, "%s", msg.c_str());
+    }
+    for (dq_plan* q : p->parts) {
+      p->pred_jit_ms += q->pred_jit_ms;
+      p->launches_per_scan += q->launches_per_scan;
+      p->bytes_per_row_x1000 += q->bytes_per_row_x1000;
+      p->pred_bytes_x1000 += q->pred_bytes_x1000;
+      p->pair_bytes_x1000 += q->pair_bytes_x1000;
+    }
   }
   p->create_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   *out = p;
@@ -1165,6 +1447,8 @@ dq_status dq_plan_set_stream(dq_plan* p, void* hip_stream) {
   if (p->own_stream) (void)hipStreamDestroy(p->stream);
   p->stream = (hipStream_t)hip_stream;
   p->own_stream = false;
+  for (dq_plan* q : p->parts)
+    if (dq_status s = dq_plan_set_stream(q, hip_stream)) return s;
   return DQ_OK;
 }
 
@@ -1179,6 +1463,17 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
   const int32_t ncols = (int32_t)p->schema.size();
   if (ncols > 0 && !cols) return set_error(DQ_E_INVALID, "dq_scan: cols is NULL");
   HIP_TRY(hipSetDevice(p->device));
+  if (!p->parts.empty()) {  // composite: every part over its own columns of this chunk, in part order
+    std::vector<dq_column_view> v;
+    for (size_t k = 0; k < p->parts.size(); ++k) {
+      v.resize(p->part_cols[k].size());
+      for (size_t j = 0; j < v.size(); ++j) v[j] = cols[p->part_cols[k][j]];
+      if (dq_status s = dq_scan(p->parts[k], v.data(), n_rows, chunk_index)) return s;
+    }
+    p->next_chunk++;
+    p->total_rows += n_rows;
+    return DQ_OK;
+  }
   ScanCols sc{};
   for (int32_t c = 0; c < ncols; ++c) {
     const dq_column_view& v = cols[c];
@@ -1197,6 +1492,20 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
   }
   p->next_chunk++;
   if (n_rows == 0) return DQ_OK;
+  if (p->pred_jit_ref) {  // a background compile: take the compiled kernel from this chunk on once it is ready
+    std::string note;
+    if (hipFunction_t fn = pred_jit_poll(p->pred_jit_ref, 0, note)) {
+      p->pred_jit = fn;
+      p->pred_jit_note = note + " (compiled in the background; used from chunk " + std::to_string(chunk_index) + ")";
+      p->pred_jit_ref.reset();
+    } else if (!pred_jit_pending(p->pred_jit_ref)) {
+      p->pred_jit_note = note;  // the compile failed: the interpreter stays
+      p->pred_jit_ref.reset();
+    }
+  }
+  // the launch groups of this scan: without the compiled kernel its HLL tasks run in the column pass
+  std::vector<dq_plan::Group> groups(p->groups);
+  if (!p->pred_jit) groups.insert(groups.end(), p->pred_fused_groups.begin(), p->pred_fused_groups.end());
 
   // where bitmaps (64 rows per word), grown on demand
   const int64_t words = ceil_div(n_rows, 64);
@@ -1226,7 +1535,7 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
   // each variant (and the pair pass) is its own launch of (tasks x ranges) workgroups: size the ranges
   // so the smallest launch still has ~kTargetWGs workgroups (load balance over 256 CUs)
   int64_t min_launch = 0;
-  for (const auto& g : p->groups) min_launch = min_launch ? std::min<int64_t>(min_launch, g.count) : g.count;
+  for (const auto& g : groups) min_launch = min_launch ? std::min<int64_t>(min_launch, g.count) : g.count;
   if (!p->pair_wgs.empty()) {
     const int64_t wg = (int64_t)p->pair_wgs.size();
     min_launch = min_launch ? std::min<int64_t>(min_launch, wg) : wg;
@@ -1248,9 +1557,9 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
     return v == CV_UTF8_H || v == CV_LUTF8_H || v == CV_UTF8_HD || v == CV_LUTF8_HD ? 2 : 1;
   };
   FinRanges fr{};
-  std::vector<std::pair<int64_t, int32_t>> vr(p->groups.size());  // (rows per range, ranges) per variant group
-  for (size_t gi = 0; gi < p->groups.size(); ++gi) {
-    const auto& g = p->groups[gi];
+  std::vector<std::pair<int64_t, int32_t>> vr(groups.size());  // (rows per range, ranges) per variant group
+  for (size_t gi = 0; gi < groups.size(); ++gi) {
+    const auto& g = groups[gi];
     const int32_t sc_v = variant_scale(g.variant);
     if (sc_v == 1) {
       vr[gi] = {rpr_col, nr_col};
@@ -1271,7 +1580,7 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
   nr_pred = (int32_t)ceil_div(n_rows, rpr_pred);
 
   // HLL tasks hashed by the compiled predicate pass: one partial per predicate-pass range
-  if (p->pred_fused_count > 0 && fr.n < kNumVariants) {
+  if (p->pred_jit && p->pred_fused_count > 0 && fr.n < kNumVariants) {
     fr.first[fr.n] = p->pred_fused_first;
     fr.end[fr.n] = p->pred_fused_first + p->pred_fused_count;
     fr.nr[fr.n] = nr_pred;
@@ -1309,8 +1618,8 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
         }))
       return s;
   }
-  for (size_t gi = 0; gi < p->groups.size(); ++gi) {
-    const auto& g = p->groups[gi];
+  for (size_t gi = 0; gi < groups.size(); ++gi) {
+    const auto& g = groups[gi];
     if (dq_status s = timed(p, 16 + g.variant, p->stream, [&] {
           return launch_column_scan(g.variant, p->d_col_tasks + g.first, g.count, g.first, sc, bm, n_rows,
                                     vr[gi].first, vr[gi].second, p->d_col_part, p->d_hll_acc, p->stream);
@@ -1345,6 +1654,15 @@ dq_status dq_finish(dq_plan* p, dq_state* out) {
   if (!p) return set_error(DQ_E_INVALID, "dq_finish: plan is NULL");
   if (!out && !p->specs.empty()) return set_error(DQ_E_INVALID, "dq_finish: out is NULL");
   HIP_TRY(hipSetDevice(p->device));
+  if (!p->parts.empty()) {
+    std::vector<dq_state> tmp;
+    for (size_t k = 0; k < p->parts.size(); ++k) {
+      tmp.assign(p->part_specs[k].size(), dq_state{});
+      if (dq_status s = dq_finish(p->parts[k], tmp.data())) return s;
+      for (size_t j = 0; j < tmp.size(); ++j) out[p->part_specs[k][j]] = tmp[j];
+    }
+    return DQ_OK;
+  }
   std::vector<ColPartial> col(p->col_tasks.size());
   std::vector<uint32_t> hll((size_t)p->n_hll * kHllCopies * 512);
   std::vector<CorrPartial> pair(p->pair_tasks.size());
@@ -1489,12 +1807,21 @@ dq_status dq_finish(dq_plan* p, dq_state* out) {
 dq_status dq_plan_reset(dq_plan* p) {
   if (!p) return set_error(DQ_E_INVALID, "dq_plan_reset: plan is NULL");
   HIP_TRY(hipSetDevice(p->device));
+  if (!p->parts.empty()) {
+    for (dq_plan* q : p->parts)
+      if (dq_status s = dq_plan_reset(q)) return s;
+    p->total_rows = 0;
+    p->next_chunk = 0;
+    return DQ_OK;
+  }
   return reset_acc(p);
 }
 
 void dq_plan_destroy(dq_plan* p) {
   if (!p) return;
   (void)hipSetDevice(p->device);
+  for (dq_plan* q : p->parts) dq_plan_destroy(q);  // (parts launch on this plan's stream; they do not own it)
+  p->parts.clear();
   if (p->stream) (void)hipStreamSynchronize(p->stream);
   free_plan_mem(p);
   if (p->own_stream && p->stream) (void)hipStreamDestroy(p->stream);
@@ -1506,6 +1833,8 @@ int64_t dq_plan_bytes_per_row_x1000(const dq_plan* p) { return p ? p->bytes_per_
 dq_status dq_plan_enable_timing(dq_plan* p, int32_t on) {
   if (!p) return set_error(DQ_E_INVALID, "dq_plan_enable_timing: plan is NULL");
   HIP_TRY(hipSetDevice(p->device));
+  for (dq_plan* q : p->parts)
+    if (dq_status s = dq_plan_enable_timing(q, on)) return s;
   if (dq_status s = resolve_timing(p)) return s;
   p->timing = on != 0;
   for (int k = 0; k < dq_plan::kTimers; ++k) { p->kernel_ms[k] = 0; p->kernel_launches[k] = 0; }
@@ -1516,6 +1845,20 @@ dq_status dq_plan_kernel_time(dq_plan* p, int32_t kernel, double* total_ms, int6
   if (!p || kernel < 0 || kernel >= dq_plan::kTimers || !total_ms || !launches)
     return set_error(DQ_E_INVALID, "dq_plan_kernel_time: bad argument");
   HIP_TRY(hipSetDevice(p->device));
+  if (!p->parts.empty()) {  // summed over the parts
+    double ms = 0.0;
+    int64_t n = 0;
+    for (dq_plan* q : p->parts) {
+      double m = 0.0;
+      int64_t k = 0;
+      if (dq_status s = dq_plan_kernel_time(q, kernel, &m, &k)) return s;
+      ms += m;
+      n += k;
+    }
+    *total_ms = ms;
+    *launches = n;
+    return DQ_OK;
+  }
   if (dq_status s = resolve_timing(p)) return s;
   if (kernel == 1) {  // all column-scan variants
     double ms = 0;
@@ -1533,6 +1876,7 @@ dq_status dq_plan_kernel_time(dq_plan* p, int32_t kernel, double* total_ms, int6
 int64_t dq_plan_variant_bytes_per_row_x1000(const dq_plan* p, int32_t variant) {
   if (!p) return 0;
   int64_t b = 0;
+  for (const dq_plan* q : p->parts) b += dq_plan_variant_bytes_per_row_x1000(q, variant);
   const size_t n_run = p->col_tasks.size() - (size_t)p->n_fused;  // fused tasks run in the pair pass
   for (size_t i = 0; i < n_run; ++i) {
     const ColTask& t = p->col_tasks[i];
@@ -1557,8 +1901,8 @@ int64_t dq_plan_explain(const dq_analyzer_spec* specs, int32_t n_specs, const dq
                         const dq_pred_node* pred_pool, int32_t n_pred, const char* const* patterns, int32_t n_patterns,
                         const dq_plan_options* opts, char* out, int64_t cap) {
   if (n_specs < 0 || (n_specs > 0 && !specs)) return set_error(DQ_E_INVALID, "dq_plan_explain: bad specs");
-  if (n_cols < 0 || n_cols > kMaxCols || (n_cols > 0 && !schema))
-    return set_error(DQ_E_INVALID, "dq_plan_explain: bad schema (at most %d columns)", kMaxCols);
+  if (n_cols < 0 || n_cols > kMaxSchemaCols || (n_cols > 0 && !schema))
+    return set_error(DQ_E_INVALID, "dq_plan_explain: bad schema (at most %d columns)", kMaxSchemaCols);
   if (n_pred < 0 || (n_pred > 0 && !pred_pool)) return set_error(DQ_E_INVALID, "dq_plan_explain: bad predicate pool");
   if (n_patterns < 0 || (n_patterns > 0 && !patterns)) return set_error(DQ_E_INVALID, "dq_plan_explain: bad patterns");
   for (int32_t k = 0; k < n_patterns; ++k)
@@ -1579,25 +1923,37 @@ int64_t dq_plan_explain(const dq_analyzer_spec* specs, int32_t n_specs, const dq
       return set_error(DQ_E_INVALID, "dq_plan_explain: unknown pred_pass %d", opts->pred_pass);
     plan.pred_pass = opts->pred_pass;
   }
-  if (dq_status st = build_plan(&plan, pred_pool, n_pred)) return st;
   std::string t;
   char line[256];
-  std::snprintf(line, sizeof line, "plan: %d analyzers, %d columns, %d launches per scan\n", n_specs, n_cols,
-                plan.launches_per_scan);
-  t += line;
-  for (const auto& g : plan.groups) {
-    std::snprintf(line, sizeof line, "column pass: variant %d, %d task(s)\n", g.variant, g.count);
+  g_capacity = false;
+  dq_status st = n_cols <= kMaxCols ? build_plan(&plan, pred_pool, n_pred)
+                                    : cap_error("more than %d columns in one plan", kMaxCols);
+  if (st == DQ_OK) {
+    std::snprintf(line, sizeof line, "plan: %d analyzers, %d columns, %d launches per scan\n", n_specs, n_cols,
+                  plan.launches_per_scan);
     t += line;
-  }
-  std::snprintf(line, sizeof line, "pair pass: %zu pair(s), %zu workgroup task(s)\n", plan.pair_tasks.size(),
-                plan.pair_wgs.size());
-  t += line;
-  if (plan.has_pred) {
-    std::snprintf(line, sizeof line, "predicate program: %d instructions, %d roots, %d counters, %d bitmaps\n",
-                  plan.prog.n_instr, plan.prog.n_roots, plan.prog.n_counters, plan.prog.n_bitmaps);
+    t += explain_text(plan);
+  } else {
+    if (!g_capacity) return st;
+    // as dq_plan_create_opts: split into several fused plans
+    std::string why = g_err;
+    std::vector<std::vector<int32_t>> ps, pc;
+    if (dq_status s2 = partition_specs(plan, pred_pool, n_pred, ps, pc)) return s2;
+    std::snprintf(line, sizeof line, "plan: %d analyzers, %d columns, over one plan's capacity (%s): %zu fused plans\n",
+                  n_specs, n_cols, why.c_str(), ps.size());
     t += line;
-    t += "predicate pass: " + plan.pred_jit_note + "\n";
-    if (!plan.pred_jit_src.empty()) t += "--- generated kernel source ---\n" + plan.pred_jit_src;
+    for (size_t k = 0; k < ps.size(); ++k) {
+      std::unique_ptr<dq_plan> q(new dq_plan());
+      if (dq_status s2 = plan_part_host(plan, pred_pool, n_pred, ps[k], pc[k], false, *q)) return s2;
+      std::snprintf(line, sizeof line, "--- part %zu: %zu analyzers, %zu columns, %d launches per scan\n", k,
+                    ps[k].size(), pc[k].size(), q->launches_per_scan);
+      t += line;
+      t += "analyzers:";
+      for (int32_t i : ps[k]) t += " " + std::to_string(i);
+      t += "\ncolumns:";
+      for (int32_t c : pc[k]) t += " " + std::to_string(c);
+      t += "\n" + explain_text(*q);
+    }
   }
   if (cap > 0) {
     const size_t n = std::min((size_t)cap - 1, t.size());
@@ -1607,7 +1963,48 @@ int64_t dq_plan_explain(const dq_analyzer_spec* specs, int32_t n_specs, const dq
   return (int64_t)t.size() + 1;
 }
 
+int32_t dq_plan_pred_wait(dq_plan* p, int32_t timeout_ms) {
+  if (!p) return set_error(DQ_E_INVALID, "dq_plan_pred_wait: plan is NULL");
+  if (!p->parts.empty()) {
+    int32_t all = 1, any_pred = 0;
+    for (dq_plan* q : p->parts) {
+      if (!q->has_pred) continue;
+      any_pred = 1;
+      const int32_t r = dq_plan_pred_wait(q, timeout_ms);
+      if (r < 0) return r;
+      all &= r;
+    }
+    return any_pred && all;
+  }
+  if (p->pred_jit_ref) {
+    HIP_TRY(hipSetDevice(p->device));
+    std::string note;
+    if (hipFunction_t fn = pred_jit_poll(p->pred_jit_ref, timeout_ms, note)) {
+      p->pred_jit = fn;
+      p->pred_jit_note = note + " (compiled in the background)";
+      p->pred_jit_ref.reset();
+    } else if (!pred_jit_pending(p->pred_jit_ref)) {
+      p->pred_jit_note = note;
+      p->pred_jit_ref.reset();
+    }
+  }
+  return p->pred_jit ? 1 : 0;
+}
+
 int32_t dq_plan_pred_compiled(const dq_plan* p, char* note, int32_t cap) {
+  if (p && !p->parts.empty()) {  // composite: 1 iff every part with predicates runs compiled
+    std::string n;
+    int32_t all = 1, any_pred = 0;
+    for (size_t k = 0; k < p->parts.size(); ++k) {
+      const dq_plan* q = p->parts[k];
+      if (!q->has_pred) continue;
+      any_pred = 1;
+      all &= dq_plan_pred_compiled(q, nullptr, 0);
+      n += (n.empty() ? "" : "; ") + std::string("part ") + std::to_string(k) + ": " + q->pred_jit_note;
+    }
+    if (note && cap > 0) std::snprintf(note, (size_t)cap, "%s", any_pred ? n.c_str() : "no predicates");
+    return any_pred && all;
+  }
   if (note && cap > 0) {
     const std::string n = !p ? "plan is NULL" : (!p->has_pred ? "no predicates" : p->pred_jit_note);
     std::snprintf(note, (size_t)cap, "%s", n.c_str());

@@ -30,8 +30,11 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <condition_variable>
 #include <map>
+#include <memory>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <utility>
 #include <vector>
@@ -563,14 +566,24 @@ namespace {
 
 // generated-source revision: part of the disk-cache key, so code objects of an older generator are not reused
 constexpr const char* kJitRevision = "dq_pred_jit r4f";
+// disk-cache file header: magic, then the full key's length (u64, little-endian) and bytes, then the code object
+constexpr char kCacheMagic[8] = {'D', 'Q', 'J', 'I', 'T', 'C', 'O', '1'};
 
 uint64_t fnv1a64(const std::string& s, uint64_t h) {
   for (unsigned char c : s) h = (h ^ c) * 0x100000001B3ull;
   return h;
 }
 
+// a directory this user owns that no one else can write (the cache holds code this process loads and runs)
+bool private_dir(const std::string& dir) {
+  struct stat st;
+  if (lstat(dir.c_str(), &st) != 0 || !S_ISDIR(st.st_mode)) return false;
+  return st.st_uid == geteuid() && (st.st_mode & (S_IWGRP | S_IWOTH)) == 0;
+}
+
 // the persistent code-object cache directory: $DQ_JIT_CACHE_DIR ("off" disables it), else
-// $XDG_CACHE_HOME/deequ_amd/jit, else $HOME/.cache/deequ_amd/jit; "" when none is usable
+// $XDG_CACHE_HOME/deequ_amd/jit, else $HOME/.cache/deequ_amd/jit; "" when none is usable -- including a
+// directory not owned by this user or writable by its group / others (a planted code object would run)
 std::string cache_dir() {
   const char* d = std::getenv("DQ_JIT_CACHE_DIR");
   std::string dir;
@@ -590,103 +603,196 @@ std::string cache_dir() {
       const std::string part = dir.substr(0, i);
       if (mkdir(part.c_str(), 0700) != 0 && errno != EEXIST) return std::string();
     }
-  return dir;
+  return private_dir(dir) ? dir : std::string();
 }
 
-bool read_file(const std::string& path, std::vector<char>& out) {
+// a cached code object built from exactly `key` (header compared byte for byte; owner checked)
+bool read_cached(const std::string& path, const std::string& key, std::vector<char>& code) {
   FILE* f = std::fopen(path.c_str(), "rb");
   if (!f) return false;
-  std::fseek(f, 0, SEEK_END);
-  const long n = std::ftell(f);
-  std::fseek(f, 0, SEEK_SET);
-  bool ok = n > 4;
+  struct stat st;
+  bool ok = fstat(fileno(f), &st) == 0 && S_ISREG(st.st_mode) && st.st_uid == geteuid();
+  char magic[8];
+  uint64_t klen = 0;
+  ok = ok && std::fread(magic, 1, 8, f) == 8 && std::memcmp(magic, kCacheMagic, 8) == 0 &&
+       std::fread(&klen, 1, 8, f) == 8 && klen == key.size();
   if (ok) {
-    out.resize((size_t)n);
-    ok = std::fread(out.data(), 1, (size_t)n, f) == (size_t)n;
+    std::string k(key.size(), '\0');
+    ok = std::fread(&k[0], 1, k.size(), f) == k.size() && k == key;
+  }
+  if (ok) {
+    const long at = std::ftell(f);
+    std::fseek(f, 0, SEEK_END);
+    const long n = std::ftell(f) - at;
+    std::fseek(f, at, SEEK_SET);
+    ok = n > 4;
+    if (ok) {
+      code.resize((size_t)n);
+      ok = std::fread(code.data(), 1, (size_t)n, f) == (size_t)n;
+    }
   }
   std::fclose(f);
   // an AMDGPU code object is an ELF file
-  return ok && out[0] == 0x7F && out[1] == 'E' && out[2] == 'L' && out[3] == 'F';
+  return ok && code[0] == 0x7F && code[1] == 'E' && code[2] == 'L' && code[3] == 'F';
 }
 
-void write_file_atomic(const std::string& path, const std::vector<char>& code) {
+void write_cached(const std::string& path, const std::string& key, const std::vector<char>& code) {
   const std::string tmp = path + ".tmp." + std::to_string((long)getpid());
   FILE* f = std::fopen(tmp.c_str(), "wb");
   if (!f) return;
-  const bool ok = std::fwrite(code.data(), 1, code.size(), f) == code.size();
+  const uint64_t klen = key.size();
+  bool ok = std::fwrite(kCacheMagic, 1, 8, f) == 8 && std::fwrite(&klen, 1, 8, f) == 8 &&
+            std::fwrite(key.data(), 1, key.size(), f) == key.size() &&
+            std::fwrite(code.data(), 1, code.size(), f) == code.size();
   if (std::fclose(f) == 0 && ok) {
     if (std::rename(tmp.c_str(), path.c_str()) == 0) return;
   }
   std::remove(tmp.c_str());
 }
 
-struct JitEntry {
-  hipFunction_t fn = nullptr;
-  std::string err;  // why there is no function (failures are cached too: a failing compile is not retried)
+// background compiles: joined at process exit (after the last plan, before hipRTC unloads)
+struct Workers {
+  std::mutex mu;
+  std::vector<std::thread> threads;
+  ~Workers() {
+    std::lock_guard<std::mutex> lock(mu);
+    for (std::thread& t : threads)
+      if (t.joinable()) t.join();
+  }
 };
 
 }  // namespace
 
-// the kernel of `src` for `device`: the process cache (successes and failures), else the disk cache, else a
-// hipRTC compile for the device's own target (gcnArchName, e.g. gfx950:sramecc+:xnack-)
-hipFunction_t pred_jit_get(const std::string& src, int device, std::string& note, double& ms) {
-  static std::mutex mu;
-  static std::map<std::pair<int, std::string>, JitEntry> cache;
-  const auto t0 = std::chrono::steady_clock::now();
-  auto done = [&](hipFunction_t fn) {
-    ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    return fn;
-  };
-  std::lock_guard<std::mutex> lock(mu);
-  auto it = cache.find({device, src});
-  if (it != cache.end()) {
-    note = it->second.fn ? "process cache" : it->second.err;
-    return done(it->second.fn);
-  }
-  JitEntry& e = cache[{device, src}];
-  hipDeviceProp_t prop;
-  if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
-    e.err = note = "hipGetDeviceProperties failed";
-    return done(nullptr);
-  }
-  const std::string arch = prop.gcnArchName;
-  int rv_major = 0, rv_minor = 0;
-  hiprtcVersion(&rv_major, &rv_minor);
-  const std::string key = std::string(kJitRevision) + "\n" + arch + "\nhiprtc " + std::to_string(rv_major) + "." +
-                          std::to_string(rv_minor) + "\n" + src;
-  char name[80];
-  std::snprintf(name, sizeof name, "%016" PRIx64 "%016" PRIx64 ".co", fnv1a64(key, 0xCBF29CE484222325ull),
-                fnv1a64(key, 0x84222325CBF29CE4ull));
-  const std::string dir = cache_dir();
+// One (device, source) kernel: PENDING while hipRTC compiles it (on a background thread for AUTO plans), CODE
+// once the code object exists (compiled or read from the disk cache), LOADED once a plan thread has loaded the
+// module, FAILED with the reason (failures stay cached: a failing compile is not retried).  Its own mutex
+// guards it, so a compile never holds the process-wide map's lock.
+struct PredJitEntry {
+  enum State { PENDING, CODE, LOADED, FAILED };
+  std::mutex mu;
+  std::condition_variable cv;
+  State state = PENDING;
   std::vector<char> code;
-  std::string origin = "disk cache";
-  bool have = !dir.empty() && read_file(dir + "/" + name, code);
-  hipModule_t mod = nullptr;
-  if (have && hipModuleLoadData(&mod, code.data()) != hipSuccess) {
-    have = false;  // a stale or damaged file: compile again (and replace it)
-    mod = nullptr;
+  hipFunction_t fn = nullptr;
+  std::string origin;  // "hiprtc" / "disk cache"
+  std::string err;
+};
+
+namespace {
+
+std::mutex g_map_mu;
+std::map<std::pair<int, std::string>, PredJitRef> g_map;
+Workers g_workers;  // declared after the map: destroyed (joined) first
+
+void compile_into(const PredJitRef& e, std::string src, std::string arch, std::string key, std::string path) {
+  std::vector<char> code;
+  std::string err;
+  const bool ok = pred_jit_compile_code(src, arch, code, err);
+  if (ok && !path.empty()) write_cached(path, key, code);
+  std::lock_guard<std::mutex> lock(e->mu);
+  if (ok) {
+    e->code.swap(code);
+    e->origin = "hiprtc";
+    e->state = PredJitEntry::CODE;
+  } else {
+    e->err = err;
+    e->state = PredJitEntry::FAILED;
   }
-  if (!have) {
-    origin = "hiprtc";
-    std::string err;
-    if (!pred_jit_compile_code(src, arch, code, err)) {
-      e.err = note = err;
-      return done(nullptr);
+  e->cv.notify_all();
+}
+
+}  // namespace
+
+PredJitRef pred_jit_request(const std::string& src, int device, bool background, double& ms) {
+  const auto t0 = std::chrono::steady_clock::now();
+  PredJitRef e;
+  bool created = false;
+  {
+    std::lock_guard<std::mutex> lock(g_map_mu);
+    PredJitRef& slot = g_map[{device, src}];
+    if (!slot) {
+      slot = std::make_shared<PredJitEntry>();
+      created = true;
     }
-    if (hipModuleLoadData(&mod, code.data()) != hipSuccess) {
-      e.err = note = "hipModuleLoadData failed";
-      return done(nullptr);
+    e = slot;
+  }
+  if (created) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
+      std::lock_guard<std::mutex> lock(e->mu);
+      e->err = "hipGetDeviceProperties failed";
+      e->state = PredJitEntry::FAILED;
+      e->cv.notify_all();
+    } else {
+      const std::string arch = prop.gcnArchName;
+      int rv_major = 0, rv_minor = 0;
+      hiprtcVersion(&rv_major, &rv_minor);
+      const std::string key = std::string(kJitRevision) + "\n" + arch + "\nhiprtc " + std::to_string(rv_major) + "." +
+                              std::to_string(rv_minor) + "\n" + src;
+      char name[80];
+      std::snprintf(name, sizeof name, "%016" PRIx64 "%016" PRIx64 ".co", fnv1a64(key, 0xCBF29CE484222325ull),
+                    fnv1a64(key, 0x84222325CBF29CE4ull));
+      const std::string dir = cache_dir();
+      const std::string path = dir.empty() ? std::string() : dir + "/" + name;
+      std::vector<char> code;
+      if (!path.empty() && read_cached(path, key, code)) {
+        std::lock_guard<std::mutex> lock(e->mu);
+        e->code.swap(code);
+        e->origin = "disk cache";
+        e->state = PredJitEntry::CODE;
+        e->cv.notify_all();
+      } else if (background) {
+        std::lock_guard<std::mutex> lock(g_workers.mu);
+        g_workers.threads.emplace_back(compile_into, e, src, arch, key, path);
+      } else {
+        compile_into(e, src, arch, key, path);
+      }
     }
-    if (!dir.empty()) write_file_atomic(dir + "/" + name, code);
   }
-  hipFunction_t fn;
-  if (hipModuleGetFunction(&fn, mod, "dq_pred_jit") != hipSuccess) {
-    e.err = note = "hipModuleGetFunction failed";
-    return done(nullptr);
+  ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return e;
+}
+
+hipFunction_t pred_jit_poll(const PredJitRef& e, int32_t wait_ms, std::string& note) {
+  if (!e) {
+    note = "no kernel requested";
+    return nullptr;
   }
-  e.fn = fn;  // the module stays loaded for the process
-  note = origin;
-  return done(fn);
+  std::unique_lock<std::mutex> lock(e->mu);
+  auto done = [&] { return e->state != PredJitEntry::PENDING; };
+  if (wait_ms < 0) e->cv.wait(lock, done);
+  else if (wait_ms > 0) e->cv.wait_for(lock, std::chrono::milliseconds(wait_ms), done);
+  switch (e->state) {
+    case PredJitEntry::PENDING:
+      note = "compiling in the background (hipRTC): the interpreter runs until it is ready";
+      return nullptr;
+    case PredJitEntry::FAILED:
+      note = e->err;
+      return nullptr;
+    case PredJitEntry::LOADED:
+      note = e->origin + " (process cache)";
+      return e->fn;
+    case PredJitEntry::CODE: {  // load the module on this (plan) thread; it stays loaded for the process
+      hipModule_t mod = nullptr;
+      hipFunction_t fn = nullptr;
+      if (hipModuleLoadData(&mod, e->code.data()) != hipSuccess) {
+        e->err = note = "hipModuleLoadData failed";
+        e->state = PredJitEntry::FAILED;
+        return nullptr;
+      }
+      if (hipModuleGetFunction(&fn, mod, "dq_pred_jit") != hipSuccess) {
+        e->err = note = "hipModuleGetFunction failed";
+        e->state = PredJitEntry::FAILED;
+        return nullptr;
+      }
+      e->fn = fn;
+      e->state = PredJitEntry::LOADED;
+      std::vector<char>().swap(e->code);
+      note = e->origin;
+      return fn;
+    }
+  }
+  return nullptr;
 }
 
 hipError_t pred_jit_launch(hipFunction_t fn, const PredJitArgs& a, int32_t nranges, hipStream_t st) {
@@ -695,4 +801,12 @@ hipError_t pred_jit_launch(hipFunction_t fn, const PredJitArgs& a, int32_t nrang
   return hipModuleLaunchKernel(fn, (unsigned)nranges, 1, 1, kBlock, 1, 1, 0, st, params, nullptr);
 }
 
+}  // namespace dq
+
+namespace dq {
+bool pred_jit_pending(const PredJitRef& e) {
+  if (!e) return false;
+  std::lock_guard<std::mutex> lock(e->mu);
+  return e->state == PredJitEntry::PENDING;
+}
 }  // namespace dq

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -36,9 +37,17 @@ std::string pred_jit_source(const PredProgram& prog, const int32_t* col_kind, st
                             const std::vector<PredJitHll>& hll);
 // hipRTC compile of `src` for `arch` (host only)
 bool pred_jit_compile_code(const std::string& src, const std::string& arch, std::vector<char>& code, std::string& err);
-// the loaded kernel of `src` on `device` (process cache, disk cache, or compiled); note: its origin, or why there
-// is none; ms: host time spent
-hipFunction_t pred_jit_get(const std::string& src, int device, std::string& note, double& ms);
+// The kernel of `src` on `device`, from the process cache, the disk cache, or hipRTC -- on a background thread
+// when `background` (the caller polls), else before returning; ms: host time spent in the request.
+struct PredJitEntry;
+using PredJitRef = std::shared_ptr<PredJitEntry>;
+PredJitRef pred_jit_request(const std::string& src, int device, bool background, double& ms);
+// The loaded function once the code object exists (the module is loaded on the calling thread), else null;
+// wait_ms: how long to wait for a pending compile (0: not at all, < 0: until it has finished).  note: the code
+// object's origin, or why there is no function.
+hipFunction_t pred_jit_poll(const PredJitRef& e, int32_t wait_ms, std::string& note);
+// true while the compile is still running
+bool pred_jit_pending(const PredJitRef& e);
 hipError_t pred_jit_launch(hipFunction_t fn, const PredJitArgs& a, int32_t nranges, hipStream_t st);
 
 }  // namespace dq

@@ -24,7 +24,10 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <type_traits>
 #include <vector>
 
@@ -310,8 +313,37 @@ struct DevHist {
   }
 };
 
-// stream-ordered scratch (hipMallocAsync from the device's default pool, kept between calls: the digest's
-// temporaries cost no hipMalloc / hipFree round trips after the first call)
+// stream-ordered scratch from a pool of this library's own per device (hipMallocFromPoolAsync): the digest's
+// temporaries cost no hipMalloc / hipFree round trips across calls, while blocks beyond kPoolKeep bytes go
+// back to the device at the next synchronisation -- and torch's (the device default) pool is left alone
+constexpr uint64_t kPoolKeep = 256ull << 20;
+hipError_t scratch_pool(int device, hipMemPool_t* out) {
+  static std::mutex mu;
+  static std::map<int, hipMemPool_t> pools;
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = pools.find(device);
+  if (it != pools.end()) {
+    *out = it->second;
+    return hipSuccess;
+  }
+  hipMemPoolProps props{};
+  props.allocType = hipMemAllocationTypePinned;
+  props.location.type = hipMemLocationTypeDevice;
+  props.location.id = device;
+  hipMemPool_t pool = nullptr;
+  hipError_t e = hipMemPoolCreate(&pool, &props);
+  if (e != hipSuccess) return e;
+  uint64_t keep = kPoolKeep;
+  e = hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+  if (e != hipSuccess) {
+    (void)hipMemPoolDestroy(pool);
+    return e;
+  }
+  pools[device] = pool;
+  *out = pool;
+  return hipSuccess;
+}
+
 struct StreamTmp {
   void* p = nullptr;
   hipStream_t s = nullptr;
@@ -320,22 +352,13 @@ struct StreamTmp {
   ~StreamTmp() {
     if (p) (void)hipFreeAsync(p, s);
   }
-  hipError_t alloc(size_t bytes, hipStream_t st) {
+  hipError_t alloc(size_t bytes, hipMemPool_t pool, hipStream_t st) {
+    if (p) (void)hipFreeAsync(p, s);
+    p = nullptr;
     s = st;
-    return hipMallocAsync(&p, std::max<size_t>(bytes, 16), st);
+    return hipMallocFromPoolAsync(&p, std::max<size_t>(bytes, 16), pool, st);
   }
 };
-hipError_t keep_pool(int device) {
-  static int kept = -1;
-  if (kept == device) return hipSuccess;
-  hipMemPool_t pool;
-  hipError_t e = hipDeviceGetDefaultMemPool(&pool, device);
-  if (e != hipSuccess) return e;
-  uint64_t keep = ~0ull;  // retain freed blocks for the next call
-  e = hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
-  if (e == hipSuccess) kept = device;
-  return e;
-}
 
 double key_to_double(int32_t type, uint64_t key) {
   if (type == DQ_TYPE_F64) {
@@ -360,6 +383,7 @@ constexpr int kDCountCopies = 8;             // bucket-count copies (blockIdx % 
 constexpr int kDStage = 2048;                // candidate keys staged per workgroup (flushed past kDStage - 1024)
 constexpr int kDCells = 2048;                // cells of the splitters' lookup table (DigestCells)
 constexpr int kDAndOrCopies = 16;            // the candidates' AND / OR: copies the workgroups spread over
+constexpr int64_t kDCandBudget = int64_t(1) << 26;  // candidates per compaction batch (~1.6 GB of scratch)
 
 // the key of row i * n / m of a chunk (i < m), and whether the row is non-null
 template <int TYPE>
@@ -446,10 +470,12 @@ __global__ __launch_bounds__(kQBlock) void dq_digest_pass(const void* __restrict
                                                           unsigned long long* __restrict__ counts,
                                                           const unsigned char* __restrict__ target,
                                                           unsigned long long* __restrict__ cand,
-                                                          unsigned long long* __restrict__ cursor) {
+                                                          unsigned long long* __restrict__ cursor,
+                                                          unsigned long long cand_cap) {
   __shared__ unsigned long long spl[kDBuckets - 1];
   __shared__ uint16_t first[kDCells + 1];
   __shared__ uint32_t hist[COUNT ? kDBuckets : 1];
+  __shared__ uint32_t eqh[COUNT ? kDBuckets : 1];  // keys equal to their bucket's lower splitter
   __shared__ unsigned char tgt[COUNT ? 1 : kDBuckets];
   __shared__ unsigned long long stage[COUNT ? 1 : kDStage];
   __shared__ uint32_t st_n;
@@ -458,7 +484,7 @@ __global__ __launch_bounds__(kQBlock) void dq_digest_pass(const void* __restrict
   for (int i = threadIdx.x; i < kDBuckets - 1; i += kQBlock) spl[i] = splitters[i];
   for (int i = threadIdx.x; i <= kDCells; i += kQBlock) first[i] = first_g[i];
   if constexpr (COUNT) {
-    for (int i = threadIdx.x; i < kDBuckets; i += kQBlock) hist[i] = 0;
+    for (int i = threadIdx.x; i < kDBuckets; i += kQBlock) hist[i] = eqh[i] = 0;
   } else {
     for (int i = threadIdx.x; i < kDBuckets; i += kQBlock) tgt[i] = target[i];
   }
@@ -502,12 +528,16 @@ __global__ __launch_bounds__(kQBlock) void dq_digest_pass(const void* __restrict
     if constexpr (COUNT) {
 #pragma unroll
       for (int u = 0; u < kDRows; ++u)
-        if (ok[u]) atomicAdd(&hist[bk[u]], 1u);
+        if (ok[u]) {
+          atomicAdd(&hist[bk[u]], 1u);
+          if (bk[u] > 0 && key[u] == spl[bk[u] - 1]) atomicAdd(&eqh[bk[u]], 1u);
+        }
     } else {
       // (every thread of the workgroup runs the same iterations: the flush below is workgroup-uniform)
 #pragma unroll
       for (int u = 0; u < kDRows; ++u) {
-        const bool take = ok[u] && tgt[bk[u]];
+        // a key equal to its bucket's lower splitter is known without compaction (a hot value's rows)
+        const bool take = ok[u] && tgt[bk[u]] && !(bk[u] > 0 && key[u] == spl[bk[u] - 1]);
         if (take) {
           c_and &= key[u];
           c_or |= key[u];
@@ -527,7 +557,8 @@ __global__ __launch_bounds__(kQBlock) void dq_digest_pass(const void* __restrict
         if (threadIdx.x == 0) st_base = atomicAdd(cursor, (unsigned long long)staged);
         __syncthreads();
         const unsigned long long b = st_base;
-        for (uint32_t i = threadIdx.x; i < staged; i += kQBlock) cand[b + i] = stage[i];
+        for (uint32_t i = threadIdx.x; i < staged; i += kQBlock)
+          if (b + i < cand_cap) cand[b + i] = stage[i];  // (the host checks the cursor against the count pass)
         __syncthreads();
         if (threadIdx.x == 0) st_n = 0;
         __syncthreads();
@@ -536,15 +567,19 @@ __global__ __launch_bounds__(kQBlock) void dq_digest_pass(const void* __restrict
   }
   __syncthreads();
   if constexpr (COUNT) {
-    for (int i = threadIdx.x; i < kDBuckets; i += kQBlock)
+    for (int i = threadIdx.x; i < kDBuckets; i += kQBlock) {
       if (hist[i]) atomicAdd(&counts[(blockIdx.x % kDCountCopies) * kDBuckets + i], (unsigned long long)hist[i]);
+      if (eqh[i])
+        atomicAdd(&counts[(kDCountCopies + blockIdx.x % kDCountCopies) * kDBuckets + i], (unsigned long long)eqh[i]);
+    }
   } else {
     const uint32_t staged = st_n;
     if (staged > 0) {
       if (threadIdx.x == 0) st_base = atomicAdd(cursor, (unsigned long long)staged);
       __syncthreads();
       const unsigned long long b = st_base;
-      for (uint32_t i = threadIdx.x; i < staged; i += kQBlock) cand[b + i] = stage[i];
+      for (uint32_t i = threadIdx.x; i < staged; i += kQBlock)
+        if (b + i < cand_cap) cand[b + i] = stage[i];
     }
     // the candidates' AND / OR (lanes, waves, then one pair per workgroup into copy blockIdx % kDAndOrCopies of
     // cursor[1 ..]): the sort skips the high bits every candidate shares
@@ -602,7 +637,7 @@ DigestCells digest_cells(int32_t type, const std::vector<unsigned long long>& sp
 __global__ void dq_digest_gather(const unsigned long long* __restrict__ sorted, const long long* __restrict__ idx,
                                  int64_t m, unsigned long long* __restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < m) out[i] = sorted[idx[i]];
+  if (i < m) out[i] = idx[i] >= 0 ? sorted[idx[i]] : 0ull;  // -1: a sample known without compaction
 }
 
 }  // namespace
@@ -857,14 +892,16 @@ dq_status dq_quantile_digest(int32_t type, const dq_column_view* cols, const int
     s_off[(size_t)c + 1] = s_off[(size_t)c] + std::min<int64_t>(want, chunk_rows[c]);
   }
   const int64_t ns_all = s_off[(size_t)n_chunks];
-  // one scratch block: sample keys | splitters | counts | cursor | sample flags | bucket flags
-  QHIP(keep_pool(device));
+  // one scratch block: sample keys | splitters | counts (per bucket, then keys equal to the bucket's lower
+  // splitter) | cursor | sample flags | bucket flags
+  hipMemPool_t pool = nullptr;
+  QHIP(scratch_pool(device, &pool));
   StreamTmp small;
   const size_t o_spl = (size_t)ns_all * 8, o_cnt = o_spl + (size_t)(kDBuckets - 1) * 8,
-               o_cur = o_cnt + (size_t)kDCountCopies * kDBuckets * 8,
+               o_cur = o_cnt + (size_t)2 * kDCountCopies * kDBuckets * 8,
                o_first = o_cur + 8 + (size_t)kDAndOrCopies * 16,
                o_ok = o_first + ((size_t)(kDCells + 1) * 2 + 7) / 8 * 8, o_tgt = o_ok + (size_t)ns_all;
-  QHIP(small.alloc(o_tgt + kDBuckets, stream));
+  QHIP(small.alloc(o_tgt + kDBuckets, pool, stream));
   char* const sb = static_cast<char*>(small.p);
   uint16_t* const d_first = reinterpret_cast<uint16_t*>(sb + o_first);
   struct {
@@ -899,28 +936,22 @@ dq_status dq_quantile_digest(int32_t type, const dq_column_view* cols, const int
   std::vector<uint16_t> first;
   const DigestCells C = digest_cells(type, spl, first);
   QHIP(hipMemcpyAsync(d_first, first.data(), first.size() * 2, hipMemcpyHostToDevice, stream));
-  QHIP(hipMemsetAsync(d_counts.p, 0, (size_t)kDCountCopies * kDBuckets * 8, stream));
-  {
-    unsigned long long cur0[1 + 2 * kDAndOrCopies];  // cursor, then (AND, OR) copies
-    cur0[0] = 0;
-    for (int i = 0; i < kDAndOrCopies; ++i) {
-      cur0[1 + 2 * i] = ~0ull;
-      cur0[2 + 2 * i] = 0ull;
-    }
-    QHIP(hipMemcpyAsync(d_cursor.p, cur0, sizeof(cur0), hipMemcpyHostToDevice, stream));
-    QHIP(hipStreamSynchronize(stream));  // cur0 is a stack array
-  }
-  // 2. per-bucket counts
+  QHIP(hipMemsetAsync(d_counts.p, 0, (size_t)2 * kDCountCopies * kDBuckets * 8, stream));
+  // 2. per-bucket counts (and of each bucket's keys equal to its lower splitter)
   if (dq_status st = for_chunks([&](auto tk, int grid, int c, int64_t rows) {
         hipLaunchKernelGGL((dq_digest_pass<decltype(tk)::value, true>), dim3(grid), dim3(kQBlock), 0, stream,
                            cols[c].values, reinterpret_cast<const uint32_t*>(cols[c].validity), rows, d_spl.p, d_first,
-                           C, d_counts.p, nullptr, nullptr, nullptr);
+                           C, d_counts.p, nullptr, nullptr, nullptr, 0ull);
       }))
     return st;
-  std::vector<unsigned long long> cnt_copies((size_t)kDCountCopies * kDBuckets), cnt((size_t)kDBuckets, 0);
+  std::vector<unsigned long long> cnt_copies((size_t)2 * kDCountCopies * kDBuckets), cnt((size_t)kDBuckets, 0),
+      eq((size_t)kDBuckets, 0);
   QHIP(hipMemcpyAsync(cnt_copies.data(), d_counts.p, cnt_copies.size() * 8, hipMemcpyDeviceToHost, stream));
   QHIP(hipStreamSynchronize(stream));
-  for (size_t i = 0; i < cnt_copies.size(); ++i) cnt[i % kDBuckets] += cnt_copies[i];
+  for (size_t i = 0; i < (size_t)kDCountCopies * kDBuckets; ++i) {
+    cnt[i % kDBuckets] += cnt_copies[i];
+    eq[i % kDBuckets] += cnt_copies[(size_t)kDCountCopies * kDBuckets + i];
+  }
   int64_t n = 0;
   for (unsigned long long x : cnt) n += (int64_t)x;
   *count = n;
@@ -930,68 +961,136 @@ dq_status dq_quantile_digest(int32_t type, const dq_column_view* cols, const int
   const int64_t m = (n - 1) / s + 1 + ((n - 1) % s != 0 ? 1 : 0);
   *n_samples = m;
   if (m > cap) return set_error(DQ_E_INVALID, "dq_quantile_digest: %lld samples, room for %lld", (long long)m, (long long)cap);
-  // 3. the bucket of every sample rank; the flagged buckets' keys are the candidates, in bucket (= key) order
+  // 3. the bucket of every sample rank.  Bucket b holds the keys in [spl[b - 1], spl[b]); its first eq[b] ranks are
+  // spl[b - 1] itself (known: no compaction), the others are candidates -- its keys above spl[b - 1]
   std::vector<int64_t> before((size_t)kDBuckets + 1, 0);
   for (int b = 0; b < kDBuckets; ++b) before[(size_t)b + 1] = before[(size_t)b] + (int64_t)cnt[(size_t)b];
-  std::vector<unsigned char> tgt((size_t)kDBuckets, 0);
+  std::vector<unsigned char> need((size_t)kDBuckets, 0);
   std::vector<int64_t> rank((size_t)m);
   std::vector<int> rb((size_t)m);
+  std::vector<unsigned long long> key_of((size_t)m, 0);
+  std::vector<unsigned char> known((size_t)m, 0);
   for (int64_t i = 0, b = 0; i < m; ++i) {
     rank[(size_t)i] = i == m - 1 ? n : 1 + i * s;
     while (before[(size_t)b + 1] < rank[(size_t)i]) ++b;  // ranks ascend: bucket b holds ranks (before[b], before[b + 1]]
     rb[(size_t)i] = (int)b;
-    tgt[(size_t)b] = 1;
+    if (rank[(size_t)i] - 1 - before[(size_t)b] < (int64_t)eq[(size_t)b]) {
+      known[(size_t)i] = 1;
+      key_of[(size_t)i] = spl[(size_t)b - 1];  // (eq[0] == 0: b > 0 here)
+    } else {
+      need[(size_t)b] = 1;
+    }
   }
-  std::vector<int64_t> cand_before((size_t)kDBuckets + 1, 0);
-  for (int b = 0; b < kDBuckets; ++b)
-    cand_before[(size_t)b + 1] = cand_before[(size_t)b] + (tgt[(size_t)b] ? (int64_t)cnt[(size_t)b] : 0);
-  const int64_t nc = cand_before[(size_t)kDBuckets];
-  // (hipCUB's item count is an int here, as in the grouping pass)
-  if (nc > (int64_t)0x7FFFFFFF)
-    return set_error(DQ_E_UNSUPPORTED, "dq_quantile_digest: %lld candidate values (at most 2^31 - 1)", (long long)nc);
-  QHIP(hipMemcpyAsync(d_target.p, tgt.data(), (size_t)kDBuckets, hipMemcpyHostToDevice, stream));
-  // second scratch block: candidates | sorted candidates | sample indices | radix-sort temp
+  // the flagged buckets in key order, in batches of at most `budget` candidates (one compaction pass + one sort
+  // each): scratch stays bounded whatever the relative error (every bucket flagged when m > kDBuckets) or the skew
+  int64_t budget = kDCandBudget;
+  if (const char* e = std::getenv("DQ_DIGEST_CAND_BUDGET"))  // test knob: exercise the batching at small sizes
+    budget = std::max<int64_t>(1, std::atoll(e));
+  std::vector<std::pair<int, int>> batches;  // [first bucket, end bucket)
+  int64_t batch_max = 0;
+  {
+    int b0 = -1;
+    int64_t acc = 0;
+    for (int b = 0; b < kDBuckets; ++b) {
+      if (!need[(size_t)b]) continue;
+      const int64_t cb = (int64_t)(cnt[(size_t)b] - eq[(size_t)b]);
+      if (cb > budget || cb > (int64_t)0x7FFFFFFF)
+        return set_error(DQ_E_UNSUPPORTED, "dq_quantile_digest: %lld candidate values in one bucket (budget %lld)",
+                         (long long)cb, (long long)budget);
+      if (b0 >= 0 && acc + cb > budget) {
+        batches.push_back({b0, b});
+        batch_max = std::max(batch_max, acc);
+        b0 = -1;
+        acc = 0;
+      }
+      if (b0 < 0) b0 = b;
+      acc += cb;
+    }
+    if (b0 >= 0) {
+      batches.push_back({b0, kDBuckets});
+      batch_max = std::max(batch_max, acc);
+    }
+  }
+  // second scratch block: candidates | sorted candidates | sample indices | gathered keys | radix-sort temp
   size_t tb = 0;
   QHIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
-                                         (int)nc, 0, 64, stream));
+                                         (int)std::max<int64_t>(1, batch_max), 0, 64, stream));
   StreamTmp big;
-  const size_t o_sorted = (size_t)nc * 8, o_idx = o_sorted + (size_t)nc * 8, o_tmp = (o_idx + (size_t)m * 8 + 255) & ~(size_t)255;
-  QHIP(big.alloc(o_tmp + tb, stream));
+  const size_t o_sorted = (size_t)batch_max * 8, o_idx = o_sorted + (size_t)batch_max * 8,
+               o_got = o_idx + (size_t)m * 8, o_tmp = (o_got + (size_t)m * 8 + 255) & ~(size_t)255;
+  QHIP(big.alloc(o_tmp + tb, pool, stream));
   char* const bb = static_cast<char*>(big.p);
   unsigned long long* const cand = reinterpret_cast<unsigned long long*>(bb);
   unsigned long long* const sorted = reinterpret_cast<unsigned long long*>(bb + o_sorted);
   long long* const d_idx = reinterpret_cast<long long*>(bb + o_idx);
-  if (dq_status st = for_chunks([&](auto tk, int grid, int c, int64_t rows) {
-        hipLaunchKernelGGL((dq_digest_pass<decltype(tk)::value, false>), dim3(grid), dim3(kQBlock), 0, stream,
-                           cols[c].values, reinterpret_cast<const uint32_t*>(cols[c].validity), rows, d_spl.p, d_first,
-                           C, nullptr, d_target.p, cand, d_cursor.p);
-      }))
-    return st;
-  // the candidates agree above their highest differing bit: sorting the bits below gives the full order
-  unsigned long long cur[1 + 2 * kDAndOrCopies];
-  QHIP(hipMemcpyAsync(cur, d_cursor.p, sizeof(cur), hipMemcpyDeviceToHost, stream));
-  QHIP(hipStreamSynchronize(stream));
-  uint64_t c_and = ~0ull, c_or = 0;
-  for (int i = 0; i < kDAndOrCopies; ++i) {
-    c_and &= cur[1 + 2 * i];
-    c_or |= cur[2 + 2 * i];
-  }
-  const int end_bit = (c_and ^ c_or) ? 64 - __builtin_clzll(c_and ^ c_or) : 1;
-  QHIP(hipcub::DeviceRadixSort::SortKeys(bb + o_tmp, tb, cand, sorted, (int)nc, 0, end_bit, stream));
-  // 4. sample i = the sorted candidate at (its rank within its bucket) + (candidates of the flagged buckets before)
-  std::vector<long long> idx((size_t)m);
-  for (int64_t i = 0; i < m; ++i) {
-    const int b = rb[(size_t)i];
-    idx[(size_t)i] = (long long)(rank[(size_t)i] - 1 - before[(size_t)b] + cand_before[(size_t)b]);
-  }
-  QHIP(hipMemcpyAsync(d_idx, idx.data(), (size_t)m * 8, hipMemcpyHostToDevice, stream));
-  hipLaunchKernelGGL(dq_digest_gather, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, stream, sorted, d_idx, m, cand);
-  QHIP(hipGetLastError());
+  unsigned long long* const d_got = reinterpret_cast<unsigned long long*>(bb + o_got);
+  std::vector<unsigned char> tgt((size_t)kDBuckets);
+  std::vector<long long> idx;
   std::vector<unsigned long long> got((size_t)m);
-  QHIP(hipMemcpyAsync(got.data(), cand, (size_t)m * 8, hipMemcpyDeviceToHost, stream));
-  QHIP(hipStreamSynchronize(stream));
+  size_t si = 0;  // next sample (ranks ascend with the buckets)
+  for (const auto& bt : batches) {
+    std::fill(tgt.begin(), tgt.end(), 0);
+    std::vector<int64_t> cand_before((size_t)kDBuckets + 1, 0);  // candidates of this batch's buckets before b
+    int64_t nc = 0;
+    for (int b = bt.first; b < bt.second; ++b) {
+      cand_before[(size_t)b] = nc;
+      if (need[(size_t)b]) {
+        tgt[(size_t)b] = 1;
+        nc += (int64_t)(cnt[(size_t)b] - eq[(size_t)b]);
+      }
+    }
+    QHIP(hipMemcpyAsync(d_target.p, tgt.data(), (size_t)kDBuckets, hipMemcpyHostToDevice, stream));
+    {
+      unsigned long long cur0[1 + 2 * kDAndOrCopies];  // cursor, then (AND, OR) copies
+      cur0[0] = 0;
+      for (int i = 0; i < kDAndOrCopies; ++i) {
+        cur0[1 + 2 * i] = ~0ull;
+        cur0[2 + 2 * i] = 0ull;
+      }
+      QHIP(hipMemcpyAsync(d_cursor.p, cur0, sizeof(cur0), hipMemcpyHostToDevice, stream));
+      QHIP(hipStreamSynchronize(stream));  // cur0 is a stack array
+    }
+    if (dq_status st = for_chunks([&](auto tk, int grid, int c, int64_t rows) {
+          hipLaunchKernelGGL((dq_digest_pass<decltype(tk)::value, false>), dim3(grid), dim3(kQBlock), 0, stream,
+                             cols[c].values, reinterpret_cast<const uint32_t*>(cols[c].validity), rows, d_spl.p,
+                             d_first, C, nullptr, d_target.p, cand, d_cursor.p, (unsigned long long)nc);
+        }))
+      return st;
+    // the candidates agree above their highest differing bit: sorting the bits below gives the full order
+    unsigned long long cur[1 + 2 * kDAndOrCopies];
+    QHIP(hipMemcpyAsync(cur, d_cursor.p, sizeof(cur), hipMemcpyDeviceToHost, stream));
+    QHIP(hipStreamSynchronize(stream));
+    if ((int64_t)cur[0] != nc)
+      return set_error(DQ_E_HIP, "dq_quantile_digest: %llu candidates, the count pass expected %lld (data changed?)",
+                       cur[0], (long long)nc);
+    uint64_t c_and = ~0ull, c_or = 0;
+    for (int i = 0; i < kDAndOrCopies; ++i) {
+      c_and &= cur[1 + 2 * i];
+      c_or |= cur[2 + 2 * i];
+    }
+    const int end_bit = (c_and ^ c_or) ? 64 - __builtin_clzll(c_and ^ c_or) : 1;
+    if (nc > 0) QHIP(hipcub::DeviceRadixSort::SortKeys(bb + o_tmp, tb, cand, sorted, (int)nc, 0, end_bit, stream));
+    // 4. sample i = the sorted candidate at (its rank within its bucket, past the bucket's eq keys) + (the batch's
+    // candidates of the buckets before)
+    idx.clear();
+    const size_t s0 = si;
+    for (; si < (size_t)m && rb[si] < bt.second; ++si) {
+      const int b = rb[si];
+      idx.push_back(known[si] ? -1
+                              : (long long)(rank[si] - 1 - before[(size_t)b] - (int64_t)eq[(size_t)b] + cand_before[(size_t)b]));
+    }
+    const int64_t mb = (int64_t)idx.size();
+    if (mb > 0) {
+      QHIP(hipMemcpyAsync(d_idx, idx.data(), (size_t)mb * 8, hipMemcpyHostToDevice, stream));
+      hipLaunchKernelGGL(dq_digest_gather, dim3((unsigned)((mb + 255) / 256)), dim3(256), 0, stream, sorted, d_idx, mb,
+                         d_got);
+      QHIP(hipGetLastError());
+      QHIP(hipMemcpyAsync(got.data() + s0, d_got, (size_t)mb * 8, hipMemcpyDeviceToHost, stream));
+      QHIP(hipStreamSynchronize(stream));
+    }
+  }
   for (int64_t i = 0; i < m; ++i) {
-    values[i] = key_to_double(type, got[(size_t)i]);
+    values[i] = key_to_double(type, known[(size_t)i] || si <= (size_t)i ? key_of[(size_t)i] : got[(size_t)i]);
     ranks[i] = rank[(size_t)i];
   }
   return DQ_OK;

@@ -277,6 +277,9 @@ def _digest_samples(data, column: str, rel: float):
         raise UnsupportedOnGpuPathException(
             f"a relativeError of {rel} over {cnt.value} values needs {m.value} samples in the quantile state "
             f"(at most {MAX_DIGEST_SAMPLES} on the GPU path)")
+    if rc == L.DQ_E_UNSUPPORTED:  # a device limit of the digest (e.g. one bucket over the candidate budget)
+        raise UnsupportedOnGpuPathException(
+            f"ApproxQuantileState of {column} is outside the GPU path: {L.lib.dq_last_error().decode('utf-8', 'replace')}")
     L.check(rc)
     return cnt.value, list(rks[:m.value]), list(vals[:m.value])
 

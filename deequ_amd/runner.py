@@ -84,6 +84,13 @@ class ScanPlan:
         on = L.lib.dq_plan_pred_compiled(self.handle, buf, len(buf))
         return bool(on), buf.value.decode("utf-8", "replace")
 
+    def pred_wait(self, timeout_ms: int = -1) -> bool:
+        """Wait for a background compile of the predicate kernel (AUTO); True when the next scan runs it."""
+        r = L.lib.dq_plan_pred_wait(self.handle, timeout_ms)
+        if r < 0:
+            L.check(r)
+        return bool(r)
+
     def create_time(self):
         """(host ms dq_plan_create spent, of which ms obtaining the compiled predicate kernel)."""
         total, jit = ctypes.c_double(), ctypes.c_double()
@@ -129,25 +136,38 @@ class ScanPlan:
             pass
 
 
-def explain(analyzers: Sequence[Analyzer], schema, pred_pass: str = "auto") -> str:
-    """The plan dq_plan_create would build for these analyzers, lowered on the host only (dq_plan_explain: no
-    GPU): launches per scan, column-pass variants, the predicate program and the generated predicate kernel."""
+def _lower_all(analyzers: Sequence[Analyzer], schema):
     b = PlanBuilder(schema)
     specs = (L.AnalyzerSpec * max(1, len(analyzers)))()
     for i, a in enumerate(analyzers):
         op, ca, cb, pr, wr = a._lower(b)
         specs[i].op, specs[i].col_a, specs[i].col_b, specs[i].pred_root, specs[i].where_root = op, ca, cb, pr, wr
+    return b, specs
+
+
+def _explain(b: PlanBuilder, specs, n_specs: int, pred_pass: str):
+    """(status, text or dq_last_error) of dq_plan_explain over lowered specs (host only)."""
     sch = b.schema_ctypes()
     pool, npred = b.pool.as_ctypes()
     pats, npats = b.pool.patterns_ctypes()
     opts = L.PlanOptions(ctypes.sizeof(L.PlanOptions), L.PRED_PASS[pred_pass])
-    args = (specs, len(analyzers), sch, len(b.columns), pool, npred, pats, npats, ctypes.byref(opts))
+    args = (specs, n_specs, sch, len(b.columns), pool, npred, pats, npats, ctypes.byref(opts))
     n = L.lib.dq_plan_explain(*args, None, 0)
     if n < 0:
-        L.check(int(n))
+        return int(n), L.lib.dq_last_error().decode("utf-8", "replace")
     buf = ctypes.create_string_buffer(int(n))
     L.lib.dq_plan_explain(*args, buf, n)
-    return buf.value.decode("utf-8", "replace")
+    return L.DQ_OK, buf.value.decode("utf-8", "replace")
+
+
+def explain(analyzers: Sequence[Analyzer], schema, pred_pass: str = "auto") -> str:
+    """The plan dq_plan_create would build for these analyzers, lowered on the host only (dq_plan_explain: no
+    GPU): launches per scan, column-pass variants, the predicate program and the generated predicate kernel;
+    an analyzer set over one plan's capacity is shown as the fused plans dq_plan_create splits it into."""
+    b, specs = _lower_all(analyzers, schema)
+    rc, text = _explain(b, specs, len(analyzers), pred_pass)
+    L.check(rc)
+    return text
 
 
 def scan_results(data, analyzers: Sequence[Analyzer], pred_pass: str = "auto") -> List[L.State]:
@@ -168,15 +188,21 @@ def scan_states(data, analyzers: Sequence[Analyzer], pred_pass: str = "auto") ->
 
 
 def gpu_eligible(analyzer: Analyzer, schema) -> Optional[Exception]:
-    """None if the analyzer lowers into the GPU plan; else the reason (-> fallback set)."""
-    b = PlanBuilder(schema)
+    """None if the analyzer lowers into a GPU plan; else the reason (-> fallback set).
+
+    Two checks, both on the host: the predicate compiler (SQL text outside the GPU grammar), then the planner
+    on this analyzer alone (dq_plan_explain: e.g. a predicate nested deeper than the device stack).  Capacity
+    limits of a plan are never a routing reason: dq_plan_create splits a set over them into several fused
+    plans, so only what does not fit a plan by itself goes to the fallback."""
     try:
-        analyzer._lower(b)
+        b, specs = _lower_all([analyzer], schema)
     except UnsupportedPredicate as e:
         return e
     except Exception:
         return None  # a missing column etc. is an aggregation error, not a routing decision
-    # a comparison on a string column is rejected by the predicate compiler itself (UnsupportedPredicate)
+    rc, msg = _explain(b, specs, 1, "auto")
+    if rc == L.DQ_E_UNSUPPORTED:
+        return UnsupportedPredicate(msg)
     return None
 
 

@@ -31,8 +31,11 @@
 extern "C" {
 #endif
 
-#define DQ_ABI_VERSION 3  /* 2: dq_state.reserved[0] = integral flag + Sum / Mean int64 partials; ingestion, pool and state-array entry points;
-                             3: dq_plan_create_opts (predicate-pass mode), dq_plan_create_time, dq_plan_explain, dq_quantile_digest */
+#define DQ_ABI_VERSION 4  /* 2: dq_state.reserved[0] = integral flag + Sum / Mean int64 partials; ingestion, pool and state-array entry points;
+                             3: dq_plan_create_opts (predicate-pass mode), dq_plan_create_time, dq_plan_explain, dq_quantile_digest;
+                             4: any number of analyzers / columns per plan (split into fused plans over the
+                                per-plan capacities), AUTO compiles the predicate kernel in the background,
+                                dq_plan_pred_wait */
 
 typedef int32_t dq_status;
 #define DQ_OK 0
@@ -247,9 +250,13 @@ dq_status dq_plan_create_ex(const dq_analyzer_spec* specs, int32_t n_specs, cons
 /* How the predicate pass of a plan runs (dq_plan_options.pred_pass).  AUTO: the kernel generated and
  * compiled for the plan's program when the generator takes it (numeric comparisons; Spark's whole-stage
  * code generation of the same expressions), else -- or when the compile fails -- the interpreter, with
- * the reason in dq_plan_pred_compiled's note.  INTERPRETER: always the interpreter (the reference
- * implementation the compiled kernel is tested against).  COMPILED: the compiled kernel or
- * DQ_E_UNSUPPORTED from dq_plan_create_opts (reason in dq_last_error) -- no silent fallback. */
+ * the reason in dq_plan_pred_compiled's note.  A kernel not yet in the process or disk code-object cache is
+ * compiled on a background thread: plan creation does not wait for hipRTC, the scan runs the interpreter
+ * until the kernel is ready and the compiled kernel from the next chunk on (bit-identical results either
+ * way; dq_plan_pred_wait blocks for it).  INTERPRETER: always the interpreter (the reference
+ * implementation the compiled kernel is tested against).  COMPILED: the compiled kernel (plan creation
+ * waits for the compile) or DQ_E_UNSUPPORTED from dq_plan_create_opts (reason in dq_last_error) -- no
+ * silent fallback. */
 enum dq_pred_pass { DQ_PRED_PASS_AUTO = 0, DQ_PRED_PASS_INTERPRETER = 1, DQ_PRED_PASS_COMPILED = 2 };
 typedef struct dq_plan_options {
   int32_t struct_size;  /* sizeof(dq_plan_options) as the caller was compiled (fields past it: defaults) */
@@ -257,7 +264,15 @@ typedef struct dq_plan_options {
   int32_t reserved[6];  /* 0 */
 } dq_plan_options;
 /* As dq_plan_create_ex with options (NULL = all defaults).  Replaces AnalysisRunner.runScanningAnalyzers'
- * plan step (AnalysisRunner.scala:279-326): one plan per run, created before the first chunk. */
+ * plan step (AnalysisRunner.scala:279-326): one plan per run, created before the first chunk.
+ * Like the reference's single data.agg (AnalysisRunner.scala:293-303) a plan takes any number of analyzers.
+ * One fused pass holds at most 64 columns, 32 distinct predicates (Compliance predicates, `where` filters,
+ * Completeness-with-`where` NOT NULL tests), 32 predicate counters, 8 distinct `where` filters of value
+ * analyzers (Sum ... ApproxCountDistinct, Correlation), 256 column tasks and a 96-instruction predicate
+ * program; a larger set is split -- analyzers grouped by their columns -- into several fused passes over
+ * the same chunks, each reading only its own columns (dq_plan_explain shows the split).  Only a spec that
+ * exceeds a limit by itself (e.g. a predicate over more than 64 columns or nested deeper than the
+ * 16-entry operand stack) fails, with DQ_E_UNSUPPORTED: route it to the fallback set. */
 dq_status dq_plan_create_opts(const dq_analyzer_spec* specs, int32_t n_specs, const dq_column_desc* schema,
                               int32_t n_cols, const dq_pred_node* pred_pool, int32_t n_pred,
                               const char* const* patterns, int32_t n_patterns, const dq_plan_options* opts,
@@ -324,6 +339,10 @@ int64_t dq_plan_kernel_bytes_per_row_x1000(const dq_plan* plan, int32_t kernel);
  * note (optional, cap bytes incl. the terminator) receives the reason the interpreter runs, or -- when
  * compiled -- where the code object came from ("hiprtc", "disk cache", "process cache"). */
 int32_t dq_plan_pred_compiled(const dq_plan* plan, char* note, int32_t cap);
+/* Wait up to timeout_ms (< 0: until done) for a background compile of the plan's predicate kernel (AUTO);
+ * then 1 when the next dq_scan runs the compiled kernel, 0 when the interpreter runs it (compile failed, not
+ * eligible, no predicates), or a negative dq_status. */
+int32_t dq_plan_pred_wait(dq_plan* plan, int32_t timeout_ms);
 /* EXPLAIN of the plan dq_plan_create_opts would build, on the host only (no device, no allocation, no
  * compile): the launches per scan, the column-pass variants, the pair pass, the predicate program and -- when
  * the predicate pass would be compiled -- the generated kernel source.  Writes at most cap bytes (incl. the

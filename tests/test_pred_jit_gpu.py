@@ -106,6 +106,7 @@ def test_c3_plan_runs_the_compiled_pass(dq):
     t = synth.c3_table(4099, seed=5)
     an = synth.c3_analyzers(t)
     plan = ScanPlan(an, t.schema)
+    assert plan.pred_wait(), plan.pred_compiled()  # AUTO: a cold compile runs in the background
     ok, origin = plan.pred_compiled()
     assert ok, origin
     plan.close()
@@ -287,3 +288,103 @@ def test_predicate_column_at_end_of_allocation(dq, n):
     ocols = {"a": O.OColumn("i64", a, va), "x": O.OColumn("f64", x, np.ones(n, bool)),
              "y": O.OColumn("i64", a[::-1].copy(), va)}
     _check_vs_oracle(dq, c, an, ocols, n)
+
+
+def _unique_predicates(tag):
+    """Predicates no other test compiles (a fresh kernel source: neither cache has it)."""
+    import time
+
+    k = (time.time_ns() // 1000) % 1_000_003 + 17
+    return [f"a > {k % 11 - 5}", f"COALESCE(b, {k}.0) < {k % 7}.5", f"a < c OR c = {tag}", f"b IS NULL OR a >= {k % 13}"]
+
+
+def test_background_compile_switches_between_chunks(dq, tmp_path, monkeypatch):
+    """AUTO with a kernel in neither cache: plan creation does not wait for hipRTC, the first chunk runs the
+    interpreter, later chunks the compiled kernel (with the fused HLL tasks), and the states are bit-identical
+    to the interpreter's and equal to the oracle."""
+    from deequ_amd.runner import ScanPlan
+    from deequ_amd.table import column_from_numpy
+
+    monkeypatch.setenv("DQ_JIT_CACHE_DIR", str(tmp_path / "jit"))
+    n, parts = 30011, 3
+    t, ocols = _abc_table(dq, n, 77)
+    an = [dq.Compliance(f"q{i}", p) for i, p in enumerate(_unique_predicates(1))]
+    an += [dq.ApproxCountDistinct("a"), dq.ApproxCountDistinct("c"), dq.Size("a > 0"), dq.Completeness("b", "c > 1")]
+    bounds = [0, 7001, 19000, n]
+    chunks = []
+    for lo, hi in zip(bounds[:-1], bounds[1:]):
+        chunks.append(dq.Table([column_from_numpy(k, ocols[k].dtype, ocols[k].values[lo:hi], ocols[k].valid[lo:hi])
+                                for k in ("a", "b", "c")]))
+    plan = ScanPlan(an, t.schema)
+    total_ms, jit_ms = plan.create_time()
+    ok, note = plan.pred_compiled()
+    assert not ok and "background" in note, note
+    assert total_ms < 100.0, total_ms  # no hipRTC inside plan creation
+    plan.scan(chunks[0])
+    assert plan.pred_wait(), plan.pred_compiled()
+    for c in chunks[1:]:
+        plan.scan(c)
+    ok, note = plan.pred_compiled()
+    assert ok and "used from chunk 1" in note, note
+    got = {a: a._from_result(r) for a, r in zip(an, plan.finish())}
+    plan.close()
+    from deequ_amd.runner import scan_states
+
+    ref = scan_states(chunks, an, "interpreter")
+    for a in an:
+        assert got[a] == ref[a] or (got[a] is None and ref[a] is None), (a, got[a], ref[a])
+    _check_vs_oracle(dq, got, an, ocols, n)
+    # the code object is now in the (private, keyed) disk cache
+    files = list((tmp_path / "jit").glob("*.co"))
+    assert files and files[0].read_bytes()[:8] == b"DQJITCO1"
+
+
+def test_concurrent_plan_creation_does_not_serialize_on_hiprtc(dq, monkeypatch):
+    """Two threads create plans with kernels in neither cache at once: both return without waiting for a
+    compile (the process-wide lock is held for the map lookup only), and both kernels become ready."""
+    import threading
+    import time
+
+    from deequ_amd.runner import ScanPlan
+
+    monkeypatch.setenv("DQ_JIT_CACHE_DIR", "off")
+    t, _ = _abc_table(dq, 1000, 3)
+    plans, errs, times = [None, None], [], [0.0, 0.0]
+    import torch
+
+    def make(k):
+        try:
+            torch.cuda.set_device(0)
+            t0 = time.perf_counter()
+            plans[k] = ScanPlan([dq.Compliance(f"t{i}", p) for i, p in enumerate(_unique_predicates(k + 10))], t.schema)
+            times[k] = time.perf_counter() - t0
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    th = [threading.Thread(target=make, args=(k,)) for k in range(2)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errs, errs
+    assert max(times) < 0.15, times
+    for p in plans:
+        assert p.pred_wait(), p.pred_compiled()
+        p.close()
+
+
+def test_jit_cache_refuses_foreign_or_shared_dirs(dq, tmp_path, monkeypatch):
+    """A cache directory writable by group / others is not used (a planted code object would run); the plan
+    still compiles its kernel (no disk cache) and nothing is written there."""
+    from deequ_amd.runner import ScanPlan
+
+    d = tmp_path / "shared"
+    d.mkdir()
+    d.chmod(0o777)
+    monkeypatch.setenv("DQ_JIT_CACHE_DIR", str(d))
+    t, _ = _abc_table(dq, 100, 4)
+    plan = ScanPlan([dq.Compliance("u", p) for p in _unique_predicates(99)], t.schema, pred_pass="compiled")
+    ok, origin = plan.pred_compiled()
+    assert ok and origin == "hiprtc", origin
+    plan.close()
+    assert not list(d.iterdir())

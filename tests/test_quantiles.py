@@ -297,6 +297,64 @@ def test_gpu_digest_small_and_ragged(dq, n):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("budget", [700, 50_000])
+def test_gpu_digest_bounded_batches(dq, monkeypatch, budget):
+    """The digest's compaction runs in batches of at most DQ_DIGEST_CAND_BUDGET candidates (scratch bounded
+    whatever the relative error): small budgets force many batches -- relativeError 1e-5 flags every bucket
+    (m > 2048 samples), the skewed column's hot value is answered from its bucket's lower splitter -- and every
+    sample rank is still the exact order statistic."""
+    from deequ_amd.quantiles import device_digest
+    from deequ_amd.table import column_from_numpy
+
+    monkeypatch.setenv("DQ_DIGEST_CAND_BUDGET", str(budget))
+    rng = np.random.default_rng(budget)
+    n = 200_003
+    for kind in ("f64", "skew", "i64"):
+        if kind == "f64":
+            v, dtype = _f64_data(rng, n), "f64"
+        elif kind == "skew":
+            v, dtype = rng.choice(np.array([7.25, -1.0, 3.5]), n, p=[0.9, 0.05, 0.05]), "f64"
+            v[rng.random(n) < 0.02] = rng.normal(0, 1, n)[rng.random(n) < 0.02][:1]
+        else:
+            v, dtype = rng.integers(-1000, 1000, n, dtype=np.int64), "i64"
+        valid = rng.random(n) >= 0.1
+        t = dq.Table([column_from_numpy("x", dtype, v, valid)])
+        for err in (1e-5, 0.001, 0.05):
+            cnt, want = O.gk_digest_exact(v, valid, err)
+            got = device_digest(t, "x", err).quantileSummaries
+            assert got.count == cnt and len(got.sampled) == len(want), (kind, err)
+            assert all(_same(a[0], b[0]) and a[1:] == b[1:] for a, b in zip(got.sampled, want)), (kind, err)
+
+
+@pytest.mark.gpu
+def test_gpu_digest_over_budget_bucket_falls_back(dq, monkeypatch):
+    """One bucket with more distinct candidates than the budget: UnsupportedOnGpuPathException (the analyzer goes
+    to the fallback set), not a bare DQError; and the device memory the digest held is returned (its pool keeps
+    at most 256 MB; torch's own pool settings are untouched)."""
+    import torch
+
+    from deequ_amd import quantiles as Q
+    from deequ_amd.metrics import UnsupportedOnGpuPathException
+    from deequ_amd.table import column_from_numpy
+
+    x = np.random.default_rng(5).normal(size=100_000)
+    t = dq.Table([column_from_numpy("x", "f64", x, np.ones(len(x), bool))])
+    monkeypatch.setenv("DQ_DIGEST_CAND_BUDGET", "10")
+    with pytest.raises(UnsupportedOnGpuPathException):
+        Q.device_digest(t, "x", 0.01)
+    monkeypatch.delenv("DQ_DIGEST_CAND_BUDGET")
+    torch.cuda.synchronize()
+    free0 = torch.cuda.mem_get_info()[0]
+    big = dq.Table([column_from_numpy("x", "f64", np.random.default_rng(6).normal(size=20_000_000),
+                                      np.ones(20_000_000, bool))])
+    free1 = torch.cuda.mem_get_info()[0]
+    Q.device_digest(big, "x", 1e-6)  # every bucket flagged: ~20 M candidates (~0.5 GB of scratch)
+    torch.cuda.synchronize()
+    free2 = torch.cuda.mem_get_info()[0]
+    assert free1 - free2 <= (256 << 20) + (64 << 20), (free0, free1, free2)
+
+
+@pytest.mark.gpu
 def test_gpu_digest_sample_limit(dq, monkeypatch):
     """relativeError 0 keeps every value (as Spark's GK does); past MAX_DIGEST_SAMPLES the GPU path refuses
     with UnsupportedOnGpuPathException (the analyzer goes to the Spark fallback) instead of building a digest
