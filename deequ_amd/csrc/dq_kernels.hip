@@ -908,30 +908,29 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
 // utf8_range hashes the rows of a 64-row group in lock-step: a NULL row costs as much as a string, and every
 // exec-masked round (the second stripe round, the 4-byte round, the byte rounds) runs whenever any lane of the
 // group needs it -- 121.8 VALU per row for C5's 8..24-byte strings, of which ~35 hashed nothing.  Here the
-// selected short strings of each 64-row group are first pushed, as one dword (rel | len << 27), into one of two
+// selected short strings of each 64-row group are first pushed, as (byte offset, length), into one of two
 // per-wave streams in LDS by their stripe-round count -- A: len < 16 (one round; none below 8), B: len >= 16
-// (two rounds, a 24..28-byte string's third deferred as in utf8_range) -- at the cost of one ballot and an
+// (two rounds, a 24..28-byte string's third deferred as in utf8_range) -- at the cost of one compare and an
 // mbcnt per stream (NULL rows are never pushed).  Every full group of 64 stream entries is then hashed with
 // all lanes live and its stripe rounds unconditional; its 32-byte windows are loaded one group ahead.  The
 // streams keep row order, so a group's windows still come from a few consecutive kilobytes of string bytes.
 // Strings longer than 28 bytes or whose window crosses the chunk's end take the general loop after the block,
-// as in utf8_range; a range whose bytes exceed 2^27 (the entry's offset field) runs utf8_range itself.
-constexpr int kStrCap = 256;       // per-wave stream dwords: A from the bottom, B from the top (<= 2 x 63 + 128)
-constexpr int kStrRelBits = 27;    // entry = rel | len << 27 (rel: the string's byte offset in the range's window)
+// as in utf8_range.
+constexpr int kStrCap = 256;  // per-wave stream entries (offset, len): A from the bottom, B from the top (<= 2 x 63 + 128)
 
 template <typename OffT>
 __device__ void utf8_hll_compact(const uint8_t* data, const OffT* offsets, const uint32_t* validity,
                                  const uint32_t* mask, int64_t row0, int64_t row1, int64_t n_rows, ColStats& s,
-                                 int32_t* regs, const uint64_t* p5, uint32_t* dq, uint32_t* st) {
+                                 int32_t* regs, const uint64_t* p5, uint32_t* dq, uint2* st) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (row0 >= row1) return;
   constexpr int W = (int)sizeof(OffT);
+  constexpr int64_t kSpan = 0x7FFFFF00;  // a buffer resource's byte range (32-bit offsets)
   const auto bp = [p5](uint32_t b) { return p5[b]; };
   int64_t cnt_w = 0;
   uint32_t qtail = 0;       // deferred 24..28-byte strings in dq[.][0, qtail)
   uint32_t ta = 0, tb = 0;  // stream A entries st[0, ta), stream B entries st[kStrCap - tb, kStrCap)
-
 
   // finish deferred strings [0, n): third stripe round, tail, HLL register max
   auto drain = [&](uint32_t n) __attribute__((always_inline)) {
@@ -958,30 +957,30 @@ __device__ void utf8_hll_compact(const uint8_t* data, const OffT* offsets, const
     qtail = rest;
   };
 
-  // sub-ranges of whole 2048-row iterations whose string bytes fit the entry's 27-bit offset (all of the range
-  // unless its strings average kilobytes); the streams are emptied at each sub-range's end
+  // int32 offsets address the chunk's bytes directly (a UTF8 chunk holds < 2 GiB: one sub-range); int64
+  // offsets run in sub-ranges of whole 2048-row iterations whose bytes fit a buffer resource, relative to the
+  // sub-range's first string.  The streams are emptied at each sub-range's end.
   for (int64_t sr0 = row0, sr1; sr0 < row1; sr0 = sr1) {
-    const int64_t lo = (int64_t)offsets[sr0] & ~int64_t(3);
+    const int64_t lo = W == 4 ? 0 : ((int64_t)offsets[sr0] & ~int64_t(3));
     sr1 = row1;
-    if ((int64_t)offsets[sr1] - lo >= (int64_t(1) << kStrRelBits)) {  // the largest fitting multiple of 2048 rows
+    if (W == 8 && (int64_t)offsets[sr1] - lo >= kSpan) {  // the largest fitting multiple of 2048 rows
       int64_t a = 1, b = (row1 - sr0 + kRowsPerIter - 1) / kRowsPerIter;  // iterations: a fits (or is the minimum)
       while (b - a > 1) {
         const int64_t c = (a + b) / 2;
-        if ((int64_t)offsets[sr0 + c * kRowsPerIter] - lo < (int64_t(1) << kStrRelBits)) a = c;
+        if ((int64_t)offsets[sr0 + c * kRowsPerIter] - lo < kSpan) a = c;
         else b = c;
       }
       sr1 = sr0 + a * kRowsPerIter < row1 ? sr0 + a * kRowsPerIter : row1;
     }
-    // the window: the chunk's bytes from the sub-range's first string (dword-aligned) to the chunk's end (a
-    // 32-byte window may read past sr1's bytes); a string at rel >= 2^27 (a 2048-row iteration holding more
-    // than 2^27 bytes) takes the general loop
+    // the window: the chunk's bytes from lo to the chunk's end (a 32-byte window may read past sr1's bytes); a
+    // string whose window leaves it takes the general loop
     const int64_t span_all = (int64_t)offsets[n_rows] - lo;
-    const int32_t span = span_all < (int64_t)0x7FFFFF00 ? (int32_t)span_all : 0x7FFFFF00;
+    const int32_t span = (int32_t)(span_all < kSpan ? span_all : kSpan);
     const __amdgpu_buffer_rsrc_t rsrc =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(data + lo), (short)0, span, 0x00020000);
     const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<OffT*>(offsets + sr0), (short)0, (int)((sr1 - sr0 + 1) * W), 0x00020000);
-    const int32_t win3 = (span - 32 < (1 << kStrRelBits) - 4 ? span - 32 : (1 << kStrRelBits) - 4) | 3;
+    const int32_t win3 = (span - 32) | 3;  // the window at rel & ~3 lies in the resource iff rel <= win3
     const bool wins_in = (int64_t)offsets[sr1 - 1] - lo <= (int64_t)win3;  // (offsets only grow)
     // offsets of 4 row groups ahead in a register ring (as utf8_range)
     constexpr int kOffRing = 4;
@@ -999,7 +998,7 @@ __device__ void utf8_hll_compact(const uint8_t* data, const OffT* offsets, const
         rb[q] = (int64_t)(((uint64_t)a1[1] << 32) | a1[0]);
       }
     };
-    auto rel_of = [&](int j) -> uint32_t {  // (saturated for int64 offsets: a huge iteration's strings stay slow)
+    auto rel_of = [&](int j) -> uint32_t {  // (int64 offsets: saturated, so a huge iteration's strings stay slow)
       const int64_t d = (int64_t)ra[j & (kOffRing - 1)] - lo;
       return W == 4 ? (uint32_t)d : (d > 0x7FFFFFFF ? 0x7FFFFFFFu : (uint32_t)d);
     };
@@ -1011,16 +1010,16 @@ __device__ void utf8_hll_compact(const uint8_t* data, const OffT* offsets, const
     int32_t vo_cur = lane_off(sr0);
 #pragma unroll
     for (int j = 0; j < kOffRing; ++j) load_offsets(vo_cur, j);
-    // one group of stream entries: e = rel | len << 27 per lane, its 32-byte window (wa, wc), `act` = live lanes;
-    // B: the group holds 16..28-byte strings (two stripe rounds, the third deferred), else 0..15-byte ones
-    auto hash_group = [&](auto kB, uint32_t e, u32x4 wa, u32x4 wc, uint64_t act) __attribute__((always_inline)) {
+    // one group of stream entries (rel, len) per lane, its 32-byte window (wa, wc), `act` = live lanes; B: the
+    // group holds 16..28-byte strings (two stripe rounds, the third deferred), else 0..15-byte ones
+    auto hash_group = [&](auto kB, uint32_t rel, uint32_t len, u32x4 wa, u32x4 wc, uint64_t act)
+                          __attribute__((always_inline)) {
       constexpr bool B = decltype(kB)::value;
       const uint32_t d[8] = {wa.x, wa.y, wa.z, wa.w, wc.x, wc.y, wc.z, wc.w};
       uint32_t wv[8];
 #pragma unroll
-      for (int k = 0; k < 7; ++k) wv[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], e);  // byte shift = rel & 3
+      for (int k = 0; k < 7; ++k) wv[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], rel);  // byte shift = rel & 3
       wv[7] = d[7];
-      const uint32_t len = e >> kStrRelBits;
       uint64_t h = kSeed + XP5 + (uint64_t)len;
       uint64_t d4p;
       if constexpr (B) {  // len >= 16: two rounds for every lane
@@ -1063,13 +1062,13 @@ __device__ void utf8_hll_compact(const uint8_t* data, const OffT* offsets, const
 
     // the pending group: taken from a stream, its windows in flight, hashed when the next group is taken
     u32x4 pa = {0, 0, 0, 0}, pc = {0, 0, 0, 0};
-    uint32_t pe = 0;
+    uint32_t prel = 0, plen = 0;
     uint64_t pact = 0;  // 0: none
     bool pb = false;
     auto hash_pending = [&]() __attribute__((always_inline)) {
       if (pact != 0) {
-        if (pb) hash_group(std::true_type{}, pe, pa, pc, pact);
-        else hash_group(std::false_type{}, pe, pa, pc, pact);
+        if (pb) hash_group(std::true_type{}, prel, plen, pa, pc, pact);
+        else hash_group(std::false_type{}, prel, plen, pa, pc, pact);
       }
     };
     // take up to 64 entries of stream B (or A) into the pending group (after hashing the previous one): the
@@ -1078,25 +1077,26 @@ __device__ void utf8_hll_compact(const uint8_t* data, const OffT* offsets, const
       const uint32_t t = fromB ? tb : ta;
       const uint32_t n = t < 64u ? t : 64u;
       const int32_t at = fromB ? kStrCap - 1 - lane : lane;  // B grows down from the top
-      const uint32_t e = st[at];
+      const uint2 e = st[at];
       if (t > 64u && (uint32_t)lane < t - 64u) {
         const int32_t src = fromB ? kStrCap - 1 - 64 - lane : 64 + lane;
         st[at] = st[src];
       }
       if (fromB) tb = t - n;
       else ta = t - n;
-      const int32_t wofs = (int32_t)(e & ((1u << kStrRelBits) - 4u));
+      const int32_t wofs = (int32_t)(e.x & ~3u);
       const u32x4 na = __builtin_amdgcn_raw_buffer_load_b128(rsrc, wofs, 0, 0);
       const u32x4 nc = __builtin_amdgcn_raw_buffer_load_b128(rsrc, wofs + 16, 0, 0);
       hash_pending();
       pa = na;
       pc = nc;
-      pe = e;
+      prel = e.x;
+      plen = e.y;
       pact = n == 64u ? ~0ull : ((1ull << n) - 1ull);
       pb = fromB;
     };
 
-    const int32_t nr = (int32_t)(sr1 - sr0);  // range-relative rows: 32-bit (scalar) loop control and compares
+    const int32_t nr = (int32_t)(sr1 - sr0);  // sub-range-relative rows: 32-bit (scalar) loop control and compares
     for (int32_t rbk = 0; rbk < nr; rbk += kRowsPerIter) {
       const int64_t blk = sr0 + rbk;
       const int64_t base = blk + wave * 512;
@@ -1121,11 +1121,18 @@ __device__ void utf8_hll_compact(const uint8_t* data, const OffT* offsets, const
           const uint64_t mf = m[j] & fastm;
           const uint64_t mb = mf & __builtin_amdgcn_uicmp(len_of(j), 15u, 34 /* ICMP_UGT */);
           const uint64_t ma = mf & ~mb;
-          const uint32_t e = rel_of(j) | (len_of(j) << kStrRelBits);
-          if (lane_bit(ma))
-            st[__builtin_amdgcn_mbcnt_hi((uint32_t)(ma >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ma, ta))] = e;
-          if (lane_bit(mb))
-            st[kStrCap - 1 - __builtin_amdgcn_mbcnt_hi((uint32_t)(mb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mb, tb))] = e;
+          const uint2 e = {rel_of(j), len_of(j)};
+          // positions: the lane's rank among the stream's pushing lanes (mbcnt) past the stream's tail (an SGPR
+          // folded into the LDS base, not the mbcnt: one SGPR operand per VALU instruction)
+          uint2* const sa = st + ta;
+          if (lane_bit(ma)) sa[__builtin_amdgcn_mbcnt_hi((uint32_t)(ma >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ma, 0u))] = e;
+          if (lane_bit(mb)) {  // B grows down: address = (its top entry) - 8 rank, one v_mad_i32_i24
+            const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(mb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mb, 0u));
+            const uint32_t top = (uint32_t)(uintptr_t)(st + (kStrCap - 1) - tb);
+            uint32_t addr;
+            asm("v_mad_i32_i24 %0, %1, -8, %2" : "=v"(addr) : "v"(rk), "s"(top));
+            *reinterpret_cast<__attribute__((address_space(3))) uint64_t*>(addr) = ((uint64_t)e.y << 32) | e.x;
+          }
           ta += (uint32_t)__builtin_popcountll(ma);
           tb += (uint32_t)__builtin_popcountll(mb);
           // row j + 4 into the slot row j frees (of the next block for j >= 4)
@@ -1205,7 +1212,7 @@ __device__ void run_numeric(const ColTask& t, const ScanCols& cols, const ScanBi
 template <int V>
 __device__ __forceinline__ void run_variant(const ColTask& t, const ScanCols& cols, const uint32_t* mask, int64_t row0,
                                             int64_t row1, int64_t n_rows, ColStats& s, int32_t* regs,
-                                            const uint64_t* p5, uint32_t* dq, uint32_t* st) {
+                                            const uint64_t* p5, uint32_t* dq, uint2* st) {
   const void* v = cols.values[t.col];
   const uint32_t* val = cols.validity[t.col];
   if constexpr (V == CV_VALIDITY) validity_range(val, mask, row0, row1, s);
@@ -1262,7 +1269,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kMinWave
   __shared__ uint64_t p5[kStr ? 256 : 1];   // b * P5 for the byte rounds of the string hash
   __shared__ uint32_t dfq[kStr ? kWaves * kDefFields * kDefCap : 1];  // deferred 24..28-byte strings
   constexpr bool kCompact = V == CV_UTF8_H || V == CV_LUTF8_H;
-  __shared__ uint32_t sst[kCompact ? kWaves * kStrCap : 1];              // the compacted string streams
+  __shared__ uint2 sst[kCompact ? kWaves * kStrCap : 1];                 // the compacted string streams
   __shared__ ColStats red[kWaves];
   const int32_t ti = blockIdx.x % ntasks;
   const int32_t range = blockIdx.x / ntasks;
