@@ -770,7 +770,7 @@ hipFunction_t pred_jit_poll(const PredJitRef& e, int32_t wait_ms, std::string& n
       note = e->err;
       return nullptr;
     case PredJitEntry::LOADED:
-      note = e->origin + " (process cache)";
+      note = "process cache";
       return e->fn;
     case PredJitEntry::CODE: {  // load the module on this (plan) thread; it stays loaded for the process
       hipModule_t mod = nullptr;
