@@ -1078,9 +1078,13 @@ __device__ void utf8_hll_compact(const uint8_t* data, const OffT* offsets, const
       const uint32_t n = t < 64u ? t : 64u;
       const int32_t at = fromB ? kStrCap - 1 - lane : lane;  // B grows down from the top
       const uint2 e = st[at];
-      if (t > 64u && (uint32_t)lane < t - 64u) {
-        const int32_t src = fromB ? kStrCap - 1 - 64 - lane : 64 + lane;
-        st[at] = st[src];
+      // (up to 127 left: one stream can take every row of two row groups -- two moves, in order)
+#pragma unroll
+      for (uint32_t k = 0; k < 2; ++k) {
+        if (t > 64u * (k + 1) && (uint32_t)lane + 64u * k < t - 64u) {
+          const int32_t d = fromB ? -64 * (int32_t)k : 64 * (int32_t)k;
+          st[at + d] = st[at + d + (fromB ? -64 : 64)];
+        }
       }
       if (fromB) tb = t - n;
       else ta = t - n;

@@ -1981,7 +1981,7 @@ int32_t dq_plan_pred_wait(dq_plan* p, int32_t timeout_ms) {
     std::string note;
     if (hipFunction_t fn = pred_jit_poll(p->pred_jit_ref, timeout_ms, note)) {
       p->pred_jit = fn;
-      p->pred_jit_note = note + " (compiled in the background)";
+      p->pred_jit_note = note + " (compiled in the background; used from chunk " + std::to_string(p->next_chunk) + ")";
       p->pred_jit_ref.reset();
     } else if (!pred_jit_pending(p->pred_jit_ref)) {
       p->pred_jit_note = note;

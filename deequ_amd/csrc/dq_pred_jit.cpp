@@ -684,15 +684,40 @@ std::mutex g_map_mu;
 std::map<std::pair<int, std::string>, PredJitRef> g_map;
 Workers g_workers;  // declared after the map: destroyed (joined) first
 
-void compile_into(const PredJitRef& e, std::string src, std::string arch, std::string key, std::string path) {
+// The code object of `src` for `device`: the disk cache, else hipRTC (then written to the disk cache).  Runs on a
+// background thread for AUTO plans: everything that can take long -- hipRTC's first call loads the compiler
+// (~0.15 s), a compile ~0.3 s -- stays off the plan-creating thread.
+void obtain_code(PredJitRef e, std::string src, int device) {
   std::vector<char> code;
-  std::string err;
-  const bool ok = pred_jit_compile_code(src, arch, code, err);
-  if (ok && !path.empty()) write_cached(path, key, code);
+  std::string err, origin;
+  bool ok = false;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
+    err = "hipGetDeviceProperties failed";
+  } else {
+    const std::string arch = prop.gcnArchName;
+    int rv_major = 0, rv_minor = 0;
+    hiprtcVersion(&rv_major, &rv_minor);
+    const std::string key = std::string(kJitRevision) + "\n" + arch + "\nhiprtc " + std::to_string(rv_major) + "." +
+                            std::to_string(rv_minor) + "\n" + src;
+    char name[80];
+    std::snprintf(name, sizeof name, "%016" PRIx64 "%016" PRIx64 ".co", fnv1a64(key, 0xCBF29CE484222325ull),
+                  fnv1a64(key, 0x84222325CBF29CE4ull));
+    const std::string dir = cache_dir();
+    const std::string path = dir.empty() ? std::string() : dir + "/" + name;
+    if (!path.empty() && read_cached(path, key, code)) {
+      ok = true;
+      origin = "disk cache";
+    } else if (pred_jit_compile_code(src, arch, code, err)) {
+      ok = true;
+      origin = "hiprtc";
+      if (!path.empty()) write_cached(path, key, code);
+    }
+  }
   std::lock_guard<std::mutex> lock(e->mu);
   if (ok) {
     e->code.swap(code);
-    e->origin = "hiprtc";
+    e->origin = origin;
     e->state = PredJitEntry::CODE;
   } else {
     e->err = err;
@@ -708,7 +733,7 @@ PredJitRef pred_jit_request(const std::string& src, int device, bool background,
   PredJitRef e;
   bool created = false;
   {
-    std::lock_guard<std::mutex> lock(g_map_mu);
+    std::lock_guard<std::mutex> lock(g_map_mu);  // held for the lookup only, never across hipRTC
     PredJitRef& slot = g_map[{device, src}];
     if (!slot) {
       slot = std::make_shared<PredJitEntry>();
@@ -717,36 +742,11 @@ PredJitRef pred_jit_request(const std::string& src, int device, bool background,
     e = slot;
   }
   if (created) {
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
-      std::lock_guard<std::mutex> lock(e->mu);
-      e->err = "hipGetDeviceProperties failed";
-      e->state = PredJitEntry::FAILED;
-      e->cv.notify_all();
+    if (background) {
+      std::lock_guard<std::mutex> lock(g_workers.mu);
+      g_workers.threads.emplace_back(obtain_code, e, src, device);
     } else {
-      const std::string arch = prop.gcnArchName;
-      int rv_major = 0, rv_minor = 0;
-      hiprtcVersion(&rv_major, &rv_minor);
-      const std::string key = std::string(kJitRevision) + "\n" + arch + "\nhiprtc " + std::to_string(rv_major) + "." +
-                              std::to_string(rv_minor) + "\n" + src;
-      char name[80];
-      std::snprintf(name, sizeof name, "%016" PRIx64 "%016" PRIx64 ".co", fnv1a64(key, 0xCBF29CE484222325ull),
-                    fnv1a64(key, 0x84222325CBF29CE4ull));
-      const std::string dir = cache_dir();
-      const std::string path = dir.empty() ? std::string() : dir + "/" + name;
-      std::vector<char> code;
-      if (!path.empty() && read_cached(path, key, code)) {
-        std::lock_guard<std::mutex> lock(e->mu);
-        e->code.swap(code);
-        e->origin = "disk cache";
-        e->state = PredJitEntry::CODE;
-        e->cv.notify_all();
-      } else if (background) {
-        std::lock_guard<std::mutex> lock(g_workers.mu);
-        g_workers.threads.emplace_back(compile_into, e, src, arch, key, path);
-      } else {
-        compile_into(e, src, arch, key, path);
-      }
+      obtain_code(e, src, device);
     }
   }
   ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();

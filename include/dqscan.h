@@ -250,10 +250,10 @@ dq_status dq_plan_create_ex(const dq_analyzer_spec* specs, int32_t n_specs, cons
 /* How the predicate pass of a plan runs (dq_plan_options.pred_pass).  AUTO: the kernel generated and
  * compiled for the plan's program when the generator takes it (numeric comparisons; Spark's whole-stage
  * code generation of the same expressions), else -- or when the compile fails -- the interpreter, with
- * the reason in dq_plan_pred_compiled's note.  A kernel not yet in the process or disk code-object cache is
- * compiled on a background thread: plan creation does not wait for hipRTC, the scan runs the interpreter
- * until the kernel is ready and the compiled kernel from the next chunk on (bit-identical results either
- * way; dq_plan_pred_wait blocks for it).  INTERPRETER: always the interpreter (the reference
+ * the reason in dq_plan_pred_compiled's note.  A kernel not yet in the process's cache is obtained (from the
+ * disk code-object cache, else compiled by hipRTC) on a background thread: plan creation does not wait for
+ * it, the scan runs the interpreter until the kernel is ready and the compiled kernel from the next chunk on
+ * (bit-identical results either way; dq_plan_pred_wait blocks for it).  INTERPRETER: always the interpreter (the reference
  * implementation the compiled kernel is tested against).  COMPILED: the compiled kernel (plan creation
  * waits for the compile) or DQ_E_UNSUPPORTED from dq_plan_create_opts (reason in dq_last_error) -- no
  * silent fallback. */

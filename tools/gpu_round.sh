@@ -11,6 +11,7 @@
 #   clock            tools/clock_probe.sh TAG (held clock under the headline kernels)
 #   parity[=CFGS]    tests/fullscale_parity.py at 1e9 rows (CFGS e.g. c3,c5) -> TAG_parity.json
 #   py=SCRIPT[,ARGS] python SCRIPT ARGS
+#   sh=SCRIPT[,ARGS] bash SCRIPT ARGS (e.g. sh=tools/ab_c5.sh,build_variants/libgold.so,deequ_amd/libdqscan.so)
 # Usage: /usr/local/graft/bin/gpurun --timeout 1200 -- bash tools/gpu_round.sh r5a test=tests/test_plan_split.py bench
 set -o pipefail
 TAG=$1; shift
@@ -43,6 +44,8 @@ for step in "$@"; do
            rc=$?; tail -5 gpurun_out/${TAG}_parity.txt | tee -a "$S" ;;
     py)    timeout -k 10 600 python -u ${arg//,/ } > gpurun_out/${TAG}_py.txt 2>&1
            rc=$?; tail -20 gpurun_out/${TAG}_py.txt | tee -a "$S" ;;
+    sh)    TAG=${TAG}_sh timeout -k 10 900 bash ${arg//,/ } > gpurun_out/${TAG}_sh.txt 2>&1
+           rc=$?; tail -20 gpurun_out/${TAG}_sh.txt | tee -a "$S" ;;
     *)     echo "unknown step $step" | tee -a "$S"; exit 2 ;;
   esac
   [ $rc -eq 0 ] || { echo "step $step failed rc=$rc" | tee -a "$S"; exit $rc; }
