@@ -904,270 +904,6 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
   if constexpr (DT) dtc.flush(s);
 }
 
-// ---- ApproxCountDistinct of a UTF8 column: the strings compacted before they are hashed (round 5) ----------------
-// utf8_range hashes the rows of a 64-row group in lock-step: a NULL row costs as much as a string, and every
-// exec-masked round (the second stripe round, the 4-byte round, the byte rounds) runs whenever any lane of the
-// group needs it -- 121.8 VALU per row for C5's 8..24-byte strings, of which ~35 hashed nothing.  Here the
-// selected short strings of each 64-row group are first pushed, as (byte offset, length), into one of two
-// per-wave streams in LDS by their stripe-round count -- A: len < 16 (one round; none below 8), B: len >= 16
-// (two rounds, a 24..28-byte string's third deferred as in utf8_range) -- at the cost of one compare and an
-// mbcnt per stream (NULL rows are never pushed).  Every full group of 64 stream entries is then hashed with
-// all lanes live and its stripe rounds unconditional; its 32-byte windows are loaded one group ahead.  The
-// streams keep row order, so a group's windows still come from a few consecutive kilobytes of string bytes.
-// Strings longer than 28 bytes or whose window crosses the chunk's end take the general loop after the block,
-// as in utf8_range.
-constexpr int kStrCap = 256;  // per-wave stream entries (offset, len): A from the bottom, B from the top (<= 2 x 63 + 128)
-
-template <typename OffT>
-__device__ void utf8_hll_compact(const uint8_t* data, const OffT* offsets, const uint32_t* validity,
-                                 const uint32_t* mask, int64_t row0, int64_t row1, int64_t n_rows, ColStats& s,
-                                 int32_t* regs, const uint64_t* p5, uint32_t* dq, uint2* st) {
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (row0 >= row1) return;
-  constexpr int W = (int)sizeof(OffT);
-  constexpr int64_t kSpan = 0x7FFFFF00;  // a buffer resource's byte range (32-bit offsets)
-  const auto bp = [p5](uint32_t b) { return p5[b]; };
-  int64_t cnt_w = 0;
-  uint32_t qtail = 0;       // deferred 24..28-byte strings in dq[.][0, qtail)
-  uint32_t ta = 0, tb = 0;  // stream A entries st[0, ta), stream B entries st[kStrCap - tb, kStrCap)
-
-  // finish deferred strings [0, n): third stripe round, tail, HLL register max
-  auto drain = [&](uint32_t n) __attribute__((always_inline)) {
-    if ((uint32_t)lane < n) {
-      const uint64_t h = ((uint64_t)dq[1 * kDefCap + lane] << 32) | dq[0 * kDefCap + lane];
-      const uint64_t k1 = ((uint64_t)dq[3 * kDefCap + lane] << 32) | dq[2 * kDefCap + lane];
-      const uint64_t b = xxh64_tail_head(xxh64_stripe_round(h, k1), (uint64_t)dq[4 * kDefCap + lane],
-                                         dq[5 * kDefCap + lane], bp);
-      const HllKey key = hll_key_from_fmix(b);
-      if (key.q >= 0) atomicMax(reinterpret_cast<int32_t*>(reinterpret_cast<char*>(regs) + key.addr), key.q);
-      else hll_update(regs, fmix_tail(b));
-    }
-  };
-  auto drain_full = [&]() __attribute__((always_inline)) {
-    drain(64u);
-    const uint32_t rest = qtail - 64u;
-    if ((uint32_t)lane < rest) {
-      uint32_t v[kDefFields];
-#pragma unroll
-      for (int f = 0; f < kDefFields; ++f) v[f] = dq[f * kDefCap + 64 + lane];
-#pragma unroll
-      for (int f = 0; f < kDefFields; ++f) dq[f * kDefCap + lane] = v[f];
-    }
-    qtail = rest;
-  };
-
-  // int32 offsets address the chunk's bytes directly (a UTF8 chunk holds < 2 GiB: one sub-range); int64
-  // offsets run in sub-ranges of whole 2048-row iterations whose bytes fit a buffer resource, relative to the
-  // sub-range's first string.  The streams are emptied at each sub-range's end.
-  for (int64_t sr0 = row0, sr1; sr0 < row1; sr0 = sr1) {
-    const int64_t lo = W == 4 ? 0 : ((int64_t)offsets[sr0] & ~int64_t(3));
-    sr1 = row1;
-    if (W == 8 && (int64_t)offsets[sr1] - lo >= kSpan) {  // the largest fitting multiple of 2048 rows
-      int64_t a = 1, b = (row1 - sr0 + kRowsPerIter - 1) / kRowsPerIter;  // iterations: a fits (or is the minimum)
-      while (b - a > 1) {
-        const int64_t c = (a + b) / 2;
-        if ((int64_t)offsets[sr0 + c * kRowsPerIter] - lo < kSpan) a = c;
-        else b = c;
-      }
-      sr1 = sr0 + a * kRowsPerIter < row1 ? sr0 + a * kRowsPerIter : row1;
-    }
-    // the window: the chunk's bytes from lo to the chunk's end (a 32-byte window may read past sr1's bytes); a
-    // string whose window leaves it takes the general loop
-    const int64_t span_all = (int64_t)offsets[n_rows] - lo;
-    const int32_t span = (int32_t)(span_all < kSpan ? span_all : kSpan);
-    const __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(data + lo), (short)0, span, 0x00020000);
-    const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<OffT*>(offsets + sr0), (short)0, (int)((sr1 - sr0 + 1) * W), 0x00020000);
-    const int32_t win3 = (span - 32) | 3;  // the window at rel & ~3 lies in the resource iff rel <= win3
-    const bool wins_in = (int64_t)offsets[sr1 - 1] - lo <= (int64_t)win3;  // (offsets only grow)
-    // offsets of 4 row groups ahead in a register ring (as utf8_range)
-    constexpr int kOffRing = 4;
-    OffT ra[kOffRing], rb[kOffRing];
-    auto lane_off = [&](int64_t blk) -> int32_t { return (int32_t)((blk + (int64_t)wave * 512 - sr0 + lane) * W); };
-    auto load_offsets = [&](int32_t vo, int j) {
-      const int q = j & (kOffRing - 1);
-      if constexpr (W == 4) {
-        ra[q] = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(orsrc, vo + j * 256, 0, 0);
-        rb[q] = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(orsrc, vo + j * 256 + 4, 0, 0);
-      } else {
-        const auto a0 = __builtin_amdgcn_raw_buffer_load_b64(orsrc, vo + j * 512, 0, 0);
-        const auto a1 = __builtin_amdgcn_raw_buffer_load_b64(orsrc, vo + j * 512 + 8, 0, 0);
-        ra[q] = (int64_t)(((uint64_t)a0[1] << 32) | a0[0]);
-        rb[q] = (int64_t)(((uint64_t)a1[1] << 32) | a1[0]);
-      }
-    };
-    auto rel_of = [&](int j) -> uint32_t {  // (int64 offsets: saturated, so a huge iteration's strings stay slow)
-      const int64_t d = (int64_t)ra[j & (kOffRing - 1)] - lo;
-      return W == 4 ? (uint32_t)d : (d > 0x7FFFFFFF ? 0x7FFFFFFFu : (uint32_t)d);
-    };
-    auto len_of = [&](int j) -> uint32_t {
-      const int q = j & (kOffRing - 1);
-      const int64_t l = (int64_t)rb[q] - (int64_t)ra[q];
-      return W == 4 ? (uint32_t)l : (l > 28 ? 29u : (uint32_t)l);
-    };
-    int32_t vo_cur = lane_off(sr0);
-#pragma unroll
-    for (int j = 0; j < kOffRing; ++j) load_offsets(vo_cur, j);
-    // one group of stream entries (rel, len) per lane, its 32-byte window (wa, wc), `act` = live lanes; B: the
-    // group holds 16..28-byte strings (two stripe rounds, the third deferred), else 0..15-byte ones
-    auto hash_group = [&](auto kB, uint32_t rel, uint32_t len, u32x4 wa, u32x4 wc, uint64_t act)
-                          __attribute__((always_inline)) {
-      constexpr bool B = decltype(kB)::value;
-      const uint32_t d[8] = {wa.x, wa.y, wa.z, wa.w, wc.x, wc.y, wc.z, wc.w};
-      uint32_t wv[8];
-#pragma unroll
-      for (int k = 0; k < 7; ++k) wv[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], rel);  // byte shift = rel & 3
-      wv[7] = d[7];
-      uint64_t h = kSeed + XP5 + (uint64_t)len;
-      uint64_t d4p;
-      if constexpr (B) {  // len >= 16: two rounds for every lane
-        h = xxh64_stripe_round(h, ((uint64_t)wv[1] << 32) | wv[0]);
-        h = xxh64_stripe_round(h, ((uint64_t)wv[3] << 32) | wv[2]);
-        d4p = ((uint64_t)wv[5] << 32) | wv[4];
-      } else {  // len < 16: one round unless len < 8
-        d4p = ((uint64_t)wv[1] << 32) | wv[0];
-        if (len >= 8u) {
-          h = xxh64_stripe_round<true>(h, d4p);
-          d4p = ((uint64_t)wv[3] << 32) | wv[2];
-        }
-      }
-      uint64_t dm = 0;
-      if constexpr (B) {
-        dm = act & __builtin_amdgcn_ballot_w64(len >= 24u);  // needs the third round: deferred
-        if (dm != 0) {
-          const uint32_t pos = qtail + __builtin_amdgcn_mbcnt_hi((uint32_t)(dm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dm, 0u));
-          if (lane_bit(dm)) {
-            dq[0 * kDefCap + pos] = (uint32_t)h;
-            dq[1 * kDefCap + pos] = (uint32_t)(h >> 32);
-            dq[2 * kDefCap + pos] = (uint32_t)d4p;
-            dq[3 * kDefCap + pos] = (uint32_t)(d4p >> 32);
-            dq[4 * kDefCap + pos] = wv[6];
-            dq[5 * kDefCap + pos] = len;
-          }
-          qtail += (uint32_t)__builtin_popcountll(dm);
-        }
-      }
-      const uint64_t b = xxh64_tail_head(h, d4p, len, bp);
-      const HllKey key = hll_key_from_fmix(b);
-      if (lane_bit(act & ~dm)) {
-        if (key.q >= 0) atomicMax(reinterpret_cast<int32_t*>(reinterpret_cast<char*>(regs) + key.addr), key.q);
-        else hll_update(regs, fmix_tail(b));  // (p = 2^-23: the rank needs the hash's low word)
-      }
-      if constexpr (B) {
-        if (qtail >= 64u) drain_full();
-      }
-    };
-
-    // the pending group: taken from a stream, its windows in flight, hashed when the next group is taken
-    u32x4 pa = {0, 0, 0, 0}, pc = {0, 0, 0, 0};
-    uint32_t prel = 0, plen = 0;
-    uint64_t pact = 0;  // 0: none
-    bool pb = false;
-    auto hash_pending = [&]() __attribute__((always_inline)) {
-      if (pact != 0) {
-        if (pb) hash_group(std::true_type{}, prel, plen, pa, pc, pact);
-        else hash_group(std::false_type{}, prel, plen, pa, pc, pact);
-      }
-    };
-    // take up to 64 entries of stream B (or A) into the pending group (after hashing the previous one): the
-    // entries left move down (one wave's LDS operations run in order)
-    auto take = [&](bool fromB) __attribute__((always_inline)) {
-      const uint32_t t = fromB ? tb : ta;
-      const uint32_t n = t < 64u ? t : 64u;
-      const int32_t at = fromB ? kStrCap - 1 - lane : lane;  // B grows down from the top
-      const uint2 e = st[at];
-      // (up to 127 left: one stream can take every row of two row groups -- two moves, in order)
-#pragma unroll
-      for (uint32_t k = 0; k < 2; ++k) {
-        if (t > 64u * (k + 1) && (uint32_t)lane + 64u * k < t - 64u) {
-          const int32_t d = fromB ? -64 * (int32_t)k : 64 * (int32_t)k;
-          st[at + d] = st[at + d + (fromB ? -64 : 64)];
-        }
-      }
-      if (fromB) tb = t - n;
-      else ta = t - n;
-      const int32_t wofs = (int32_t)(e.x & ~3u);
-      const u32x4 na = __builtin_amdgcn_raw_buffer_load_b128(rsrc, wofs, 0, 0);
-      const u32x4 nc = __builtin_amdgcn_raw_buffer_load_b128(rsrc, wofs + 16, 0, 0);
-      hash_pending();
-      pa = na;
-      pc = nc;
-      prel = e.x;
-      plen = e.y;
-      pact = n == 64u ? ~0ull : ((1ull << n) - 1ull);
-      pb = fromB;
-    };
-
-    const int32_t nr = (int32_t)(sr1 - sr0);  // sub-range-relative rows: 32-bit (scalar) loop control and compares
-    for (int32_t rbk = 0; rbk < nr; rbk += kRowsPerIter) {
-      const int64_t blk = sr0 + rbk;
-      const int64_t base = blk + wave * 512;
-      const int32_t rem = nr - rbk - wave * 512;
-      const bool full = rbk + kRowsPerIter <= nr;
-      const int32_t vo_next = lane_off(blk + kRowsPerIter);
-      uint64_t m[8];
-      block_masks(validity, mask, base, rem, full, m);
-      uint64_t slow = 0;
-#pragma unroll
-      for (int jj = 0; jj < 8; jj += 2) {
-#pragma unroll
-        for (int j = jj; j < jj + 2; ++j) {  // push the selected short strings of row group j
-          cnt_w += __builtin_popcountll(m[j]);
-          uint64_t fastm = __builtin_amdgcn_uicmp(len_of(j), 28u, 37 /* ICMP_ULE */);
-          if (!wins_in) {  // the chunk's last range (or a huge sub-range): the window compare (asm: not hoisted)
-            uint64_t wm;
-            asm volatile("v_cmp_le_i32_e64 %0, %1, %2" : "=s"(wm) : "v"(rel_of(j)), "s"(win3));
-            fastm &= wm;
-          }
-          slow |= m[j] & ~fastm;
-          const uint64_t mf = m[j] & fastm;
-          const uint64_t mb = mf & __builtin_amdgcn_uicmp(len_of(j), 15u, 34 /* ICMP_UGT */);
-          const uint64_t ma = mf & ~mb;
-          const uint2 e = {rel_of(j), len_of(j)};
-          // positions: the lane's rank among the stream's pushing lanes (mbcnt) past the stream's tail (an SGPR
-          // folded into the LDS base, not the mbcnt: one SGPR operand per VALU instruction)
-          uint2* const sa = st + ta;
-          if (lane_bit(ma)) sa[__builtin_amdgcn_mbcnt_hi((uint32_t)(ma >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ma, 0u))] = e;
-          if (lane_bit(mb)) {  // B grows down: address = (its top entry) - 8 rank, one v_mad_i32_i24
-            const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(mb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mb, 0u));
-            const uint32_t top = (uint32_t)(uintptr_t)(st + (kStrCap - 1) - tb);
-            uint32_t addr;
-            asm("v_mad_i32_i24 %0, %1, -8, %2" : "=v"(addr) : "v"(rk), "s"(top));
-            *reinterpret_cast<__attribute__((address_space(3))) uint64_t*>(addr) = ((uint64_t)e.y << 32) | e.x;
-          }
-          ta += (uint32_t)__builtin_popcountll(ma);
-          tb += (uint32_t)__builtin_popcountll(mb);
-          // row j + 4 into the slot row j frees (of the next block for j >= 4)
-          if (j + kOffRing < 8) load_offsets(vo_cur, j + kOffRing);
-          else load_offsets(vo_next, j + kOffRing - 8);
-        }
-        // every full group: two row groups add at most 128 entries, so the streams end below 64 again
-        while (ta >= 64u || tb >= 64u) take(tb >= 64u);
-      }
-      vo_cur = vo_next;
-      // rare: long strings / windows past the chunk's end -- the general hash of exactly those rows
-      if (slow != 0) {
-        block_masks(validity, mask, base, rem, full, m);
-#pragma unroll 1
-        for (int j = 0; j < 8; ++j) {
-          if (lane_bit(m[j])) {
-            const int64_t row = base + j * 64 + lane;
-            const int64_t o0 = (int64_t)offsets[row], o1 = (int64_t)offsets[row + 1];
-            if (o1 - o0 > 28 || o0 - lo > (int64_t)win3) hll_update(regs, xxh64_bytes(data, o0, o1 - o0));
-          }
-        }
-      }
-    }
-    // the last groups: whatever the streams hold, then the pending one
-    while (ta != 0u || tb != 0u) take(tb != 0u);
-    hash_pending();
-  }
-  if (qtail != 0) drain(qtail);
-  if (lane == 0) s.count += cnt_w;
-}
-
 // DataType of a double column: Spark casts the value to a string with Double.toString, which is
 // plain decimal (matches FRACTIONAL) iff the value is finite and zero or 1e-3 <= |x| < 1e7, and
 // otherwise "NaN", "Infinity" or computerized scientific notation ("1.0E7": a STRING).  Counts the
@@ -1216,7 +952,7 @@ __device__ void run_numeric(const ColTask& t, const ScanCols& cols, const ScanBi
 template <int V>
 __device__ __forceinline__ void run_variant(const ColTask& t, const ScanCols& cols, const uint32_t* mask, int64_t row0,
                                             int64_t row1, int64_t n_rows, ColStats& s, int32_t* regs,
-                                            const uint64_t* p5, uint32_t* dq, uint2* st) {
+                                            const uint64_t* p5, uint32_t* dq) {
   const void* v = cols.values[t.col];
   const uint32_t* val = cols.validity[t.col];
   if constexpr (V == CV_VALIDITY) validity_range(val, mask, row0, row1, s);
@@ -1230,18 +966,12 @@ __device__ __forceinline__ void run_variant(const ColTask& t, const ScanCols& co
   else if constexpr (V == CV_I32_SH) numeric_range<CK_I32, true, true>(v, val, mask, row0, row1, s, regs);
   else if constexpr (V == CV_I32_H) numeric_range<CK_I32, false, true>(v, val, mask, row0, row1, s, regs);
   else if constexpr (V == CV_F64_D) f64_dtype_range(reinterpret_cast<const double*>(v), val, mask, row0, row1, s);
-  else if constexpr (V == CV_UTF8_H)
-    utf8_hll_compact<int32_t>(reinterpret_cast<const uint8_t*>(v), reinterpret_cast<const int32_t*>(cols.offsets[t.col]),
-                              val, mask, row0, row1, n_rows, s, regs, p5, dq, st);
-  else if constexpr (V == CV_LUTF8_H)
-    utf8_hll_compact<int64_t>(reinterpret_cast<const uint8_t*>(v), reinterpret_cast<const int64_t*>(cols.offsets[t.col]),
-                              val, mask, row0, row1, n_rows, s, regs, p5, dq, st);
-  else if constexpr (V == CV_UTF8_D || V == CV_UTF8_HD)
-    utf8_range<int32_t, V != CV_UTF8_D, true>(
+  else if constexpr (V == CV_UTF8_H || V == CV_UTF8_D || V == CV_UTF8_HD)
+    utf8_range<int32_t, V != CV_UTF8_D, V != CV_UTF8_H>(
         reinterpret_cast<const uint8_t*>(v), reinterpret_cast<const int32_t*>(cols.offsets[t.col]), val, mask, row0,
         row1, n_rows, s, regs, p5, dq);
   else
-    utf8_range<int64_t, V != CV_LUTF8_D, true>(
+    utf8_range<int64_t, V != CV_LUTF8_D, V != CV_LUTF8_H>(
         reinterpret_cast<const uint8_t*>(v), reinterpret_cast<const int64_t*>(cols.offsets[t.col]), val, mask, row0,
         row1, n_rows, s, regs, p5, dq);
 }
@@ -1257,7 +987,7 @@ __device__ __forceinline__ void run_variant(const ColTask& t, const ScanCols& co
 #define DQ_NUM_WAVES 6
 #endif
 template <int V>
-constexpr int kMinWaves = (V == CV_UTF8_H || V == CV_LUTF8_H) && DQ_STR_WAVES > 0 ? DQ_STR_WAVES
+constexpr int kMinWaves = V == CV_UTF8_H && DQ_STR_WAVES > 0 ? DQ_STR_WAVES
                           : (V == CV_F64_SH || V == CV_I64_SH) && DQ_NUM_WAVES > 0 ? DQ_NUM_WAVES : 1;
 
 template <int V>
@@ -1272,8 +1002,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kMinWave
   __shared__ int32_t regs[kHll ? 512 : 1];  // q = pw - 1, -1 = empty (see hll_q_exact)
   __shared__ uint64_t p5[kStr ? 256 : 1];   // b * P5 for the byte rounds of the string hash
   __shared__ uint32_t dfq[kStr ? kWaves * kDefFields * kDefCap : 1];  // deferred 24..28-byte strings
-  constexpr bool kCompact = V == CV_UTF8_H || V == CV_LUTF8_H;
-  __shared__ uint2 sst[kCompact ? kWaves * kStrCap : 1];                 // the compacted string streams
   __shared__ ColStats red[kWaves];
   const int32_t ti = blockIdx.x % ntasks;
   const int32_t range = blockIdx.x / ntasks;
@@ -1289,9 +1017,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kMinWave
   ColStats s;
   stats_init(s);
   const uint32_t* mask = t.where >= 0 ? reinterpret_cast<const uint32_t*>(bm.where_bits[t.where]) : nullptr;
-  const int32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  run_variant<V>(t, cols, mask, row0, row1, n_rows, s, regs, p5, dfq + (kStr ? wv * kDefFields * kDefCap : 0),
-                 sst + (kCompact ? wv * kStrCap : 0));
+  run_variant<V>(t, cols, mask, row0, row1, n_rows, s, regs, p5,
+                 dfq + (kStr ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * kDefFields * kDefCap : 0));
   block_reduce_store(s, partials + (size_t)(part_base + ti) * kMaxWG + range, red);
   if constexpr (kHll) {
     // registers only grow: merge into the plan accumulator with device-scope atomicMax, skipping

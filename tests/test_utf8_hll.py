@@ -1,11 +1,12 @@
-"""ApproxCountDistinct of string columns through the compacted hash path (dq_kernels.hip utf8_hll_compact).
+"""ApproxCountDistinct of string columns through the lock-step string hash (dq_kernels.hip utf8_range).
 
-The selected strings of <= 28 bytes are pushed into two per-wave streams by stripe-round count (len < 16,
-len >= 16) and hashed in full 64-lane groups; NULL rows are never hashed; longer strings and windows past the
-chunk's end take the general loop; a 2048-row iteration with more than 2^27 string bytes makes its own
-sub-range, whose far strings also take the general loop.  Every case: the 52 HLL words bit-exact against the
-oracle (XXH64 seed 42 over the UTF-8 bytes, StatefulHyperloglogPlus.scala:89-115), for int32 (UTF8) and
-int64 (LARGE_UTF8) offsets.
+Lengths 0..40 around every round boundary of XXH64 (no / one / two / three stripe rounds, the 4-byte and
+byte rounds, the deferred third round of 24..28-byte strings, > 28 bytes in the general loop), NULL rows,
+ragged sizes around the 64-row group and the 2048-row iteration, windows past the chunk's end, and 600 KB
+strings whose 2048-row iteration spans more than a buffer resource.  Every case: the 52 HLL words bit-exact
+against the oracle (XXH64 seed 42 over the UTF-8 bytes, StatefulHyperloglogPlus.scala:89-115), for int32
+(UTF8) and int64 (LARGE_UTF8) offsets.  (Round 5 measured a compacted-stream variant of this pass against these
+same cases; DESIGN.md section 7 records why it was not kept.)
 """
 from __future__ import annotations
 
@@ -67,9 +68,9 @@ def test_every_length(dq, n, large):
 
 
 @pytest.mark.parametrize("lo,hi", [(0, 7), (8, 15), (16, 23), (24, 28), (16, 28), (8, 24), (29, 40)])
-def test_one_stream_only(dq, lo, hi):
-    """Every string in one stream (A: < 16 bytes, B: >= 16, the 24..28-byte ones deferred), or none of them
-    (> 28 bytes: the general loop only)."""
+def test_one_length_band(dq, lo, hi):
+    """One band of lengths per column: one stripe round, two, the deferred third, or none of them (> 28
+    bytes: the general loop only)."""
     rng = np.random.default_rng(lo * 100 + hi)
     n = 40_000
     vals = _strings(rng, n, rng.integers(lo, hi + 1, n), 0.05, distinct=30_000)
@@ -97,9 +98,8 @@ def test_strings_at_the_chunk_end(dq, large):
 
 @pytest.mark.parametrize("large", [False, True])
 def test_huge_iteration_subranges(dq, large):
-    """Every 8th row holds a 600 KB string: a 2048-row iteration spans ~150 MB > 2^27 bytes, so the range is
-    cut into sub-ranges (one iteration each) and the short strings past 2^27 bytes of their sub-range take the
-    general loop with the big ones."""
+    """Every 8th row holds a 600 KB string: a 2048-row iteration spans ~150 MB of string bytes, so short
+    strings far from their range's first byte take the general loop with the big ones."""
     import xxhash
 
     rng = np.random.default_rng(5)
