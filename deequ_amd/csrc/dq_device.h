@@ -21,8 +21,8 @@ constexpr int kRowsPerIter = kBlock * kRowsPerLane;  // 2048 rows per workgroup 
 constexpr int kMaxWG = 4096;                // max row ranges (workgroups) per task per scan
 constexpr int kTargetWGs = 8192;            // column/pair launch: aim for ~32 workgroups per CU
 constexpr int kMaxCols = 64;                // columns one plan reads (ScanCols); more: dq_plan_create splits
-constexpr int kMaxColTasks = 256;
-constexpr int kMaxSchemaCols = 1 << 16;     // columns of one dq_plan_create call (split over plans of kMaxCols)           // column tasks of one plan
+constexpr int kMaxColTasks = 256;           // column tasks of one plan
+constexpr int kMaxSchemaCols = 1 << 16;     // columns of one dq_plan_create call (split over plans of kMaxCols)
 constexpr int kMaxWhere = 8;
 constexpr int kHllCopies = 8;             // accumulator copies per HLL column (spreads the merge atomics)
 constexpr int kPredAccCopies = 16;        // predicate-counter accumulator copies (compiled pass: one per blockIdx % 16)
