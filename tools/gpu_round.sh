@@ -35,8 +35,8 @@ for step in "$@"; do
            rc=$?; tail -c 600 gpurun_out/${TAG}_bench.json | tee -a "$S"; echo >> "$S" ;;
     prof)  timeout -k 10 1100 bash tools/profile_round.sh "$TAG" > gpurun_out/${TAG}_prof.txt 2>&1
            rc=$?; tail -5 gpurun_out/${TAG}_prof.txt | tee -a "$S" ;;
-    pmc5)  timeout -k 10 600 bash tools/pmc_c5.sh "${TAG}_pmc5" > gpurun_out/${TAG}_pmc5.txt 2>&1
-           rc=$?; tail -30 gpurun_out/${TAG}_pmc5.txt | tee -a "$S" ;;
+    pmc5)  timeout -k 10 600 bash tools/pmc_c5.sh "${TAG}_pmc5" > gpurun_out/${TAG}_pmc5.out 2>&1
+           rc=$?; tail -30 gpurun_out/${TAG}_pmc5.out | tee -a "$S" ;;
     clock) timeout -k 10 400 bash tools/clock_probe.sh "${TAG}_clock" > gpurun_out/${TAG}_clock.txt 2>&1
            rc=$?; tail -10 gpurun_out/${TAG}_clock.txt | tee -a "$S" ;;
     parity) timeout -k 10 1000 python -u tests/fullscale_parity.py ${arg:+--cfg ${arg//,/ }} \
