@@ -49,9 +49,12 @@ enum ColVariant : int32_t {
 constexpr int kNumVariants = 17;
 
 // per-variant row-range counts of one scan (dq_finalize merges nr[i] partials for tasks [first, end))
+// column-task ranges whose range count differs from the scan's default (string passes, the validity pass, a
+// predicate pass's fused HLL tasks): at most one entry per launch group of a scan
+constexpr int kMaxFinRanges = 2 * kNumVariants + 1;
 struct FinRanges {
   int32_t n;
-  int32_t first[kNumVariants], end[kNumVariants], nr[kNumVariants];
+  int32_t first[kMaxFinRanges], end[kMaxFinRanges], nr[kMaxFinRanges];
 };
 
 struct ColTask {

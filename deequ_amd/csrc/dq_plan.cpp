@@ -30,6 +30,18 @@
 #include "dq_pred_jit.h"
 
 // predicate-pass workgroups per chunk (A/B builds: -DDQ_PRED_WGS=...)
+// rows per range at least this many: below it a launch's time goes to dispatching workgroups and to their
+// fixed work (shift search, reductions, partial records), not to the rows -- a 10 M-row chunk (C1) otherwise
+// ran 4-12 K workgroups of 2-4 K rows; every chunk of >= 16 K x 8192 rows is unaffected
+#ifndef DQ_MIN_RANGE_ROWS
+#define DQ_MIN_RANGE_ROWS 16384
+#endif
+// the validity-only pass (Completeness of a column): 8 KB of bitmap per 64 K rows, so its floor is higher (C1,
+// 10 M rows: validity 21 -> 9-11 us, i64 moments 41 -> 31 us, finalize 13 -> 9 us; 256 K measured the same,
+// profiles/r5_ab.txt r5i / r5j)
+#ifndef DQ_MIN_VALIDITY_RANGE_ROWS
+#define DQ_MIN_VALIDITY_RANGE_ROWS 65536
+#endif
 #ifndef DQ_PRED_WGS
 #define DQ_PRED_WGS 2048
 #endif
@@ -477,6 +489,8 @@ struct dq_plan {
   PairTask* d_pair_tasks = nullptr;
   PairWG* d_pair_wgs = nullptr;
   int32_t* d_pair_redo = nullptr;         // [pair_wgs][kPairWaves][kMaxWG] ranges left to the checked fold
+  char* h_stage = nullptr;                // pinned host copy of the accumulators (dq_finish: truly async D2H)
+  size_t h_stage_bytes = 0;
   PredProgram* d_prog = nullptr;
   ColPartial* d_col_part = nullptr;
   CorrPartial* d_pair_part = nullptr;
@@ -563,6 +577,9 @@ static dq_status free_plan_mem(dq_plan* p) {
   for (int i = 0; i < kMaxWhere; ++i)
     if (p->d_where_bits[i]) (void)hipFree(p->d_where_bits[i]);
   if (p->d_ones) (void)hipFree(p->d_ones);
+  if (p->h_stage) (void)hipHostFree(p->h_stage);
+  p->h_stage = nullptr;
+  p->h_stage_bytes = 0;
   return DQ_OK;
 }
 
@@ -1542,45 +1559,54 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
   }
   const int64_t want = std::max<int64_t>(64, std::min<int64_t>(kMaxWG, kTargetWGs / std::max<int64_t>(1, min_launch)));
   // rows per range and range count for `want` ranges
-  auto size_ranges = [&](int64_t w, int64_t& rpr, int32_t& nr) {
+  auto size_ranges = [&](int64_t w, int64_t& rpr, int32_t& nr, int64_t min_rows) {
+    w = std::min<int64_t>(w, std::max<int64_t>(1, n_rows / min_rows));
     nr = (int32_t)std::min<int64_t>(w, ceil_div(n_rows, kRowsPerIter));
     rpr = ceil_div(ceil_div(n_rows, nr), kRowsPerIter) * kRowsPerIter;
     nr = (int32_t)ceil_div(n_rows, rpr);
   };
   int32_t nr_col;
   int64_t rpr_col;
-  size_ranges(want, rpr_col, nr_col);
+  size_ranges(want, rpr_col, nr_col, DQ_MIN_RANGE_ROWS);
   // per-variant workgroup counts: the string hash balances better with twice the ranges (uneven string
   // lengths, deferred-round drains): utf8_hll 1.979 -> 1.949 ms per 125 M x 4 on the C5 headline (x3 1.963,
   // x4 1.965 ms); halving the fp64 hash's ranges measured no change
   auto variant_scale = [](int32_t v) -> int32_t {
     return v == CV_UTF8_H || v == CV_LUTF8_H || v == CV_UTF8_HD || v == CV_LUTF8_HD ? 2 : 1;
   };
+  auto variant_min_rows = [](int32_t v) -> int64_t {
+    return v == CV_VALIDITY ? DQ_MIN_VALIDITY_RANGE_ROWS : DQ_MIN_RANGE_ROWS;
+  };
   FinRanges fr{};
   std::vector<std::pair<int64_t, int32_t>> vr(groups.size());  // (rows per range, ranges) per variant group
   for (size_t gi = 0; gi < groups.size(); ++gi) {
     const auto& g = groups[gi];
     const int32_t sc_v = variant_scale(g.variant);
-    if (sc_v == 1) {
+    const int64_t min_rows = variant_min_rows(g.variant);
+    if (sc_v == 1 && min_rows == DQ_MIN_RANGE_ROWS) {
       vr[gi] = {rpr_col, nr_col};
       continue;
     }
-    size_ranges(std::max<int64_t>(64, std::min<int64_t>(kMaxWG, want * sc_v)), vr[gi].first, vr[gi].second);
-    if (fr.n < kNumVariants) {
-      fr.first[fr.n] = g.first;
-      fr.end[fr.n] = g.first + g.count;
-      fr.nr[fr.n] = vr[gi].second;
-      ++fr.n;
+    size_ranges(std::max<int64_t>(64, std::min<int64_t>(kMaxWG, want * sc_v)), vr[gi].first, vr[gi].second, min_rows);
+    if (vr[gi].second == nr_col && vr[gi].first == rpr_col) continue;  // the default ranges after all
+    if (fr.n >= kMaxFinRanges - 1) {  // (cannot happen: one entry per group) the default ranges
+      vr[gi] = {rpr_col, nr_col};
+      continue;
     }
+    fr.first[fr.n] = g.first;
+    fr.end[fr.n] = g.first + g.count;
+    fr.nr[fr.n] = vr[gi].second;
+    ++fr.n;
   }
   // predicate pass: ~2048 workgroups of whole 2048-row iterations (HBM-bound; counters leave by atomics;
   // 1024-16384 workgroups measured within 2 % on C3)
-  int32_t nr_pred = (int32_t)std::min<int64_t>(DQ_PRED_WGS, ceil_div(n_rows, kRowsPerIter));
+  int32_t nr_pred = (int32_t)std::min<int64_t>(
+      DQ_PRED_WGS, std::min<int64_t>(ceil_div(n_rows, kRowsPerIter), std::max<int64_t>(1, n_rows / DQ_MIN_RANGE_ROWS)));
   int64_t rpr_pred = ceil_div(ceil_div(n_rows, nr_pred), kRowsPerIter) * kRowsPerIter;
   nr_pred = (int32_t)ceil_div(n_rows, rpr_pred);
 
   // HLL tasks hashed by the compiled predicate pass: one partial per predicate-pass range
-  if (p->pred_jit && p->pred_fused_count > 0 && fr.n < kNumVariants) {
+  if (p->pred_jit && p->pred_fused_count > 0) {  // (fr has room: the loop above leaves one entry)
     fr.first[fr.n] = p->pred_fused_first;
     fr.end[fr.n] = p->pred_fused_first + p->pred_fused_count;
     fr.nr[fr.n] = nr_pred;
@@ -1667,15 +1693,28 @@ dq_status dq_finish(dq_plan* p, dq_state* out) {
   std::vector<uint32_t> hll((size_t)p->n_hll * kHllCopies * 512);
   std::vector<CorrPartial> pair(p->pair_tasks.size());
   PredPartial pred{};
-  if (!col.empty()) HIP_TRY(hipMemcpyAsync(col.data(), p->d_col_acc, col.size() * sizeof(ColPartial), hipMemcpyDeviceToHost, p->stream));
-  if (!hll.empty())
-    HIP_TRY(hipMemcpyAsync(hll.data(), p->d_hll_acc, hll.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, p->stream));
-  if (!pair.empty()) HIP_TRY(hipMemcpyAsync(pair.data(), p->d_pair_acc, pair.size() * sizeof(CorrPartial), hipMemcpyDeviceToHost, p->stream));
   std::vector<PredPartial> pred_copies(p->has_pred ? kPredAccCopies : 0);
-  if (p->has_pred)
-    HIP_TRY(hipMemcpyAsync(pred_copies.data(), p->d_pred_acc, kPredAccCopies * sizeof(PredPartial), hipMemcpyDeviceToHost,
-                           p->stream));
+  // the accumulators come back through one pinned staging buffer (copies to pageable memory are staged and
+  // synchronous inside the runtime: 3-4 of them were ~10 us each of a 10 M-row scan's ~0.13 ms)
+  const size_t b_col = col.size() * sizeof(ColPartial), b_hll = hll.size() * sizeof(uint32_t),
+               b_pair = pair.size() * sizeof(CorrPartial), b_pred = pred_copies.size() * sizeof(PredPartial);
+  const size_t o_hll = b_col, o_pair = o_hll + b_hll, o_pred = o_pair + b_pair, b_all = o_pred + b_pred;
+  if (b_all > p->h_stage_bytes) {
+    if (p->h_stage) (void)hipHostFree(p->h_stage);
+    p->h_stage = nullptr;
+    p->h_stage_bytes = 0;
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&p->h_stage), b_all, hipHostMallocDefault));
+    p->h_stage_bytes = b_all;
+  }
+  if (b_col) HIP_TRY(hipMemcpyAsync(p->h_stage, p->d_col_acc, b_col, hipMemcpyDeviceToHost, p->stream));
+  if (b_hll) HIP_TRY(hipMemcpyAsync(p->h_stage + o_hll, p->d_hll_acc, b_hll, hipMemcpyDeviceToHost, p->stream));
+  if (b_pair) HIP_TRY(hipMemcpyAsync(p->h_stage + o_pair, p->d_pair_acc, b_pair, hipMemcpyDeviceToHost, p->stream));
+  if (b_pred) HIP_TRY(hipMemcpyAsync(p->h_stage + o_pred, p->d_pred_acc, b_pred, hipMemcpyDeviceToHost, p->stream));
   HIP_TRY(hipStreamSynchronize(p->stream));
+  if (b_col) std::memcpy(col.data(), p->h_stage, b_col);
+  if (b_hll) std::memcpy(hll.data(), p->h_stage + o_hll, b_hll);
+  if (b_pair) std::memcpy(pair.data(), p->h_stage + o_pair, b_pair);
+  if (b_pred) std::memcpy(pred_copies.data(), p->h_stage + o_pred, b_pred);
   for (const PredPartial& c : pred_copies)  // integer sums: the order of the copies does not matter
     for (int k = 0; k < kMaxCounters; ++k) {
       pred.t[k] += c.t[k];
