@@ -140,9 +140,10 @@ def test_kat_states_match_oracle(dq, kats):
 
 
 # ---------------------------------------------------------------------------------------------
-# 2. randomised single-column parity vs the C oracle, edge sizes around the 2048-row block
+# 2. randomised single-column parity vs the C oracle, edge sizes around the 2048-row block and the
+#    rows-per-range floors of small chunks (16 K rows; 64 K for the validity-only pass: dq_plan.cpp)
 # ---------------------------------------------------------------------------------------------
-SIZES = [0, 1, 7, 63, 64, 65, 2047, 2048, 2049, 4097, 100_003]
+SIZES = [0, 1, 7, 63, 64, 65, 2047, 2048, 2049, 4097, 16_383, 16_385, 65_537, 100_003]
 
 
 def _rand_table(dq, n, seed, null_frac):

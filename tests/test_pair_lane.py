@@ -116,7 +116,7 @@ def _check(dq, cols, states, analyzers, n, where_mask):
             assert got.metricValue() == s.max or (math.isnan(got.metricValue()) and math.isnan(s.max)), (a, got, s.max)
 
 
-@pytest.mark.parametrize("n", [0, 1, 63, 64, 65, 127, 128, 129, 255, 256, 257, 511, 2047, 2049, 100_003])
+@pytest.mark.parametrize("n", [0, 1, 63, 64, 65, 127, 128, 129, 255, 256, 257, 511, 2047, 2049, 16_385, 100_003])
 @pytest.mark.parametrize("where", [None, "w > 2"])
 def test_pair_pass_vs_oracle(dq, n, where):
     from deequ_amd.runner import scan_states
