@@ -311,7 +311,9 @@ dq_status dq_plan_set_stream(dq_plan* plan, void* hip_stream);
 /* Scan one chunk of rows (asynchronous on the plan's stream).  chunk_index must increase by one
  * per call starting at 0: chunk results are merged in that order, so results are deterministic. */
 dq_status dq_scan(dq_plan* plan, const dq_column_view* cols, int64_t n_rows, int64_t chunk_index);
-/* Synchronise and write one dq_state per spec (caller-allocated, n_specs entries). */
+/* Synchronise and write one dq_state per spec (caller-allocated, n_specs entries).  The plan's device
+ * accumulators come back through a small pinned host buffer the plan allocates on its first finish
+ * (hipHostMalloc; freed by dq_plan_destroy). */
 dq_status dq_finish(dq_plan* plan, dq_state* out_states);
 /* Forget all scanned chunks (keeps allocations). */
 dq_status dq_plan_reset(dq_plan* plan);
