@@ -54,6 +54,16 @@ def _where12():
     return out
 
 
+def _corr_wide(schema):
+    """Correlations over 75 numeric columns (f64 / i64 / i32 neighbours) with their Means: > 64 columns, so the
+    pair groups land in several plans; each Correlation's two columns stay in one plan."""
+    out = []
+    for k in range(0, 100, 4):
+        a, b, c = f"c{k}", f"c{k + 1}", f"c{k + 2}"
+        out += [dq.Correlation(a, b), dq.Correlation(b, c), dq.Correlation(c, a), dq.Mean(a), dq.StandardDeviation(b)]
+    return out
+
+
 def _parts(text):
     m = re.search(r": (\d+) fused plans", text)
     return int(m.group(1)) if m else 1
@@ -70,11 +80,11 @@ def _part_columns(text):
 # ---------------------------------------------------------------------------------------------------------
 # host-only: the split dq_plan_create performs, as dq_plan_explain reports it
 # ---------------------------------------------------------------------------------------------------------
-@pytest.mark.parametrize("case", ["profile100", "compliance40", "where12"])
+@pytest.mark.parametrize("case", ["profile100", "compliance40", "where12", "corr100"])
 def test_split_explain(case):
-    schema = _wide_schema(100 if case == "profile100" else 36)
+    schema = _wide_schema(36 if case in ("compliance40", "where12") else 100)
     analyzers = {"profile100": _profile, "compliance40": lambda s: _compliance40(),
-                 "where12": lambda s: _where12()}[case](schema)
+                 "where12": lambda s: _where12(), "corr100": _corr_wide}[case](schema)
     text = explain(analyzers, schema)
     assert _parts(text) >= 2, text[:400]
     members = _part_members(text)
@@ -163,11 +173,13 @@ def _spec(a):
         return ("Size", a.where)
     if name == "Compliance":
         return ("Compliance", a.instance, a.predicate, a.where)
+    if name == "Correlation":
+        return ("Correlation", a.firstColumn, a.secondColumn, a.where)
     return (name, a.column, a.where)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["profile100", "compliance40", "where12"])
+@pytest.mark.parametrize("case", ["profile100", "compliance40", "where12", "corr100"])
 def test_split_states_vs_oracle(case):
     import torch
 
@@ -176,11 +188,11 @@ def test_split_states_vs_oracle(case):
     from tests.test_gpu_parity import assert_state_close
     from deequ_amd.runner import ScanPlan, scan_states
 
-    n = 6000 if case == "profile100" else 20011
-    data = _wide_data(100 if case == "profile100" else 36, n, seed=len(case))
+    n = 6000 if case in ("profile100", "corr100") else 20011
+    data = _wide_data(36 if case in ("compliance40", "where12") else 100, n, seed=len(case))
     t = _table(data, 0, n)
     analyzers = {"profile100": _profile, "compliance40": lambda s: _compliance40(),
-                 "where12": lambda s: _where12()}[case](t.schema)
+                 "where12": lambda s: _where12(), "corr100": _corr_wide}[case](t.schema)
     plan = ScanPlan(analyzers, t.schema)
     try:
         assert plan.num_launches() > 0
