@@ -1703,18 +1703,29 @@ dq_status dq_finish(dq_plan* p, dq_state* out) {
     if (p->h_stage) (void)hipHostFree(p->h_stage);
     p->h_stage = nullptr;
     p->h_stage_bytes = 0;
-    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&p->h_stage), b_all, hipHostMallocDefault));
-    p->h_stage_bytes = b_all;
+    if (hipHostMalloc(reinterpret_cast<void**>(&p->h_stage), b_all, hipHostMallocDefault) == hipSuccess) {
+      p->h_stage_bytes = b_all;
+    } else {  // no pinned memory left: the copies go straight to the pageable vectors below
+      (void)hipGetLastError();
+      p->h_stage = nullptr;
+    }
   }
-  if (b_col) HIP_TRY(hipMemcpyAsync(p->h_stage, p->d_col_acc, b_col, hipMemcpyDeviceToHost, p->stream));
-  if (b_hll) HIP_TRY(hipMemcpyAsync(p->h_stage + o_hll, p->d_hll_acc, b_hll, hipMemcpyDeviceToHost, p->stream));
-  if (b_pair) HIP_TRY(hipMemcpyAsync(p->h_stage + o_pair, p->d_pair_acc, b_pair, hipMemcpyDeviceToHost, p->stream));
-  if (b_pred) HIP_TRY(hipMemcpyAsync(p->h_stage + o_pred, p->d_pred_acc, b_pred, hipMemcpyDeviceToHost, p->stream));
+  char* const hs = p->h_stage;
+  void* const dst_col = hs ? (void*)hs : (void*)col.data();
+  void* const dst_hll = hs ? (void*)(hs + o_hll) : (void*)hll.data();
+  void* const dst_pair = hs ? (void*)(hs + o_pair) : (void*)pair.data();
+  void* const dst_pred = hs ? (void*)(hs + o_pred) : (void*)pred_copies.data();
+  if (b_col) HIP_TRY(hipMemcpyAsync(dst_col, p->d_col_acc, b_col, hipMemcpyDeviceToHost, p->stream));
+  if (b_hll) HIP_TRY(hipMemcpyAsync(dst_hll, p->d_hll_acc, b_hll, hipMemcpyDeviceToHost, p->stream));
+  if (b_pair) HIP_TRY(hipMemcpyAsync(dst_pair, p->d_pair_acc, b_pair, hipMemcpyDeviceToHost, p->stream));
+  if (b_pred) HIP_TRY(hipMemcpyAsync(dst_pred, p->d_pred_acc, b_pred, hipMemcpyDeviceToHost, p->stream));
   HIP_TRY(hipStreamSynchronize(p->stream));
-  if (b_col) std::memcpy(col.data(), p->h_stage, b_col);
-  if (b_hll) std::memcpy(hll.data(), p->h_stage + o_hll, b_hll);
-  if (b_pair) std::memcpy(pair.data(), p->h_stage + o_pair, b_pair);
-  if (b_pred) std::memcpy(pred_copies.data(), p->h_stage + o_pred, b_pred);
+  if (hs) {
+    if (b_col) std::memcpy(col.data(), hs, b_col);
+    if (b_hll) std::memcpy(hll.data(), hs + o_hll, b_hll);
+    if (b_pair) std::memcpy(pair.data(), hs + o_pair, b_pair);
+    if (b_pred) std::memcpy(pred_copies.data(), hs + o_pred, b_pred);
+  }
   for (const PredPartial& c : pred_copies)  // integer sums: the order of the copies does not matter
     for (int k = 0; k < kMaxCounters; ++k) {
       pred.t[k] += c.t[k];
