@@ -825,6 +825,25 @@ __global__ __launch_bounds__(64 * kPairWaves) void dq_pair_redo(const PairWG* __
                                              true);
 }
 
+// workgroups of the pair pass one CU holds at once (the occupancy API for the launch the flags select)
+hipError_t pair_scan_residency(bool all_f64, bool ring, bool minmax, int32_t* per_cu) {
+  int nb = 0;
+  hipError_t e;
+  const int threads = 64 * kPairWaves;
+  if (all_f64 && ring) {
+    e = minmax ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, dq_pair_scan<true, true, true>, threads, 0)
+               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, dq_pair_scan<true, false, true>, threads, 0);
+  } else if (all_f64) {
+    e = minmax ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, dq_pair_scan<true, true, false>, threads, 0)
+               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, dq_pair_scan<true, false, false>, threads, 0);
+  } else {
+    e = minmax ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, dq_pair_scan<false, true, false>, threads, 0)
+               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, dq_pair_scan<false, false, false>, threads, 0);
+  }
+  *per_cu = nb;
+  return e;
+}
+
 hipError_t launch_pair_scan(const PairWG* wgs, int32_t nwg, const ScanCols& cols, const ScanBitmaps& bm,
                             const uint32_t* ones, int64_t n_rows, int64_t rows_per_range, int32_t nranges,
                             CorrPartial* pair_part, ColPartial* col_part, int32_t* redo, bool all_f64, bool ring,

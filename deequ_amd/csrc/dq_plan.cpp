@@ -45,6 +45,9 @@
 #ifndef DQ_F64_HLL_DIV
 #define DQ_F64_HLL_DIV 2  // fp64 stats+HLL / HLL launches: ranges / 2 (see variant_div in dq_scan)
 #endif
+#ifndef DQ_PAIR_ONE_ROUND
+#define DQ_PAIR_ONE_ROUND 1  // Correlation pass sized to one resident round (0: the column passes' ranges; A/B builds)
+#endif
 #ifndef DQ_PRED_WGS
 #define DQ_PRED_WGS 2048
 #endif
@@ -62,6 +65,7 @@ hipError_t launch_pair_scan(const PairWG* wgs, int32_t nwg, const ScanCols& cols
                             const uint32_t* ones, int64_t n_rows, int64_t rows_per_range, int32_t nranges,
                             CorrPartial* pair_part, ColPartial* col_part, int32_t* redo, bool all_f64, bool ring,
                             bool minmax, hipStream_t st);
+hipError_t pair_scan_residency(bool all_f64, bool ring, bool minmax, int32_t* per_cu);
 hipError_t launch_finalize(int32_t ncol, int32_t nranges_col, const ColPartial* col_part, ColPartial* col_acc,
                            int32_t npair, int32_t nranges_pair, const CorrPartial* pair_part, CorrPartial* pair_acc,
                            int32_t has_pred, int32_t nranges_pred, const PredPartial* pred_part, PredPartial* pred_acc, const FinRanges& fr,
@@ -480,6 +484,8 @@ struct dq_plan {
   std::vector<int32_t> pred_jit_cols;                   // its slots' plan columns
   std::vector<int32_t> pred_jit_hll_task, pred_jit_hll_slot;  // fused HLL tasks (post-sort index) / accumulators
   int32_t pred_fused_first = 0, pred_fused_count = 0;  // those tasks sort last (after the pair-fused ones)
+  int32_t pair_fused_first = 0, pair_fused_count = 0;  // moments tasks the pair pass computes
+  int32_t pair_resident[2] = {0, 0};  // pair-pass workgroups the device holds at once (ring / not), 0 = not asked
   std::string pred_jit_note;                            // why the interpreter runs, or the kernel's origin
   int32_t pred_pass = DQ_PRED_PASS_AUTO;                // dq_plan_options.pred_pass
   bool host_only = false;                               // dq_plan_explain: lower on the host, no device work
@@ -1042,6 +1048,8 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
     for (int32_t& t : p->pred_jit_hll_task) t = new_index[t];
     p->pred_fused_count = (int32_t)std::count(fused.begin(), fused.end(), 2);
     p->pred_fused_first = (int32_t)p->col_tasks.size() - p->pred_fused_count;
+    p->pair_fused_count = (int32_t)std::count(fused.begin(), fused.end(), 1);
+    p->pair_fused_first = p->pred_fused_first - p->pair_fused_count;
     for (int32_t k = 0; k < (int32_t)p->col_tasks.size(); ++k) {
       if (fused[order[k]]) break;  // fused tasks sort last: their partials come from the pair / predicate pass
       if (p->groups.empty() || p->groups.back().variant != p->col_tasks[k].variant)
@@ -1596,7 +1604,7 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
     }
     size_ranges(std::max<int64_t>(64, std::min<int64_t>(kMaxWG, want * sc_v / div_v)), vr[gi].first, vr[gi].second, min_rows);
     if (vr[gi].second == nr_col && vr[gi].first == rpr_col) continue;  // the default ranges after all
-    if (fr.n >= kMaxFinRanges - 1) {  // (cannot happen: one entry per group) the default ranges
+    if (fr.n >= kMaxFinRanges - 2) {  // (cannot happen: one entry per group) the default ranges
       vr[gi] = {rpr_col, nr_col};
       continue;
     }
@@ -1612,8 +1620,44 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
   int64_t rpr_pred = ceil_div(ceil_div(n_rows, nr_pred), kRowsPerIter) * kRowsPerIter;
   nr_pred = (int32_t)ceil_div(n_rows, rpr_pred);
 
+  // the Correlation pass: one resident round -- as many ranges as leave every workgroup of the launch resident
+  // at once (the occupancy API x CUs / pair workgroups).  Each workgroup ends with a heavy epilogue (the
+  // butterfly sums of 70 accumulators per wave, a counts pass over the range's bitmaps), so the fewer,
+  // longer ranges win -- but only while the launch fills the chip in one round: C4 (one pair group, 4
+  // workgroups per CU) 1.523-1.528 ms per 125 M rows at 4096 ranges, 1.434-1.435 at 1024, 1.97 at 1365
+  // (a partial second round), 2.28 at 512 (half the CUs' slots idle) -- profiles/r5_ab.txt r5t / r5u / r5w.
+  // (The column passes, whose epilogue is light, measured slower at one round: fp64 hash 1.42 -> 1.50-1.51,
+  // int64 0.79 -> 0.82-0.83, strings 1.94 -> 2.20 ms, r5w.)  Its fused moments tasks' partials follow its
+  // range count.
+  const bool pair_ring = [&] {
+    if (p->pair_wgs.empty() || !p->pair_all_f64) return false;
+    for (const PairWG& wg : p->pair_wgs)
+      for (const PairWaveTask& t : wg.wave)
+        for (int c = 0; c < kPairPos; ++c)
+          if (((uintptr_t)sc.values[t.cols[c]] & 15u) != 0) return false;
+    return true;
+  }();
+  int64_t rpr_pair = rpr_col;
+  int32_t nr_pair = nr_col;
+  if (!p->pair_wgs.empty() && DQ_PAIR_ONE_ROUND) {
+    int32_t& res = p->pair_resident[pair_ring ? 1 : 0];
+    if (res == 0) {
+      int32_t per_cu = 0, cus = 0;
+      HIP_TRY(pair_scan_residency(p->pair_all_f64, pair_ring, p->pair_minmax, &per_cu));
+      HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, p->device));
+      res = std::max<int32_t>(1, per_cu * cus);
+    }
+    const int64_t per_round = std::max<int64_t>(1, res / (int64_t)p->pair_wgs.size());
+    size_ranges(std::min<int64_t>(kMaxWG, per_round), rpr_pair, nr_pair, DQ_MIN_RANGE_ROWS);
+    if (nr_pair != nr_col && p->pair_fused_count > 0) {
+      fr.first[fr.n] = p->pair_fused_first;
+      fr.end[fr.n] = p->pair_fused_first + p->pair_fused_count;
+      fr.nr[fr.n] = nr_pair;
+      ++fr.n;
+    }
+  }
   // HLL tasks hashed by the compiled predicate pass: one partial per predicate-pass range
-  if (p->pred_jit && p->pred_fused_count > 0) {  // (fr has room: the loop above leaves one entry)
+  if (p->pred_jit && p->pred_fused_count > 0) {  // (fr has room: the loop above leaves two entries)
     fr.first[fr.n] = p->pred_fused_first;
     fr.end[fr.n] = p->pred_fused_first + p->pred_fused_count;
     fr.nr[fr.n] = nr_pred;
@@ -1660,21 +1704,18 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
       return s;
   }
   if (!p->pair_wgs.empty()) {
-    // the LDS-ring path's 16-byte DMA needs 16-byte aligned fp64 columns (dq_scan's contract; checked here)
-    bool ring = p->pair_all_f64;
-    for (const PairWG& wg : p->pair_wgs)
-      for (const PairWaveTask& t : wg.wave)
-        for (int c = 0; c < kPairPos && ring; ++c) ring = ((uintptr_t)sc.values[t.cols[c]] & 15u) == 0;
+    // the LDS-ring path's 16-byte DMA needs 16-byte aligned fp64 columns (dq_scan's contract; checked above)
+    const bool ring = pair_ring;
     if (dq_status s = timed(p, 2, p->stream, [&] {
-          return launch_pair_scan(p->d_pair_wgs, (int32_t)p->pair_wgs.size(), sc, bm, p->d_ones, n_rows, rpr_col,
-                                  nr_col, p->d_pair_part, p->d_col_part, p->d_pair_redo, p->pair_all_f64, ring,
+          return launch_pair_scan(p->d_pair_wgs, (int32_t)p->pair_wgs.size(), sc, bm, p->d_ones, n_rows, rpr_pair,
+                                  nr_pair, p->d_pair_part, p->d_col_part, p->d_pair_redo, p->pair_all_f64, ring,
                                   p->pair_minmax, p->stream);
         }))
       return s;
   }
   if (dq_status s = timed(p, 3, p->stream, [&] {
         return launch_finalize((int32_t)p->col_tasks.size(), nr_col, p->d_col_part, p->d_col_acc,
-                               (int32_t)p->pair_tasks.size(), nr_col, p->d_pair_part, p->d_pair_acc,
+                               (int32_t)p->pair_tasks.size(), nr_pair, p->d_pair_part, p->d_pair_acc,
                                0 /* the predicate pass accumulates itself */, nr_pred, p->d_pred_part, p->d_pred_acc,
                                fr, p->stream);
       }))

@@ -1,13 +1,14 @@
 #!/bin/bash
 # A/B of builds on one BASELINE config (diagnostic): optional GPU tests with TEST_LIB (pytest -k TEST_K over
-# TEST_FILES), then the config's bench line (CFG, default c4) for each library given, in the order given.
+# TEST_FILES, comma-separated), then the config's bench line (CFG, default c4) for each library given, in order.
 # Stops at the first failure.  Usage (GPU box): TEST_LIB=build_variants/libX.so bash tools/ab_cfg.sh old.so new.so old.so new.so
 set -u
+TEST_FILES=${TEST_FILES:-tests}  # comma-separated
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 mkdir -p gpurun_out
 TAG=${TAG:-abcfg}
 if [ -n "${TEST_LIB:-}" ]; then
-  DQ_LIB_PATH=$TEST_LIB timeout -k 10 600 python -u -m pytest ${TEST_FILES:-tests} -m gpu -x -q --timeout 300 \
+  DQ_LIB_PATH=$TEST_LIB timeout -k 10 600 python -u -m pytest ${TEST_FILES//,/ } -m gpu -x -q --timeout 300 \
     --timeout-method thread -p no:cacheprovider ${TEST_K:+-k "$TEST_K"} > gpurun_out/${TAG}_pytest.log 2>&1
   rc=$?; tail -3 gpurun_out/${TAG}_pytest.log; [ $rc -eq 0 ] || exit $rc
 fi
