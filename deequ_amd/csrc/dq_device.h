@@ -196,6 +196,7 @@ struct ScanCols {
 
 struct ScanBitmaps {
   uint64_t* where_bits[kMaxWhere];
+  int64_t* rare_rows;  // per column task: the rows the string pass's fast path skipped since the reset
 };
 
 }  // namespace dq

@@ -220,4 +220,52 @@ DQ_HD uint64_t xxh64_short_head_split(const uint32_t (&w)[8], uint32_t len, BP b
   return xxh64_tail_head(h, ((uint64_t)w[7] << 32) | w[6], len, bp);
 }
 
+// The rounds after a long string's 32-byte stripes, or all of a short string's: with h = the merged stripe
+// state (or seed + P5) + len, the min(3, r >> 3) 8-byte rounds, the 4-byte and byte rounds of the r < 32
+// bytes t[0..7] (bytes past r: anything), up to fmix_head.
+template <typename BP>
+DQ_HD uint64_t xxh64_rem_head(uint64_t h, const uint32_t (&t)[8], uint32_t r, BP bp) {
+  const uint32_t nw = r >> 3;
+  uint64_t d4p = ((uint64_t)t[1] << 32) | t[0];
+  for (uint32_t k = 0; k < 3; ++k) {
+    if (k < nw) {
+      h = xxh64_stripe_round(h, ((uint64_t)t[2 * k + 1] << 32) | t[2 * k]);
+      d4p = ((uint64_t)t[2 * k + 3] << 32) | t[2 * k + 2];
+    }
+  }
+  return xxh64_tail_head(h, d4p, r, bp);
+}
+
+// One 32-byte stripe w[0..7] into the four accumulators (XXH64's long-input loop)
+DQ_HD void xxh64_stripe32(uint64_t (&v)[4], const uint32_t* w) {
+  for (int k = 0; k < 4; ++k)
+    v[k] = mul_c(rotl64(v[k] + mul_c(((uint64_t)w[2 * k + 1] << 32) | w[2 * k], XP2), 31), XP1);
+}
+DQ_HD uint64_t xxh64_merge4(const uint64_t (&v)[4]) {
+  uint64_t h = rotl64(v[0], 1) + rotl64(v[1], 7) + rotl64(v[2], 12) + rotl64(v[3], 18);
+  for (int k = 0; k < 4; ++k) h = mul_add_c(h ^ mul_c(rotl64(mul_c(v[k], XP2), 31), XP1), XP1, XP4);
+  return h;
+}
+constexpr uint64_t kXxhV0 = kSeed + XP1 + XP2, kXxhV1 = kSeed + XP2, kXxhV2 = kSeed, kXxhV3 = kSeed - XP1;
+
+// XXH64.hashUnsafeBytes of a string of len <= 63 bytes up to fmix_head, from its bytes as little-endian dwords
+// w[0..15] (bytes past len: anything): when len >= 32, one stripe and the merge; then the remainder.  The host
+// check of the formulation the UTF8 kernel's rare path runs (dq_kernels.hip xxh64_window_head, which loops the
+// stripes for any length).
+template <typename BP>
+DQ_HD uint64_t xxh64_upto63_head(const uint32_t (&w)[16], uint32_t len, BP bp) {
+  uint64_t h = kSeed + XP5;
+  uint32_t t[8];
+  for (int k = 0; k < 8; ++k) t[k] = w[k];
+  uint32_t r = len;
+  if (len >= 32) {
+    uint64_t v[4] = {kXxhV0, kXxhV1, kXxhV2, kXxhV3};
+    xxh64_stripe32(v, w);
+    h = xxh64_merge4(v);
+    for (int k = 0; k < 8; ++k) t[k] = w[8 + k];
+    r = len - 32;
+  }
+  return xxh64_rem_head(h + (uint64_t)len, t, r, bp);
+}
+
 }  // namespace dq

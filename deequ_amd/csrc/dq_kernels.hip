@@ -695,10 +695,46 @@ constexpr int kStrAhead = DQ_STR_AHEAD;  // string windows in flight ahead of th
 constexpr uint32_t kDefCap = 128;  // < 64 left after a drain + <= 64 pushed per row group
 constexpr int kDefFields = 6;      // h lo, h hi, w4, w5, w6, len
 
-template <typename OffT, bool HLL, bool DT>
+// 32 bytes from byte `pos` of a window resource as little-endian dwords: three 16-byte loads from pos & ~3,
+// realigned with v_alignbyte
+__device__ __forceinline__ void load_bytes32(__amdgpu_buffer_rsrc_t rsrc, uint32_t pos, uint32_t (&w)[8]) {
+  const int32_t a0 = (int32_t)(pos & ~3u);
+  const u32x4 q0 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, a0, 0, 0);
+  const u32x4 q1 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, a0 + 16, 0, 0);
+  const u32x4 q2 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, a0 + 32, 0, 0);
+  const uint32_t d[9] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x};
+#pragma unroll
+  for (int k = 0; k < 8; ++k) w[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], pos);
+}
+
+// XXH64.hashUnsafeBytes (up to fmix_head) of the n bytes at byte `rel` of a window resource, for the LONG string
+// pass's rare path: 32-byte stripes from 16-byte loads (a lane leaves the loop after its last stripe), the merge,
+// then the remainder's rounds (dq_hash.h xxh64_rem_head; xxh64_upto63_head is the same formulation on the host).
+// Every load lies below ((rel + (n & ~31)) & ~3) + 48, which the caller keeps inside the resource.
+template <typename BP>
+__device__ uint64_t xxh64_window_head(__amdgpu_buffer_rsrc_t rsrc, uint32_t rel, uint32_t n, BP bp) {
+  uint64_t h = kSeed + XP5;
+  uint32_t pos = rel;
+  if (n >= 32) {
+    uint64_t v[4] = {kXxhV0, kXxhV1, kXxhV2, kXxhV3};
+    const uint32_t end = rel + (n & ~31u);
+    do {
+      uint32_t w[8];
+      load_bytes32(rsrc, pos, w);
+      xxh64_stripe32(v, w);
+      pos += 32;
+    } while (pos < end);
+    h = xxh64_merge4(v);
+  }
+  uint32_t t[8];
+  load_bytes32(rsrc, pos, t);
+  return xxh64_rem_head(h + (uint64_t)n, t, n & 31u, bp);
+}
+
+template <typename OffT, bool HLL, bool DT, bool LONG>
 __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint32_t* validity,
                            const uint32_t* mask, int64_t row0, int64_t row1, int64_t n_rows, ColStats& s,
-                           int32_t* regs, const uint64_t* p5, uint32_t* dq) {
+                           int32_t* regs, const uint64_t* p5, uint32_t* dq, uint32_t* rare) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (row0 >= row1) return;
@@ -879,8 +915,43 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
     vo_cur = vo_next;
     // rare: long / window-crossing strings, or a rank that needs the hash's low word (2^-23).  The
     // HLL update is idempotent, so the block's selected rows are simply redone; DataType counts only
-    // the rows the fast path skipped.
+    // the rows the fast path skipped.  The LONG instantiation (chosen by dq_scan for columns whose
+    // earlier chunks had many such rows) redoes only those rows, and every row of a lane whose fast-path
+    // rank needed the low word, from 16-byte loads (xxh64_window_head; the byte-addressed loop only for the
+    // last strings of the chunk, whose loads would leave the chunk's bytes).
     if ((slow | __builtin_amdgcn_ballot_w64(qmin < 0)) != 0) {
+      // the rows the fast path skipped, counted in the wave's LDS slot (no register across the block loop)
+      if (lane == 0) atomicAdd(rare, (uint32_t)__builtin_popcountll(slow));
+      if constexpr (LONG) {
+        const bool redo_all = qmin < 0;
+        block_masks(validity, mask, base, rem, full, m);
+#pragma unroll 1
+        for (int j = 0; j < 8; ++j) {
+          if (lane_bit(m[j])) {
+            const int64_t row = base + j * 64 + lane;
+            const int64_t o0 = (int64_t)offsets[row], o1 = (int64_t)offsets[row + 1];
+            const int64_t rel = o0 - lo, n = o1 - o0;
+            const bool was_fast = n <= 28 && rel <= (int64_t)win3;
+            if constexpr (HLL) {
+              if (!was_fast || redo_all) {
+                if (win >= 0 && (((rel + (n & ~int64_t(31))) & ~int64_t(3)) + 48 <= (int64_t)win + 32)) {
+                  const uint64_t b = xxh64_window_head(rsrc, (uint32_t)rel, (uint32_t)n, bp);
+                  const HllKey key = hll_key_from_fmix(b);
+                  if (key.q >= 0) atomicMax(reinterpret_cast<int32_t*>(reinterpret_cast<char*>(regs) + key.addr), key.q);
+                  else hll_update(regs, fmix_tail(b));
+                } else {
+                  hll_update(regs, xxh64_bytes(data, o0, n));
+                }
+              }
+            }
+            if constexpr (DT) {
+              if (!was_fast) dtc.add(dt_class_bytes(data + o0, n), true);
+            }
+          }
+        }
+        qmin = 0;
+        continue;
+      }
       block_masks(validity, mask, base, rem, full, m);
 #pragma unroll 1
       for (int j = 0; j < 8; ++j) {
@@ -949,10 +1020,10 @@ __device__ void run_numeric(const ColTask& t, const ScanCols& cols, const ScanBi
 // each launch carries only its own inner loop (small I-cache footprint); the tasks of one variant
 // share a launch, interleaved task-fastest: workgroup b -> task b % ntasks, row range b / ntasks.
 // ------------------------------------------------------------------------------------------
-template <int V>
+template <int V, bool LONG>
 __device__ __forceinline__ void run_variant(const ColTask& t, const ScanCols& cols, const uint32_t* mask, int64_t row0,
                                             int64_t row1, int64_t n_rows, ColStats& s, int32_t* regs,
-                                            const uint64_t* p5, uint32_t* dq) {
+                                            const uint64_t* p5, uint32_t* dq, uint32_t* rare) {
   const void* v = cols.values[t.col];
   const uint32_t* val = cols.validity[t.col];
   if constexpr (V == CV_VALIDITY) validity_range(val, mask, row0, row1, s);
@@ -967,13 +1038,13 @@ __device__ __forceinline__ void run_variant(const ColTask& t, const ScanCols& co
   else if constexpr (V == CV_I32_H) numeric_range<CK_I32, false, true>(v, val, mask, row0, row1, s, regs);
   else if constexpr (V == CV_F64_D) f64_dtype_range(reinterpret_cast<const double*>(v), val, mask, row0, row1, s);
   else if constexpr (V == CV_UTF8_H || V == CV_UTF8_D || V == CV_UTF8_HD)
-    utf8_range<int32_t, V != CV_UTF8_D, V != CV_UTF8_H>(
+    utf8_range<int32_t, V != CV_UTF8_D, V != CV_UTF8_H, LONG>(
         reinterpret_cast<const uint8_t*>(v), reinterpret_cast<const int32_t*>(cols.offsets[t.col]), val, mask, row0,
-        row1, n_rows, s, regs, p5, dq);
+        row1, n_rows, s, regs, p5, dq, rare);
   else
-    utf8_range<int64_t, V != CV_LUTF8_D, V != CV_LUTF8_H>(
+    utf8_range<int64_t, V != CV_LUTF8_D, V != CV_LUTF8_H, LONG>(
         reinterpret_cast<const uint8_t*>(v), reinterpret_cast<const int64_t*>(cols.offsets[t.col]), val, mask, row0,
-        row1, n_rows, s, regs, p5, dq);
+        row1, n_rows, s, regs, p5, dq, rare);
 }
 
 // Minimum waves per SIMD the register allocator must leave room for (0 = no constraint); a
@@ -986,12 +1057,15 @@ __device__ __forceinline__ void run_variant(const ColTask& t, const ScanCols& co
 #ifndef DQ_NUM_WAVES
 #define DQ_NUM_WAVES 6
 #endif
-template <int V>
+template <int V, bool LONG>
 constexpr int kMinWaves = V == CV_UTF8_H && DQ_STR_WAVES > 0 ? DQ_STR_WAVES
-                          : (V == CV_F64_SH || V == CV_I64_SH) && DQ_NUM_WAVES > 0 ? DQ_NUM_WAVES : 1;
+                          : (V == CV_F64_SH || V == CV_I64_SH) && DQ_NUM_WAVES > 0 ? DQ_NUM_WAVES
+                          : V == CV_LUTF8_H && LONG ? 5  // (the register window would otherwise cost a wave)
+                                                    : 1;
 
-template <int V>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kMinWaves<V>))) void dq_column_scan(const ColTask* __restrict__ tasks, int32_t ntasks,
+// LONG: the string variants' rare path for columns of long strings (utf8_range)
+template <int V, bool LONG = false>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kMinWaves<V, LONG>))) void dq_column_scan(const ColTask* __restrict__ tasks, int32_t ntasks,
                                                          int32_t part_base, ScanCols cols, ScanBitmaps bm,
                                                          int64_t n_rows, int64_t rows_per_range,
                                                          ColPartial* __restrict__ partials,
@@ -1002,6 +1076,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kMinWave
   __shared__ int32_t regs[kHll ? 512 : 1];  // q = pw - 1, -1 = empty (see hll_q_exact)
   __shared__ uint64_t p5[kStr ? 256 : 1];   // b * P5 for the byte rounds of the string hash
   __shared__ uint32_t dfq[kStr ? kWaves * kDefFields * kDefCap : 1];  // deferred 24..28-byte strings
+  __shared__ uint32_t rare[kStr ? kWaves : 1];  // per wave: the rows the string fast path skipped
   __shared__ ColStats red[kWaves];
   const int32_t ti = blockIdx.x % ntasks;
   const int32_t range = blockIdx.x / ntasks;
@@ -1011,15 +1086,26 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kMinWave
   if (row1 > n_rows) row1 = n_rows;
   if constexpr (kHll) {
     for (int i = threadIdx.x; i < 512; i += kBlock) regs[i] = -1;
-    if constexpr (kStr) p5[threadIdx.x] = (uint64_t)threadIdx.x * XP5;
+    if constexpr (kStr) {
+      p5[threadIdx.x] = (uint64_t)threadIdx.x * XP5;
+      if (threadIdx.x < kWaves) rare[threadIdx.x] = 0;
+    }
     __syncthreads();
   }
   ColStats s;
   stats_init(s);
   const uint32_t* mask = t.where >= 0 ? reinterpret_cast<const uint32_t*>(bm.where_bits[t.where]) : nullptr;
-  run_variant<V>(t, cols, mask, row0, row1, n_rows, s, regs, p5,
-                 dfq + (kStr ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * kDefFields * kDefCap : 0));
+  const int32_t wv = kStr ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0;
+  run_variant<V, LONG>(t, cols, mask, row0, row1, n_rows, s, regs, p5, dfq + wv * kDefFields * kDefCap, rare + wv);
   block_reduce_store(s, partials + (size_t)(part_base + ti) * kMaxWG + range, red);
+  if constexpr (kStr) {
+    // the task's rare-path rows for dq_scan's choice of variant (finalize publishes them to the host)
+    if (threadIdx.x == 0 && bm.rare_rows) {
+      uint32_t r = 0;
+      for (int w = 0; w < kWaves; ++w) r += rare[w];
+      if (r) atomicAdd(reinterpret_cast<unsigned long long*>(bm.rare_rows + part_base + ti), (unsigned long long)r);
+    }
+  }
   if constexpr (kHll) {
     // registers only grow: merge into the plan accumulator with device-scope atomicMax, skipping
     // registers the (possibly stale) accumulator already covers -- max is order-free, so the
@@ -1584,7 +1670,8 @@ __global__ __launch_bounds__(kBlock) void dq_finalize(int32_t ncol, int32_t nran
                                                       const CorrPartial* __restrict__ pair_part,
                                                       CorrPartial* __restrict__ pair_acc, int32_t has_pred,
                                                       int32_t nranges_pred, const PredPartial* __restrict__ pred_part,
-                                                      PredPartial* __restrict__ pred_acc, FinRanges fr) {
+                                                      PredPartial* __restrict__ pred_acc, FinRanges fr,
+                                                      int64_t* __restrict__ rare_dev, int64_t* rare_host) {
   __shared__ ColStats cs[kBlock];
   __shared__ CorrStats ps[kBlock];
   const int b = blockIdx.x, tid = threadIdx.x;
@@ -1605,6 +1692,13 @@ __global__ __launch_bounds__(kBlock) void dq_finalize(int32_t ncol, int32_t nran
       ColStats acc = stats_load(col_acc + b);
       stats_merge(acc, cs[0]);
       stats_store(col_acc + b, acc);
+      // the task's rare-path rows since the reset, to the host (mapped pinned memory; dq_scan reads it
+      // without waiting, to choose the string pass's variant for the next chunks)
+      // (only a changed count crosses PCIe: rare_dev[ncol + b] is the value last published)
+      if (rare_host && rare_dev[b] != rare_dev[ncol + b]) {
+        rare_dev[ncol + b] = rare_dev[b];
+        __hip_atomic_store(rare_host + b, rare_dev[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
     }
   } else if (b < ncol + npair) {
     const int p = b - ncol;
@@ -1646,12 +1740,13 @@ __global__ __launch_bounds__(kBlock) void dq_finalize(int32_t ncol, int32_t nran
   }
 }
 
-__global__ void dq_init_acc(ColPartial* col_acc, int32_t ncol, CorrPartial* pair_acc, int32_t npair) {
+__global__ void dq_init_acc(ColPartial* col_acc, int32_t ncol, CorrPartial* pair_acc, int32_t npair, int64_t* rare_dev) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < ncol) {
     ColStats s;
     stats_init(s);
     stats_store(col_acc + i, s);
+    if (rare_dev) rare_dev[i] = 0;
   }
   if (i < npair) {
     CorrPartial& q = pair_acc[i];
@@ -1677,7 +1772,15 @@ hipError_t launch_pred_scan(const PredProgram* prog, const ScanCols& cols, const
 template <int V>
 static void launch_v(const ColTask* tasks, int32_t ntasks, int32_t part_base, const ScanCols& cols,
                      const ScanBitmaps& bm, int64_t n_rows, int64_t rows_per_range, int32_t nranges,
-                     ColPartial* partials, uint32_t* hll_acc, hipStream_t st) {
+                     ColPartial* partials, uint32_t* hll_acc, bool long_str, hipStream_t st) {
+  constexpr bool kStrHll = V == CV_UTF8_H || V == CV_LUTF8_H || V == CV_UTF8_HD || V == CV_LUTF8_HD;
+  if constexpr (kStrHll) {
+    if (long_str) {
+      hipLaunchKernelGGL((dq_column_scan<V, true>), dim3((uint32_t)ntasks * (uint32_t)nranges), dim3(kBlock), 0, st,
+                         tasks, ntasks, part_base, cols, bm, n_rows, rows_per_range, partials, hll_acc);
+      return;
+    }
+  }
   hipLaunchKernelGGL(dq_column_scan<V>, dim3((uint32_t)ntasks * (uint32_t)nranges), dim3(kBlock), 0, st, tasks, ntasks,
                      part_base, cols, bm, n_rows, rows_per_range, partials, hll_acc);
 }
@@ -1685,9 +1788,12 @@ static void launch_v(const ColTask* tasks, int32_t ntasks, int32_t part_base, co
 // tasks [first, first + ntasks) of the plan's task table all have variant `variant`
 hipError_t launch_column_scan(int32_t variant, const ColTask* tasks, int32_t ntasks, int32_t part_base,
                               const ScanCols& cols, const ScanBitmaps& bm, int64_t n_rows, int64_t rows_per_range,
-                              int32_t nranges, ColPartial* partials, uint32_t* hll_acc, hipStream_t st) {
-#define DQ_V(V)                                                                                             \
-  case V: launch_v<V>(tasks, ntasks, part_base, cols, bm, n_rows, rows_per_range, nranges, partials, hll_acc, st); break;
+                              int32_t nranges, ColPartial* partials, uint32_t* hll_acc, bool long_str, hipStream_t st) {
+#define DQ_V(V)                                                                                            \
+  case V:                                                                                                  \
+    launch_v<V>(tasks, ntasks, part_base, cols, bm, n_rows, rows_per_range, nranges, partials, hll_acc, long_str, \
+                st);                                                                                       \
+    break;
   switch (variant) {
     DQ_V(CV_VALIDITY) DQ_V(CV_F64_S) DQ_V(CV_F64_SH) DQ_V(CV_F64_H) DQ_V(CV_I64_S) DQ_V(CV_I64_SH) DQ_V(CV_I64_H)
     DQ_V(CV_I32_S) DQ_V(CV_I32_SH) DQ_V(CV_I32_H) DQ_V(CV_UTF8_H) DQ_V(CV_LUTF8_H)
@@ -1702,18 +1808,20 @@ hipError_t launch_column_scan(int32_t variant, const ColTask* tasks, int32_t nta
 hipError_t launch_finalize(int32_t ncol, int32_t nranges_col, const ColPartial* col_part, ColPartial* col_acc,
                            int32_t npair, int32_t nranges_pair, const CorrPartial* pair_part, CorrPartial* pair_acc,
                            int32_t has_pred, int32_t nranges_pred, const PredPartial* pred_part, PredPartial* pred_acc,
-                           const FinRanges& fr, hipStream_t st) {
+                           const FinRanges& fr, int64_t* rare_dev, int64_t* rare_host, hipStream_t st) {
   const uint32_t nb = (uint32_t)(ncol + npair + (has_pred ? 1 : 0));
   if (nb == 0) return hipSuccess;
   hipLaunchKernelGGL(dq_finalize, dim3(nb), dim3(kBlock), 0, st, ncol, nranges_col, col_part, col_acc, npair,
-                     nranges_pair, pair_part, pair_acc, has_pred, nranges_pred, pred_part, pred_acc, fr);
+                     nranges_pair, pair_part, pair_acc, has_pred, nranges_pred, pred_part, pred_acc, fr, rare_dev,
+                     rare_host);
   return hipGetLastError();
 }
 
-hipError_t launch_init_acc(ColPartial* col_acc, int32_t ncol, CorrPartial* pair_acc, int32_t npair, hipStream_t st) {
+hipError_t launch_init_acc(ColPartial* col_acc, int32_t ncol, CorrPartial* pair_acc, int32_t npair, int64_t* rare_dev,
+                           hipStream_t st) {
   const int n = ncol > npair ? ncol : npair;
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(dq_init_acc, dim3((n + 255) / 256), dim3(256), 0, st, col_acc, ncol, pair_acc, npair);
+  hipLaunchKernelGGL(dq_init_acc, dim3((n + 255) / 256), dim3(256), 0, st, col_acc, ncol, pair_acc, npair, rare_dev);
   return hipGetLastError();
 }
 

@@ -60,7 +60,7 @@ hipError_t launch_pred_scan(const PredProgram* prog, const ScanCols& cols, const
                             bool has_regex);
 hipError_t launch_column_scan(int32_t variant, const ColTask* tasks, int32_t ntasks, int32_t part_base,
                               const ScanCols& cols, const ScanBitmaps& bm, int64_t n_rows, int64_t rows_per_range,
-                              int32_t nranges, ColPartial* partials, uint32_t* hll_acc, hipStream_t st);
+                              int32_t nranges, ColPartial* partials, uint32_t* hll_acc, bool long_str, hipStream_t st);
 hipError_t launch_pair_scan(const PairWG* wgs, int32_t nwg, const ScanCols& cols, const ScanBitmaps& bm,
                             const uint32_t* ones, int64_t n_rows, int64_t rows_per_range, int32_t nranges,
                             CorrPartial* pair_part, ColPartial* col_part, int32_t* redo, bool all_f64, bool ring,
@@ -68,9 +68,10 @@ hipError_t launch_pair_scan(const PairWG* wgs, int32_t nwg, const ScanCols& cols
 hipError_t pair_scan_residency(bool all_f64, bool ring, bool minmax, int32_t* per_cu);
 hipError_t launch_finalize(int32_t ncol, int32_t nranges_col, const ColPartial* col_part, ColPartial* col_acc,
                            int32_t npair, int32_t nranges_pair, const CorrPartial* pair_part, CorrPartial* pair_acc,
-                           int32_t has_pred, int32_t nranges_pred, const PredPartial* pred_part, PredPartial* pred_acc, const FinRanges& fr,
+                           int32_t has_pred, int32_t nranges_pred, const PredPartial* pred_part, PredPartial* pred_acc, const FinRanges& fr, int64_t* rare_dev, int64_t* rare_host,
                            hipStream_t st);
-hipError_t launch_init_acc(ColPartial* col_acc, int32_t ncol, CorrPartial* pair_acc, int32_t npair, hipStream_t st);
+hipError_t launch_init_acc(ColPartial* col_acc, int32_t ncol, CorrPartial* pair_acc, int32_t npair, int64_t* rare_dev,
+                           hipStream_t st);
 
 static thread_local char g_err[1024] = "";
 // set with the error when a plan exceeds a fixed per-plan capacity (columns, predicates, counters, `where`
@@ -499,6 +500,17 @@ struct dq_plan {
   PairWG* d_pair_wgs = nullptr;
   int32_t* d_pair_redo = nullptr;         // [pair_wgs][kPairWaves][kMaxWG] ranges left to the checked fold
   char* h_stage = nullptr;                // pinned host copy of the accumulators (dq_finish: truly async D2H)
+  // the string pass's variant per UTF8 HLL task: the string kernels count each task's rare-path rows since the
+  // reset (d_rare_dev), the finalize kernel publishes them into mapped pinned memory (h_rare; d_rare its device
+  // address), dq_scan reads them without waiting and runs the LONG variant for a task group once more than
+  // 1 / 16 of the rows took the rare path
+  int64_t* d_rare_dev = nullptr;
+  int64_t* h_rare = nullptr;
+  int64_t* d_rare = nullptr;
+  std::vector<uint8_t> str_long;  // per column task
+  int32_t str_path = 0;           // DQ_STR_PATH: 0 auto, 1 fast variant only, 2 LONG variant only
+  int64_t prev_rows = 0;          // rows of the scan before the last reset (its counts stay published until
+                                  // this scan's first finalize)
   size_t h_stage_bytes = 0;
   PredProgram* d_prog = nullptr;
   ColPartial* d_col_part = nullptr;
@@ -580,12 +592,15 @@ static dq_status free_plan_mem(dq_plan* p) {
   for (hipEvent_t e : p->ev_pool) (void)hipEventDestroy(e);
   p->ev_pool.clear();
   void* ptrs[] = {p->d_col_tasks, p->d_pair_tasks, p->d_pair_wgs, p->d_prog, p->d_col_part, p->d_pair_part,
-                  p->d_pred_part, p->d_col_acc, p->d_hll_acc, p->d_pair_acc, p->d_pred_acc, p->d_regex, p->d_pair_redo};
+                  p->d_pred_part, p->d_col_acc, p->d_hll_acc, p->d_pair_acc, p->d_pred_acc, p->d_regex, p->d_pair_redo,
+                  p->d_rare_dev};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   for (int i = 0; i < kMaxWhere; ++i)
     if (p->d_where_bits[i]) (void)hipFree(p->d_where_bits[i]);
   if (p->d_ones) (void)hipFree(p->d_ones);
+  if (p->h_rare) (void)hipHostFree(p->h_rare);
+  p->h_rare = p->d_rare = nullptr;
   if (p->h_stage) (void)hipHostFree(p->h_stage);
   p->h_stage = nullptr;
   p->h_stage_bytes = 0;
@@ -594,9 +609,10 @@ static dq_status free_plan_mem(dq_plan* p) {
 
 static dq_status reset_acc(dq_plan* p) {
   HIP_TRY(launch_init_acc(p->d_col_acc, (int32_t)p->col_tasks.size(), p->d_pair_acc, (int32_t)p->pair_tasks.size(),
-                          p->stream));
+                          p->d_rare_dev, p->stream));
   if (p->n_hll) HIP_TRY(hipMemsetAsync(p->d_hll_acc, 0, (size_t)p->n_hll * kHllCopies * 512 * sizeof(uint32_t), p->stream));
   if (p->has_pred) HIP_TRY(hipMemsetAsync(p->d_pred_acc, 0, kPredAccCopies * sizeof(PredPartial), p->stream));
+  if (p->total_rows > 0) p->prev_rows = p->total_rows;
   p->total_rows = 0;
   p->next_chunk = 0;
   return DQ_OK;
@@ -1129,6 +1145,22 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
   if (dq_status s = dmalloc(&p->d_pair_part, npt * kMaxWG * sizeof(CorrPartial))) return s;
   if (dq_status s = dmalloc(&p->d_pred_part, sizeof(PredPartial))) return s;  // unused (kept for the finalize ABI)
   if (dq_status s = dmalloc(&p->d_col_acc, nct * sizeof(ColPartial))) return s;
+  // counters [0, nct) (zeroed by every reset) and the values last published to h_rare [nct, 2 nct)
+  if (dq_status s = dmalloc(&p->d_rare_dev, 2 * nct * sizeof(int64_t))) return s;
+  if (nct) HIP_TRY(hipMemsetAsync(p->d_rare_dev, 0, 2 * nct * sizeof(int64_t), p->stream));
+  p->str_long.assign(nct, 0);
+  if (const char* e = std::getenv("DQ_STR_PATH")) p->str_path = std::strcmp(e, "fast") == 0 ? 1 : std::strcmp(e, "long") == 0 ? 2 : 0;
+  if (nct && hipHostMalloc(reinterpret_cast<void**>(&p->h_rare), nct * sizeof(int64_t), hipHostMallocMapped) == hipSuccess) {
+    std::memset(p->h_rare, 0, nct * sizeof(int64_t));
+    void* dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, p->h_rare, 0) == hipSuccess) {
+      p->d_rare = static_cast<int64_t*>(dp);
+    } else {
+      (void)hipHostFree(p->h_rare);
+      p->h_rare = nullptr;
+    }
+  }
+  (void)hipGetLastError();  // (no mapped memory: the fast variant throughout)
   if (dq_status s = dmalloc(&p->d_hll_acc, (size_t)p->n_hll * kHllCopies * 512 * sizeof(uint32_t))) return s;
   if (dq_status s = dmalloc(&p->d_pair_acc, npt * sizeof(CorrPartial))) return s;
   // (kPredAccCopies copies: the compiled predicate pass spreads its counter atomics over them; the host adds them)
@@ -1548,6 +1580,7 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
   }
   ScanBitmaps bm{};
   for (int b = 0; b < kMaxWhere; ++b) bm.where_bits[b] = p->d_where_bits[b];
+  bm.rare_rows = p->d_rare_dev;
   // all-ones bitmap standing in for a missing validity / where bitmap in the pair pass and the compiled
   // predicate pass
   if ((!p->pair_wgs.empty() || p->pred_jit) && words + 1 > p->ones_cap_words) {
@@ -1695,11 +1728,26 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
         }))
       return s;
   }
+  // the string pass's variant for a task group (see dq_plan::h_rare): the published rare-path rows are since the
+  // reset and may be a chunk behind (read without waiting); the choice only changes speed, never the result
+  auto str_long_of = [&](const dq_plan::Group& g) -> bool {
+    if (g.variant != CV_UTF8_H && g.variant != CV_LUTF8_H && g.variant != CV_UTF8_HD && g.variant != CV_LUTF8_HD)
+      return false;
+    if (p->str_path != 0) return p->str_path == 2;
+    const int64_t rows = p->total_rows > 0 ? p->total_rows : p->prev_rows;
+    bool any = false;
+    for (int32_t t = g.first; t < g.first + g.count; ++t) {
+      if (p->h_rare && rows > 0) p->str_long[t] = __atomic_load_n(p->h_rare + t, __ATOMIC_RELAXED) * 16 > rows;
+      any = any || p->str_long[t];
+    }
+    return any;
+  };
   for (size_t gi = 0; gi < groups.size(); ++gi) {
     const auto& g = groups[gi];
     if (dq_status s = timed(p, 16 + g.variant, p->stream, [&] {
           return launch_column_scan(g.variant, p->d_col_tasks + g.first, g.count, g.first, sc, bm, n_rows,
-                                    vr[gi].first, vr[gi].second, p->d_col_part, p->d_hll_acc, p->stream);
+                                    vr[gi].first, vr[gi].second, p->d_col_part, p->d_hll_acc, str_long_of(g),
+                                    p->stream);
         }))
       return s;
   }
@@ -1717,7 +1765,7 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
         return launch_finalize((int32_t)p->col_tasks.size(), nr_col, p->d_col_part, p->d_col_acc,
                                (int32_t)p->pair_tasks.size(), nr_pair, p->d_pair_part, p->d_pair_acc,
                                0 /* the predicate pass accumulates itself */, nr_pred, p->d_pred_part, p->d_pred_acc,
-                               fr, p->stream);
+                               fr, p->d_rare_dev, p->d_rare, p->stream);
       }))
     return s;
   p->total_rows += n_rows;

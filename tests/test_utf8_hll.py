@@ -1,7 +1,8 @@
 """ApproxCountDistinct of string columns through the lock-step string hash (dq_kernels.hip utf8_range).
 
 Lengths 0..40 around every round boundary of XXH64 (no / one / two / three stripe rounds, the 4-byte and
-byte rounds, the deferred third round of 24..28-byte strings, > 28 bytes in the general loop), NULL rows,
+byte rounds, the deferred third round of 24..28-byte strings, > 28 bytes in the rare path: the 64-byte
+register window up to 63 bytes, the byte-addressed loop beyond), NULL rows,
 ragged sizes around the 64-row group and the 2048-row iteration, windows past the chunk's end, and 600 KB
 strings whose 2048-row iteration spans more than a buffer resource.  Every case: the 52 HLL words bit-exact
 against the oracle (XXH64 seed 42 over the UTF-8 bytes, StatefulHyperloglogPlus.scala:89-115), for int32
@@ -57,9 +58,18 @@ def _strings(rng, n, lens, null_frac, distinct=None):
     return out
 
 
+@pytest.fixture(params=["fast", "long"])
+def str_path(request, monkeypatch):
+    """The string pass's two instantiations (DQ_STR_PATH; dq_scan otherwise picks one from the rare-path rows
+    of the earlier chunks): the rare path redoing the whole block, or only its long rows from a register
+    window."""
+    monkeypatch.setenv("DQ_STR_PATH", request.param)
+    return request.param
+
+
 @pytest.mark.parametrize("large", [False, True])
 @pytest.mark.parametrize("n", [1, 63, 64, 65, 2047, 2049, 70_001])
-def test_every_length(dq, n, large):
+def test_every_length(dq, n, large, str_path):
     """Lengths 0..40 (none / one / two / three stripe rounds, the 4-byte and byte rounds, > 28 bytes) with
     12 % NULLs, ragged sizes around the 64-row group and the 2048-row iteration."""
     rng = np.random.default_rng(n + 7 * large)
@@ -67,14 +77,44 @@ def test_every_length(dq, n, large):
     assert _words(dq, vals, large) == _oracle(vals)
 
 
-@pytest.mark.parametrize("lo,hi", [(0, 7), (8, 15), (16, 23), (24, 28), (16, 28), (8, 24), (29, 40)])
-def test_one_length_band(dq, lo, hi):
+@pytest.mark.parametrize("lo,hi", [(0, 7), (8, 15), (16, 23), (24, 28), (16, 28), (8, 24), (29, 40), (29, 63),
+                                   (32, 48), (16, 48), (48, 63), (0, 140)])
+@pytest.mark.parametrize("large", [False, True])
+def test_one_length_band(dq, lo, hi, large, str_path):
     """One band of lengths per column: one stripe round, two, the deferred third, or none of them (> 28
-    bytes: the general loop only)."""
+    bytes: the rare path -- a 64-byte register window up to 63 bytes, one 32-byte stripe from 32 on, the
+    byte-addressed loop beyond)."""
     rng = np.random.default_rng(lo * 100 + hi)
     n = 40_000
     vals = _strings(rng, n, rng.integers(lo, hi + 1, n), 0.05, distinct=30_000)
-    assert _words(dq, vals, False) == _oracle(vals)
+    assert _words(dq, vals, large) == _oracle(vals)
+
+
+def test_variant_switch_across_chunks(dq, monkeypatch):
+    """Automatic choice (DQ_STR_PATH unset): chunks of short strings, then long ones, then short ones again
+    through one plan -- the string pass changes variant between chunks (from the rare-path rows the finalize
+    publishes) and the registers stay bit-exact against the oracle over all chunks."""
+    import torch
+
+    from deequ_amd.runner import ScanPlan
+    from deequ_amd.table import utf8_column
+
+    monkeypatch.delenv("DQ_STR_PATH", raising=False)
+    rng = np.random.default_rng(21)
+    bands = [(8, 24), (30, 63), (30, 63), (30, 63), (0, 28), (8, 90), (8, 24)]
+    chunks = [_strings(rng, 30_000, rng.integers(lo, hi + 1, 30_000), 0.08, distinct=50_000) for lo, hi in bands]
+    a = dq.ApproxCountDistinct("s")
+    t0 = dq.Table([utf8_column("s", chunks[0])])
+    plan = ScanPlan([a], t0.schema)
+    for rep in range(2):  # a second pass after reset starts from the published counts of the first
+        plan.reset()
+        for c in chunks:
+            plan.scan(dq.Table([utf8_column("s", c)]))
+            torch.cuda.synchronize()  # (the finalize has published the counts the next chunk's choice reads)
+        got = tuple(a._from_result(plan.finish()[0]).words)
+        allv = [v for c in chunks for v in c]
+        assert got == _oracle(allv), rep
+    plan.close()
 
 
 def test_nulls_and_empty(dq):
