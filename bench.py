@@ -20,6 +20,7 @@ from __future__ import annotations
 import argparse
 import gc
 import json
+import re
 import os
 import socket
 import subprocess
@@ -32,12 +33,12 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md (HBM3E peak 8.0 TB/s)
 # FETCH_SIZE summary of this round's kernels (tools/profile_round.sh -> tools/summarize_prof.py):
 # per-dispatch HBM read bytes of each kernel at the default 125 M-row chunk, gfx950-corrected
-PMC_FILE = os.path.join(ROOT, "profiles", "r5x_pmc.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r5fin_pmc.json")
 # tools/clock_probe.sh: held clock per kernel, one file per probe box (boxes hold 1.87-1.98 GHz under the same
 # kernels); the floor at the held clock takes the highest clock any probe saw (the conservative floor)
 CLOCK_FILES = [os.path.join(ROOT, "profiles", f) for f in ("r3_clock.json", "r3z_clock.json", "r4z_clock.json",
                                                          "r4z_cfg_clock.json", "r5l_clock.json", "r5p_clock.json",
-                                                         "r5x_clock.json")]
+                                                         "r5x_clock.json", "r5fin_clock.json")]
 DEFAULT_CHUNK = 125_000_000  # 8 chunks per 1e9 rows; a UTF8 chunk's bytes (~2.0e9) stay < 2 GiB
 
 
@@ -457,11 +458,17 @@ def pmc_file():
     return _PMC_CACHE["d"]
 
 
+def _kname(name):
+    """A kernel name without the string variants' second template argument (dq_column_scan<10, false> is the
+    common instantiation the bench's short strings run; round-5 profiles name it so)."""
+    return re.sub(r", (false|true)>", lambda m: ">" if m.group(1) == "false" else ", true>", name)
+
+
 def pmc_record(kernel):
     """The PMC pass record of `kernel` (FETCH_SIZE bytes, SQ instruction counts per launch), or None."""
     d = pmc_file()
     for r in (d or {}).get("kernels", []):
-        if r["kernel"] == kernel:
+        if _kname(r["kernel"]) == kernel:
             return r
     return None
 
@@ -495,7 +502,7 @@ def valu_bound(kernel, avg_ms):
     for path in CLOCK_FILES:
         try:
             with open(path) as f:
-                clk = json.load(f).get("void " + kernel)
+                clk = {_kname(k): v for k, v in json.load(f).items()}.get("void " + kernel)
         except (OSError, ValueError):
             clk = None
         if clk:
