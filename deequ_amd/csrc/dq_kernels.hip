@@ -754,6 +754,61 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
   int32_t qmin = 0;
   DtCounts dtc;
   const auto bp = [p5](uint32_t b) { return p5[b]; };
+  const int32_t win3 = win < 0 ? -1 : (win | 3);  // (rel & ~3) <= win  <=>  rel <= win | 3
+  if constexpr (LONG) {
+    // Columns of mostly long strings: every selected row hashed once from 16-byte loads (xxh64_window_head:
+    // the 32-byte stripe loop for the long ones, the remainder rounds for all), no fast path to redo.  Row
+    // j + 1's offsets are loaded while row j is hashed; the rows the fast path would have skipped are still
+    // counted (dq_scan keeps this instantiation while they stay over 1 / 16).
+    auto offs = [&](int32_t vo, int j, OffT& a, OffT& b) {
+      if constexpr (W == 4) {
+        a = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(orsrc, vo + j * 256, 0, 0);
+        b = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(orsrc, vo + j * 256 + 4, 0, 0);
+      } else {
+        const auto a0 = __builtin_amdgcn_raw_buffer_load_b64(orsrc, vo + j * 512, 0, 0);
+        const auto a1 = __builtin_amdgcn_raw_buffer_load_b64(orsrc, vo + j * 512 + 8, 0, 0);
+        a = (int64_t)(((uint64_t)a0[1] << 32) | a0[0]);
+        b = (int64_t)(((uint64_t)a1[1] << 32) | a1[0]);
+      }
+    };
+    const int32_t nr = (int32_t)(row1 - row0);
+    for (int32_t rb = 0; rb < nr; rb += kRowsPerIter) {
+      const int64_t base = row0 + rb + wave * 512;
+      const int32_t rem = nr - rb - wave * 512;
+      const bool full = rb + kRowsPerIter <= nr;
+      const int32_t vo = (rb + wave * 512 + lane) * W;  // the lane's row of the block, from row0, in bytes
+      uint64_t m[8];
+      block_masks(validity, mask, base, rem, full, m);
+      OffT na, nb;
+      offs(vo, 0, na, nb);
+#pragma unroll 1
+      for (int j = 0; j < 8; ++j) {
+        const OffT ca = na, cb = nb;
+        if (j < 7) offs(vo, j + 1, na, nb);
+        cnt_w += __builtin_popcountll(m[j]);
+        const int64_t rel = (int64_t)ca - lo, n = (int64_t)cb - (int64_t)ca;
+        const bool sel = lane_bit(m[j]);
+        const uint64_t longm = __builtin_amdgcn_ballot_w64(sel && !(n <= 28 && rel <= (int64_t)win3));
+        if (lane == 0 && longm != 0) atomicAdd(rare, (uint32_t)__builtin_popcountll(longm));
+        if (sel) {
+          if constexpr (HLL) {
+            if (win >= 0 && (((rel + (n & ~int64_t(31))) & ~int64_t(3)) + 48 <= (int64_t)win + 32)) {
+              const uint64_t b = xxh64_window_head(rsrc, (uint32_t)rel, (uint32_t)n, bp);
+              const HllKey key = hll_key_from_fmix(b);
+              if (key.q >= 0) atomicMax(reinterpret_cast<int32_t*>(reinterpret_cast<char*>(regs) + key.addr), key.q);
+              else hll_update(regs, fmix_tail(b));
+            } else {
+              hll_update(regs, xxh64_bytes(data, lo + rel, n));
+            }
+          }
+          if constexpr (DT) dtc.add(dt_class_bytes(data + lo + rel, n), true);
+        }
+      }
+    }
+    if (lane == 0) s.count += cnt_w;
+    if constexpr (DT) dtc.flush(s);
+    return;
+  }
   // Software pipeline over the lane's rows j = 0..7 of each block, continuing into the next block:
   // row j + 4's offsets are loaded into the ring slot row j frees (kOffRing = 4 rows of offsets in
   // registers, loaded 4 rows before use), and the 32-byte windows of rows j + 1 .. j + kStrAhead are in
@@ -793,7 +848,6 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
     const int64_t l = (int64_t)rb[q] - (int64_t)ra[q];
     return W == 4 ? (uint32_t)l : (l > 28 ? 29u : (uint32_t)l);
   };
-  const int32_t win3 = win < 0 ? -1 : (win | 3);  // (rel & ~3) <= win  <=>  rel <= win | 3
   // the 32-byte windows of the next kStrAhead strings in flight (rows 0 .. kStrAhead - 1 of the first block)
   u32x4 win_a[kStrAhead], win_c[kStrAhead];
 #pragma unroll
@@ -915,43 +969,10 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
     vo_cur = vo_next;
     // rare: long / window-crossing strings, or a rank that needs the hash's low word (2^-23).  The
     // HLL update is idempotent, so the block's selected rows are simply redone; DataType counts only
-    // the rows the fast path skipped.  The LONG instantiation (chosen by dq_scan for columns whose
-    // earlier chunks had many such rows) redoes only those rows, and every row of a lane whose fast-path
-    // rank needed the low word, from 16-byte loads (xxh64_window_head; the byte-addressed loop only for the
-    // last strings of the chunk, whose loads would leave the chunk's bytes).
+    // the rows the fast path skipped.  (Columns with many such rows run the LONG instantiation above.)
     if ((slow | __builtin_amdgcn_ballot_w64(qmin < 0)) != 0) {
       // the rows the fast path skipped, counted in the wave's LDS slot (no register across the block loop)
       if (lane == 0) atomicAdd(rare, (uint32_t)__builtin_popcountll(slow));
-      if constexpr (LONG) {
-        const bool redo_all = qmin < 0;
-        block_masks(validity, mask, base, rem, full, m);
-#pragma unroll 1
-        for (int j = 0; j < 8; ++j) {
-          if (lane_bit(m[j])) {
-            const int64_t row = base + j * 64 + lane;
-            const int64_t o0 = (int64_t)offsets[row], o1 = (int64_t)offsets[row + 1];
-            const int64_t rel = o0 - lo, n = o1 - o0;
-            const bool was_fast = n <= 28 && rel <= (int64_t)win3;
-            if constexpr (HLL) {
-              if (!was_fast || redo_all) {
-                if (win >= 0 && (((rel + (n & ~int64_t(31))) & ~int64_t(3)) + 48 <= (int64_t)win + 32)) {
-                  const uint64_t b = xxh64_window_head(rsrc, (uint32_t)rel, (uint32_t)n, bp);
-                  const HllKey key = hll_key_from_fmix(b);
-                  if (key.q >= 0) atomicMax(reinterpret_cast<int32_t*>(reinterpret_cast<char*>(regs) + key.addr), key.q);
-                  else hll_update(regs, fmix_tail(b));
-                } else {
-                  hll_update(regs, xxh64_bytes(data, o0, n));
-                }
-              }
-            }
-            if constexpr (DT) {
-              if (!was_fast) dtc.add(dt_class_bytes(data + o0, n), true);
-            }
-          }
-        }
-        qmin = 0;
-        continue;
-      }
       block_masks(validity, mask, base, rem, full, m);
 #pragma unroll 1
       for (int j = 0; j < 8; ++j) {

@@ -622,14 +622,19 @@ def _dt_string(rng) -> bytes:
     return sign + bytes(body)
 
 
+@pytest.mark.parametrize("path", ["auto", "long"])
 @pytest.mark.parametrize("large", [False, True])
 @pytest.mark.parametrize("n", [1, 64, 513, 4099, 70_001])
-def test_datatype_vs_oracle(dq, n, large):
+def test_datatype_vs_oracle(dq, n, large, path, monkeypatch):
     """DataType (StatefulDataType.scala:36-67) on strings of every class and length (the <= 28-byte
     SWAR path and the byte path), alone and fused with ApproxCountDistinct, with and without `where`;
     on f64 values around the Double.toString boundaries (1e-3, 1e7, +-0, NaN, +-inf) and on integral
-    columns -- bit-exact histograms vs the oracle."""
+    columns -- bit-exact histograms vs the oracle.  path "long": the string HLL variants' LONG
+    instantiation (DQ_STR_PATH; the one dq_scan picks for columns of long strings)."""
     from deequ_amd.runner import scan_states
+
+    if path == "long":
+        monkeypatch.setenv("DQ_STR_PATH", "long")
     from deequ_amd.table import column_from_numpy, utf8_column
 
     rng = np.random.default_rng(77 + n + int(large))
