@@ -759,7 +759,7 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
     // Columns of mostly long strings: every selected row hashed once from 16-byte loads (xxh64_window_head:
     // the 32-byte stripe loop for the long ones, the remainder rounds for all), no fast path to redo.  Row
     // j + 1's offsets are loaded while row j is hashed; the rows the fast path would have skipped are still
-    // counted (dq_scan keeps this instantiation while they stay over 1 / 16).
+    // counted (dq_scan keeps this instantiation while they stay over 1 / 4096).
     auto offs = [&](int32_t vo, int j, OffT& a, OffT& b) {
       if constexpr (W == 4) {
         a = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(orsrc, vo + j * 256, 0, 0);

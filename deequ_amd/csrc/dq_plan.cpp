@@ -503,7 +503,9 @@ struct dq_plan {
   // the string pass's variant per UTF8 HLL task: the string kernels count each task's rare-path rows since the
   // reset (d_rare_dev), the finalize kernel publishes them into mapped pinned memory (h_rare; d_rare its device
   // address), dq_scan reads them without waiting and runs the LONG variant for a task group once more than
-  // 1 / 16 of the rows took the rare path
+  // 1 / 4096 of the rows took the rare path (the common variant redoes a whole 512-row block for one such row:
+  // at 4.5 % of them it ran 5.86 ms per 1e8 rows x 4 columns against LONG's 2.44; on short strings alone
+  // 1.80 against 2.34, profiles/r5_ab.txt r5aj)
   int64_t* d_rare_dev = nullptr;
   int64_t* h_rare = nullptr;
   int64_t* d_rare = nullptr;
@@ -1737,7 +1739,7 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
     const int64_t rows = p->total_rows > 0 ? p->total_rows : p->prev_rows;
     bool any = false;
     for (int32_t t = g.first; t < g.first + g.count; ++t) {
-      if (p->h_rare && rows > 0) p->str_long[t] = __atomic_load_n(p->h_rare + t, __ATOMIC_RELAXED) * 16 > rows;
+      if (p->h_rare && rows > 0) p->str_long[t] = __atomic_load_n(p->h_rare + t, __ATOMIC_RELAXED) * 4096 > rows;
       any = any || p->str_long[t];
     }
     return any;

@@ -19,7 +19,11 @@ def main():
     ap.add_argument("--bands", default="8:24,16:48,24:40,32:64,64:128")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--dtype", action="store_true", help="also DataType per column (UTF8_HD variant)")
+    ap.add_argument("--path", choices=["auto", "fast", "long"], default="auto",
+                    help="DQ_STR_PATH: the string pass's instantiation (auto: dq_scan's choice)")
     args = ap.parse_args()
+    if args.path != "auto":
+        os.environ["DQ_STR_PATH"] = args.path
     import torch
 
     from deequ_amd import synth
@@ -57,7 +61,7 @@ def main():
             if n:
                 ker[v] = round(ms / n * 1e8 / args.rows, 4)
         nbytes = sum(c.data_bytes for c in cols)
-        rec = {"band": band, "rows": args.rows, "ms_per_scan": round(sec * 1e3, 3), "rows_per_s": args.rows / sec,
+        rec = {"band": band, "path": args.path, "rows": args.rows, "ms_per_scan": round(sec * 1e3, 3), "rows_per_s": args.rows / sec,
                "string_GBps": nbytes / sec / 1e9, "variant_ms_per_1e8_rows": ker}
         print(json.dumps(rec), flush=True)
         out.append(rec)
