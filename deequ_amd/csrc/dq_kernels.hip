@@ -801,7 +801,15 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
               hll_update(regs, xxh64_bytes(data, lo + rel, n));
             }
           }
-          if constexpr (DT) dtc.add(dt_class_bytes(data + lo + rel, n), true);
+          if constexpr (DT) {
+            if (n <= 28 && win >= 0 && (rel & ~int64_t(3)) + 48 <= (int64_t)win + 32) {  // SWAR on the window
+              uint32_t w8[8];
+              load_bytes32(rsrc, (uint32_t)rel, w8);
+              dtc.add(dt_class_short(w8, (uint32_t)n, true), true);
+            } else {
+              dtc.add(dt_class_bytes(data + lo + rel, n), true);
+            }
+          }
         }
       }
     }
