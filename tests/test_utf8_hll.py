@@ -117,7 +117,7 @@ def test_variant_switch_across_chunks(dq, monkeypatch):
     plan.close()
 
 
-def test_nulls_and_empty(dq):
+def test_nulls_and_empty(dq, str_path):
     rng = np.random.default_rng(3)
     assert _words(dq, [None] * 5000, False) == _oracle([None] * 5000)
     vals = [b"" if i % 3 else None for i in range(10_000)]
@@ -127,7 +127,7 @@ def test_nulls_and_empty(dq):
 
 
 @pytest.mark.parametrize("large", [False, True])
-def test_strings_at_the_chunk_end(dq, large):
+def test_strings_at_the_chunk_end(dq, large, str_path):
     """The last strings' 32-byte windows reach past the chunk's bytes: they take the general loop."""
     rng = np.random.default_rng(11)
     n = 4099
@@ -137,7 +137,7 @@ def test_strings_at_the_chunk_end(dq, large):
 
 
 @pytest.mark.parametrize("large", [False, True])
-def test_huge_iteration_subranges(dq, large):
+def test_huge_iteration_subranges(dq, large, str_path):
     """Every 8th row holds a 600 KB string: a 2048-row iteration spans ~150 MB of string bytes, so short
     strings far from their range's first byte take the general loop with the big ones."""
     import xxhash
