@@ -928,7 +928,18 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
   if (p->regex_blob.size() > (size_t)kMaxRegexWords)
     return cap_error("compiled patterns need %zu KB (LDS budget %d KB)", p->regex_blob.size() * 2 / 1024,
                      kMaxRegexWords * 2 / 1024);
-  if (p->probe) return DQ_OK;  // capacity probe (dq_plan_create's split): every capacity check is above
+  if (p->probe) {  // capacity probe (dq_plan_create's split): every capacity check is above
+    // COMPILED: the generated kernel's own limits (<= 8 value columns, 16 counters, ...) are capacities too,
+    // so the greedy split never grows a part past what pred_jit_eligible takes
+    if (p->has_pred && p->pred_pass == DQ_PRED_PASS_COMPILED) {
+      std::vector<int32_t> kinds(ncols);
+      for (int c = 0; c < ncols; ++c) kinds[c] = kind_of(p->schema[c].type);
+      if (!pred_jit_eligible(p->prog, kinds.data(), ncols, true))
+        return cap_error("compiled predicate pass: program not eligible (regex / string atoms, > 8 columns, or > 16 "
+                         "counters / 8 where bitmaps / 96 instructions)");
+    }
+    return DQ_OK;
+  }
 
   // the predicate program compiled into its own kernel when the generator takes it; HLL-only tasks (no
   // `where`) on its columns are hashed there (fused = 2) instead of re-reading the column in the column pass
@@ -978,8 +989,10 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
       p->pred_jit_note = "program not eligible (regex / string atoms, > 8 columns, or > 16 counters / 8 where "
                          "bitmaps / 96 instructions)";
     }
+    // (a capacity error: a program too large for the generated kernel splits into parts that fit it; a spec
+    // whose program cannot be compiled even alone still fails, with the split's "spec i" message)
     if (!p->pred_jit && !(p->host_only && !p->pred_jit_src.empty()) && p->pred_pass == DQ_PRED_PASS_COMPILED)
-      return set_error(DQ_E_UNSUPPORTED, "compiled predicate pass required: %s", p->pred_jit_note.c_str());
+      return cap_error("compiled predicate pass required: %s", p->pred_jit_note.c_str());
   } else if (p->has_pred) {
     p->pred_jit_note = "interpreter requested (DQ_PRED_PASS_INTERPRETER)";
   }
@@ -1503,16 +1516,40 @@ dq_status dq_plan_create_opts(const dq_analyzer_spec* specs, int32_t n_specs, co
 dq_status dq_plan_set_stream(dq_plan* p, void* hip_stream) {
   if (!p) return set_error(DQ_E_INVALID, "dq_plan_set_stream: plan is NULL");
   HIP_TRY(hipSetDevice(p->device));
+  // a composite plan's parts launch on the parent's stream (they never own one): one sync of the old stream
+  // covers their work too, then every part moves to the new stream before the old one may be destroyed
   HIP_TRY(hipStreamSynchronize(p->stream));
+  for (dq_plan* q : p->parts) {
+    if (q->stream != p->stream) HIP_TRY(hipStreamSynchronize(q->stream));  // (not reachable: parts share it)
+    if (q->own_stream) (void)hipStreamDestroy(q->stream);
+    q->stream = (hipStream_t)hip_stream;
+    q->own_stream = false;
+  }
   // NULL is the device's null stream (what torch's default stream reports), not "keep the plan's
   // own stream": the plan's own stream is non-blocking and would not wait for producers on it.
   if (p->own_stream) (void)hipStreamDestroy(p->stream);
   p->stream = (hipStream_t)hip_stream;
   p->own_stream = false;
-  for (dq_plan* q : p->parts)
-    if (dq_status s = dq_plan_set_stream(q, hip_stream)) return s;
   return DQ_OK;
 }
+
+}  // extern "C"
+
+// dq_scan's contract for one column view (dqscan.h dq_column_view)
+static dq_status check_view(const dq_column_desc& cd, const dq_column_view& v, int32_t c, int64_t n_rows) {
+  const int32_t t = cd.type;
+  if (v.reserved != 0) return set_error(DQ_E_INVALID, "dq_scan: column %d reserved field must be 0", c);
+  if (n_rows > 0 && !v.values) return set_error(DQ_E_INVALID, "dq_scan: column %d has no values buffer", c);
+  if (((uintptr_t)v.values & 15) != 0)
+    return set_error(DQ_E_INVALID, "dq_scan: column %d values buffer must be 16-byte aligned", c);
+  if (((uintptr_t)v.validity & 3) != 0)
+    return set_error(DQ_E_INVALID, "dq_scan: column %d validity bitmap must be 4-byte aligned", c);
+  if ((t == DQ_TYPE_UTF8 || t == DQ_TYPE_LARGE_UTF8) && n_rows > 0 && !v.offsets)
+    return set_error(DQ_E_INVALID, "dq_scan: UTF8 column %d has no offsets", c);
+  return DQ_OK;
+}
+
+extern "C" {
 
 dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_t chunk_index) {
   if (!p) return set_error(DQ_E_INVALID, "dq_scan: plan is NULL");
@@ -1526,6 +1563,16 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
   if (ncols > 0 && !cols) return set_error(DQ_E_INVALID, "dq_scan: cols is NULL");
   HIP_TRY(hipSetDevice(p->device));
   if (!p->parts.empty()) {  // composite: every part over its own columns of this chunk, in part order
+    // every view any part reads is checked before the first part scans: a rejected view must leave every
+    // part's chunk count where it was (a partly scanned chunk could not be retried, and dq_finish would
+    // merge states over different row sets)
+    for (size_t k = 0; k < p->parts.size(); ++k) {
+      for (int32_t c : p->part_cols[k])
+        if (dq_status s = check_view(p->schema[c], cols[c], c, n_rows)) return s;
+      if (p->parts[k]->next_chunk != chunk_index)
+        return set_error(DQ_E_INVALID, "dq_scan: part %zu is at chunk %lld (expected %lld)", k,
+                         (long long)p->parts[k]->next_chunk, (long long)chunk_index);
+    }
     std::vector<dq_column_view> v;
     for (size_t k = 0; k < p->parts.size(); ++k) {
       v.resize(p->part_cols[k].size());
@@ -1537,17 +1584,10 @@ dq_status dq_scan(dq_plan* p, const dq_column_view* cols, int64_t n_rows, int64_
     return DQ_OK;
   }
   ScanCols sc{};
+  for (int32_t c = 0; c < ncols; ++c)
+    if (dq_status s = check_view(p->schema[c], cols[c], c, n_rows)) return s;
   for (int32_t c = 0; c < ncols; ++c) {
     const dq_column_view& v = cols[c];
-    int32_t t = p->schema[c].type;
-    if (v.reserved != 0) return set_error(DQ_E_INVALID, "dq_scan: column %d reserved field must be 0", c);
-    if (n_rows > 0 && !v.values) return set_error(DQ_E_INVALID, "dq_scan: column %d has no values buffer", c);
-    if (((uintptr_t)v.values & 15) != 0)
-      return set_error(DQ_E_INVALID, "dq_scan: column %d values buffer must be 16-byte aligned", c);
-    if (((uintptr_t)v.validity & 3) != 0)
-      return set_error(DQ_E_INVALID, "dq_scan: column %d validity bitmap must be 4-byte aligned", c);
-    if ((t == DQ_TYPE_UTF8 || t == DQ_TYPE_LARGE_UTF8) && n_rows > 0 && !v.offsets)
-      return set_error(DQ_E_INVALID, "dq_scan: UTF8 column %d has no offsets", c);
     sc.values[c] = v.values;
     sc.validity[c] = p->schema[c].nullable ? reinterpret_cast<const uint32_t*>(v.validity) : nullptr;
     sc.offsets[c] = v.offsets;

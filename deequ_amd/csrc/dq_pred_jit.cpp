@@ -167,8 +167,8 @@ const char* cmp_op(int c) {
 // a VerificationSuite with many Compliance checks -- stay on the interpreter, whose cost grows per atom anyway.
 constexpr int kJitMaxCounters = 16, kJitMaxBitmaps = 8, kJitMaxInstr = 96;
 
-bool pred_jit_eligible(const PredProgram& prog, const int32_t* col_kind, int32_t ncols) {
-  if (prog.regex_words > 0 || prog.n_loads == 0) return false;
+bool pred_jit_eligible(const PredProgram& prog, const int32_t* col_kind, int32_t ncols, bool constant_ok) {
+  if (prog.regex_words > 0 || (prog.n_loads == 0 && !constant_ok)) return false;
   if (prog.n_counters > kJitMaxCounters || prog.n_bitmaps > kJitMaxBitmaps || prog.n_instr > kJitMaxInstr) return false;
   std::vector<int32_t> cols;
   for (int i = 0; i < prog.n_instr; ++i) {
@@ -185,7 +185,7 @@ bool pred_jit_eligible(const PredProgram& prog, const int32_t* col_kind, int32_t
       if (!seen) cols.push_back(c);
     }
   }
-  return !cols.empty() && cols.size() <= 8;
+  return (constant_ok || !cols.empty()) && cols.size() <= 8;
 }
 
 // The kernel source of `prog`; slot_col receives the program's distinct columns in slot order (the order of

@@ -32,7 +32,8 @@ struct PredJitHll {
 };
 
 // col_kind[c]: CK_* of plan column c
-bool pred_jit_eligible(const PredProgram& prog, const int32_t* col_kind, int32_t ncols);
+// constant_ok: a program with no atoms passes (the split's capacity probe: a constant root can join any part)
+bool pred_jit_eligible(const PredProgram& prog, const int32_t* col_kind, int32_t ncols, bool constant_ok = false);
 std::string pred_jit_source(const PredProgram& prog, const int32_t* col_kind, std::vector<int32_t>& slot_col,
                             const std::vector<PredJitHll>& hll);
 // hipRTC compile of `src` for `arch` (host only)

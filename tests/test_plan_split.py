@@ -224,3 +224,73 @@ def test_split_runner_no_failures():
         single = a.calculate(t).value.get()
         fused = ctx.metric(a).value.get()
         assert single == fused or (single != single and fused != fused), (a, single, fused)
+
+
+@pytest.mark.gpu
+def test_split_set_stream_twice_then_scan():
+    """dq_plan_set_stream on a split plan moves every part to the new stream before the parent's own stream is
+    destroyed (the parts never own one); setting it twice and scanning gives the oracle's states."""
+    import ctypes
+
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    from oracle import dq_oracle as O
+    from tests.test_gpu_parity import assert_state_close
+    from deequ_amd.runner import ScanPlan
+
+    n = 5003
+    data = _wide_data(36, n, seed=41)
+    t = _table(data, 0, n)
+    analyzers = _compliance40()
+    plan = ScanPlan(analyzers, t.schema)
+    try:
+        assert "fused plans" in explain(analyzers, t.schema)
+        s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+        L.check(L.lib.dq_plan_set_stream(plan.handle, ctypes.c_void_p(s1.cuda_stream)))
+        L.check(L.lib.dq_plan_set_stream(plan.handle, ctypes.c_void_p(s2.cuda_stream)))
+        torch.cuda.synchronize()  # the table's uploads, on torch's stream, are done before s2 reads them
+        plan.scan(t)
+        states = [a._from_result(r) for a, r in zip(analyzers, plan.finish())]
+    finally:
+        plan.close()
+    cols = _oracle_cols(t, n)
+    for a, s in zip(analyzers, states):
+        assert_state_close(s, O.compute_state(_spec(a), cols, n), scale=1.0)
+
+
+@pytest.mark.gpu
+def test_split_scan_rejects_views_before_any_part_scans():
+    """A column view that a later part of a split plan rejects fails dq_scan before any part has counted the
+    chunk: the same chunk_index can then be scanned with good views, and the states are the oracle's."""
+    import ctypes
+
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    from oracle import dq_oracle as O
+    from tests.test_gpu_parity import assert_state_close
+    from deequ_amd.runner import ScanPlan
+
+    n = 4099
+    data = _wide_data(100, n, seed=43)
+    t = _table(data, 0, n)
+    analyzers = _profile(t.schema)
+    plan = ScanPlan(analyzers, t.schema)
+    try:
+        views = (L.ColumnView * len(plan.columns))()
+        for i, name in enumerate(plan.columns):
+            views[i] = t.columns[name].view()
+        bad = len(plan.columns) - 1  # read by the last part only
+        good = views[bad].values
+        views[bad].values = good + 4  # not 16-byte aligned
+        rc = L.lib.dq_scan(plan.handle, views, n, 0)
+        assert rc == L.DQ_E_INVALID, rc
+        views[bad].values = good
+        L.check(L.lib.dq_scan(plan.handle, views, n, 0))
+        states = [a._from_result(r) for a, r in zip(analyzers, plan.finish())]
+    finally:
+        plan.close()
+    cols = _oracle_cols(t, n)
+    for a, s in zip(analyzers, states):
+        assert_state_close(s, O.compute_state(_spec(a), cols, n), scale=1.0)
