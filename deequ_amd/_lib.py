@@ -8,7 +8,7 @@ from __future__ import annotations
 import ctypes
 import os
 
-ABI_VERSION = 4  # include/dqscan.h DQ_ABI_VERSION
+ABI_VERSION = 5  # include/dqscan.h DQ_ABI_VERSION
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DQ_LIB_PATH") or os.path.join(_HERE, "libdqscan.so")  # override: diagnostic A/B builds
@@ -22,12 +22,16 @@ DQ_E_OOM = -5
 DQ_E_STATE = -6
 
 TYPE_F64, TYPE_I64, TYPE_I32, TYPE_UTF8, TYPE_LARGE_UTF8 = 1, 2, 3, 4, 5
+# round 6: FloatType, ShortType, ByteType, BooleanType (bit-packed), DateType (int32 days), TimestampType (int64 us)
+TYPE_F32, TYPE_I16, TYPE_I8, TYPE_BOOL, TYPE_DATE32, TYPE_TIMESTAMP = 6, 7, 8, 9, 10, 11
 
 # column-pass kernel variants (deequ_amd/csrc/dq_device.h ColVariant)
 VARIANT_NAMES = {0: "validity", 1: "f64_stats", 2: "f64_stats_hll", 3: "f64_hll", 4: "i64_stats",
                  5: "i64_stats_hll", 6: "i64_hll", 7: "i32_stats", 8: "i32_stats_hll", 9: "i32_hll",
                  10: "utf8_hll", 11: "large_utf8_hll", 12: "utf8_dtype", 13: "utf8_hll_dtype",
-                 14: "large_utf8_dtype", 15: "large_utf8_hll_dtype", 16: "f64_dtype"}
+                 14: "large_utf8_dtype", 15: "large_utf8_hll_dtype", 16: "f64_dtype",
+                 17: "f32_stats", 18: "f32_stats_hll", 19: "f32_hll", 20: "i16_stats", 21: "i16_stats_hll",
+                 22: "i16_hll", 23: "i8_stats", 24: "i8_stats_hll", 25: "i8_hll", 26: "f32_dtype", 27: "bool"}
 
 OP_SIZE = 1
 OP_COMPLETENESS = 2

@@ -25,6 +25,10 @@ from .states import State, state_from_c
 from .table import NUMERIC
 
 Schema = Sequence  # list of (name, dtype, nullable)
+# the Spark SQL type each column dtype carries (WrongColumnTypeException text, Analyzer.scala:330-332)
+SPARK_TYPE = {"f64": "DoubleType", "f32": "FloatType", "i64": "LongType", "i32": "IntegerType", "i16": "ShortType",
+              "i8": "ByteType", "bool": "BooleanType", "date32": "DateType", "timestamp": "TimestampType",
+              "utf8": "StringType", "large_utf8": "StringType"}
 
 
 def _opt(x: Optional[str]) -> str:
@@ -46,7 +50,7 @@ class Preconditions:
             if t not in NUMERIC:
                 raise WrongColumnTypeException(
                     f"Expected type of column {column} to be one of (ByteType,ShortType,IntegerType,LongType,"
-                    f"FloatType,DoubleType,DecimalType), but found {t} instead!")
+                    f"FloatType,DoubleType,DecimalType), but found {SPARK_TYPE.get(t, t)} instead!")
         return check
 
     @staticmethod

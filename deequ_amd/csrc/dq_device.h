@@ -32,8 +32,16 @@ constexpr int kMaxInstr = 96;
 constexpr int kPredStack = 16;              // predicate pass: operand stack depth
 constexpr int kMaxRegexWords = 32768;       // compiled regex DFAs of one plan (64 KB of LDS)
 
-// column kinds seen by the kernels
-enum ColKind : int32_t { CK_F64 = 1, CK_I64 = 2, CK_I32 = 3, CK_UTF8 = 4, CK_LUTF8 = 5 };
+// column kinds seen by the kernels (physical layouts: DATE32 columns are CK_I32, TIMESTAMP columns CK_I64 --
+// the planner's preconditions keep their non-numeric analyzers away)
+enum ColKind : int32_t {
+  CK_F64 = 1, CK_I64 = 2, CK_I32 = 3, CK_UTF8 = 4, CK_LUTF8 = 5,
+  CK_F32 = 6, CK_I16 = 7, CK_I8 = 8, CK_BOOL = 9,  // (BOOL: LSB-first value bitmap)
+};
+constexpr bool ck_float(int k) { return k == CK_F64 || k == CK_F32; }
+constexpr int ck_bytes(int k) {
+  return k == CK_F64 || k == CK_I64 ? 8 : k == CK_I32 || k == CK_F32 ? 4 : k == CK_I16 ? 2 : 1;
+}
 
 // column-pass variants (kind x what is accumulated); VALIDITY = count of selected rows only
 enum ColVariant : int32_t {
@@ -45,8 +53,14 @@ enum ColVariant : int32_t {
   // DataType (StatefulDataType.scala:36-69): string columns classify every selected value (alone or
   // fused with the HLL pass); double columns count the values whose Double.toString is fractional
   CV_UTF8_D = 12, CV_UTF8_HD = 13, CV_LUTF8_D = 14, CV_LUTF8_HD = 15, CV_F64_D = 16,
+  // round 6: FloatType / ShortType / ByteType values (converted to double exactly, hashed as Spark 2.2 does), the
+  // DataType count of a float column, and a boolean column's selected / TRUE counts (+ its two HLL hashes)
+  CV_F32_S = 17, CV_F32_SH = 18, CV_F32_H = 19,
+  CV_I16_S = 20, CV_I16_SH = 21, CV_I16_H = 22,
+  CV_I8_S = 23, CV_I8_SH = 24, CV_I8_H = 25,
+  CV_F32_D = 26, CV_BOOL = 27,
 };
-constexpr int kNumVariants = 17;
+constexpr int kNumVariants = 28;
 
 // per-variant row-range counts of one scan (dq_finalize merges nr[i] partials for tasks [first, end))
 // column-task ranges whose range count differs from the scan's default (string passes, the validity pass, a
@@ -80,7 +94,7 @@ struct PairGroup {
   int32_t first_pair;               // pairs [first_pair, first_pair + npairs) of the pair-task table
   int32_t where;                    // where-bitmap index or -1
   int32_t cols[kTileCols];          // plan column indices
-  int32_t kinds[kTileCols];         // CK_F64 / CK_I64 / CK_I32
+  int32_t kinds[kTileCols];         // numeric kinds (CK_F64 / CK_F32 / CK_I64 / CK_I32 / CK_I16 / CK_I8)
   int8_t pi[kTilePairs], pj[kTilePairs];  // local column index of x / y per pair
 };
 
@@ -102,7 +116,7 @@ struct PairWaveTask {
   uint32_t mom_mask;               // bit m: position 2 m has a column-moments task
   uint32_t swap_mask;              // bit q: the pair task's first column is position kPairSlotB[q]
   int32_t cols[kPairPos];          // plan column indices (an unused position repeats a used column)
-  int32_t kinds[kPairPos];         // CK_F64 / CK_I64 / CK_I32
+  int32_t kinds[kPairPos];         // numeric kinds (CK_F64 / CK_F32 / CK_I64 / CK_I32 / CK_I16 / CK_I8)
   int32_t pair_out[kPairSlots];    // pair-task index of each active slot
   int32_t mom_out[kPairMoments];   // column-task index of each moments position
 };

@@ -38,7 +38,26 @@ int32_t type_of_format(const char* f) {
   if (std::strcmp(f, "i") == 0) return DQ_TYPE_I32;
   if (std::strcmp(f, "u") == 0) return DQ_TYPE_UTF8;
   if (std::strcmp(f, "U") == 0) return DQ_TYPE_LARGE_UTF8;
+  if (std::strcmp(f, "f") == 0) return DQ_TYPE_F32;
+  if (std::strcmp(f, "s") == 0) return DQ_TYPE_I16;
+  if (std::strcmp(f, "c") == 0) return DQ_TYPE_I8;
+  if (std::strcmp(f, "b") == 0) return DQ_TYPE_BOOL;
+  if (std::strcmp(f, "tdD") == 0) return DQ_TYPE_DATE32;
+  // timestamp[us, tz]: Spark's TimestampType is UTC microseconds whatever the session zone (other units are not
+  // TimestampType values: a producer converts them)
+  if (std::strncmp(f, "tsu:", 4) == 0) return DQ_TYPE_TIMESTAMP;
   return 0;
+}
+
+// bytes per value of a fixed-width type (BOOL: bit-packed, 0)
+int64_t value_width(int32_t type) {
+  switch (type) {
+    case DQ_TYPE_F64: case DQ_TYPE_I64: case DQ_TYPE_TIMESTAMP: return 8;
+    case DQ_TYPE_I32: case DQ_TYPE_F32: case DQ_TYPE_DATE32: return 4;
+    case DQ_TYPE_I16: return 2;
+    case DQ_TYPE_I8: return 1;
+    default: return 0;
+  }
 }
 
 // parallel copy of a list of pieces over up to `threads` CPU threads.  A piece is a memcpy, or -- for an
@@ -138,7 +157,7 @@ dq_status dq_arrow_import(const struct ArrowSchema* schema, const struct ArrowAr
   if (!schema->release || !array->release) return set_error(DQ_E_INVALID, "dq_arrow_import: released Arrow structure");
   const int32_t type = type_of_format(schema->format);
   if (!type)
-    return set_error(DQ_E_UNSUPPORTED, "Arrow format '%s' is not a GPU column type (g, l, i, u, U)",
+    return set_error(DQ_E_UNSUPPORTED, "Arrow format '%s' is not a GPU column type (g, f, l, i, s, c, b, tdD, tsu:, u, U)",
                      schema->format ? schema->format : "(null)");
   if (schema->n_children != 0 || array->n_children != 0 || schema->dictionary || array->dictionary)
     return set_error(DQ_E_UNSUPPORTED, "nested / dictionary-encoded Arrow arrays are not GPU columns");
@@ -163,12 +182,18 @@ dq_status dq_arrow_import(const struct ArrowSchema* schema, const struct ArrowAr
                                            schema->format, str ? "offsets" : "values");
   c.nullable = validity ? 1 : 0;
   // a slice (RecordBatch.slice, to_batches(max_chunksize)): row 0 is bit off % 8 of byte off / 8; dq_upload
-  // shifts the bitmap into place while it copies
+  // shifts the bitmap into place while it copies (a boolean array's value bits too)
+  const bool bits = type == DQ_TYPE_BOOL;
   c.validity = validity ? validity + off / 8 : nullptr;
   c.validity_bytes = validity ? (n + 7) / 8 : 0;
-  c.validity_bit = validity ? (int32_t)(off & 7) : 0;
-  if (!str) {
-    const int64_t w = type == DQ_TYPE_I32 ? 4 : 8;
+  c.validity_bit = validity || bits ? (int32_t)(off & 7) : 0;
+  if (bits) {
+    c.values = static_cast<const char*>(array->buffers[1]) + off / 8;
+    c.value_bytes = (n + 7) / 8;
+    c.offsets = nullptr;
+    c.offset_bytes = 0;
+  } else if (!str) {
+    const int64_t w = value_width(type);
     c.values = static_cast<const char*>(array->buffers[1]) + off * w;
     c.value_bytes = n * w;
     c.offsets = nullptr;
@@ -264,7 +289,7 @@ dq_status dq_upload(dq_uploader* u, const dq_host_column* cols, int32_t n_cols, 
     for (int k = 0; k < 3; ++k) {
       if (pos[3 * (size_t)c + k] < 0) continue;
       Piece p{u->pinned[(size_t)s] + pos[3 * (size_t)c + k], static_cast<const char*>(src[k]), len[k]};
-      if (k == 1 && h.validity_bit) {
+      if ((k == 1 || (k == 0 && h.type == DQ_TYPE_BOOL)) && h.validity_bit) {  // bitmaps of a slice
         p.kind = 3;
         p.shift = h.validity_bit;
         p.src_bytes = (h.validity_bit + h.n_rows + 7) / 8;

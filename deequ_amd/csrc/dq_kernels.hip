@@ -303,6 +303,10 @@ struct LaneMoments {
 template <int KIND>
 __device__ __forceinline__ double range_value(__amdgpu_buffer_rsrc_t vr, int64_t rel) {
   if constexpr (KIND == CK_I32) return (double)(int32_t)__builtin_amdgcn_raw_buffer_load_b32(vr, (int)(rel * 4), 0, 0);
+  if constexpr (KIND == CK_F32)
+    return (double)__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(vr, (int)(rel * 4), 0, 0));
+  if constexpr (KIND == CK_I16) return (double)(int16_t)__builtin_amdgcn_raw_buffer_load_b16(vr, (int)(rel * 2), 0, 0);
+  if constexpr (KIND == CK_I8) return (double)(int8_t)__builtin_amdgcn_raw_buffer_load_b8(vr, (int)rel, 0, 0);
   const auto w2 = __builtin_amdgcn_raw_buffer_load_b64(vr, (int)(rel * 8), 0, 0);
   if constexpr (KIND == CK_F64) return __builtin_bit_cast(double, ((uint64_t)w2[1] << 32) | w2[0]);
   return __builtin_fma((double)(int32_t)w2[1], 4294967296.0, (double)w2[0]);
@@ -398,16 +402,16 @@ __device__ __forceinline__ void masked_moments(LaneMoments& a, double& lo, doubl
 }
 
 // One 512-row block of a wave: x[j] the lane's value of row group j as a double, bits[j] its raw 64-bit
-// pattern (i32: sign-extended), m[j] the selection masks (every selected value finite: a block with a
+// pattern (i32 / i16 / i8: sign-extended; f32: its 32 bits), m[j] the selection masks (every selected value finite: a block with a
 // selected NaN / +-inf takes the caller's rolled path).
 template <int KIND, bool STATS, bool HLL>
 __device__ __forceinline__ void numeric_block(const double (&x)[8], const uint64_t (&bits)[8], const uint64_t (&m)[8],
                                               double shift, ColStats& s, LaneMoments& a, int32_t* regs, int32_t& qmin) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    if (STATS) masked_moments<KIND != CK_F64, false>(a, s.fmin, s.fmax, x[j], bits[j], shift, m[j], m[j]);
+    if (STATS) masked_moments<!ck_float(KIND), false>(a, s.fmin, s.fmax, x[j], bits[j], shift, m[j], m[j]);
     if (HLL) {
-      const HllKey key = KIND == CK_I32 ? hll_key_int((uint32_t)bits[j]) : hll_key_long(bits[j]);
+      const HllKey key = ck_bytes(KIND) <= 4 ? hll_key_int((uint32_t)bits[j]) : hll_key_long(bits[j]);
       qmin = min(qmin, key.q);
       if (lane_bit(m[j])) atomicMax(reinterpret_cast<int32_t*>(reinterpret_cast<char*>(regs) + key.addr), key.q);
     }
@@ -418,25 +422,27 @@ __device__ __forceinline__ void numeric_block(const double (&x)[8], const uint64
     if (__builtin_amdgcn_ballot_w64(qmin < 0) != 0) {
 #pragma unroll 1
       for (int j = 0; j < 8; ++j) {
-        if (lane_bit(m[j])) hll_update(regs, KIND == CK_I32 ? xxh64_int((uint32_t)bits[j]) : xxh64_long(bits[j]));
+        if (lane_bit(m[j])) hll_update(regs, ck_bytes(KIND) <= 4 ? xxh64_int((uint32_t)bits[j]) : xxh64_long(bits[j]));
       }
       qmin = 0;
     }
   }
 }
 
-// The checked form of one 512-row block of an fp64 column (a selected NaN / +-inf in it, or the whole range
-// re-run by numeric_range): one row group at a time, values re-read and the selection rebuilt per group -- a
+// The checked form of one 512-row block of a floating-point column (a selected NaN / +-inf in it, or the whole
+// range re-run by numeric_range): one row group at a time, values re-read and the selection rebuilt per group -- a
 // rolled loop whose state is one group's, so it adds no registers to the common path.  NaN rows hash as the
-// canonical NaN (doubleToLongBits) and stay out of min / max (Spark orders NaN above every value) but enter
-// the moments (which become NaN, as Spark's); +-inf rows stay out of the shifted moments and are counted:
-// dq_finish adds them back into the sum (Spark's sequential sum is then +-inf, or NaN with both signs) and
-// the moments become NaN.
-template <bool STATS, bool HLL>
-__device__ __forceinline__ void f64_block_checked(__amdgpu_buffer_rsrc_t vr, const uint32_t* validity,
-                                                  const uint32_t* mask, int64_t base, int32_t rem, int32_t vo,
-                                                  double shift, ColStats& s, LaneMoments& a, int32_t* regs,
-                                                  int64_t& cnt_w, int64_t& nan_v, int64_t& pinf_v, int64_t& ninf_v) {
+// canonical NaN (doubleToLongBits / floatToIntBits) and stay out of min / max (Spark orders NaN above every value)
+// but enter the moments (which become NaN, as Spark's); +-inf rows stay out of the shifted moments and are
+// counted: dq_finish adds them back into the sum (Spark's sequential sum is then +-inf, or NaN with both signs) and
+// the moments become NaN.  KIND: CK_F64 (hashLong of the bits) or CK_F32 (the value widened to double exactly,
+// hashInt of the bits: Spark 2.2's XxHash64 of a FloatType value).
+template <int KIND, bool STATS, bool HLL>
+__device__ __forceinline__ void float_block_checked(__amdgpu_buffer_rsrc_t vr, const uint32_t* validity,
+                                                    const uint32_t* mask, int64_t base, int32_t rem, int32_t vo,
+                                                    double shift, ColStats& s, LaneMoments& a, int32_t* regs,
+                                                    int64_t& cnt_w, int64_t& nan_v, int64_t& pinf_v, int64_t& ninf_v) {
+  constexpr bool kF32 = KIND == CK_F32;
   const int lane = threadIdx.x & 63;
 #pragma unroll 1
   for (int j = 0; j < 8; ++j) {
@@ -451,9 +457,16 @@ __device__ __forceinline__ void f64_block_checked(__amdgpu_buffer_rsrc_t vr, con
       if (mask) mj &= ((uint64_t)(two ? ((const_u32s)mask)[w + 1] : 0u) << 32) | ((const_u32s)mask)[w];
       if (left < 64) mj &= (1ull << left) - 1ull;
     }
-    const auto w2 = __builtin_amdgcn_raw_buffer_load_b64(vr, vo + j * 512, 0, 2 /* nt */);
-    uint64_t b = ((uint64_t)w2[1] << 32) | w2[0];
-    const double xv = __builtin_bit_cast(double, b);
+    uint64_t b;
+    double xv;
+    if constexpr (kF32) {
+      b = __builtin_amdgcn_raw_buffer_load_b32(vr, vo + j * 256, 0, 2 /* nt */);
+      xv = (double)__builtin_bit_cast(float, (uint32_t)b);
+    } else {
+      const auto w2 = __builtin_amdgcn_raw_buffer_load_b64(vr, vo + j * 512, 0, 2 /* nt */);
+      b = ((uint64_t)w2[1] << 32) | w2[0];
+      xv = __builtin_bit_cast(double, b);
+    }
     const uint64_t nf = __builtin_amdgcn_ballot_w64(!__builtin_isfinite(xv)) & mj;
     const uint64_t nanm = __builtin_amdgcn_ballot_w64(xv != xv) & mj;
     const uint64_t inf = nf & ~nanm, pinf = __builtin_amdgcn_ballot_w64(xv > 0.0) & inf;
@@ -470,31 +483,38 @@ __device__ __forceinline__ void f64_block_checked(__amdgpu_buffer_rsrc_t vr, con
       cnt_w += __builtin_popcountll(mj);
     }
     if (HLL) {
-      if (lane_bit(nanm)) b = 0x7FF8000000000000ull;
-      const HllKey key = hll_key_long(b);
+      if (lane_bit(nanm)) b = kF32 ? 0x7FC00000ull : 0x7FF8000000000000ull;
+      const HllKey key = kF32 ? hll_key_int((uint32_t)b) : hll_key_long(b);
       if (lane_bit(mj)) {
         if (key.q >= 0) atomicMax(reinterpret_cast<int32_t*>(reinterpret_cast<char*>(regs) + key.addr), key.q);
-        else hll_update(regs, xxh64_long(b));
+        else hll_update(regs, kF32 ? xxh64_int((uint32_t)b) : xxh64_long(b));
       }
     }
   }
 }
 
-// Numeric column (f64 / i64 / i32): each wave takes 512-row blocks, lane l holding rows
+// Numeric column (f64 / f32 / i64 / i32 / i16 / i8): each wave takes 512-row blocks, lane l holding rows
 // base + 64 j + l (j < 8): coalesced 512-byte (8-byte types) loads per instruction, selection masks
 // in SGPRs.  Per row: stats as shifted sums (STATS), XXH64 + exec-masked LDS register max (HLL).
 //
 // Non-finite fp64 values.  With moments (STATS) the common pass does not classify values at all: a selected
 // NaN / +-inf makes the wave's shifted sums non-finite (as does a finite value whose square overflows), which
 // the workgroup checks at the range's end; if any wave saw one, the workgroup resets its HLL registers and
-// re-runs the range in the checked form (f64_block_checked: canonical NaN hash, +-inf out of the moments,
+// re-runs the range in the checked form (float_block_checked: canonical NaN hash, +-inf out of the moments,
 // counts) -- one VALU per value less on the common path.  Without moments (HLL only) each value is
 // classified (one v_cmp_class) and a block holding a selected non-finite value takes the checked form.
+template <int K> struct KindT { using T = double; };
+template <> struct KindT<CK_I64> { using T = int64_t; };
+template <> struct KindT<CK_I32> { using T = int32_t; };
+template <> struct KindT<CK_F32> { using T = float; };
+template <> struct KindT<CK_I16> { using T = int16_t; };
+template <> struct KindT<CK_I8> { using T = int8_t; };
+
 template <int KIND, bool STATS, bool HLL>
 __device__ void numeric_range(const void* values, const uint32_t* validity, const uint32_t* mask,
                               int64_t row0, int64_t row1, ColStats& s, int32_t* regs) {
-  using T = typename std::conditional<KIND == CK_I32, int32_t, typename std::conditional<KIND == CK_I64, int64_t, double>::type>::type;
-  constexpr bool kLazy = KIND == CK_F64 && STATS;  // non-finite values found from the sums at the range's end
+  using T = typename KindT<KIND>::T;
+  constexpr bool kLazy = ck_float(KIND) && STATS;  // non-finite values found from the sums at the range's end
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const T* v = reinterpret_cast<const T*>(values);
@@ -526,8 +546,15 @@ __device__ void numeric_range(const void* values, const uint32_t* validity, cons
         bits[j] = ((uint64_t)w2[1] << 32) | w2[0];
         if (KIND == CK_F64) x[j] = __builtin_bit_cast(double, bits[j]);
         else x[j] = __builtin_fma((double)(int32_t)w2[1], 4294967296.0, (double)w2[0]);  // exact int64 -> double
-      } else {
-        const int32_t w = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(vr, vo + j * 256, 0, 2 /* nt */);
+      } else if constexpr (KIND == CK_F32) {  // FloatType: Spark's Cast(child, DoubleType) is exact
+        const uint32_t w = __builtin_amdgcn_raw_buffer_load_b32(vr, vo + j * 256, 0, 2 /* nt */);
+        bits[j] = w;
+        x[j] = (double)__builtin_bit_cast(float, w);
+      } else {  // IntegerType / ShortType / ByteType: sign-extending loads (buffer_load_sshort / sbyte)
+        int32_t w;
+        if constexpr (sizeof(T) == 4) w = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(vr, vo + j * 256, 0, 2 /* nt */);
+        else if constexpr (sizeof(T) == 2) w = (int16_t)__builtin_amdgcn_raw_buffer_load_b16(vr, vo + j * 128, 0, 2 /* nt */);
+        else w = (int8_t)__builtin_amdgcn_raw_buffer_load_b8(vr, vo + j * 64, 0, 2 /* nt */);
         bits[j] = (uint64_t)(int64_t)w;
         x[j] = (double)w;
       }
@@ -536,12 +563,13 @@ __device__ void numeric_range(const void* values, const uint32_t* validity, cons
     // HLL-only fp64: one v_cmp_class per value (NaN or +-inf); only their OR stays live on the common path
     // (keeping the 8 masks for the rare path spilled SGPRs into v_writelane / v_readlane on every block)
     uint64_t nf_any = 0;
-    if constexpr (KIND == CK_F64 && !kLazy) {
+    if constexpr (ck_float(KIND) && !kLazy) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) nf_any |= __builtin_amdgcn_ballot_w64(!__builtin_isfinite(x[j])) & m[j];
     }
-    if (KIND == CK_F64 && !kLazy && nf_any != 0) {
-      f64_block_checked<STATS, HLL>(vr, validity, mask, base, rem, vo, shift, s, a, regs, cnt_w, nan_v, pinf_v, ninf_v);
+    if (ck_float(KIND) && !kLazy && nf_any != 0) {
+      float_block_checked<KIND, STATS, HLL>(vr, validity, mask, base, rem, vo, shift, s, a, regs, cnt_w, nan_v, pinf_v,
+                                            ninf_v);
     } else {
 #pragma unroll
       for (int j = 0; j < 8; ++j) cnt_w += __builtin_popcountll(m[j]);
@@ -566,9 +594,9 @@ __device__ void numeric_range(const void* values, const uint32_t* validity, cons
       cnt_w = 0;
       __syncthreads();
       for (int32_t rb = 0; rb < nr; rb += kRowsPerIter) {
-        const int32_t vo = (rb + wave * 512 + lane) * 8;
-        f64_block_checked<STATS, HLL>(vr, validity, mask, row0 + rb + wave * 512, nr - rb - wave * 512, vo, shift, s,
-                                      a, regs, cnt_w, nan_v, pinf_v, ninf_v);
+        const int32_t vo = (rb + wave * 512 + lane) * (int32_t)sizeof(T);
+        float_block_checked<KIND, STATS, HLL>(vr, validity, mask, row0 + rb + wave * 512, nr - rb - wave * 512, vo,
+                                              shift, s, a, regs, cnt_w, nan_v, pinf_v, ninf_v);
       }
     }
   }
@@ -576,19 +604,19 @@ __device__ void numeric_range(const void* values, const uint32_t* validity, cons
     // the wave's moments from its lanes' shifted sums (fixed butterfly order: deterministic); lane 0 holds
     // them, the other lanes only min / max (n = 0: neutral in stats_merge)
     const double S1 = wave_sum_f64(a.sd), S2 = wave_sum_f64(a.sdd);
-    const int64_t is = KIND == CK_F64 ? 0 : wave_sum_i64(a.is);
+    const int64_t is = ck_float(KIND) ? 0 : wave_sum_i64(a.is);
     if (lane == 0 && cnt_w > 0) {
       const double n = (double)cnt_w, q = S1 / n;
       s.n = n;
       s.mean = shift + q;
       const double m2 = __builtin_fma(-S1, q, S2);
       s.m2 = m2 < 0.0 ? 0.0 : m2;  // rounding can leave a constant column's m2 at -ulp; a NaN stays NaN
-      if (KIND == CK_F64) s.sum = __builtin_fma(n, shift, S1);
+      if (ck_float(KIND)) s.sum = __builtin_fma(n, shift, S1);
       else s.isum = is;
     }
   }
   if (lane == 0) s.count += cnt_w;
-  if (KIND == CK_F64 && lane == 0) {
+  if (ck_float(KIND) && lane == 0) {
     s.nan_count += nan_v;
     s.pinf += pinf_v;
     s.ninf += ninf_v;
@@ -979,21 +1007,26 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
     // HLL update is idempotent, so the block's selected rows are simply redone; DataType counts only
     // the rows the fast path skipped.  (Columns with many such rows run the LONG instantiation above.)
     if ((slow | __builtin_amdgcn_ballot_w64(qmin < 0)) != 0) {
-      // the rows the fast path skipped, counted in the wave's LDS slot (no register across the block loop)
-      if (lane == 0) atomicAdd(rare, (uint32_t)__builtin_popcountll(slow));
+      // the rows the fast path skipped, counted per row as the LONG instantiation counts them (`slow` is an OR
+      // over the block's row groups, i.e. lanes, not rows), in the wave's LDS slot (no register across the
+      // block loop)
       block_masks(validity, mask, base, rem, full, m);
+      uint32_t skipped = 0;
 #pragma unroll 1
       for (int j = 0; j < 8; ++j) {
+        bool was_fast = true;
         if (lane_bit(m[j])) {
           const int64_t row = base + j * 64 + lane;
           const int64_t o0 = (int64_t)offsets[row], o1 = (int64_t)offsets[row + 1];
+          was_fast = o1 - o0 <= 28 && o0 - lo <= (int64_t)win3;
           if constexpr (HLL) hll_update(regs, xxh64_bytes(data, o0, o1 - o0));
           if constexpr (DT) {
-            const bool was_fast = o1 - o0 <= 28 && o0 - lo <= (int64_t)win3;
             if (!was_fast) dtc.add(dt_class_bytes(data + o0, o1 - o0), true);
           }
         }
+        skipped += (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(!was_fast));
       }
+      if (lane == 0 && skipped) atomicAdd(rare, skipped);
       qmin = 0;
     }
   }
@@ -1004,22 +1037,46 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
   if constexpr (DT) dtc.flush(s);
 }
 
-// DataType of a double column: Spark casts the value to a string with Double.toString, which is
-// plain decimal (matches FRACTIONAL) iff the value is finite and zero or 1e-3 <= |x| < 1e7, and
-// otherwise "NaN", "Infinity" or computerized scientific notation ("1.0E7": a STRING).  Counts the
-// selected rows (s.count) and the fractional ones (s.isum).
-__device__ void f64_dtype_range(const double* values, const uint32_t* validity, const uint32_t* mask, int64_t row0,
-                                int64_t row1, ColStats& s) {
+// DataType of a double / float column: Spark casts the value to a string with Double.toString /
+// Float.toString, which is plain decimal (matches FRACTIONAL) iff the value is finite and zero or
+// 1e-3 <= |x| < 1e7 (the exact value: the float nearest 1e-3 lies above the double 1e-3, so the test
+// in double is the float's), and otherwise "NaN", "Infinity" or computerized scientific notation
+// ("1.0E7": a STRING).  Counts the selected rows (s.count) and the fractional ones (s.isum).
+template <typename T>
+__device__ void float_dtype_range(const T* values, const uint32_t* validity, const uint32_t* mask, int64_t row0,
+                                  int64_t row1, ColStats& s) {
   uint32_t cnt = 0, frac = 0;
   for (int64_t r = row0 + threadIdx.x; r < row1; r += kBlock) {
     const uint32_t bit = (word_or_ones(validity, r >> 5) & word_or_ones(mask, r >> 5)) >> (r & 31);
     const bool sel = bit & 1u;
-    const double x = __builtin_nontemporal_load(values + r), a = __builtin_fabs(x);
+    const double x = (double)__builtin_nontemporal_load(values + r), a = __builtin_fabs(x);
     cnt += sel;
     frac += sel && (x == 0.0 || (a >= 1e-3 && a < 1e7));
   }
   s.count += cnt;
   s.isum += frac;
+}
+
+// BooleanType column: the selected rows (s.count) and the selected TRUE values (s.isum) from popcounts of the
+// value / validity (& where) words; the workgroup's `any TRUE` / `any FALSE` (ApproxCountDistinct: Spark 2.2
+// hashes a boolean as hashInt(1 / 0), so the registers follow from those two facts) go to flags[0] / flags[1].
+__device__ void bool_range(const uint32_t* values, const uint32_t* validity, const uint32_t* mask, int64_t row0,
+                           int64_t row1, ColStats& s, int32_t* flags) {
+  const int64_t w0 = row0 >> 5, w1 = (row1 + 31) >> 5;  // row0 is a multiple of 2048
+  int64_t c = 0, t = 0;
+  for (int64_t w = w0 + threadIdx.x; w < w1; w += kBlock) {
+    uint32_t sel = word_or_ones(validity, w);
+    if (mask) sel &= mask[w];
+    const int64_t r = w << 5;
+    if (r + 32 > row1) sel &= (1u << (row1 - r)) - 1u;
+    const uint32_t v = values[w];
+    c += __popc(sel);
+    t += __popc(sel & v);
+  }
+  s.count += c;
+  s.isum += t;
+  if (t) flags[0] = 1;
+  if (c > t) flags[1] = 1;
 }
 
 // Only the count of selected rows (Completeness): popcount of validity (& where) words.
@@ -1065,7 +1122,18 @@ __device__ __forceinline__ void run_variant(const ColTask& t, const ScanCols& co
   else if constexpr (V == CV_I32_S) numeric_range<CK_I32, true, false>(v, val, mask, row0, row1, s, regs);
   else if constexpr (V == CV_I32_SH) numeric_range<CK_I32, true, true>(v, val, mask, row0, row1, s, regs);
   else if constexpr (V == CV_I32_H) numeric_range<CK_I32, false, true>(v, val, mask, row0, row1, s, regs);
-  else if constexpr (V == CV_F64_D) f64_dtype_range(reinterpret_cast<const double*>(v), val, mask, row0, row1, s);
+  else if constexpr (V == CV_F32_S) numeric_range<CK_F32, true, false>(v, val, mask, row0, row1, s, regs);
+  else if constexpr (V == CV_F32_SH) numeric_range<CK_F32, true, true>(v, val, mask, row0, row1, s, regs);
+  else if constexpr (V == CV_F32_H) numeric_range<CK_F32, false, true>(v, val, mask, row0, row1, s, regs);
+  else if constexpr (V == CV_I16_S) numeric_range<CK_I16, true, false>(v, val, mask, row0, row1, s, regs);
+  else if constexpr (V == CV_I16_SH) numeric_range<CK_I16, true, true>(v, val, mask, row0, row1, s, regs);
+  else if constexpr (V == CV_I16_H) numeric_range<CK_I16, false, true>(v, val, mask, row0, row1, s, regs);
+  else if constexpr (V == CV_I8_S) numeric_range<CK_I8, true, false>(v, val, mask, row0, row1, s, regs);
+  else if constexpr (V == CV_I8_SH) numeric_range<CK_I8, true, true>(v, val, mask, row0, row1, s, regs);
+  else if constexpr (V == CV_I8_H) numeric_range<CK_I8, false, true>(v, val, mask, row0, row1, s, regs);
+  else if constexpr (V == CV_F64_D) float_dtype_range(reinterpret_cast<const double*>(v), val, mask, row0, row1, s);
+  else if constexpr (V == CV_F32_D) float_dtype_range(reinterpret_cast<const float*>(v), val, mask, row0, row1, s);
+  else if constexpr (V == CV_BOOL) bool_range(reinterpret_cast<const uint32_t*>(v), val, mask, row0, row1, s, regs);
   else if constexpr (V == CV_UTF8_H || V == CV_UTF8_D || V == CV_UTF8_HD)
     utf8_range<int32_t, V != CV_UTF8_D, V != CV_UTF8_H, LONG>(
         reinterpret_cast<const uint8_t*>(v), reinterpret_cast<const int32_t*>(cols.offsets[t.col]), val, mask, row0,
@@ -1100,9 +1168,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kMinWave
                                                          ColPartial* __restrict__ partials,
                                                          uint32_t* __restrict__ hll_acc) {
   constexpr bool kHll = !(V == CV_VALIDITY || V == CV_F64_S || V == CV_I64_S || V == CV_I32_S || V == CV_F64_D ||
-                         V == CV_UTF8_D || V == CV_LUTF8_D);
+                         V == CV_UTF8_D || V == CV_LUTF8_D || V == CV_F32_S || V == CV_I16_S || V == CV_I8_S ||
+                         V == CV_F32_D || V == CV_BOOL);
+  constexpr bool kBool = V == CV_BOOL;  // (its two HLL hashes are constants: flags instead of registers)
   constexpr bool kStr = V == CV_UTF8_H || V == CV_LUTF8_H || V == CV_UTF8_HD || V == CV_LUTF8_HD;
-  __shared__ int32_t regs[kHll ? 512 : 1];  // q = pw - 1, -1 = empty (see hll_q_exact)
+  __shared__ int32_t regs[kHll ? 512 : 2];  // q = pw - 1, -1 = empty (see hll_q_exact); CV_BOOL: any TRUE / FALSE
   __shared__ uint64_t p5[kStr ? 256 : 1];   // b * P5 for the byte rounds of the string hash
   __shared__ uint32_t dfq[kStr ? kWaves * kDefFields * kDefCap : 1];  // deferred 24..28-byte strings
   __shared__ uint32_t rare[kStr ? kWaves : 1];  // per wave: the rows the string fast path skipped
@@ -1113,6 +1183,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kMinWave
   const int64_t row0 = (int64_t)range * rows_per_range;
   int64_t row1 = row0 + rows_per_range;
   if (row1 > n_rows) row1 = n_rows;
+  if constexpr (kBool) {
+    if (threadIdx.x < 2) regs[threadIdx.x] = 0;
+    __syncthreads();
+  }
   if constexpr (kHll) {
     for (int i = threadIdx.x; i < 512; i += kBlock) regs[i] = -1;
     if constexpr (kStr) {
@@ -1133,6 +1207,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kMinWave
       uint32_t r = 0;
       for (int w = 0; w < kWaves; ++w) r += rare[w];
       if (r) atomicAdd(reinterpret_cast<unsigned long long*>(bm.rare_rows + part_base + ti), (unsigned long long)r);
+    }
+  }
+  if constexpr (kBool) {
+    // (block_reduce_store's barrier ordered every thread's flag store before this read)
+    if (threadIdx.x == 0 && t.hll_slot >= 0) {
+      uint32_t* dst = hll_acc + ((size_t)t.hll_slot * kHllCopies + (blockIdx.x % kHllCopies)) * 512;
+      for (int b = 0; b < 2; ++b) {
+        if (!regs[b]) continue;
+        const uint64_t x = xxh64_int(b == 0 ? 1u : 0u);  // hashInt(true -> 1, false -> 0)
+        atomicMax(dst + (uint32_t)(x >> 55), (uint32_t)(hll_q_exact(x) + 1));
+      }
     }
   }
   if constexpr (kHll) {
@@ -1183,10 +1268,6 @@ __device__ __forceinline__ void corr_merge(CorrStats& a, const CorrStats& b) {
 // roots and per-lane counter partials in the wave's LDS scratch.  Counters reach the accumulator by
 // 64-bit integer atomics (order-free, so the result is deterministic).
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ int64_t load_as_int(const void* p, int kind, int64_t row) {
-  if (kind == CK_I64) return reinterpret_cast<const int64_t*>(p)[row];
-  return (int64_t)reinterpret_cast<const int32_t*>(p)[row];
-}
 // Spark comparison of doubles (nanSafeCompare / genEqual): NaN == NaN, NaN > everything.
 __device__ __forceinline__ int cmp_dbl(double a, double b) {
   bool an = a != a, bn = b != b;
@@ -1216,18 +1297,43 @@ struct PredScratch {
   }
 };
 
-// raw values of one column for the block (all 8 row-group loads issued before any is used; i32
-// sign-extended), through a bounds-checked buffer descriptor over the workgroup's rows [row0, row1):
-// rows past row1 read 0
+// raw values of one column for the block (all 8 row-group loads issued before any is used) as 64-bit words:
+// integers sign-extended (i32 / i16 / i8 / date32; a boolean 0 / 1), fp64 bits, f32 as the bits of the exactly
+// widened double -- through a bounds-checked buffer descriptor over the workgroup's rows [row0, row1): rows past
+// row1 read 0
 __device__ __forceinline__ void pred_load(const void* p, int kind, int64_t row0, int64_t row1, int64_t base, int lane,
                                           uint64_t (&v)[8]) {
-  const int sz = kind == CK_I32 ? 4 : 8;
+  if (kind == CK_BOOL) {  // value bits: row r is bit r & 31 of word r >> 5 (row0 is a multiple of 256)
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<char*>(reinterpret_cast<const char*>(p) + (row0 >> 3)), (short)0, (int)(((row1 - row0 + 31) >> 5) * 4),
+        0x00020000);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t w = __builtin_amdgcn_raw_buffer_load_b32(r, (int)(((base - row0) >> 5) + 2 * j + (lane >> 5)) * 4, 0, 0);
+      v[j] = (w >> (lane & 31)) & 1u;
+    }
+    return;
+  }
+  const int sz = ck_bytes(kind);
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<char*>(reinterpret_cast<const char*>(p) + row0 * sz), (short)0, (int)((row1 - row0) * sz), 0x00020000);
   if (kind == CK_I32) {
 #pragma unroll
     for (int j = 0; j < 8; ++j)
       v[j] = (uint64_t)(int64_t)(int32_t)__builtin_amdgcn_raw_buffer_load_b32(r, lane * 4, (int)((base - row0 + 64 * j) * 4), 2);
+  } else if (kind == CK_F32) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      v[j] = __builtin_bit_cast(uint64_t, (double)__builtin_bit_cast(
+                                              float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)((base - row0 + 64 * j + lane) * 4), 0, 2)));
+  } else if (kind == CK_I16) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      v[j] = (uint64_t)(int64_t)(int16_t)__builtin_amdgcn_raw_buffer_load_b16(r, (int)((base - row0 + 64 * j + lane) * 2), 0, 2);
+  } else if (kind == CK_I8) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      v[j] = (uint64_t)(int64_t)(int8_t)__builtin_amdgcn_raw_buffer_load_b8(r, (int)(base - row0 + 64 * j + lane), 0, 2);
   } else {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -1237,7 +1343,7 @@ __device__ __forceinline__ void pred_load(const void* p, int kind, int64_t row0,
   }
 }
 __device__ __forceinline__ double pred_as_double(uint64_t v, int kind) {
-  return kind == CK_F64 ? __builtin_bit_cast(double, v) : (double)(int64_t)v;
+  return ck_float(kind) ? __builtin_bit_cast(double, v) : (double)(int64_t)v;
 }
 
 // validity word of the lane's 32 rows (lanes 0..15: rows base + 32 L .. + 31) through a bounds-checked
@@ -1827,6 +1933,8 @@ hipError_t launch_column_scan(int32_t variant, const ColTask* tasks, int32_t nta
     DQ_V(CV_VALIDITY) DQ_V(CV_F64_S) DQ_V(CV_F64_SH) DQ_V(CV_F64_H) DQ_V(CV_I64_S) DQ_V(CV_I64_SH) DQ_V(CV_I64_H)
     DQ_V(CV_I32_S) DQ_V(CV_I32_SH) DQ_V(CV_I32_H) DQ_V(CV_UTF8_H) DQ_V(CV_LUTF8_H)
     DQ_V(CV_UTF8_D) DQ_V(CV_UTF8_HD) DQ_V(CV_LUTF8_D) DQ_V(CV_LUTF8_HD) DQ_V(CV_F64_D)
+    DQ_V(CV_F32_S) DQ_V(CV_F32_SH) DQ_V(CV_F32_H) DQ_V(CV_I16_S) DQ_V(CV_I16_SH) DQ_V(CV_I16_H)
+    DQ_V(CV_I8_S) DQ_V(CV_I8_SH) DQ_V(CV_I8_H) DQ_V(CV_F32_D) DQ_V(CV_BOOL)
     default: return hipErrorInvalidValue;
   }
 #undef DQ_V

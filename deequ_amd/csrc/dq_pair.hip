@@ -99,16 +99,22 @@ __device__ __forceinline__ uint64_t vbits64_tail(const uint32_t* bm, int64_t bas
   return x;
 }
 
-// raw 64-bit value of element `idx` of a column (fp64 bits, or the integer sign-extended) and its double
+// raw 64-bit value of element `idx` of a column (fp64 bits; f32: the bits of the exactly widened double, Spark's
+// Cast(child, DoubleType); integers sign-extended) and its double
 __device__ __forceinline__ int64_t load_raw(const char* col, int kind, int64_t idx) {
-  if (kind == CK_I32) return reinterpret_cast<const int32_t*>(col)[idx];
-  return reinterpret_cast<const int64_t*>(col)[idx];
+  switch (kind) {
+    case CK_I32: return reinterpret_cast<const int32_t*>(col)[idx];
+    case CK_I16: return reinterpret_cast<const int16_t*>(col)[idx];
+    case CK_I8: return reinterpret_cast<const int8_t*>(col)[idx];
+    case CK_F32: return __builtin_bit_cast(int64_t, (double)reinterpret_cast<const float*>(col)[idx]);
+    default: return reinterpret_cast<const int64_t*>(col)[idx];
+  }
 }
 __device__ __forceinline__ double raw_to_double(int64_t raw, int kind) {
-  if (kind == CK_F64) return __builtin_bit_cast(double, raw);
+  if (ck_float(kind)) return __builtin_bit_cast(double, raw);
   return __builtin_fma((double)(int32_t)(raw >> 32), 4294967296.0, (double)(uint32_t)raw);  // exact int64 -> double
 }
-__device__ __forceinline__ int elem_bytes(int kind) { return kind == CK_I32 ? 4 : 8; }
+__device__ __forceinline__ int elem_bytes(int kind) { return ck_bytes(kind); }
 
 // the shift of a column in a range (pointers at the range's first row, nr rows): the mean of its first 64-row group holding finite selected values
 __device__ double range_shift(const char* col, int kind, const uint32_t* vb, const uint32_t* where, int64_t nr,
@@ -218,7 +224,7 @@ __device__ __forceinline__ void fold(PairAcc& A, const int64_t (&raw)[kPairPos],
           A.lo[k] = hw_min(A.lo[k], x[c]);
           A.hi[k] = hw_max(A.hi[k], x[c]);
         }
-        if constexpr (!F64) A.is[k] = (int64_t)((uint64_t)A.is[k] + (uint64_t)(kind[c] != CK_F64 ? raw[c] : 0));
+        if constexpr (!F64) A.is[k] = (int64_t)((uint64_t)A.is[k] + (uint64_t)(!ck_float(kind[c]) ? raw[c] : 0));
       }
     }
   }
@@ -336,7 +342,7 @@ __device__ __forceinline__ void fold_fast(PairAcc& A, const int64_t (&raw)[kPair
   if constexpr (!F64) {
 #pragma unroll
     for (int k = 0; k < kPairMoments; ++k)
-      if (kind[2 * k] != CK_F64 && lane_bit(m[2 * k])) A.is[k] = (int64_t)((uint64_t)A.is[k] + (uint64_t)raw[2 * k]);
+      if (!ck_float(kind[2 * k]) && lane_bit(m[2 * k])) A.is[k] = (int64_t)((uint64_t)A.is[k] + (uint64_t)raw[2 * k]);
   }
 }
 

@@ -104,17 +104,39 @@ static dq_status cap_error(const char* fmt, ...) {
                        #expr, hipGetErrorString(e_), __FILE__, __LINE__);                          \
   } while (0)
 
-static bool is_numeric(int32_t t) { return t == DQ_TYPE_F64 || t == DQ_TYPE_I64 || t == DQ_TYPE_I32; }
-static bool is_integral(int32_t t) { return t == DQ_TYPE_I64 || t == DQ_TYPE_I32; }
+// Preconditions.isNumeric (Analyzer.scala:322-334): ByteType .. DoubleType (DecimalType: not a GPU column type)
+static bool is_numeric(int32_t t) {
+  return t == DQ_TYPE_F64 || t == DQ_TYPE_I64 || t == DQ_TYPE_I32 || t == DQ_TYPE_F32 || t == DQ_TYPE_I16 ||
+         t == DQ_TYPE_I8;
+}
+static bool is_integral(int32_t t) { return t == DQ_TYPE_I64 || t == DQ_TYPE_I32 || t == DQ_TYPE_I16 || t == DQ_TYPE_I8; }
+static bool is_floating(int32_t t) { return t == DQ_TYPE_F64 || t == DQ_TYPE_F32; }
+static bool is_string(int32_t t) { return t == DQ_TYPE_UTF8 || t == DQ_TYPE_LARGE_UTF8; }
 static int32_t kind_of(int32_t t) {
   switch (t) {
     case DQ_TYPE_F64: return CK_F64;
-    case DQ_TYPE_I64: return CK_I64;
-    case DQ_TYPE_I32: return CK_I32;
+    case DQ_TYPE_I64: case DQ_TYPE_TIMESTAMP: return CK_I64;
+    case DQ_TYPE_I32: case DQ_TYPE_DATE32: return CK_I32;
+    case DQ_TYPE_F32: return CK_F32;
+    case DQ_TYPE_I16: return CK_I16;
+    case DQ_TYPE_I8: return CK_I8;
+    case DQ_TYPE_BOOL: return CK_BOOL;
     case DQ_TYPE_UTF8: return CK_UTF8;
     default: return CK_LUTF8;
   }
 }
+// algorithmic bytes per row (x1000) of a column's value (or UTF8 offset) buffer
+static int64_t value_bytes_x1000(int32_t t) {
+  switch (t) {
+    case DQ_TYPE_I32: case DQ_TYPE_F32: case DQ_TYPE_DATE32: case DQ_TYPE_UTF8: return 4000;
+    case DQ_TYPE_I16: return 2000;
+    case DQ_TYPE_I8: return 1000;
+    case DQ_TYPE_BOOL: return 125;
+    default: return 8000;
+  }
+}
+// (double)(float)v as Java's long -> float conversion rounds it (to nearest, ties to even)
+static double int_as_float(int64_t v) { return (double)(float)v; }
 
 // Where one analyzer's aggregation-result slots come from.
 struct SpecOut {
@@ -279,15 +301,37 @@ struct Lowering {
   }
 
   // column CMP literal, with Spark 2.2 coercions (integral vs decimal exact, anything vs double in double)
-  dq_status emit_col_lit(const Operand& o, int cmp, const Lit& lit) {
+  dq_status emit_col_lit(const Operand& o, int cmp, Lit lit) {
     const dq_column_desc& cd = (*schema)[o.col];
-    if (!is_numeric(cd.type)) return set_error(DQ_E_UNSUPPORTED, "comparison on a non-numeric column (%d)", o.col);
+    const bool boolean = cd.type == DQ_TYPE_BOOL;
+    if (!is_numeric(cd.type) && !boolean)
+      return set_error(DQ_E_UNSUPPORTED, "comparison on a non-numeric column (%d)", o.col);
     PredInstr p{};
     p.op = PO_ATOM_CMP; p.col_a = o.col; p.col_b = -1; p.kind_a = kind_of(cd.type); p.kind_b = 0;
-    p.null_res = o.has_fallback ? lit_cmp_result(cmp, o.fallback, lit) : NR_NULL;
+    Lit fb = o.fallback;
+    if (boolean) {
+      // BooleanType vs a boolean literal (Spark orders false < true); against a number Spark 2.2 rewrites
+      // (BooleanEquality) or casts -- not restated here: the fallback
+      if ((lit.k != Lit::BOOL && lit.k != Lit::NUL) || (o.has_fallback && fb.k != Lit::BOOL && fb.k != Lit::NUL))
+        return set_error(DQ_E_UNSUPPORTED, "boolean column compared with a non-boolean literal");
+      if (lit.k == Lit::BOOL) lit.k = Lit::INT;
+      if (fb.k == Lit::BOOL) fb.k = Lit::INT;
+    } else if (cd.type == DQ_TYPE_F32) {
+      // FloatType vs an integral literal compares in FloatType (the literal cast to float: findTightestCommonType);
+      // vs a decimal or double literal in DoubleType (DecimalPrecision: the decimal cast to double) -- the float
+      // widens to double exactly, so every case is a double compare with the literal rounded accordingly.  A
+      // COALESCE(col, lit) fallback takes the operand's widened type the same way.
+      auto as_float_cmp = [](Lit& l) {
+        if (l.k == Lit::INT || (l.k == Lit::DEC && l.scale == 0)) { l.d = int_as_float(l.i); l.k = Lit::DBL; }
+        else if (l.k == Lit::DEC) { l.d = lit_to_double(l); l.k = Lit::DBL; }
+      };
+      as_float_cmp(lit);
+      if (o.has_fallback) as_float_cmp(fb);
+    }
+    p.null_res = o.has_fallback ? lit_cmp_result(cmp, fb, lit) : NR_NULL;
     if (lit.k == Lit::NUL) { push_const(NR_NULL); return DQ_OK; }
     if (lit.k == Lit::BOOL) return set_error(DQ_E_UNSUPPORTED, "boolean literal compared with a number");
-    if (cd.type == DQ_TYPE_F64 || lit.k == Lit::DBL) {
+    if (is_floating(cd.type) || lit.k == Lit::DBL) {
       p.ctype = CT_DBL; p.cmp = to_cmpop(cmp); p.lit_d = lit_to_double(lit);
     } else if (lit.k == Lit::INT || (lit.k == Lit::DEC && lit.scale == 0)) {
       p.ctype = CT_INT; p.cmp = to_cmpop(cmp); p.lit_i = lit.i;
@@ -390,6 +434,16 @@ struct Lowering {
       }
       case DQ_PRED_LIT_BOOL: push_const(n.i64 ? NR_TRUE : NR_FALSE); return DQ_OK;
       case DQ_PRED_LIT_NULL: push_const(NR_NULL); return DQ_OK;
+      case DQ_PRED_COLUMN: {  // a BooleanType column as a predicate: its value (NULL stays NULL), i.e. col = TRUE
+        if (dq_status s = check_col(n.a)) return s;
+        if ((*schema)[n.a].type != DQ_TYPE_BOOL)
+          return set_error(DQ_E_UNSUPPORTED, "column %d is not a boolean expression", n.a);
+        PredInstr p{};
+        p.op = PO_ATOM_CMP; p.col_a = n.a; p.col_b = -1; p.kind_a = CK_BOOL; p.kind_b = 0;
+        p.null_res = NR_NULL; p.ctype = CT_INT; p.cmp = C_EQ; p.lit_i = 1;
+        out.push_back(p);
+        return DQ_OK;
+      }
       case DQ_PRED_CMP: {
         if (dq_status s = check_idx(n.a)) return s;
         if (dq_status s = check_idx(n.b)) return s;
@@ -419,11 +473,18 @@ struct Lowering {
         if (dq_status s = check_col(ca)) return s;
         if (dq_status s = check_col(cb)) return s;
         int32_t ta = (*schema)[ca].type, tb = (*schema)[cb].type;
-        if (!is_numeric(ta) || !is_numeric(tb)) return set_error(DQ_E_UNSUPPORTED, "comparison of non-numeric columns");
+        const bool bools = ta == DQ_TYPE_BOOL && tb == DQ_TYPE_BOOL;
+        if (!bools && (!is_numeric(ta) || !is_numeric(tb)))
+          return set_error(DQ_E_UNSUPPORTED, "comparison of non-numeric columns");
+        // FloatType vs Int / LongType compares in FloatType (the integer rounded to float), which a double
+        // compare does not restate for integers beyond 2^24: the fallback (ShortType / ByteType are exact)
+        auto wide_int = [](int32_t t) { return t == DQ_TYPE_I32 || t == DQ_TYPE_I64; };
+        if ((ta == DQ_TYPE_F32 && wide_int(tb)) || (tb == DQ_TYPE_F32 && wide_int(ta)))
+          return set_error(DQ_E_UNSUPPORTED, "float column compared with an int / long column");
         PredInstr p{};
         p.op = PO_ATOM_CMP; p.col_a = ca; p.col_b = cb; p.kind_a = kind_of(ta); p.kind_b = kind_of(tb);
         p.null_res = NR_NULL; p.cmp = to_cmpop(cmp);
-        p.ctype = (is_integral(ta) && is_integral(tb)) ? CT_INT : CT_DBL;
+        p.ctype = bools || (is_integral(ta) && is_integral(tb)) ? CT_INT : CT_DBL;
         out.push_back(p);
         return DQ_OK;
       }
@@ -678,7 +739,8 @@ static void plan_pair_wgs(const dq_plan* p, const PairGroup& g, std::vector<Pair
     for (size_t t = 0; t < p->col_tasks.size(); ++t) {
       const ColTask& ct = p->col_tasks[t];
       if (ct.col == g.cols[c] && ct.where == g.where && !fused[t] &&
-          (ct.variant == CV_F64_S || ct.variant == CV_I64_S || ct.variant == CV_I32_S)) {
+          (ct.variant == CV_F64_S || ct.variant == CV_I64_S || ct.variant == CV_I32_S || ct.variant == CV_F32_S ||
+           ct.variant == CV_I16_S || ct.variant == CV_I8_S)) {
         PairWaveTask& w = wg.wave[c % 2];
         const int k = (c - c % 2) / 2;
         w.mom_mask |= 1u << k;
@@ -756,8 +818,8 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
     return DQ_OK;
   };
   auto col_task = [&](int32_t col, int32_t bm, bool stats, bool hll, int32_t& t, bool dtype = false) -> dq_status {
-    // a double column's DataType count is a variant of its own (CV_F64_D)
-    auto key = std::make_tuple(col, bm, dtype && p->schema[col].type == DQ_TYPE_F64 ? 1 : 0);
+    // a double / float column's DataType count is a variant of its own (CV_F64_D / CV_F32_D)
+    auto key = std::make_tuple(col, bm, dtype && is_floating(p->schema[col].type) ? 1 : 0);
     auto it = col_task_of.find(key);
     if (it == col_task_of.end()) {
       if ((int32_t)p->col_tasks.size() >= kMaxColTasks) return cap_error("more than %d column tasks", kMaxColTasks);
@@ -845,8 +907,11 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
         o.col_type = p->schema[s.col_a].type;
         int32_t bm;
         if (dq_status st = bitmap(where_slot, bm)) return st;
-        // integral columns: Long/Int.toString always matches INTEGRAL -> the selected-row count suffices
-        if (dq_status st = col_task(s.col_a, bm, false, false, o.col_task, !is_integral(o.col_type))) return st;
+        // only floating-point and string values need classifying: an integral value's string always matches
+        // INTEGRAL, a boolean's ("true" / "false") BOOLEAN, a date's / timestamp's ("2020-01-31 ...") STRING -- the
+        // selected-row count suffices (dq_finish puts it in the type's class)
+        const bool classify = is_floating(o.col_type) || is_string(o.col_type);
+        if (dq_status st = col_task(s.col_a, bm, false, false, o.col_task, classify)) return st;
         break;
       }
       case DQ_OP_CORRELATION: {
@@ -883,11 +948,21 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
     int32_t type = p->schema[ct.col].type;
     if (hll) ct.hll_slot = p->n_hll++;
     if (dtype && type == DQ_TYPE_F64) ct.variant = CV_F64_D;
+    else if (dtype && type == DQ_TYPE_F32) ct.variant = CV_F32_D;
     else if (!stats && !hll && !dtype) ct.variant = CV_VALIDITY;
     else if (type == DQ_TYPE_UTF8) ct.variant = hll && dtype ? CV_UTF8_HD : (dtype ? CV_UTF8_D : CV_UTF8_H);
     else if (type == DQ_TYPE_LARGE_UTF8) ct.variant = hll && dtype ? CV_LUTF8_HD : (dtype ? CV_LUTF8_D : CV_LUTF8_H);
+    else if (type == DQ_TYPE_BOOL) ct.variant = CV_BOOL;  // (HLL only: a boolean is not numeric)
     else {
-      int base = type == DQ_TYPE_F64 ? CV_F64_S : (type == DQ_TYPE_I64 ? CV_I64_S : CV_I32_S);
+      int base;
+      switch (kind_of(type)) {
+        case CK_F64: base = CV_F64_S; break;
+        case CK_I64: base = CV_I64_S; break;  // (+ TimestampType: hashLong of the micros)
+        case CK_F32: base = CV_F32_S; break;
+        case CK_I16: base = CV_I16_S; break;
+        case CK_I8: base = CV_I8_S; break;
+        default: base = CV_I32_S; break;  // (+ DateType: hashInt of the days)
+      }
       ct.variant = base + (stats && hll ? 1 : (stats ? 0 : 2));
     }
   }
@@ -1116,7 +1191,7 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
   int64_t b1000 = 0;
   for (int c = 0; c < ncols; ++c) {
     int32_t t = p->schema[c].type;
-    if (need_values[c]) b1000 += (t == DQ_TYPE_I32 || t == DQ_TYPE_UTF8) ? 4000 : 8000;  // value or offset bytes
+    if (need_values[c]) b1000 += value_bytes_x1000(t);  // value or offset bytes
     if (need_validity[c] && p->schema[c].nullable) b1000 += 125;
   }
   p->bytes_per_row_x1000 = b1000;
@@ -1126,7 +1201,7 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
       int64_t b = 0;
       for (int c = 0; c < ncols; ++c) {
         int32_t t = p->schema[c].type;
-        if (vals[c]) b += (t == DQ_TYPE_I32 || t == DQ_TYPE_UTF8) ? 4000 : 8000;
+        if (vals[c]) b += value_bytes_x1000(t);
         if (valid[c] && p->schema[c].nullable) b += 125;
       }
       return b;
@@ -1454,7 +1529,7 @@ dq_status dq_plan_create_opts(const dq_analyzer_spec* specs, int32_t n_specs, co
     return set_error(DQ_E_INVALID, "dq_plan_create: bad schema (at most %d columns)", kMaxSchemaCols);
   if (n_pred < 0 || (n_pred > 0 && !pred_pool)) return set_error(DQ_E_INVALID, "dq_plan_create: bad predicate pool");
   for (int32_t c = 0; c < n_cols; ++c)
-    if (schema[c].type < DQ_TYPE_F64 || schema[c].type > DQ_TYPE_LARGE_UTF8)
+    if (schema[c].type < DQ_TYPE_F64 || schema[c].type > DQ_TYPE_MAX)
       return set_error(DQ_E_TYPE, "dq_plan_create: column %d has unknown type %d", c, schema[c].type);
   int ndev = 0;
   HIP_TRY(hipGetDeviceCount(&ndev));
@@ -1915,15 +1990,15 @@ dq_status dq_finish(dq_plan* p, dq_state* out) {
         if (o.has_where) { s.u.ratio.count = pred.t[o.ctr_b]; s.has_value[1] = pred.nn[o.ctr_b] > 0; }
         else { s.u.ratio.count = rows; s.has_value[1] = 1; }
         break;
-      case DQ_OP_SUM:
-        s.u.sum.sum = o.col_type == DQ_TYPE_F64 ? f64_sum(*c) : (double)c->isum;
-        s.integral = o.col_type != DQ_TYPE_F64;
+      case DQ_OP_SUM:  // Spark's Sum: LongType for integral children, DoubleType (each value cast) otherwise
+        s.u.sum.sum = is_floating(o.col_type) ? f64_sum(*c) : (double)c->isum;
+        s.integral = !is_floating(o.col_type);
         s.u.sum.partial = s.integral ? c->isum : 0;
         set1(c->count > 0);
         break;
       case DQ_OP_MEAN:
-        s.u.mean.sum = o.col_type == DQ_TYPE_F64 ? f64_sum(*c) : (double)c->isum;
-        s.integral = o.col_type != DQ_TYPE_F64;
+        s.u.mean.sum = is_floating(o.col_type) ? f64_sum(*c) : (double)c->isum;
+        s.integral = !is_floating(o.col_type);
         s.u.mean.partial = s.integral ? c->isum : 0;
         s.u.mean.count = c->count;
         s.has_value[0] = c->count > 0;
@@ -1965,11 +2040,13 @@ dq_status dq_finish(dq_plan* p, dq_state* out) {
           d.num_fractional = c->isum;
           d.num_integral = c->nan_count;
           d.num_boolean = (int64_t)c->sum;
-        } else if (o.col_type == DQ_TYPE_F64) {
+        } else if (is_floating(o.col_type)) {
           d.num_fractional = c->isum;
-        } else {
+        } else if (is_integral(o.col_type)) {
           d.num_integral = c->count;
-        }
+        } else if (o.col_type == DQ_TYPE_BOOL) {
+          d.num_boolean = c->count;
+        }  // DateType / TimestampType: every value a STRING
         d.num_string = c->count - d.num_fractional - d.num_integral - d.num_boolean;
         set1(true);  // the UDAF result is never NULL
         break;
@@ -2070,7 +2147,7 @@ int64_t dq_plan_variant_bytes_per_row_x1000(const dq_plan* p, int32_t variant) {
     const ColTask& t = p->col_tasks[i];
     if (t.variant != variant) continue;
     const dq_column_desc& cd = p->schema[t.col];
-    if (t.variant != CV_VALIDITY) b += (cd.type == DQ_TYPE_I32 || cd.type == DQ_TYPE_UTF8) ? 4000 : 8000;
+    if (t.variant != CV_VALIDITY) b += value_bytes_x1000(cd.type);
     if (cd.nullable) b += 125;
     if (t.where >= 0) b += 125;
   }
@@ -2096,7 +2173,7 @@ int64_t dq_plan_explain(const dq_analyzer_spec* specs, int32_t n_specs, const dq
   for (int32_t k = 0; k < n_patterns; ++k)
     if (!patterns[k]) return set_error(DQ_E_INVALID, "dq_plan_explain: pattern %d is NULL", k);
   for (int32_t c = 0; c < n_cols; ++c)
-    if (schema[c].type < DQ_TYPE_F64 || schema[c].type > DQ_TYPE_LARGE_UTF8)
+    if (schema[c].type < DQ_TYPE_F64 || schema[c].type > DQ_TYPE_MAX)
       return set_error(DQ_E_TYPE, "dq_plan_explain: column %d has unknown type %d", c, schema[c].type);
   if (cap < 0 || (cap > 0 && !out)) return set_error(DQ_E_INVALID, "dq_plan_explain: bad output buffer");
   std::unique_ptr<dq_plan> holder(new dq_plan());

@@ -21,6 +21,17 @@ _TYPES = {"f64": L.TYPE_F64, "i64": L.TYPE_I64, "i32": L.TYPE_I32, "utf8": L.TYP
           "large_utf8": L.TYPE_LARGE_UTF8}
 
 
+def _gpu_type(dtype: str) -> int:
+    """The grouping / quantile kernels' column type; the round-6 scan types (f32, i16, i8, bool, date32,
+    timestamp) are not theirs: such an analyzer stays on the Spark fallback."""
+    t = _TYPES.get(dtype)
+    if t is None:
+        from .metrics import UnsupportedOnGpuPathException
+
+        raise UnsupportedOnGpuPathException(f"column type {dtype} is not a grouping / quantile GPU column type")
+    return t
+
+
 class FreqTable:
     """Owner of a device dq_freq_table (sorted distinct keys + counts)."""
 
@@ -65,7 +76,7 @@ def build_frequencies(data, columns: Sequence[str]) -> "FrequenciesAndNumRows":
 
     chunks = _chunks(data)
     schema = {name: dt for name, dt, _ in chunks[0].schema}
-    types = (ctypes.c_int32 * len(columns))(*[_TYPES[schema[c]] for c in columns])
+    types = (ctypes.c_int32 * len(columns))(*[_gpu_type(schema[c]) for c in columns])
     views = (L.ColumnView * max(1, len(chunks) * len(columns)))()
     rows = (ctypes.c_int64 * max(1, len(chunks)))()
     for k, t in enumerate(chunks):
@@ -241,7 +252,7 @@ class MutualInformation(FrequencyBasedAnalyzer):  # MutualInformation.scala:32-8
 
         chunks = _chunks(data)
         schema = {name: dt for name, dt, _ in chunks[0].schema}
-        types = (ctypes.c_int32 * 2)(*[_TYPES[schema[c]] for c in self.columns])
+        types = (ctypes.c_int32 * 2)(*[_gpu_type(schema[c]) for c in self.columns])
         views = (L.ColumnView * max(1, 2 * len(chunks)))()
         rows = (ctypes.c_int64 * max(1, len(chunks)))()
         for k, t in enumerate(chunks):

@@ -14,7 +14,8 @@ from typing import Dict, List, Sequence
 
 from . import _lib as L
 
-_FORMAT_DTYPE = {"g": "f64", "l": "i64", "i": "i32", "u": "utf8", "U": "large_utf8"}
+_FORMAT_DTYPE = {"g": "f64", "l": "i64", "i": "i32", "u": "utf8", "U": "large_utf8", "f": "f32", "s": "i16",
+                 "c": "i8", "b": "bool", "tdD": "date32"}  # + "tsu:<tz>" -> timestamp
 
 
 class ArrowSchemaC(ctypes.Structure):
@@ -98,7 +99,10 @@ def arrow_schema(batch) -> List[tuple]:
     out = []
     for f in batch.schema:
         dt = {pa.float64(): "f64", pa.int64(): "i64", pa.int32(): "i32", pa.string(): "utf8",
-              pa.large_string(): "large_utf8"}.get(f.type)
+              pa.large_string(): "large_utf8", pa.float32(): "f32", pa.int16(): "i16", pa.int8(): "i8",
+              pa.bool_(): "bool", pa.date32(): "date32"}.get(f.type)
+        if dt is None and pa.types.is_timestamp(f.type) and f.type.unit == "us":
+            dt = "timestamp"
         if dt is None:
             raise TypeError(f"column {f.name}: Arrow type {f.type} is not a GPU column type")
         out.append((f.name, dt, f.nullable))

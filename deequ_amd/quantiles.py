@@ -26,7 +26,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 from . import _lib as L
 from .analyzers import Analyzer, Preconditions, data_schema
-from .grouping import _TYPES, _java_double_to_string
+from .grouping import _gpu_type, _java_double_to_string
 from .metrics import (DoubleMetric, EmptyStateException, Entity, Failure, IllegalAnalyzerParameterException,
                       KeyedDoubleMetric, Success, UnsupportedOnGpuPathException, wrap_if_necessary)
 from .states import State
@@ -58,7 +58,7 @@ def device_quantiles(data, column: str, quantiles: Sequence[float], relative_err
         res = (ctypes.c_double * len(part))()
         cnt = ctypes.c_int64()
         stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-        L.check(L.lib.dq_approx_quantiles(_TYPES[schema[column]], views, rows, len(chunks), q, len(part),
+        L.check(L.lib.dq_approx_quantiles(_gpu_type(schema[column]), views, rows, len(chunks), q, len(part),
                                           float(relative_error), torch.cuda.current_device(), stream, res,
                                           ctypes.byref(cnt)))
         n_total = cnt.value
@@ -271,7 +271,7 @@ def _digest_samples(data, column: str, rel: float):
     rks = (ctypes.c_int64 * max(1, cap))()
     m, cnt = ctypes.c_int64(), ctypes.c_int64()
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    rc = L.lib.dq_quantile_digest(_TYPES[schema[column]], views, rows, len(chunks), rel, torch.cuda.current_device(),
+    rc = L.lib.dq_quantile_digest(_gpu_type(schema[column]), views, rows, len(chunks), rel, torch.cuda.current_device(),
                                   stream, vals, rks, cap, ctypes.byref(m), ctypes.byref(cnt))
     if rc == L.DQ_E_INVALID and m.value > cap:
         raise UnsupportedOnGpuPathException(
@@ -304,7 +304,7 @@ def _rank_select(data, column: str):
         res = (ctypes.c_double * len(qs))()
         cnt = ctypes.c_int64()
         stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-        L.check(L.lib.dq_approx_quantiles(_TYPES[schema[column]], views, rows, len(chunks), q, len(qs), 0.0,
+        L.check(L.lib.dq_approx_quantiles(_gpu_type(schema[column]), views, rows, len(chunks), q, len(qs), 0.0,
                                           torch.cuda.current_device(), stream, res, ctypes.byref(cnt)))
         return cnt.value, list(res[:len(qs)])
 

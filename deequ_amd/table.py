@@ -1,7 +1,7 @@
 """HBM-resident columnar tables (Arrow physical layout) handed to the scan.
 
 A Column owns device buffers (torch CUDA/HIP tensors are used purely as device allocations):
-values (f64 / i64 / i32, or UTF-8 bytes), an optional LSB-first validity bitmap, and int32
+values (f64 / f32 / i64 / i32 / i16 / i8 / date32 / timestamp, bit-packed bool, or UTF-8 bytes), an optional LSB-first validity bitmap, and int32
 (utf8) / int64 (large_utf8) offsets.  Buffers are allocated with the padding dqscan.h requires:
 values 16-byte aligned, bitmaps readable in whole 32-bit words, UTF-8 data readable up to the
 next 4-byte boundary past the last string.
@@ -16,9 +16,14 @@ import numpy as np
 from . import _lib as L
 
 DTYPES = {"f64": L.TYPE_F64, "i64": L.TYPE_I64, "i32": L.TYPE_I32, "utf8": L.TYPE_UTF8,
-          "large_utf8": L.TYPE_LARGE_UTF8}
-NUMERIC = ("f64", "i64", "i32")
-_NP = {"f64": np.float64, "i64": np.int64, "i32": np.int32}
+          "large_utf8": L.TYPE_LARGE_UTF8, "f32": L.TYPE_F32, "i16": L.TYPE_I16, "i8": L.TYPE_I8,
+          "bool": L.TYPE_BOOL, "date32": L.TYPE_DATE32, "timestamp": L.TYPE_TIMESTAMP}
+# Preconditions.isNumeric (Analyzer.scala:322-334): ByteType .. DoubleType
+NUMERIC = ("f64", "i64", "i32", "f32", "i16", "i8")
+# fixed-width physical layouts (bool: bit-packed values; date32: int32 days since 1970-01-01; timestamp: int64 us)
+_NP = {"f64": np.float64, "i64": np.int64, "i32": np.int32, "f32": np.float32, "i16": np.int16, "i8": np.int8,
+       "date32": np.int32, "timestamp": np.int64}
+FIXED = tuple(_NP) + ("bool",)
 
 
 def _torch():
@@ -95,7 +100,10 @@ class Table:
             vals = list(vals)
             valid = np.array([v is not None for v in vals], dtype=bool)
             nl = True if nullable is None else nullable.get(name, True)
-            if dtype in NUMERIC:
+            if dtype == "bool":
+                arr = np.array([False if v is None else bool(v) for v in vals], dtype=bool)
+                cols.append(column_from_numpy(name, dtype, arr, valid, device=device, nullable=nl))
+            elif dtype in FIXED:
                 arr = np.array([0 if v is None else v for v in vals], dtype=_NP[dtype])
                 cols.append(column_from_numpy(name, dtype, arr, valid, device=device, nullable=nl))
             else:
@@ -107,9 +115,14 @@ class Table:
 def column_from_numpy(name: str, dtype: str, values: np.ndarray, valid: Optional[np.ndarray] = None,
                       device: str = "cuda", nullable: bool = True) -> Column:
     torch = _torch()
-    values = np.ascontiguousarray(values, dtype=_NP[dtype])
-    n = len(values)
-    raw = _pad_u8(values.view(np.uint8), 16, 16)
+    if dtype == "bool":  # Arrow boolean: LSB-first bit-packed values, read as whole 32-bit words
+        n = len(values)
+        raw = pack_validity(np.asarray(values, dtype=bool))
+        raw = _pad_u8(raw, 16, 16)
+    else:
+        values = np.ascontiguousarray(values, dtype=_NP[dtype])
+        n = len(values)
+        raw = _pad_u8(values.view(np.uint8), 16, 16)
     vt = torch.from_numpy(raw).to(device)
     bt = None
     if valid is not None and nullable:

@@ -31,11 +31,12 @@
 extern "C" {
 #endif
 
-#define DQ_ABI_VERSION 4  /* 2: dq_state.reserved[0] = integral flag + Sum / Mean int64 partials; ingestion, pool and state-array entry points;
+#define DQ_ABI_VERSION 5  /* 2: dq_state.reserved[0] = integral flag + Sum / Mean int64 partials; ingestion, pool and state-array entry points;
                              3: dq_plan_create_opts (predicate-pass mode), dq_plan_create_time, dq_plan_explain, dq_quantile_digest;
                              4: any number of analyzers / columns per plan (split into fused plans over the
                                 per-plan capacities), AUTO compiles the predicate kernel in the background,
-                                dq_plan_pred_wait */
+                                dq_plan_pred_wait;
+                             5: column types F32 / I16 / I8 / BOOL / DATE32 / TIMESTAMP (scan, predicates, Arrow import) */
 
 typedef int32_t dq_status;
 #define DQ_OK 0
@@ -46,14 +47,28 @@ typedef int32_t dq_status;
 #define DQ_E_OOM (-5)         /* device allocation failed */
 #define DQ_E_STATE (-6)       /* state algebra misuse (op mismatch, bad byte image) */
 
-/* Column physical types (Arrow layouts). */
+/* Column physical types (Arrow layouts) and the Spark SQL types they carry.  The numeric types are the ones
+ * Preconditions.isNumeric accepts (analyzers/Analyzer.scala:322-334; DecimalType stays on the fallback):
+ * F64 / F32 / I64 / I32 / I16 / I8.  Values are converted to double exactly as Spark casts them (Sum of an
+ * integral type is Spark's wrapping LongType sum); ApproxCountDistinct hashes each type as Spark 2.2's
+ * XxHash64Function does: hashLong for LongType / TimestampType / DoubleType (doubleToLongBits), hashInt for
+ * IntegerType / ShortType / ByteType / DateType (the value widened to int), FloatType (floatToIntBits) and
+ * BooleanType (1 / 0).  BOOL / DATE32 / TIMESTAMP are not numeric: Completeness, Size, ApproxCountDistinct,
+ * DataType and IS [NOT] NULL atoms (BOOL also = / != against TRUE / FALSE). */
 enum dq_type {
   DQ_TYPE_F64 = 1,        /* DoubleType: 8-byte values */
   DQ_TYPE_I64 = 2,        /* LongType: 8-byte values */
   DQ_TYPE_I32 = 3,        /* IntegerType: 4-byte values */
   DQ_TYPE_UTF8 = 4,       /* StringType: int32 offsets[n+1] + data bytes */
-  DQ_TYPE_LARGE_UTF8 = 5  /* StringType with int64 offsets[n+1] (chunks > 2 GiB) */
+  DQ_TYPE_LARGE_UTF8 = 5, /* StringType with int64 offsets[n+1] (chunks > 2 GiB) */
+  DQ_TYPE_F32 = 6,        /* FloatType: 4-byte values */
+  DQ_TYPE_I16 = 7,        /* ShortType: 2-byte values */
+  DQ_TYPE_I8 = 8,         /* ByteType: 1-byte values */
+  DQ_TYPE_BOOL = 9,       /* BooleanType: LSB-first bit-packed values (Arrow `b`), bit 0 = row 0 of the chunk */
+  DQ_TYPE_DATE32 = 10,    /* DateType: int32 days since 1970-01-01 (Arrow `tdD`) */
+  DQ_TYPE_TIMESTAMP = 11  /* TimestampType: int64 microseconds since the epoch (Arrow `tsu:<timezone>`) */
 };
+#define DQ_TYPE_MAX 11
 
 /* Analyzer ops: the GPU-eligible ScanShareableAnalyzers. */
 enum dq_op {
@@ -186,8 +201,10 @@ typedef struct dq_host_column {
   int32_t validity_bit;    /* 0..7: dq_upload shifts the bitmap so that row 0 lands on bit 0 */
   int32_t reserved;
 } dq_host_column;
-/* Map an exported Arrow array (formats g = float64, l = int64, i = int32, u = utf8, U = large_utf8) to
- * host column buffers; slices at any row offset are rebased by dq_upload.  DQ_E_UNSUPPORTED: other
+/* Map an exported Arrow array (formats g = float64, f = float32, l = int64, i = int32, s = int16, c = int8,
+ * b = boolean, tdD = date32, tsu:<tz> = timestamp[us], u = utf8, U = large_utf8) to host column buffers; slices
+ * at any row offset are rebased by dq_upload (a boolean slice's value bits are shifted like its validity:
+ * validity_bit holds the slice's bit offset of both bitmaps).  DQ_E_UNSUPPORTED: other
  * types, nested / dictionary arrays.  DQ_E_INVALID: a required buffer is NULL (an empty array may
  * export NULL buffers: it maps to an empty column). */
 dq_status dq_arrow_import(const struct ArrowSchema* schema, const struct ArrowArray* array, dq_host_column* out);

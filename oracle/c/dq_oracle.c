@@ -23,7 +23,9 @@
 #include <omp.h>
 #endif
 
-enum { K_F64 = 1, K_I64 = 2, K_I32 = 3, K_UTF8 = 4, K_LARGE_UTF8 = 5 };
+enum { K_F64 = 1, K_I64 = 2, K_I32 = 3, K_UTF8 = 4, K_LARGE_UTF8 = 5,
+       /* round 6: FloatType, ShortType, ByteType, BooleanType (LSB-first bit-packed values) */
+       K_F32 = 6, K_I16 = 7, K_I8 = 8, K_BOOL = 9 };
 
 #define P1 0x9E3779B185EBCA87ULL
 #define P2 0xC2B2AE3D27D4EB4FULL
@@ -92,11 +94,25 @@ uint64_t dqo_xxh64_bytes(const uint8_t* p, int64_t n, uint64_t seed) {
 
 static inline int bit(const uint8_t* bm, int64_t i) { return bm ? (bm[i >> 3] >> (i & 7)) & 1 : 1; }
 
+static inline int is_float(int kind) { return kind == K_F64 || kind == K_F32; }
+static inline int is_num(int kind) { return kind != K_UTF8 && kind != K_LARGE_UTF8 && kind != K_BOOL; }
+/* an integral value widened to long (Spark's Sum of Byte / Short / Int / Long is a LongType sum) */
+static inline int64_t as_long(int kind, const void* v, int64_t i) {
+  switch (kind) {
+    case K_I64: return ((const int64_t*)v)[i];
+    case K_I16: return ((const int16_t*)v)[i];
+    case K_I8: return ((const int8_t*)v)[i];
+    case K_BOOL: return bit((const uint8_t*)v, i);
+    default: return ((const int32_t*)v)[i];
+  }
+}
+/* Cast(child, DoubleType): exact for every type here (a float widens exactly) */
 static inline double as_double(int kind, const void* v, int64_t i) {
   switch (kind) {
     case K_F64: return ((const double*)v)[i];
+    case K_F32: return (double)((const float*)v)[i];
     case K_I64: return (double)((const int64_t*)v)[i];
-    default: return (double)((const int32_t*)v)[i];
+    default: return (double)as_long(kind, v, i);
   }
 }
 
@@ -124,9 +140,8 @@ static void stats_partial(int kind, const void* values, const uint8_t* validity,
     if (!bit(validity, i) || !bit(mask, i)) continue;
     double x = as_double(kind, values, i);
     s->count++;
-    if (kind == K_F64) s->sum_f64 += x;
-    else s->sum_i64 = (int64_t)((uint64_t)s->sum_i64 + (uint64_t)(kind == K_I64 ? ((const int64_t*)values)[i]
-                                                                            : (int64_t)((const int32_t*)values)[i]));
+    if (is_float(kind)) s->sum_f64 += x;
+    else s->sum_i64 = (int64_t)((uint64_t)s->sum_i64 + (uint64_t)as_long(kind, values, i));
     /* CentralMomentAgg.updateExpressions */
     double newN = s->n + 1.0;
     double delta = x - s->avg;
@@ -134,14 +149,14 @@ static void stats_partial(int kind, const void* values, const uint8_t* validity,
     s->avg = s->avg + deltaN;
     s->m2 = s->m2 + delta * (delta - deltaN);
     s->n = newN;
-    if (kind == K_F64) {
+    if (is_float(kind)) {
       if (first) { s->min = x; s->max = x; }
       else {
         if (nan_safe_lt(x, s->min)) s->min = x;
         if (nan_safe_lt(s->max, x)) s->max = x;
       }
     } else {
-      int64_t iv = kind == K_I64 ? ((const int64_t*)values)[i] : (int64_t)((const int32_t*)values)[i];
+      int64_t iv = as_long(kind, values, i);
       if (first) { s->imin = iv; s->imax = iv; }
       else {
         if (iv < s->imin) s->imin = iv;
@@ -167,7 +182,7 @@ static void stats_merge(int kind, dqo_col_stats* a, const dqo_col_stats* b) {
     } else {
       a->sum_f64 += b->sum_f64;
       a->sum_i64 = (int64_t)((uint64_t)a->sum_i64 + (uint64_t)b->sum_i64);
-      if (kind == K_F64) {
+      if (is_float(kind)) {
         if (nan_safe_lt(b->min, a->min)) a->min = b->min;
         if (nan_safe_lt(a->max, b->max)) a->max = b->max;
       } else {
@@ -180,7 +195,7 @@ static void stats_merge(int kind, dqo_col_stats* a, const dqo_col_stats* b) {
 }
 
 static void stats_finish(int kind, dqo_col_stats* s) {
-  if (kind != K_F64) {
+  if (!is_float(kind)) {
     s->sum_f64 = (double)s->sum_i64;
     s->min = (double)s->imin;
     s->max = (double)s->imax;
@@ -258,7 +273,15 @@ static inline uint64_t hash_row(int kind, const void* values, const void* offset
       return dqo_xxh64_long(bits, 42);
     }
     case K_I64: return dqo_xxh64_long(((const int64_t*)values)[i], 42);
-    case K_I32: return dqo_xxh64_int(((const int32_t*)values)[i], 42);
+    case K_I32: case K_I16: case K_I8: case K_BOOL:  /* hashInt of the value widened to int (boolean: 1 / 0) */
+      return dqo_xxh64_int((int32_t)as_long(kind, values, i), 42);
+    case K_F32: {  /* hashInt(java.lang.Float.floatToIntBits(f)): every NaN as 0x7fc00000 */
+      float f = ((const float*)values)[i];
+      int32_t bits;
+      if (f != f) bits = 0x7FC00000;
+      else memcpy(&bits, &f, 4);
+      return dqo_xxh64_int(bits, 42);
+    }
     case K_UTF8: {
       const int32_t* o = (const int32_t*)offsets;
       return dqo_xxh64_bytes((const uint8_t*)values + o[i], o[i + 1] - o[i], 42);
@@ -309,7 +332,7 @@ void dqo_profile_scan(int ncols, const int* kinds, const void* const* values, co
   for (int p = 0; p < nparts; ++p) {
     int64_t lo = part_bound(n, p, nparts), hi = part_bound(n, p + 1, nparts);
     for (int c = 0; c < ncols; ++c) {
-      if (kinds[c] == K_F64 || kinds[c] == K_I64 || kinds[c] == K_I32)
+      if (is_num(kinds[c]))
         stats_partial(kinds[c], values[c], validity[c], NULL, lo, hi, &parts[(size_t)p * ncols + c]);
       else {
         dqo_col_stats* s = &parts[(size_t)p * ncols + c];
@@ -327,12 +350,12 @@ void dqo_profile_scan(int ncols, const int* kinds, const void* const* values, co
     uint8_t* r = out_regs + (size_t)c * 512;
     memset(r, 0, 512);
     for (int p = 0; p < nparts; ++p) {
-      if (kinds[c] == K_F64 || kinds[c] == K_I64 || kinds[c] == K_I32) stats_merge(kinds[c], &acc, &parts[(size_t)p * ncols + c]);
+      if (is_num(kinds[c])) stats_merge(kinds[c], &acc, &parts[(size_t)p * ncols + c]);
       else acc.count += parts[(size_t)p * ncols + c].count;
       const uint8_t* pr = pregs + ((size_t)p * ncols + c) * 512;
       for (int i = 0; i < 512; ++i) if (pr[i] > r[i]) r[i] = pr[i];
     }
-    if (kinds[c] == K_F64 || kinds[c] == K_I64 || kinds[c] == K_I32) stats_finish(kinds[c], &acc);
+    if (is_num(kinds[c])) stats_finish(kinds[c], &acc);
     out_stats[c] = acc;
   }
   free(parts);

@@ -616,9 +616,35 @@ def merge_states(*states):
 # --------------------------------------------------------------------------------------
 
 
+INTEGRAL = ("i64", "i32", "i16", "i8")  # LongType, IntegerType, ShortType, ByteType
+FLOATING = ("f64", "f32")                # DoubleType, FloatType
+
+
+def int_to_f32(v: int) -> float:
+    """(float) v as Java's int / long -> float conversion rounds it (nearest, ties to even), exactly."""
+    a = abs(int(v))
+    nb = a.bit_length()
+    if nb <= 24:
+        return float(v)
+    shift = nb - 24
+    q, r = divmod(a, 1 << shift)
+    half = 1 << (shift - 1)
+    if r > half or (r == half and q & 1):
+        q += 1
+    return math.copysign(float(q << shift), v)
+
+
+def float_to_int_bits(f: float) -> int:
+    """java.lang.Float.floatToIntBits (every NaN as 0x7fc00000), as a signed int."""
+    if f != f:
+        return 0x7FC00000
+    return struct.unpack("<i", struct.pack("<f", f))[0]
+
+
 @dataclass
 class OColumn:
-    """A column for the oracle: dtype in {f64,i64,i32,utf8}; values + boolean validity."""
+    """A column for the oracle: dtype in {f64, f32, i64, i32, i16, i8, bool, date32, timestamp, utf8}; values +
+    boolean validity (bool: a bool array; date32: int32 days; timestamp: int64 microseconds, UTC)."""
 
     dtype: str
     values: object  # np.ndarray for numerics, list[bytes|None] for utf8
@@ -812,11 +838,17 @@ class OracleExpr:
             c = cols[e[1]]
             if c.dtype == "f64":
                 return [float(x) for x in c.values], "dbl", c.valid.copy()
-            if c.dtype in ("i64", "i32"):
+            if c.dtype == "f32":  # FloatType: compared in float against integers, in double otherwise
+                return [float(x) for x in c.values], "flt", c.valid.copy()
+            if c.dtype in INTEGRAL:
                 return [int(x) for x in c.values], "int", c.valid.copy()
+            if c.dtype == "bool":
+                return [bool(x) for x in c.values], "bool", c.valid.copy()
             if c.dtype == "utf8":
                 return list(c.values), "str", c.valid.copy()
-            raise ValueError(c.dtype)
+            if c.dtype in ("date32", "timestamp"):  # only their NULLs are read (IS [NOT] NULL)
+                return [int(x) for x in c.values], c.dtype, c.valid.copy()
+            raise NotImplementedError(c.dtype)
         if kind == "coalesce":
             parts = [self._ev(a, cols, n) for a in e[1]]
             typ = _widen([p[1] for p in parts if p[1] != "null"])
@@ -832,6 +864,8 @@ class OracleExpr:
             op = e[1]
             av, at, an = self._ev(e[2], cols, n)
             bv, bt, bn = self._ev(e[3], cols, n)
+            if {at, bt} & {"date32", "timestamp"}:
+                raise NotImplementedError("date / timestamp comparison")  # outside the restated grammar
             if at == "str" or bt == "str":
                 if at != bt:
                     raise NotImplementedError("string/number comparison")
@@ -925,15 +959,21 @@ class NpPredicate:
             dtype, vals, valid = cols[e[1]]
             if dtype == "f64":
                 return "dbl", np.asarray(vals, dtype=np.float64), np.asarray(valid, dtype=bool)
-            if dtype in ("i64", "i32"):
+            if dtype == "f32":
+                return "flt", np.asarray(vals, dtype=np.float32).astype(np.float64), np.asarray(valid, dtype=bool)
+            if dtype in INTEGRAL:
                 return "int", np.asarray(vals, dtype=np.int64), np.asarray(valid, dtype=bool)
+            if dtype == "bool":
+                return "bool", np.asarray(vals, dtype=bool), np.asarray(valid, dtype=bool)
+            if dtype in ("date32", "timestamp"):  # only their NULLs are read (IS [NOT] NULL)
+                return dtype, np.asarray(vals, dtype=np.int64), np.asarray(valid, dtype=bool)
             raise NotImplementedError(dtype)
         if kind == "coalesce":
             parts = [self._ev(a, cols, n) for a in e[1]]
             typ = _widen([p[0] for p in parts if p[0] != "null"])
             if typ in ("int", "dec"):
                 vals, np_t = np.zeros(n, dtype=np.int64), np.int64
-            elif typ == "dbl":
+            elif typ in ("dbl", "flt"):
                 vals, np_t = np.zeros(n, dtype=np.float64), np.float64
             else:
                 raise NotImplementedError(typ)
@@ -946,6 +986,8 @@ class NpPredicate:
                         raise NotImplementedError("non-integral decimal in COALESCE over an integral column")
                     pv = int(pv)
                 take = ~nn & pn
+                if typ == "flt" and not isinstance(pv, np.ndarray):  # an integer literal cast to float
+                    pv = int_to_f32(int(pv)) if pk == "int" else float(pv)
                 src = np.broadcast_to(np.asarray(float(pv) if typ == "dbl" and not isinstance(pv, np.ndarray) else pv,
                                                  dtype=np_t), (n,))
                 vals[take] = src[take].astype(np_t)
@@ -958,8 +1000,16 @@ class NpPredicate:
             nn = an & bn
             if ak == "null" or bk == "null":
                 return "bool", np.zeros(n, dtype=bool), np.zeros(n, dtype=bool)
+            if {ak, bk} & {"date32", "timestamp"}:
+                raise NotImplementedError("date / timestamp comparison")
             if "dbl" in (ak, bk):
                 return "bool", _np_cmp_dbl(op, _as_f64(av), _as_f64(bv)) & nn, nn
+            if "flt" in (ak, bk):  # FloatType: integers rounded to float, decimals to double (_widen)
+                av, bv = _flt_operand(ak, av, bk), _flt_operand(bk, bv, ak)
+                return "bool", _np_cmp_dbl(op, _as_f64(av), _as_f64(bv)) & nn, nn
+            if ak == "bool" or bk == "bool":  # boolean vs boolean: false < true
+                av = np.asarray(av).astype(np.int64) if isinstance(av, np.ndarray) else int(av)
+                bv = np.asarray(bv).astype(np.int64) if isinstance(bv, np.ndarray) else int(bv)
             return "bool", _np_cmp_exact(op, av, bv, n) & nn, nn
         if kind == "in":
             ak, av, an = self._ev(e[1], cols, n)
@@ -992,6 +1042,18 @@ class NpPredicate:
 
 def _as_f64(v):
     return v.astype(np.float64) if isinstance(v, np.ndarray) else np.float64(float(v))
+
+
+def _flt_operand(kind, v, other):
+    """An operand of a comparison with a FloatType side, as the double Spark compares: integers (ShortType /
+    ByteType columns: exact; literals: rounded) cast to float, unless the other side is a decimal (double)."""
+    if kind == "int" and other != "dec":
+        if isinstance(v, np.ndarray):
+            return v.astype(np.float32).astype(np.float64)  # (|v| < 2^24 for i16 / i8: exact)
+        return int_to_f32(int(v))
+    if isinstance(v, np.ndarray):
+        return v
+    return float(v)
 
 
 def _np_cmp_dbl(op, x, y):
@@ -1035,13 +1097,18 @@ def _np_cmp_exact(op, x, y, n):
 
 
 def _widen(types):
+    """Spark 2.2's common type of a comparison / COALESCE: findTightestCommonType over the numeric precedence
+    (int < float < double; an integer literal against a FloatType column is cast to float), DecimalPrecision
+    (a decimal with a float / double: double; with an integer: decimal)."""
     types = [t for t in types if t != "null"]
     if not types:
         return "null"
-    if "dbl" in types:
+    if "dbl" in types or ("flt" in types and "dec" in types):
         return "dbl"
     if "dec" in types:
         return "dec"
+    if "flt" in types:
+        return "flt"
     if "bool" in types:
         return "bool"
     if "str" in types:
@@ -1054,6 +1121,8 @@ def _coerce(v, frm, to):
 
     if v is None:
         return None
+    if to == "flt":
+        return float(v) if frm == "flt" else int_to_f32(int(v))
     if to == "dbl":
         return float(v)
     if to == "dec":
@@ -1086,7 +1155,8 @@ def _partitions(n: int, n_partitions: int):
 
 
 def _as_double_list(c: OColumn):
-    if c.dtype == "f64":
+    """Cast(child, DoubleType) of every value (exact for float and every integral type)."""
+    if c.dtype in FLOATING:
         return [float(x) for x in c.values]
     return [float(int(x)) for x in c.values]
 
@@ -1160,7 +1230,7 @@ def spark_sum(c: OColumn, sel: np.ndarray, n_partitions: int = 1):
     for lo, hi in _partitions(len(sel), n_partitions):
         if not sel[lo:hi].any():
             continue
-        if c.dtype in ("i64", "i32"):
+        if c.dtype in INTEGRAL:  # Sum of an integral child: LongType (wrapping)
             s = 0
             for i in range(lo, hi):
                 if sel[i]:
@@ -1173,7 +1243,7 @@ def spark_sum(c: OColumn, sel: np.ndarray, n_partitions: int = 1):
         parts.append(s)
     tot = parts[0]
     for p in parts[1:]:
-        tot = to_i64(tot + p) if c.dtype in ("i64", "i32") else tot + p
+        tot = to_i64(tot + p) if c.dtype in INTEGRAL else tot + p
     return float(tot)
 
 
@@ -1190,7 +1260,7 @@ def spark_min(c: OColumn, sel: np.ndarray, is_max: bool = False):
         return None
     best = None
     for i in np.nonzero(sel)[0]:
-        v = int(c.values[i]) if c.dtype in ("i64", "i32") else float(c.values[i])
+        v = int(c.values[i]) if c.dtype in INTEGRAL else float(c.values[i])
         if best is None:
             best = v
         elif is_max:
@@ -1205,12 +1275,18 @@ def spark_min(c: OColumn, sel: np.ndarray, is_max: bool = False):
 def hll_words_for(c: OColumn, sel: np.ndarray) -> Tuple[int, ...]:
     """stateful_approx_count_distinct registers for a column (XxHash64 seed 42)."""
     idx = np.nonzero(sel)[0]
-    if c.dtype == "i64":
+    # Spark 2.2 XxHash64Function per type: hashLong for LongType / TimestampType / DoubleType (doubleToLongBits),
+    # hashInt for IntegerType / ShortType / ByteType / DateType (widened to int), FloatType (floatToIntBits) and
+    # BooleanType (1 / 0)
+    if c.dtype in ("i64", "timestamp"):
         h = np_xxh64_long(np.asarray(c.values)[idx])
     elif c.dtype == "f64":
         h = np_xxh64_long(np_double_to_long_bits(np.asarray(c.values)[idx]))
-    elif c.dtype == "i32":
-        h = np_xxh64_int(np.asarray(c.values)[idx])
+    elif c.dtype in ("i32", "i16", "i8", "date32", "bool"):
+        h = np_xxh64_int(np.asarray(c.values)[idx].astype(np.int64))
+    elif c.dtype == "f32":
+        h = np_xxh64_int(np.array([float_to_int_bits(float(x)) for x in np.asarray(c.values, dtype=np.float32)[idx]],
+                                  dtype=np.int64))
     elif c.dtype == "utf8":
         h = np.array([xxh64_bytes(c.values[i]) & MASK64 for i in idx], dtype=np.uint64)
     else:
@@ -1263,12 +1339,36 @@ def datatype_class(value: bytes) -> int:
     return 4
 
 
+def java_float_to_string(f: float) -> str:
+    """java.lang.Float.toString: the same forms as Double.toString (plain decimal for 1e-3 <= |f| < 1e7 and
+    zero, else computerized scientific notation, "NaN", "Infinity") with float's shortest digits."""
+    if math.isnan(f) or math.isinf(f) or f == 0.0 or not (1e-3 <= abs(f) < 1e7):
+        if math.isnan(f) or math.isinf(f) or f == 0.0:
+            return java_double_to_string(f)
+        m, e = np.format_float_scientific(np.float32(f), unique=True, exp_digits=1).split("e")
+        return f"{m if '.' in m and not m.endswith('.') else m.rstrip('.') + '.0'}E{int(e)}"
+    r = np.format_float_positional(np.float32(f), unique=True)
+    return r + "0" if r.endswith(".") else r
+
+
 def _value_string(c: "OColumn", i: int) -> bytes:
-    """CAST(value AS STRING) of a column value, as UTF-8."""
+    """CAST(value AS STRING) of a column value, as UTF-8 (timestamps in UTC)."""
+    import datetime
+
     if c.dtype in ("utf8", "large_utf8"):
         return c.values[i]
     if c.dtype == "f64":
         return java_double_to_string(float(c.values[i])).encode()
+    if c.dtype == "f32":
+        return java_float_to_string(float(c.values[i])).encode()
+    if c.dtype == "bool":
+        return b"true" if c.values[i] else b"false"
+    if c.dtype == "date32":
+        return (datetime.date(1970, 1, 1) + datetime.timedelta(days=int(c.values[i]))).isoformat().encode()
+    if c.dtype == "timestamp":  # DateTimeUtils.timestampToString: yyyy-MM-dd HH:mm:ss[.fraction, zeros trimmed]
+        t = datetime.datetime(1970, 1, 1) + datetime.timedelta(microseconds=int(c.values[i]))
+        frac = f"{t.microsecond:06d}".rstrip("0")
+        return (t.strftime("%Y-%m-%d %H:%M:%S") + ("." + frac if frac else "")).encode()
     return str(int(c.values[i])).encode()
 
 

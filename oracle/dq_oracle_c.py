@@ -9,7 +9,8 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "_build", "libdqoracle.so")
-KINDS = {"f64": 1, "i64": 2, "i32": 3, "utf8": 4, "large_utf8": 5}
+KINDS = {"f64": 1, "i64": 2, "i32": 3, "utf8": 4, "large_utf8": 5, "f32": 6, "i16": 7, "i8": 8, "bool": 9,
+         "date32": 3, "timestamp": 2}
 
 
 class ColStats(ctypes.Structure):

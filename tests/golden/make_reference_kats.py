@@ -136,6 +136,17 @@ datasets = {
     "checkUrls": {"columns": {"some": ["utf8", [  # checks/CheckTest.scala:383-386
         "https://www.example.com/foo/?bar=baz&inga=42&quux", "http:// shouldfail.com"]]}},
     "checkEmails": {"columns": {"some": ["utf8", ["someone@somewhere.org", "someone@else.com"]]}},  # :354-355
+    # checks/CheckTest.scala:765-785 (runAndAssertSuccessFor): one column "some" of each numeric type, rows
+    # (1, null) -- isNonNegative / isPositive for ByteType .. DoubleType (:478-489)
+    **{f"numericRowNull_{t}": {"columns": {"some": [t, [1.0 if t.startswith("f") else 1, N]]}}
+       for t in ("i8", "i16", "i32", "i64", "f32", "f64")},
+    # AnalyzerTests.scala:322-328: getDfWithNumericValues with att1 cast to FloatType
+    "dfWithNumericValuesAsFloat": {
+        "columns": {"item": ["utf8", ["1", "2", "3", "4", "5", "6"]],
+                    "att1_float": ["f32", [1.0, 2.0, 3.0, 4.0, 5.0, 6.0]]}
+    },
+    # profiles/ColumnProfilerTest.scala:177-190: a BooleanType column (true x3, false x2, null)
+    "dfBooleanColumn": {"columns": {"attribute": ["bool", [True, True, True, False, False, N]]}},
 }
 
 S = "analyzers/AnalyzerTests.scala"
@@ -201,7 +212,7 @@ cases = [
     ("dfWithNumericValues", ["Compliance", "nr9", "`att2` IS NULL OR (`att2` > -1.0 AND `att2` <= 7.0)", N], 1.0, "checks/CheckTest.scala:259-275", []),
     ("dfWithNumericValues", ["Compliance", "att1 is non-negative", "COALESCE(att1, 0.0) >= 0", N], 1.0, "predicate form Check.scala:676 (isNonNegative); expected value computed by hand", []),
     ("dfWithNumericValues", ["Compliance", "att2 is positive", "COALESCE(att2, 1.0) > 0", N], 0.5, "predicate form Check.scala:687 (isPositive); expected value computed by hand", []),
-    # DataType (AnalyzerTests.scala:295-421; the FloatType case :322-328 needs a float column: not a GPU type)
+    # DataType (AnalyzerTests.scala:295-421; the FloatType case :322-328 is below with the round-6 column types)
     ("dfFull", ["DataType", "att1", N], {"DataTypeHistogram": [0, 0, 0, 0, 4]}, S + ":295-300", []),
     ("dfWithNumericValues", ["DataType", "att1", N], {"DataTypeHistogram": [0, 0, 6, 0, 0]}, S + ":302-306", []),
     ("dfWithNegativeNumbers", ["DataType", "att1", N], {"DataTypeHistogram": [0, 0, 4, 0, 0]}, S + ":308-312", []),
@@ -251,6 +262,21 @@ cases = [
     ("dfFull", ["MutualInformation", ["att1", "att1"]], -(0.75 * math.log(0.75) + 0.25 * math.log(0.25)), S + ":157-167 (equals Entropy(att1))", []),
     ("dataWithNullColumns", ["MutualInformation", ["numericCol", "numericCol2"]], "EmptyState", "analyzers/NullHandlingTests.scala:116", []),
     ("dataWithNullColumns", ["MutualInformation", ["numericCol", "numericCol3"]], "EmptyState", "analyzers/NullHandlingTests.scala:117", []),
+    # column types beyond Int / Long / Double (round 6): checks/CheckTest.scala:478-489 via :765-785 -- the
+    # default assertion of isNonNegative / isPositive is `_ == 1.0` (Check.scala:670-688), and the checks succeed
+    *[(f"numericRowNull_{t}", ["Compliance", "some is non-negative", "COALESCE(some, 0.0) >= 0", N], 1.0,
+       "checks/CheckTest.scala:478-482,765-785 (isNonNegative succeeds; predicate form Check.scala:676)", [])
+      for t in ("i8", "i16", "i32", "i64", "f32", "f64")],
+    *[(f"numericRowNull_{t}", ["Compliance", "some is positive", "COALESCE(some, 1.0) > 0", N], 1.0,
+       "checks/CheckTest.scala:484-488,765-785 (isPositive succeeds; predicate form Check.scala:687)", [])
+      for t in ("i8", "i16", "i32", "i64", "f32", "f64")],
+    ("dfWithNumericValuesAsFloat", ["DataType", "att1_float", N], {"DataTypeHistogram": [0, 6, 0, 0, 0]}, S + ":322-328", []),
+    ("dfBooleanColumn", ["Completeness", "attribute", N], 5.0 / 6.0,
+     "profiles/ColumnProfilerTest.scala:177-190 fixture; expected value computed by hand (5 of 6 non-null)", []),
+    ("dfBooleanColumn", ["DataType", "attribute", N], {"DataTypeHistogram": [1, 0, 0, 5, 0]},
+     "profiles/ColumnProfilerTest.scala:177-190 fixture; StatefulDataType.scala:62-67 on \"true\" / \"false\" (by hand)", []),
+    ("dfBooleanColumn", ["ApproxCountDistinct", "attribute", N], 2.0,
+     "profiles/ColumnProfilerTest.scala:177-190 fixture (two distinct values); expected value computed by hand", []),
     # partition merge (analyzers/StateAggregationIntegrationTest.scala:56-104)
     ("stateAggregation", ["Completeness", "origin", N], 0.625, "analyzers/StateAggregationIntegrationTest.scala:77", []),
 ]

@@ -8,6 +8,10 @@ import numpy as np
 from oracle import dq_oracle as O
 
 
+_INT_NP = {"i64": np.int64, "i32": np.int32, "i16": np.int16, "i8": np.int8, "date32": np.int32,
+           "timestamp": np.int64}
+
+
 def oracle_columns(ds: dict):
     """reference_kats dataset -> ({name: OColumn}, n)"""
     cols = {}
@@ -16,10 +20,12 @@ def oracle_columns(ds: dict):
         valid = np.array([v is not None for v in vals], dtype=bool)
         if t == "utf8":
             v = [None if x is None else x.encode("utf-8") for x in vals]
-        elif t == "f64":
-            v = np.array([0.0 if x is None else x for x in vals], dtype=np.float64)
+        elif t in ("f64", "f32"):
+            v = np.array([0.0 if x is None else x for x in vals], dtype=np.float64 if t == "f64" else np.float32)
+        elif t == "bool":
+            v = np.array([False if x is None else bool(x) for x in vals], dtype=bool)
         else:
-            v = np.array([0 if x is None else x for x in vals], dtype=np.int64 if t == "i64" else np.int32)
+            v = np.array([0 if x is None else x for x in vals], dtype=_INT_NP[t])
         cols[name] = O.OColumn(t, v, valid)
         n = len(vals)
     return cols, n
@@ -38,12 +44,13 @@ def host_column(col, n):
     bm = None if col.validity is None else col.validity.cpu().numpy()
     valid = np.ones(n, dtype=bool) if bm is None else np.unpackbits(bm, bitorder="little")[:n].astype(bool)
     raw = col.values.cpu().numpy()
-    if col.dtype == "f64":
-        return raw[: n * 8].view(np.float64).copy(), valid, bm
-    if col.dtype == "i64":
-        return raw[: n * 8].view(np.int64).copy(), valid, bm
-    if col.dtype == "i32":
-        return raw[: n * 4].view(np.int32).copy(), valid, bm
+    fixed = {"f64": np.float64, "i64": np.int64, "i32": np.int32, "f32": np.float32, "i16": np.int16, "i8": np.int8,
+             "date32": np.int32, "timestamp": np.int64}
+    if col.dtype in fixed:
+        w = np.dtype(fixed[col.dtype]).itemsize
+        return raw[: n * w].view(fixed[col.dtype]).copy(), valid, bm
+    if col.dtype == "bool":
+        return np.unpackbits(raw, bitorder="little")[:n].astype(bool), valid, bm
     offs_raw = col.offsets.cpu().numpy()
     offs = offs_raw[: (n + 1) * (4 if col.dtype == "utf8" else 8)].view(np.int32 if col.dtype == "utf8" else np.int64)
     data = raw.tobytes()

@@ -68,9 +68,51 @@ def test_arrow_import_maps_buffers():
     assert im.host.n_rows == 0 and im.host.value_bytes == 0 and not im.host.values
     im.close()
     with pytest.raises(L.DQError):
-        ImportedArray(pa.array([1.5, 2.5], type=pa.float32()))
+        ImportedArray(pa.array([1, 2], type=pa.uint32()))
+    with pytest.raises(L.DQError):
+        ImportedArray(pa.array([1, 2], type=pa.timestamp("ms")))  # not TimestampType's unit
     with pytest.raises(L.DQError):
         ImportedArray(pa.array(["a", "b"]).dictionary_encode())
+
+
+def _typed_batch(n, seed):
+    """One column of each round-6 type (FloatType, ShortType, ByteType, BooleanType, DateType, TimestampType)."""
+    rng = np.random.default_rng(seed)
+    f = (rng.normal(size=n) * 100).astype(np.float32)
+    h = rng.integers(-30000, 30000, n).astype(np.int16)
+    c = rng.integers(-128, 128, n).astype(np.int8)
+    b = rng.random(n) > 0.4
+    d = rng.integers(-20000, 30000, n).astype(np.int32)
+    ts = rng.integers(-(1 << 50), 1 << 50, n)
+    masks = [rng.random(n) > q for q in (0.1, 0.2, 0.0, 0.15, 0.3, 0.05)]
+    arrs = [pa.array(f, mask=~masks[0]), pa.array(h, mask=~masks[1]), pa.array(c),
+            pa.array(b, mask=~masks[3]), pa.array(d, type=pa.int32(), mask=~masks[4]).cast(pa.date32()),
+            pa.array(ts, mask=~masks[5]).cast(pa.timestamp("us", tz="UTC"))]
+    return pa.record_batch(arrs, names=["f", "h", "c", "b", "d", "t"]), (f, h, c, b, d, ts), masks
+
+
+def test_arrow_import_round6_types():
+    """dq_arrow_import maps float32 / int16 / int8 / bool / date32 / timestamp[us, tz] arrays; a boolean slice's
+    value bits carry the slice's bit offset like its validity."""
+    from deequ_amd import _lib as L
+    from deequ_amd.ingest import ImportedArray, arrow_schema
+
+    bt, _, _ = _typed_batch(1000, 3)
+    assert [d for _, d, _ in arrow_schema(bt)] == ["f32", "i16", "i8", "bool", "date32", "timestamp"]
+    want = {"f": (L.TYPE_F32, 4), "h": (L.TYPE_I16, 2), "c": (L.TYPE_I8, 1), "d": (L.TYPE_DATE32, 4),
+            "t": (L.TYPE_TIMESTAMP, 8)}
+    for name, (t, w) in want.items():
+        arr = bt.column(bt.schema.get_field_index(name))
+        im = ImportedArray(arr)
+        assert im.host.type == t and im.host.values == arr.buffers()[1].address and im.host.value_bytes == 1000 * w
+        im.close()
+    arr = bt.column(3)
+    im = ImportedArray(arr)
+    assert im.host.type == L.TYPE_BOOL and im.host.values == arr.buffers()[1].address and im.host.value_bytes == 125
+    im.close()
+    im = ImportedArray(arr.slice(11, 300))
+    assert im.host.values == arr.buffers()[1].address + 1 and im.host.validity_bit == 3 and im.host.value_bytes == 38
+    im.close()
 
 
 @pytest.mark.gpu
@@ -136,3 +178,45 @@ def test_arrow_ingest_vs_oracle_and_device_scan():
     want = scan_results(tables, an)
     for a, g, w in zip(an, got, want):
         assert bytes(g) == bytes(w), a
+
+
+@pytest.mark.gpu
+def test_arrow_ingest_round6_types_vs_device_scan():
+    """Host Arrow batches of the round-6 types, sliced at odd row offsets (boolean value bits shifted like the
+    validity by dq_upload), scanned through the pinned upload: the same states as the device tables, and the
+    oracle's HLL words / counts."""
+    import torch
+
+    import deequ_amd as dq
+    from deequ_amd.ingest import scan_arrow
+    from deequ_amd.runner import scan_results
+    from deequ_amd.states import state_from_c
+    from deequ_amd.table import column_from_numpy
+    from oracle import dq_oracle as O
+
+    assert torch.cuda.is_available()
+    n, parts = 200_000, [0, 70_001, 140_013, 200_000]
+    bt, (f, h, c, b, d, ts), masks = _typed_batch(n, 9)
+    an = [dq.Mean("f"), dq.StandardDeviation("h"), dq.Sum("c"), dq.Minimum("f"), dq.Maximum("h"),
+          dq.ApproxCountDistinct("b"), dq.ApproxCountDistinct("d"), dq.ApproxCountDistinct("t"),
+          dq.ApproxCountDistinct("f"), dq.Completeness("b"), dq.Compliance("bt", "b"), dq.Completeness("d"),
+          dq.Correlation("f", "c"), dq.DataType("b"), dq.DataType("f")]
+    batches = [bt.slice(parts[k], parts[k + 1] - parts[k]) for k in range(3)]
+    got = scan_arrow(batches, an)
+    tables = []
+    for k in range(3):
+        sl = slice(parts[k], parts[k + 1])
+        cols = [column_from_numpy(name, dt, v[sl], m[sl]) for name, dt, v, m in
+                zip("fhcbdt", ["f32", "i16", "i8", "bool", "date32", "timestamp"], (f, h, c, b, d, ts), masks)]
+        cols[2] = column_from_numpy("c", "i8", c[sl], np.ones(parts[k + 1] - parts[k], bool), nullable=False)
+        tables.append(dq.Table(cols))
+    want = scan_results(tables, an)
+    for a, g, w in zip(an, got, want):
+        assert bytes(g) == bytes(w), a
+    st = {a: state_from_c(g) for a, g in zip(an, got)}
+    ocols = {"b": O.OColumn("bool", b, masks[3]), "d": O.OColumn("date32", d, masks[4]),
+             "t": O.OColumn("timestamp", ts, masks[5]), "f": O.OColumn("f32", f, masks[0])}
+    for a in (an[5], an[6], an[7], an[8]):
+        assert st[a].words == O.compute_state(("ApproxCountDistinct", a.column, None), ocols, n).words, a
+    assert (st[an[9]].numMatches, st[an[9]].count) == (int(masks[3].sum()), n)
+    assert st[an[10]].numMatches == int((b & masks[3]).sum())
