@@ -53,7 +53,9 @@ def parse(argv=None):
     p.add_argument("--cpu-sample", type=int, default=62_500_000, help="rows timed on the CPU baseline (0 = skip)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="repeat the CPU sample for at least this long")
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = this host's CPU share (see host_cpu_share)")
-    p.add_argument("--configs", default="c1,c2,c3,c4", help="other BASELINE configs to measure at N=1 ('' = none)")
+    p.add_argument("--configs", default="c1,c2,c3,c4,c5e,types",
+                   help="other configs to measure at N=1 ('' = none): BASELINE C1-C4, c5e = C5 with empty NULL string "
+                        "slots (Spark / Arrow writers), types = the round-6 column types")
     p.add_argument("--config-steps", type=int, default=5)
     p.add_argument("--config-rows", type=int, default=0, help="rows of C2-C4 (0 = BASELINE's 1e9; profiling runs)")
     p.add_argument("--skip-headline", action="store_true", help="profiling runs: only the --configs")
@@ -178,7 +180,7 @@ def main():
 
     if args.skip_headline:
         deferred_cpu = []
-        out = {"configs": {cfg: run_config(cfg, args, deferred_cpu) for cfg in args.configs.split(",") if cfg}}
+        out = {"configs": {cfg: run_config(cfg, args, deferred_cpu) for cfg in re.split(r"[,+]", args.configs) if cfg}}
         for run in deferred_cpu:
             run()
         print(json.dumps(out), flush=True)
@@ -294,7 +296,7 @@ def main():
         torch.cuda.empty_cache()
     if world == 1 and args.configs:
         out["configs"] = {}
-        for cfg in [c for c in args.configs.split(",") if c]:
+        for cfg in [c for c in re.split(r"[,+]", args.configs) if c]:
             out["configs"][cfg] = run_config(cfg, args, deferred_cpu)
             torch.cuda.empty_cache()
     for run in deferred_cpu:
@@ -340,7 +342,8 @@ def config_setup(cfg, n, chunk):
     import deequ_amd as dq
     from deequ_amd import synth
 
-    gen = {"c1": synth.item_table, "c2": synth.c2_table, "c3": synth.c3_table, "c4": synth.c4_table}[cfg]
+    gen = {"c1": synth.item_table, "c2": synth.c2_table, "c3": synth.c3_table, "c4": synth.c4_table,
+           "c5e": lambda m, r, s: synth.c5_table(m, r, s, null_empty=True), "types": synth.types_table}[cfg]
     tables = []
     r = 0
     while r < n:
@@ -358,6 +361,14 @@ def config_setup(cfg, n, chunk):
     elif cfg == "c3":
         analyzers = synth.c3_analyzers(tables[0])
         desc = "C3 4 x i64 + 4 x utf8 (10% nulls): Size + ApproxCountDistinct x8 + Compliance x4"
+    elif cfg == "c5e":
+        analyzers = synth.profile_analyzers(tables[0])
+        desc = ("C5 with empty NULL string slots (Spark / Arrow writers emit no bytes for a NULL): the headline's "
+                "columns and 93 analyzers, string payload of non-NULL rows only")
+    elif cfg == "types":
+        analyzers = synth.profile_analyzers(tables[0]) + [dq.DataType(c) for c in names]
+        desc = ("round-6 column types (f32, i16, i8, bool, date32, timestamp; 10% nulls): Size + Completeness + "
+                "ApproxCountDistinct + DataType per column, Min/Max/Mean/StdDev/Sum of the numeric ones")
     else:
         analyzers = [dq.Correlation(names[i], names[j]) for i in range(8) for j in range(i + 1, 8)]
         analyzers += [dq.Mean(c) for c in names] + [dq.StandardDeviation(c) for c in names]
@@ -407,7 +418,7 @@ def run_config(cfg, args, deferred_cpu) -> dict:
     gc.enable()
     kernels = kernel_report(plan, tables, n)
     # C1's string columns are read for Completeness only (validity bytes): exclude their payload
-    algo = plan.bytes_per_row() * n + (str_bytes if cfg == "c3" else 0)
+    algo = plan.bytes_per_row() * n + (str_bytes if cfg in ("c3", "c5e") else 0)
     dom_name, dom = max(kernels.items(), key=lambda kv: kv[1]["ms_total"])
     rec = {"workload": desc, "rows": n, "analyzers": len(analyzers), "ms_per_step": dt * 1e3, "rows_per_s": n / dt,
            "step_ms": [round(x, 3) for x in step_ms], "ms_per_step_median": sorted(step_ms)[len(step_ms) // 2],

@@ -722,6 +722,22 @@ struct DtCounts {
 constexpr int kStrAhead = DQ_STR_AHEAD;  // string windows in flight ahead of the one being hashed (1..7)
 constexpr uint32_t kDefCap = 128;  // < 64 left after a drain + <= 64 pushed per row group
 constexpr int kDefFields = 6;      // h lo, h hi, w4, w5, w6, len
+// Round 6: the short-string hash by stripe-count class.  The block loop loads and realigns
+// every string's window in row order as before, then pushes each selected string's window into one of two
+// per-wave LDS stacks -- class A: < 16 bytes (at most one 8-byte round), class B: 16..28 bytes (two, the third
+// deferred as before) -- and hashes a class 64 strings at a time once it holds 64: NULL rows never reach a
+// hash, and class A never runs the second round that a wave of mixed lengths otherwise runs for all 64 lanes.
+// Class A entries: the 16 window bytes with len in byte 15 (unused below 16 bytes); class B: bytes 0..27 + len.
+#ifndef DQ_STR_CLS
+#define DQ_STR_CLS 0
+#endif
+// Capacities: a class is hashed once it holds >= 64 (so < 64 are left); a push that would overflow it first
+// hashes what it holds (partial: only when one row group brings > kClsCap - 64 of a class, i.e. > 32).  96
+// entries per class and 96 deferred strings keep the string pass at 5 workgroups (waves per SIMD) per CU:
+// 5 x (4.4 KB + 4 x 6.75 KB) of the 160 KB LDS.
+constexpr uint32_t kClsCap = 96;
+constexpr uint32_t kClsWords = kClsCap * (4 + 8);     // per wave: A quads, then B's two quad arrays
+constexpr uint32_t kDefCapCls = 96;                   // the deferred queue of the class instantiation
 
 // 32 bytes from byte `pos` of a window resource as little-endian dwords: three 16-byte loads from pos & ~3,
 // realigned with v_alignbyte
@@ -762,7 +778,9 @@ __device__ uint64_t xxh64_window_head(__amdgpu_buffer_rsrc_t rsrc, uint32_t rel,
 template <typename OffT, bool HLL, bool DT, bool LONG>
 __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint32_t* validity,
                            const uint32_t* mask, int64_t row0, int64_t row1, int64_t n_rows, ColStats& s,
-                           int32_t* regs, const uint64_t* p5, uint32_t* dq, uint32_t* rare) {
+                           int32_t* regs, const uint64_t* p5, uint32_t* dq, uint32_t* rare, uint32_t* cls) {
+  constexpr bool CLS = DQ_STR_CLS && HLL && !DT && !LONG;
+  constexpr uint32_t DCAP = CLS ? kDefCapCls : kDefCap;  // the deferred queue's capacity (its SoA stride)
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (row0 >= row1) return;
@@ -896,10 +914,10 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
   // high word does not carry it)
   auto drain = [&](uint32_t n) __attribute__((always_inline)) {
     if ((uint32_t)lane < n) {
-      const uint64_t h = ((uint64_t)dq[1 * kDefCap + lane] << 32) | dq[0 * kDefCap + lane];
-      const uint64_t k1 = ((uint64_t)dq[3 * kDefCap + lane] << 32) | dq[2 * kDefCap + lane];
-      const uint64_t b = xxh64_tail_head(xxh64_stripe_round(h, k1), (uint64_t)dq[4 * kDefCap + lane],
-                                         dq[5 * kDefCap + lane], bp);
+      const uint64_t h = ((uint64_t)dq[1 * DCAP + lane] << 32) | dq[0 * DCAP + lane];
+      const uint64_t k1 = ((uint64_t)dq[3 * DCAP + lane] << 32) | dq[2 * DCAP + lane];
+      const uint64_t b = xxh64_tail_head(xxh64_stripe_round(h, k1), (uint64_t)dq[4 * DCAP + lane],
+                                         dq[5 * DCAP + lane], bp);
       const HllKey key = hll_key_from_fmix(b);
       if (key.q >= 0) atomicMax(reinterpret_cast<int32_t*>(reinterpret_cast<char*>(regs) + key.addr), key.q);
       else hll_update(regs, fmix_tail(b));
@@ -912,11 +930,75 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
     if ((uint32_t)lane < rest) {
       uint32_t v[kDefFields];
 #pragma unroll
-      for (int f = 0; f < kDefFields; ++f) v[f] = dq[f * kDefCap + 64 + lane];
+      for (int f = 0; f < kDefFields; ++f) v[f] = dq[f * DCAP + 64 + lane];
 #pragma unroll
-      for (int f = 0; f < kDefFields; ++f) dq[f * kDefCap + lane] = v[f];
+      for (int f = 0; f < kDefFields; ++f) dq[f * DCAP + lane] = v[f];
     }
     qtail = rest;
+  };
+  // class stacks (CLS): the wave's entries [0, qa) of class A and [0, qb) of class B
+  uint32_t qa = 0, qb = 0;
+  // hash n <= 64 entries [top, top + n) of class A (isb false: at most one 8-byte round) or B (two rounds; a string of
+  // 24..28 bytes goes on to the deferred queue for its third) -- one body for both classes (class A's lanes skip the
+  // second round, so its waves skip it): the row loop has one drain site per row group, like its inline hash had
+  auto cls_drain = [&](uint32_t top, uint32_t n, bool isb) __attribute__((always_inline)) {
+    const bool act = (uint32_t)lane < n;
+    uint32_t w[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    uint32_t L = 0;
+    if (act) {
+      if (isb) {
+        const u32x4 q0 = reinterpret_cast<const u32x4*>(cls + 4 * kClsCap)[top + lane];
+        const u32x4 q1 = reinterpret_cast<const u32x4*>(cls + 8 * kClsCap)[top + lane];
+        w[0] = q0.x; w[1] = q0.y; w[2] = q0.z; w[3] = q0.w; w[4] = q1.x; w[5] = q1.y; w[6] = q1.z;
+        L = q1.w;
+      } else {
+        const u32x4 q = reinterpret_cast<const u32x4*>(cls)[top + lane];
+        w[0] = q.x; w[1] = q.y; w[2] = q.z; w[3] = q.w;
+        L = q.w >> 24;
+      }
+    }
+    uint64_t d4p;
+    const uint64_t h2 = xxh64_stripes<2>(w, L, d4p);
+    const uint64_t dm = __builtin_amdgcn_ballot_w64(act && L >= 24u);
+    if (qtail + (uint32_t)__builtin_popcountll(dm) > DCAP) {  // (rare) make room: finish what the queue holds
+      drain(qtail);
+      qtail = 0;
+    }
+    if (dm != 0) {
+      const uint32_t pos = qtail + __builtin_amdgcn_mbcnt_hi((uint32_t)(dm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dm, 0u));
+      if (lane_bit(dm)) {
+        dq[0 * DCAP + pos] = (uint32_t)h2;
+        dq[1 * DCAP + pos] = (uint32_t)(h2 >> 32);
+        dq[2 * DCAP + pos] = (uint32_t)d4p;
+        dq[3 * DCAP + pos] = (uint32_t)(d4p >> 32);
+        dq[4 * DCAP + pos] = w[6];
+        dq[5 * DCAP + pos] = L;
+      }
+      qtail += (uint32_t)__builtin_popcountll(dm);
+    }
+    if (act && L < 24u) {
+      const uint64_t b = xxh64_tail_head(h2, d4p, L, bp);
+      const HllKey key = hll_key_from_fmix(b);
+      if (key.q >= 0) atomicMax(reinterpret_cast<int32_t*>(reinterpret_cast<char*>(regs) + key.addr), key.q);
+      else hll_update(regs, fmix_tail(b));
+    }
+  };
+  // drain what class A / B must give up before a push of na / nb entries: 64 once a class holds >= 64 (< 64 are
+  // left), or everything when the push would overflow kClsCap (only a class with < 64 and > kClsCap - na); one
+  // drain site (a rolled loop over the two classes)
+  auto cls_make_room = [&](uint32_t na, uint32_t nb) __attribute__((always_inline)) {
+    const uint32_t da = qa >= 64u ? 64u : (qa + na > kClsCap ? qa : 0u);
+    const uint32_t db = qb >= 64u ? 64u : (qb + nb > kClsCap ? qb : 0u);
+#pragma unroll 1
+    for (int c = 0; c < 2; ++c) {
+      const uint32_t n = c ? db : da;
+      if (n == 0) continue;
+      const uint32_t top = (c ? qb : qa) - n;
+      cls_drain(top, n, c != 0);
+      if (c) qb = top;
+      else qa = top;
+    }
+    if (qtail >= 64u) drain_full();
   };
   // every 32-byte window of the range lies inside the chunk's bytes iff its last row's does (offsets only
   // grow): then no row needs the per-row window compare (all but the chunk's last range; one scalar load --
@@ -968,7 +1050,30 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
       for (int k = 0; k < 7; ++k) wv[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
       wv[7] = d[7];  // only ever feeds the unused half of the tail pair for len >= 24
       if constexpr (DT) dtc.add(dt_class_short(wv, len_of(j), lane_bit(m[j])), lane_bit(m[j]));
-      if constexpr (HLL) {
+      if constexpr (CLS) {
+        // push the row group's selected fast-path strings by class: rank among the pushing lanes, class A from
+        // qa up, class B from qb up (rank_B = rank - rank_A: one mbcnt pair less)
+        const uint32_t L = len_of(j);
+        const uint64_t mb = m[j] & __builtin_amdgcn_ballot_w64(L >= 16u);
+        const uint64_t ma = m[j] & ~mb;
+        cls_make_room((uint32_t)__builtin_popcountll(ma), (uint32_t)__builtin_popcountll(mb));
+        const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(m[j] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m[j], 0u));
+        const uint32_t ra = __builtin_amdgcn_mbcnt_hi((uint32_t)(ma >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ma, 0u));
+        if (lane_bit(ma)) {
+          u32x4 q;
+          q.x = wv[0]; q.y = wv[1]; q.z = wv[2]; q.w = (wv[3] & 0x00FFFFFFu) | (L << 24);
+          reinterpret_cast<u32x4*>(cls)[qa + ra] = q;
+        } else if (lane_bit(mb)) {
+          const uint32_t pb = qb + rk - ra;
+          u32x4 q0, q1;
+          q0.x = wv[0]; q0.y = wv[1]; q0.z = wv[2]; q0.w = wv[3];
+          q1.x = wv[4]; q1.y = wv[5]; q1.z = wv[6]; q1.w = L;
+          reinterpret_cast<u32x4*>(cls + 4 * kClsCap)[pb] = q0;
+          reinterpret_cast<u32x4*>(cls + 8 * kClsCap)[pb] = q1;
+        }
+        qa += (uint32_t)__builtin_popcountll(ma);
+        qb += (uint32_t)__builtin_popcountll(mb);
+      } else if constexpr (HLL) {
         uint64_t d4p;
         const uint64_t h2 = xxh64_stripes<2>(wv, len_of(j), d4p);
         const uint64_t dm = m[j] & __builtin_amdgcn_ballot_w64(len_of(j) >= 24u);  // needs the third round
@@ -977,12 +1082,12 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
           // v_mov of it into the mbcnt)
           const uint32_t pos = qtail + __builtin_amdgcn_mbcnt_hi((uint32_t)(dm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dm, 0u));
           if (lane_bit(dm)) {
-            dq[0 * kDefCap + pos] = (uint32_t)h2;
-            dq[1 * kDefCap + pos] = (uint32_t)(h2 >> 32);
-            dq[2 * kDefCap + pos] = (uint32_t)d4p;
-            dq[3 * kDefCap + pos] = (uint32_t)(d4p >> 32);
-            dq[4 * kDefCap + pos] = wv[6];
-            dq[5 * kDefCap + pos] = len_of(j);
+            dq[0 * DCAP + pos] = (uint32_t)h2;
+            dq[1 * DCAP + pos] = (uint32_t)(h2 >> 32);
+            dq[2 * DCAP + pos] = (uint32_t)d4p;
+            dq[3 * DCAP + pos] = (uint32_t)(d4p >> 32);
+            dq[4 * DCAP + pos] = wv[6];
+            dq[5 * DCAP + pos] = len_of(j);
           }
           qtail += (uint32_t)__builtin_popcountll(dm);
         }
@@ -1030,6 +1135,10 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
       qmin = 0;
     }
   }
+  if constexpr (CLS) {  // the classes' last entries (each <= kClsCap: one or two drains)
+#pragma unroll 1
+    while (qa | qb) cls_make_room(kClsCap, kClsCap);
+  }
   if constexpr (HLL) {
     if (qtail != 0) drain(qtail);
   }
@@ -1045,16 +1154,38 @@ __device__ void utf8_range(const uint8_t* data, const OffT* offsets, const uint3
 template <typename T>
 __device__ void float_dtype_range(const T* values, const uint32_t* validity, const uint32_t* mask, int64_t row0,
                                   int64_t row1, ColStats& s) {
-  uint32_t cnt = 0, frac = 0;
-  for (int64_t r = row0 + threadIdx.x; r < row1; r += kBlock) {
-    const uint32_t bit = (word_or_ones(validity, r >> 5) & word_or_ones(mask, r >> 5)) >> (r & 31);
-    const bool sel = bit & 1u;
-    const double x = (double)__builtin_nontemporal_load(values + r), a = __builtin_fabs(x);
-    cnt += sel;
-    frac += sel && (x == 0.0 || (a >= 1e-3 && a < 1e7));
+  // lane-per-row 512-row blocks as numeric_range: coalesced loads through a bounds-checked descriptor, the
+  // selection as scalar lane masks, counts from popcounts (wave-uniform)
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const __amdgpu_buffer_rsrc_t vr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<T*>(values + row0), (short)0, (int)((row1 - row0) * (int64_t)sizeof(T)), 0x00020000);
+  int64_t cnt = 0, frac = 0;
+  const int32_t nr = (int32_t)(row1 - row0);
+  for (int32_t rb = 0; rb < nr; rb += kRowsPerIter) {
+    const int64_t base = row0 + rb + wave * 512;
+    const int32_t rem = nr - rb - wave * 512;
+    uint64_t m[8];
+    block_masks(validity, mask, base, rem, rb + kRowsPerIter <= nr, m);
+    const int32_t vo = (rb + wave * 512 + lane) * (int32_t)sizeof(T);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      double x;
+      if constexpr (sizeof(T) == 8) {
+        const auto w2 = __builtin_amdgcn_raw_buffer_load_b64(vr, vo + j * 512, 0, 2 /* nt */);
+        x = __builtin_bit_cast(double, ((uint64_t)w2[1] << 32) | w2[0]);
+      } else {
+        x = (double)__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(vr, vo + j * 256, 0, 2 /* nt */));
+      }
+      const double a = __builtin_fabs(x);
+      cnt += __builtin_popcountll(m[j]);
+      frac += __builtin_popcountll(__builtin_amdgcn_ballot_w64(x == 0.0 || (a >= 1e-3 && a < 1e7)) & m[j]);
+    }
   }
-  s.count += cnt;
-  s.isum += frac;
+  if (lane == 0) {
+    s.count += cnt;
+    s.isum += frac;
+  }
 }
 
 // BooleanType column: the selected rows (s.count) and the selected TRUE values (s.isum) from popcounts of the
@@ -1109,7 +1240,7 @@ __device__ void run_numeric(const ColTask& t, const ScanCols& cols, const ScanBi
 template <int V, bool LONG>
 __device__ __forceinline__ void run_variant(const ColTask& t, const ScanCols& cols, const uint32_t* mask, int64_t row0,
                                             int64_t row1, int64_t n_rows, ColStats& s, int32_t* regs,
-                                            const uint64_t* p5, uint32_t* dq, uint32_t* rare) {
+                                            const uint64_t* p5, uint32_t* dq, uint32_t* rare, uint32_t* cls) {
   const void* v = cols.values[t.col];
   const uint32_t* val = cols.validity[t.col];
   if constexpr (V == CV_VALIDITY) validity_range(val, mask, row0, row1, s);
@@ -1137,11 +1268,11 @@ __device__ __forceinline__ void run_variant(const ColTask& t, const ScanCols& co
   else if constexpr (V == CV_UTF8_H || V == CV_UTF8_D || V == CV_UTF8_HD)
     utf8_range<int32_t, V != CV_UTF8_D, V != CV_UTF8_H, LONG>(
         reinterpret_cast<const uint8_t*>(v), reinterpret_cast<const int32_t*>(cols.offsets[t.col]), val, mask, row0,
-        row1, n_rows, s, regs, p5, dq, rare);
+        row1, n_rows, s, regs, p5, dq, rare, cls);
   else
     utf8_range<int64_t, V != CV_LUTF8_D, V != CV_LUTF8_H, LONG>(
         reinterpret_cast<const uint8_t*>(v), reinterpret_cast<const int64_t*>(cols.offsets[t.col]), val, mask, row0,
-        row1, n_rows, s, regs, p5, dq, rare);
+        row1, n_rows, s, regs, p5, dq, rare, cls);
 }
 
 // Minimum waves per SIMD the register allocator must leave room for (0 = no constraint); a
@@ -1155,7 +1286,8 @@ __device__ __forceinline__ void run_variant(const ColTask& t, const ScanCols& co
 #define DQ_NUM_WAVES 6
 #endif
 template <int V, bool LONG>
-constexpr int kMinWaves = V == CV_UTF8_H && DQ_STR_WAVES > 0 ? DQ_STR_WAVES
+constexpr int kMinWaves = V == CV_UTF8_H && !LONG && DQ_STR_CLS ? 5  // (the class stacks' LDS: 5 workgroups per CU)
+                          : V == CV_UTF8_H && DQ_STR_WAVES > 0 ? DQ_STR_WAVES
                           : (V == CV_F64_SH || V == CV_I64_SH) && DQ_NUM_WAVES > 0 ? DQ_NUM_WAVES
                           : V == CV_LUTF8_H && LONG ? 5  // (the register window would otherwise cost a wave)
                                                     : 1;
@@ -1174,8 +1306,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kMinWave
   constexpr bool kStr = V == CV_UTF8_H || V == CV_LUTF8_H || V == CV_UTF8_HD || V == CV_LUTF8_HD;
   __shared__ int32_t regs[kHll ? 512 : 2];  // q = pw - 1, -1 = empty (see hll_q_exact); CV_BOOL: any TRUE / FALSE
   __shared__ uint64_t p5[kStr ? 256 : 1];   // b * P5 for the byte rounds of the string hash
-  __shared__ uint32_t dfq[kStr ? kWaves * kDefFields * kDefCap : 1];  // deferred 24..28-byte strings
+  constexpr uint32_t kDCap = DQ_STR_CLS && (V == CV_UTF8_H || V == CV_LUTF8_H) && !LONG ? kDefCapCls : kDefCap;
+  __shared__ uint32_t dfq[kStr ? kWaves * kDefFields * kDCap : 1];  // deferred 24..28-byte strings
   __shared__ uint32_t rare[kStr ? kWaves : 1];  // per wave: the rows the string fast path skipped
+  constexpr bool kCls = DQ_STR_CLS && (V == CV_UTF8_H || V == CV_LUTF8_H) && !LONG;
+  __shared__ __attribute__((aligned(16))) uint32_t clsbuf[kCls ? kWaves * kClsWords : 4];  // class stacks
   __shared__ ColStats red[kWaves];
   const int32_t ti = blockIdx.x % ntasks;
   const int32_t range = blockIdx.x / ntasks;
@@ -1199,7 +1334,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kMinWave
   stats_init(s);
   const uint32_t* mask = t.where >= 0 ? reinterpret_cast<const uint32_t*>(bm.where_bits[t.where]) : nullptr;
   const int32_t wv = kStr ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0;
-  run_variant<V, LONG>(t, cols, mask, row0, row1, n_rows, s, regs, p5, dfq + wv * kDefFields * kDefCap, rare + wv);
+  run_variant<V, LONG>(t, cols, mask, row0, row1, n_rows, s, regs, p5, dfq + wv * kDefFields * kDCap, rare + wv,
+                       clsbuf + (kCls ? wv * kClsWords : 0));
   block_reduce_store(s, partials + (size_t)(part_base + ti) * kMaxWG + range, red);
   if constexpr (kStr) {
     // the task's rare-path rows for dq_scan's choice of variant (finalize publishes them to the host)

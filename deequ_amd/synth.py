@@ -9,7 +9,7 @@ import ctypes
 import os
 from typing import List, Sequence
 
-from .table import Column, Table
+from .table import NUMERIC, Column, Table
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _lib = None
@@ -94,12 +94,20 @@ def i32_column(name, n, seed, distinct, base=0, null_frac=0.0, row0=0) -> Column
     return Column(name, "i32", n, v, bm, None, nullable=bm is not None)
 
 
-def utf8_column(name, n, seed, distinct, lmin=8, lmax=24, null_frac=0.0, row0=0, large=False) -> Column:
+def utf8_column(name, n, seed, distinct, lmin=8, lmax=24, null_frac=0.0, row0=0, large=False,
+                null_empty=False) -> Column:
+    """null_empty: NULL rows get empty slots (offsets[r + 1] == offsets[r]), as Spark's and Arrow's writers
+    emit them; otherwise the validity is drawn independently of the lengths (a NULL row keeps its bytes)."""
     import torch
 
     lens = torch.empty(n + 1, dtype=torch.int64, device="cuda")
     lens[0] = 0
     _check(lib().dqs_utf8_lengths(lens[1:].data_ptr(), row0, n, seed, distinct, lmin, lmax, _stream()))
+    bm = validity(n, seed ^ 0xABCDEF, null_frac, row0)
+    if null_empty and bm is not None:
+        r = torch.arange(n, device="cuda")
+        lens[1:] *= ((bm[r >> 3].to(torch.int64) >> (r & 7)) & 1)
+        del r
     offs = torch.cumsum(lens, 0)
     del lens
     total = int(offs[-1].item())
@@ -114,7 +122,6 @@ def utf8_column(name, n, seed, distinct, lmin=8, lmax=24, null_frac=0.0, row0=0,
         o = _alloc((n + 1) * 4)
         _check(lib().dqs_i64_to_i32(o.data_ptr(), offs.data_ptr(), n + 1, _stream()))
     del offs
-    bm = validity(n, seed ^ 0xABCDEF, null_frac, row0)
     return Column(name, "large_utf8" if large else "utf8", n, data, bm, o, nullable=bm is not None, data_bytes=total)
 
 
@@ -130,9 +137,10 @@ def c2_table(n, row0=0, seed=42, null_frac=0.10) -> Table:
     return Table([f64_column(f"c{c}", n, seed + c, 1000.0 * c, 1.0 + c, null_frac, row0) for c in range(8)])
 
 
-def c3_table(n, row0=0, seed=42, null_frac=0.10) -> Table:
+def c3_table(n, row0=0, seed=42, null_frac=0.10, null_empty=False) -> Table:
     cols = [i64_column(f"i{c}", n, seed + 100 + c, INT_DISTINCT[c], 0, null_frac, row0) for c in range(4)]
-    cols += [utf8_column(f"s{c}", n, seed + 200 + c, STR_DISTINCT[c], 8, 24, null_frac, row0) for c in range(4)]
+    cols += [utf8_column(f"s{c}", n, seed + 200 + c, STR_DISTINCT[c], 8, 24, null_frac, row0, null_empty=null_empty)
+             for c in range(4)]
     return Table(cols)
 
 
@@ -144,10 +152,38 @@ def c4_table(n, row0=0, seed=42, null_frac=0.10) -> Table:
     return Table(cols)
 
 
-def c5_table(n, row0=0, seed=42, null_frac=0.10) -> Table:
-    """16 mixed columns: C2's 8 fp64 + C3's 4 int64 + 4 UTF8."""
+def c5_table(n, row0=0, seed=42, null_frac=0.10, null_empty=False) -> Table:
+    """16 mixed columns: C2's 8 fp64 + C3's 4 int64 + 4 UTF8 (null_empty: NULL string slots empty)."""
     return Table(list(c2_table(n, row0, seed, null_frac).columns.values()) +
-                 list(c3_table(n, row0, seed, null_frac).columns.values()))
+                 list(c3_table(n, row0, seed, null_frac, null_empty).columns.values()))
+
+
+def types_table(n, row0=0, seed=42, null_frac=0.10) -> Table:
+    """The round-6 column types, one column each: FloatType ~ N(100, 30), ShortType / ByteType uniform, BooleanType
+    (30 % true), DateType (days in [-50000, 50000)), TimestampType (micros in +-2^52); 10 % nulls (torch-generated
+    on the device, seeded by row0 so chunks differ)."""
+    import torch
+
+    g = torch.Generator(device="cuda")
+    g.manual_seed(seed * 1_000_003 + row0)
+    cols = []
+
+    def col(name, dtype, t, nbytes, k):
+        v = _alloc(nbytes)
+        v[:nbytes].copy_(t.contiguous().view(torch.uint8).reshape(-1)[:nbytes])
+        bm = validity(n, seed + 7 * k, null_frac, row0)
+        cols.append(Column(name, dtype, n, v, bm, None, nullable=bm is not None))
+
+    col("f", "f32", torch.randn(n, device="cuda", generator=g) * 30.0 + 100.0, 4 * n, 1)
+    col("h", "i16", torch.randint(-32768, 32768, (n,), device="cuda", generator=g, dtype=torch.int16), 2 * n, 2)
+    col("c", "i8", torch.randint(-128, 128, (n,), device="cuda", generator=g, dtype=torch.int8), n, 3)
+    bits = torch.rand(((n + 7) // 8) * 8, device="cuda", generator=g) < 0.3
+    packed = (bits.view(-1, 8).to(torch.uint8) << torch.arange(8, device="cuda", dtype=torch.uint8)).sum(1, dtype=torch.uint8)
+    col("b", "bool", packed, (n + 7) // 8, 4)
+    col("d", "date32", torch.randint(-50000, 50000, (n,), device="cuda", generator=g, dtype=torch.int32), 4 * n, 5)
+    col("t", "timestamp", torch.randint(-(1 << 52), 1 << 52, (n,), device="cuda", generator=g, dtype=torch.int64),
+        8 * n, 6)
+    return Table(cols)
 
 
 def profile_analyzers(table: Table):
@@ -158,7 +194,7 @@ def profile_analyzers(table: Table):
     out = [Size()]
     for name, dtype, _ in table.schema:
         out += [Completeness(name), ApproxCountDistinct(name)]
-        if dtype in ("f64", "i64", "i32"):
+        if dtype in NUMERIC:
             out += [Minimum(name), Maximum(name), Mean(name), StandardDeviation(name), Sum(name)]
     return out
 
