@@ -60,11 +60,20 @@ __device__ __forceinline__ uint64_t canon_f64(uint64_t bits) {
   return mag > 0x7FF0000000000000ull ? 0x7FF8000000000000ull : bits;  // any NaN -> Double.NaN
 }
 
+// the grouping key of a fixed-width value: its exact bits (UnsafeRow's binary equality: NaN canonical, -0.0 and
+// 0.0 distinct), integers sign-extended, a boolean 0 / 1
 __device__ __forceinline__ uint64_t value_bits(const GroupCols& g, int c, int64_t r) {
   switch (g.type[c]) {
     case DQ_TYPE_F64: return canon_f64(reinterpret_cast<const uint64_t*>(g.values[c])[r]);
-    case DQ_TYPE_I64: return reinterpret_cast<const uint64_t*>(g.values[c])[r];
-    default: return (uint64_t)(int64_t)reinterpret_cast<const int32_t*>(g.values[c])[r];
+    case DQ_TYPE_I64: case DQ_TYPE_TIMESTAMP: return reinterpret_cast<const uint64_t*>(g.values[c])[r];
+    case DQ_TYPE_F32: {
+      const uint32_t b = reinterpret_cast<const uint32_t*>(g.values[c])[r];
+      return (b & 0x7FFFFFFFu) > 0x7F800000u ? 0x7FC00000ull : (uint64_t)b;  // any NaN -> Float.NaN
+    }
+    case DQ_TYPE_I16: return (uint64_t)(int64_t)reinterpret_cast<const int16_t*>(g.values[c])[r];
+    case DQ_TYPE_I8: return (uint64_t)(int64_t)reinterpret_cast<const int8_t*>(g.values[c])[r];
+    case DQ_TYPE_BOOL: return (reinterpret_cast<const uint32_t*>(g.values[c])[r >> 5] >> (r & 31)) & 1u;
+    default: return (uint64_t)(int64_t)reinterpret_cast<const int32_t*>(g.values[c])[r];  // IntegerType, DateType
   }
 }
 
@@ -553,7 +562,7 @@ static dq_status freq_build_impl(const int32_t* types, int32_t n_cols, const dq_
   if (n_chunks < 0 || n_chunks > kMaxGroupChunks || (n_chunks > 0 && (!cols || !chunk_rows)))
     return set_error(DQ_E_INVALID, "dq_freq_build: bad chunks (at most %d)", kMaxGroupChunks);
   for (int c = 0; c < n_cols; ++c)
-    if (types[c] < DQ_TYPE_F64 || types[c] > DQ_TYPE_LARGE_UTF8)
+    if (types[c] < DQ_TYPE_F64 || types[c] > DQ_TYPE_MAX)
       return set_error(DQ_E_TYPE, "dq_freq_build: column %d has unknown type %d", c, types[c]);
   int64_t total = 0;
   for (int k = 0; k < n_chunks; ++k) {
@@ -567,7 +576,8 @@ static dq_status freq_build_impl(const int32_t* types, int32_t n_cols, const dq_
   t->device = device;
   t->stream = reinterpret_cast<hipStream_t>(hip_stream);
   t->types.assign(types, types + n_cols);
-  const bool numeric1 = n_cols == 1 && (types[0] == DQ_TYPE_F64 || types[0] == DQ_TYPE_I64 || types[0] == DQ_TYPE_I32);
+  // one fixed-width column: grouped by its exact value bits (strings and tuples: by hash, checked exactly)
+  const bool numeric1 = n_cols == 1 && types[0] != DQ_TYPE_UTF8 && types[0] != DQ_TYPE_LARGE_UTF8;
   t->hashed = numeric1 && !mi ? 0 : 1;
 
   // test hook: keep only some bits of the primary tuple hash, to force collisions between distinct tuples

@@ -640,6 +640,53 @@ __global__ void dq_digest_gather(const unsigned long long* __restrict__ sorted, 
   if (i < m) out[i] = idx[i] >= 0 ? sorted[idx[i]] : 0ull;  // -1: a sample known without compaction
 }
 
+// FloatType / ShortType / ByteType columns (ApproxQuantile's isNumeric precondition takes them): widened on the
+// device into a scratch column per chunk -- float -> double and short / byte -> int are exact, and the order
+// statistic of the widened values is the widened order statistic -- then the F64 / I32 select and digest run
+// unchanged.  One extra streaming pass (read 1-4 B, write 4-8 B per row) ahead of passes that read the column
+// several times.
+__global__ void widen_column(const void* __restrict__ src, int32_t type, void* __restrict__ dst, int64_t n) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+    if (type == DQ_TYPE_F32) reinterpret_cast<double*>(dst)[r] = (double)__builtin_nontemporal_load(reinterpret_cast<const float*>(src) + r);
+    else if (type == DQ_TYPE_I16) reinterpret_cast<int32_t*>(dst)[r] = __builtin_nontemporal_load(reinterpret_cast<const int16_t*>(src) + r);
+    else reinterpret_cast<int32_t*>(dst)[r] = __builtin_nontemporal_load(reinterpret_cast<const int8_t*>(src) + r);
+  }
+}
+
+struct Widened {
+  int32_t type = 0;
+  std::vector<dq_column_view> views;
+  std::vector<void*> bufs;
+  hipStream_t stream = nullptr;
+  ~Widened() {
+    if (!bufs.empty()) (void)hipStreamSynchronize(stream);
+    for (void* b : bufs) (void)hipFree(b);
+  }
+};
+
+bool is_narrow(int32_t type) { return type == DQ_TYPE_F32 || type == DQ_TYPE_I16 || type == DQ_TYPE_I8; }
+
+dq_status widen(int32_t type, const dq_column_view* cols, const int64_t* chunk_rows, int32_t n_chunks, int32_t device,
+                hipStream_t stream, Widened& w) {
+  QHIP(hipSetDevice(device));
+  w.type = type == DQ_TYPE_F32 ? DQ_TYPE_F64 : DQ_TYPE_I32;
+  w.stream = stream;
+  const int64_t bytes = type == DQ_TYPE_F32 ? 8 : 4;
+  w.views.assign(cols, cols + n_chunks);
+  for (int c = 0; c < n_chunks; ++c) {
+    const int64_t n = chunk_rows[c];
+    if (n == 0) continue;
+    void* d = nullptr;
+    QHIP(hipMalloc(&d, (size_t)(n * bytes + 16)));
+    w.bufs.push_back(d);
+    const int grid = (int)std::min<int64_t>(4096, (n + 255) / 256);
+    hipLaunchKernelGGL(widen_column, dim3(grid), dim3(256), 0, stream, cols[c].values, type, d, n);
+    QHIP(hipGetLastError());
+    w.views[c].values = d;
+  }
+  return DQ_OK;
+}
+
 }  // namespace
 }  // namespace dq
 
@@ -654,6 +701,14 @@ dq_status dq_approx_quantiles(int32_t type, const dq_column_view* cols, const in
     return set_error(DQ_E_INVALID, "dq_approx_quantiles: NULL argument");
   if (n_q < 1 || n_q > DQ_MAX_QUANTILES)
     return set_error(DQ_E_INVALID, "dq_approx_quantiles: %d quantiles (1..%d per call)", n_q, DQ_MAX_QUANTILES);
+  if (is_narrow(type)) {
+    for (int c = 0; c < n_chunks; ++c)
+      if (chunk_rows[c] > 0 && !cols[c].values) return set_error(DQ_E_INVALID, "dq_approx_quantiles: chunk %d has no values", c);
+    Widened w;
+    if (dq_status s = widen(type, cols, chunk_rows, n_chunks, device, reinterpret_cast<hipStream_t>(hip_stream), w)) return s;
+    return dq_approx_quantiles(w.type, w.views.data(), chunk_rows, n_chunks, quantiles, n_q, relative_error, device,
+                               hip_stream, out, count);
+  }
   if (type != DQ_TYPE_F64 && type != DQ_TYPE_I64 && type != DQ_TYPE_I32)
     return set_error(DQ_E_TYPE, "dq_approx_quantiles: column type %d is not numeric", type);
   // ApproxQuantile.scala:46-56 PARAM_CHECKS (MetricCalculationException messages)
@@ -852,6 +907,14 @@ dq_status dq_quantile_digest(int32_t type, const dq_column_view* cols, const int
                              int64_t cap, int64_t* n_samples, int64_t* count) {
   if (!cols || !chunk_rows || !n_samples || !count || n_chunks < 0 || cap < 0 || (cap > 0 && (!values || !ranks)))
     return set_error(DQ_E_INVALID, "dq_quantile_digest: NULL argument");
+  if (is_narrow(type)) {
+    for (int c = 0; c < n_chunks; ++c)
+      if (chunk_rows[c] > 0 && !cols[c].values) return set_error(DQ_E_INVALID, "dq_quantile_digest: chunk %d has no values", c);
+    Widened w;
+    if (dq_status s = widen(type, cols, chunk_rows, n_chunks, device, reinterpret_cast<hipStream_t>(hip_stream), w)) return s;
+    return dq_quantile_digest(w.type, w.views.data(), chunk_rows, n_chunks, relative_error, device, hip_stream, values,
+                              ranks, cap, n_samples, count);
+  }
   if (type != DQ_TYPE_F64 && type != DQ_TYPE_I64 && type != DQ_TYPE_I32)
     return set_error(DQ_E_TYPE, "dq_quantile_digest: column type %d is not numeric", type);
   if (!(relative_error >= 0.0 && relative_error <= 1.0))

@@ -18,18 +18,56 @@ from .metrics import DoubleMetric, EmptyStateException, Entity, Failure, Success
 from .states import State
 
 _TYPES = {"f64": L.TYPE_F64, "i64": L.TYPE_I64, "i32": L.TYPE_I32, "utf8": L.TYPE_UTF8,
-          "large_utf8": L.TYPE_LARGE_UTF8}
+          "large_utf8": L.TYPE_LARGE_UTF8, "f32": L.TYPE_F32, "i16": L.TYPE_I16, "i8": L.TYPE_I8,
+          "bool": L.TYPE_BOOL, "date32": L.TYPE_DATE32, "timestamp": L.TYPE_TIMESTAMP}
 
 
 def _gpu_type(dtype: str) -> int:
-    """The grouping / quantile kernels' column type; the round-6 scan types (f32, i16, i8, bool, date32,
-    timestamp) are not theirs: such an analyzer stays on the Spark fallback."""
+    """The grouping / quantile kernels' column type code."""
     t = _TYPES.get(dtype)
     if t is None:
         from .metrics import UnsupportedOnGpuPathException
 
-        raise UnsupportedOnGpuPathException(f"column type {dtype} is not a grouping / quantile GPU column type")
+        raise UnsupportedOnGpuPathException(f"column type {dtype} is not a GPU column type")
     return t
+
+
+def _java_float_to_string(f: float) -> str:
+    """java.lang.Float.toString (CAST(float AS STRING)): Double.toString's forms with float's shortest digits."""
+    import math
+
+    import numpy as np
+
+    if math.isnan(f) or math.isinf(f) or f == 0.0:
+        return _java_double_to_string(f)
+    if 1e-3 <= abs(f) < 1e7:
+        r = np.format_float_positional(np.float32(f), unique=True)
+        return r + "0" if r.endswith(".") else r
+    m, e = np.format_float_scientific(np.float32(f), unique=True, exp_digits=1).split("e")
+    return f"{m + '0' if m.endswith('.') else m}E{int(e)}"
+
+
+def _render_fixed(dtype: str, key: int) -> str:
+    """CAST(value AS STRING) of a fixed-width grouping key (value bits, integers sign-extended; timestamps in UTC
+    as Spark's DateTimeUtils.timestampToString with the session zone UTC)."""
+    import datetime
+
+    import numpy as np
+
+    v = int(np.uint64(key).astype(np.int64))
+    if dtype == "f64":
+        return _java_double_to_string(float(np.uint64(key).view(np.float64)))
+    if dtype == "f32":
+        return _java_float_to_string(float(np.uint32(key & 0xFFFFFFFF).view(np.float32)))
+    if dtype == "bool":
+        return "true" if v else "false"
+    if dtype == "date32":
+        return (datetime.date(1970, 1, 1) + datetime.timedelta(days=v)).isoformat()
+    if dtype == "timestamp":
+        t = datetime.datetime(1970, 1, 1) + datetime.timedelta(microseconds=v)
+        frac = f"{t.microsecond:06d}".rstrip("0")
+        return t.strftime("%Y-%m-%d %H:%M:%S") + ("." + frac if frac else "")
+    return str(v)
 
 
 class FreqTable:
@@ -352,10 +390,8 @@ class Histogram(Analyzer):  # Histogram.scala:33-99
     def _render(self, data, dtype: str, key: int, rep: int) -> str:
         import numpy as np
 
-        if dtype in ("i64", "i32"):
-            return str(int(np.uint64(key).astype(np.int64)))
-        if dtype == "f64":
-            return _java_double_to_string(float(np.uint64(key).view(np.float64)))
+        if dtype not in ("utf8", "large_utf8"):
+            return _render_fixed(dtype, key)
         if rep == (1 << 64) - 1:
             raise NotImplementedError("Histogram of a merged string frequency table (no representative rows)")
         from .runner import _chunks

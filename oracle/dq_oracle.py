@@ -1458,6 +1458,9 @@ def _group_key(c: "OColumn", i: int):
     if c.dtype == "f64":
         v = float(c.values[i])
         return ("f", b"nan" if math.isnan(v) else struct.pack("<d", v))
+    if c.dtype == "f32":  # FloatType in an UnsafeRow: NaN canonical, -0.0 and 0.0 distinct
+        v = float(c.values[i])
+        return ("f", b"nan" if math.isnan(v) else struct.pack("<f", v))
     if c.dtype in ("utf8", "large_utf8"):
         return ("s", c.values[i])
     return ("i", int(c.values[i]))
@@ -1714,6 +1717,8 @@ def gk_digest_exact(values: np.ndarray, valid: np.ndarray, relative_error: float
 def approx_quantiles_exact(values: np.ndarray, valid: np.ndarray, quantiles: Sequence[float],
                            relative_error: float = 0.01) -> Optional[List[float]]:
     v = np.asarray(values)[np.asarray(valid, bool)]
+    if v.dtype == np.float32:  # FloatType: the exactly widened doubles
+        v = v.astype(np.float64)
     n = len(v)
     if n == 0:
         return None

@@ -215,15 +215,94 @@ def test_mixed_profile_chunks_vs_oracle(dq):
             a, got, want)
 
 
-def test_non_numeric_preconditions_and_grouping_fallback(dq):
-    """Mean over a BooleanType / DateType / TimestampType column fails its isNumeric precondition (the reference's
-    WrongColumnTypeException text); a grouping analyzer over a round-6 type stays on the Spark fallback."""
-    from deequ_amd.metrics import UnsupportedOnGpuPathException, WrongColumnTypeException
+def test_non_numeric_preconditions(dq):
+    """Mean / Maximum / Sum / ApproxQuantile over a BooleanType / DateType / TimestampType column fail their isNumeric
+    precondition with the reference's WrongColumnTypeException text."""
+    from deequ_amd.metrics import WrongColumnTypeException
 
     t, _ = _table(dq, 1000, seed=1, null_frac=0.0)
-    an = [dq.Mean("c_bool"), dq.Maximum("c_date32"), dq.Sum("c_timestamp"), dq.Uniqueness(["c_i8"])]
+    an = [dq.Mean("c_bool"), dq.Maximum("c_date32"), dq.Sum("c_timestamp"), dq.ApproxQuantile("c_bool", 0.5)]
     ctx = dq.AnalysisRunner.onData(t).addAnalyzers(an).run()
-    for a, spark in zip(an[:3], ("BooleanType", "DateType", "TimestampType")):
+    for a, spark in zip(an, ("BooleanType", "DateType", "TimestampType", "BooleanType")):
         err = ctx.metric(a).value.failed
         assert isinstance(err, WrongColumnTypeException) and f"but found {spark} instead" in str(err), err
-    assert isinstance(ctx.metric(an[3]).value.failed, UnsupportedOnGpuPathException)
+
+
+def _group_data(n, seed):
+    """Low-cardinality columns of the round-6 types (duplicates, NaN / -0.0 / 0.0 in the float column)."""
+    rng = np.random.default_rng(seed)
+    f = rng.choice(np.array([1.5, -2.25, 0.0, -0.0, np.nan, 3e9, 1e-5, 7.0], dtype=np.float32), n)
+    h = rng.integers(-150, 150, n).astype(np.int16)
+    c = rng.integers(-128, 128, n).astype(np.int8)
+    b = rng.random(n) < 0.3
+    d = rng.integers(18000, 18400, n).astype(np.int32)
+    ts = rng.choice(np.array([0, 1_600_000_000_123_400, -86_400_000_001, 5_000_000], dtype=np.int64), n)
+    out = {}
+    for name, t, v in (("f", "f32", f), ("h", "i16", h), ("c", "i8", c), ("b", "bool", b), ("d", "date32", d),
+                       ("t", "timestamp", ts)):
+        out[name] = (t, v, rng.random(n) >= 0.1)
+    return out
+
+
+@pytest.mark.parametrize("n", [1, 4099, 70_001])
+def test_grouping_and_histogram_new_types_vs_oracle(dq, n):
+    """Uniqueness / Distinctness / CountDistinct / Entropy / MutualInformation / Histogram over the round-6 types:
+    single columns grouped by their exact value (NaN canonical, -0.0 != 0.0), tuples by hash with the exact check;
+    Histogram bins = the oracle's CAST-to-string frequencies (timestamps in UTC)."""
+    from deequ_amd.table import column_from_numpy
+    from tests.helpers import close
+
+    data = _group_data(n, 13 + n)
+    t = dq.Table([column_from_numpy(k, ty, v, m) for k, (ty, v, m) in data.items()])
+    ocols = {k: O.OColumn(ty, v, m) for k, (ty, v, m) in data.items()}
+    an = [dq.Uniqueness("f"), dq.Distinctness("h"), dq.CountDistinct("c"), dq.Entropy("b"), dq.Uniqueness("d"),
+          dq.CountDistinct("t"), dq.Uniqueness(["f", "b"]), dq.CountDistinct(["h", "d", "t"]),
+          dq.MutualInformation("b", "c"), dq.MutualInformation("f", "t")]
+    ctx = dq.AnalysisRunner.onData(t).addAnalyzers(an).run()
+    for a in an:
+        spec = (type(a).__name__, a.columns[0] if type(a).__name__ == "Entropy" else a.columns)
+        ref = O.compute_state(spec, ocols, n)
+        m = ctx.metric(a)
+        if ref is None:
+            assert m.value.isFailure, (a, m)
+            continue
+        want, got = ref.metricValue(), m.value.get()
+        ok = close(got, want, 1e-12, 1e-15) if type(a).__name__ in ("Entropy", "MutualInformation") else got == want
+        assert ok, (a, got, want)
+    for col in data:
+        want = O.histogram(ocols, col, n)
+        h = dq.Histogram(col).calculate(t).value.get()
+        assert h.numberOfBins == len(want), (col, h.numberOfBins, len(want))
+        for k, v in h.values.items():
+            assert want[k] == v.absolute, (col, k, v.absolute, want.get(k))
+
+
+@pytest.mark.parametrize("n", [1, 1000, 100_003])
+@pytest.mark.parametrize("dtype", ["f32", "i16", "i8"])
+def test_quantiles_new_types_vs_oracle(dq, n, dtype):
+    """ApproxQuantile(s) over FloatType / ShortType / ByteType columns (widened exactly on the device, then the
+    F64 / I32 select and digest): the exact order statistic of Spark's target rank, over two chunks."""
+    from deequ_amd.table import column_from_numpy
+
+    rng = np.random.default_rng(n + len(dtype))
+    v = _values(dtype, n, rng, special=(dtype == "f32"))
+    valid = rng.random(n) >= 0.1
+    cut = n // 2
+    chunks = [dq.Table([column_from_numpy("x", dtype, v[:cut], valid[:cut])]),
+              dq.Table([column_from_numpy("x", dtype, v[cut:], valid[cut:])])]
+    qs = [0.0, 0.1, 0.5, 0.9, 1.0]
+    for err in (0.01, 0.0):
+        want = O.approx_quantiles_exact(v, valid, qs, err)
+        m = dq.ApproxQuantiles("x", qs, err).calculate(chunks)
+        if want is None:
+            assert m.value.isSuccess and m.value.get() == {}, m
+            continue
+        from deequ_amd.grouping import _java_double_to_string
+
+        got = m.value.get()
+        for q, w in zip(qs, want):
+            g = got[_java_double_to_string(q)]
+            assert g == w or (math.isnan(g) and math.isnan(w)), (dtype, n, err, q, g, w)
+        single = dq.ApproxQuantile("x", 0.5, err).calculate(chunks).value.get()
+        w = want[qs.index(0.5)]
+        assert single == w or (math.isnan(single) and math.isnan(w))
