@@ -57,6 +57,10 @@ typedef unsigned int uint32_t;
 typedef int int32_t;
 typedef unsigned long long uint64_t;
 typedef long long int64_t;
+typedef unsigned short uint16_t;
+typedef short int16_t;
+typedef unsigned char uint8_t;
+typedef signed char int8_t;
 typedef unsigned long long uintptr_t;
 typedef const __attribute__((address_space(4))) uint32_t* dq_const_u32s;
 )DQJIT";
@@ -139,13 +143,20 @@ std::string u64lit(uint64_t v) {
 }
 
 // value expression of slot s row group j as int64 / double
+// (the loads leave a 4- / 2- / 1-byte value zero-extended in the slot's uint64_t)
 std::string as_int(int s, int kind) {
   const std::string v = "v" + std::to_string(s) + "[j]";
-  return kind == CK_I32 ? "(int64_t)(int32_t)(uint32_t)" + v : "(int64_t)" + v;
+  switch (kind) {
+    case CK_I32: return "(int64_t)(int32_t)(uint32_t)" + v;
+    case CK_I16: return "(int64_t)(int16_t)(uint16_t)" + v;
+    case CK_I8: return "(int64_t)(int8_t)(uint8_t)" + v;
+    default: return "(int64_t)" + v;
+  }
 }
 std::string as_dbl(int s, int kind) {
   const std::string v = "v" + std::to_string(s) + "[j]";
   if (kind == CK_F64) return "__longlong_as_double((long long)" + v + ")";
+  if (kind == CK_F32) return "(double)__builtin_bit_cast(float, (uint32_t)" + v + ")";  // exact, as Spark's cast
   return "(double)" + as_int(s, kind);
 }
 const char* cmp_op(int c) {
@@ -179,7 +190,7 @@ bool pred_jit_eligible(const PredProgram& prog, const int32_t* col_kind, int32_t
       if (c < 0) continue;
       if (c >= ncols) return false;
       const int k = col_kind[c];
-      if (k != CK_F64 && k != CK_I64 && k != CK_I32) return false;
+      if (k != CK_F64 && k != CK_I64 && k != CK_I32 && k != CK_F32 && k != CK_I16 && k != CK_I8) return false;
       bool seen = false;
       for (int32_t x : cols) seen = seen || x == c;
       if (!seen) cols.push_back(c);
@@ -258,7 +269,7 @@ std::string pred_jit_source(const PredProgram& prog, const int32_t* col_kind, st
   s += "  const int64_t row1 = row0 + A.rows_per_range < A.n_rows ? row0 + A.rows_per_range : A.n_rows;\n";
   for (int i = 0; i < ns; ++i) {
     const int k = col_kind[slot_col[i]];
-    const int sz = k == CK_I32 ? 4 : 8;
+    const int sz = ck_bytes(k);
     s += "  const uint32_t* vb" + std::to_string(i) + " = A.validity[" + std::to_string(i) + "];\n";
     if (need_vals[i])
       s += "  const __amdgpu_buffer_rsrc_t vr" + std::to_string(i) +
@@ -279,9 +290,15 @@ std::string pred_jit_source(const PredProgram& prog, const int32_t* col_kind, st
   auto load_vals = [&](int i, const std::string& soff, const std::string& j, const std::string& dst) {
     const int k = col_kind[slot_col[i]];
     const std::string si = std::to_string(i);
-    if (k == CK_I32)
+    if (k == CK_I32 || k == CK_F32)
       return dst + " = (uint64_t)__builtin_amdgcn_raw_buffer_load_b32(vr" + si + ", (lane + " + soff + " + 64 * " + j +
              ") * 4, 0, 2);\n";
+    if (k == CK_I16)
+      return dst + " = (uint64_t)__builtin_amdgcn_raw_buffer_load_b16(vr" + si + ", (lane + " + soff + " + 64 * " + j +
+             ") * 2, 0, 2);\n";
+    if (k == CK_I8)
+      return dst + " = (uint64_t)__builtin_amdgcn_raw_buffer_load_b8(vr" + si + ", (lane + " + soff + " + 64 * " + j +
+             "), 0, 2);\n";
     return "{ const auto w2 = __builtin_amdgcn_raw_buffer_load_b64(vr" + si + ", (lane + " + soff + " + 64 * " + j +
            ") * 8, 0, 2); " + dst + " = ((uint64_t)w2[1] << 32) | w2[0]; }\n";
   };

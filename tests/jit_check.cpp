@@ -107,6 +107,18 @@ int main(int argc, char** argv) {
     const int32_t kinds[2] = {CK_F64, CK_I32};
     run(outdir, "mixed", make(code, 2, 2, 1), kinds, 2, {});
   }
+  // FloatType / ShortType / ByteType atoms (round 6): 4- / 2- / 1-byte loads, float widened to double
+  {
+    std::vector<PredInstr> code = {cmp(0, C_GE, 16777216, CK_F32, -1, NR_NULL, CT_DBL), op(PO_STORE, 0),
+                                   cmp(1, C_LT, -100, CK_I16), cmp(2, C_NE, 0, CK_I8, -1, NR_TRUE), op(PO_AND),
+                                   op(PO_STORE, 1)};
+    PredInstr mix = cmp(2, C_LT, 0, CK_I8, 1, NR_NULL, CT_INT);  // i8 vs i16 column
+    mix.kind_b = CK_I16;
+    code.push_back(mix);
+    code.push_back(op(PO_STORE, 2));
+    const int32_t kinds[3] = {CK_F32, CK_I16, CK_I8};
+    run(outdir, "narrow", make(code, 3, 3, 0), kinds, 3, {});
+  }
   // a string column in the program: not eligible (the interpreter runs it)
   {
     std::vector<PredInstr> code = {isnull(0), op(PO_STORE, 0)};

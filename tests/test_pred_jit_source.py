@@ -28,7 +28,7 @@ def test_generated_kernels_compile(tmp_path):
     out = subprocess.run([str(exe), str(tmp_path)], capture_output=True, text=True, check=True, timeout=300)
     res = {line.split()[0]: [int(x) for x in line.split()[1:]] for line in out.stdout.splitlines()}
     assert res["string"][0] == 0, "a string column must stay on the interpreter"
-    for name in ("c3", "mixed"):
+    for name in ("c3", "mixed", "narrow"):
         eligible, rc, nbytes = res[name]
         assert eligible == 1 and rc == 0 and nbytes > 0, (name, res[name], out.stderr[-2000:])
         notes = subprocess.run([READELF, "--notes", str(tmp_path / f"{name}.co")], capture_output=True, text=True,

@@ -306,3 +306,35 @@ def test_quantiles_new_types_vs_oracle(dq, n, dtype):
         single = dq.ApproxQuantile("x", 0.5, err).calculate(chunks).value.get()
         w = want[qs.index(0.5)]
         assert single == w or (math.isnan(single) and math.isnan(w))
+
+
+NARROW_PREDICATES = [
+    "c_f32 > 3", "c_f32 >= 16777217", "COALESCE(c_f32, 0.0) >= 0", "c_f32 < c_i16", "c_i16 > 2.5",
+    "COALESCE(c_i16, 1.0) > 0", "c_i8 = 5", "c_i8 < c_i16", "c_i8 IS NULL OR c_f32 > 1e2", "NOT (c_i8 > 0)",
+]
+
+
+@pytest.mark.parametrize("n", [4097, 70_001])
+def test_compiled_predicate_pass_narrow_types(dq, n):
+    """The predicate kernel generated and compiled for a program over FloatType / ShortType / ByteType columns
+    (4- / 2- / 1-byte loads, float widened exactly): DQ_PRED_PASS_COMPILED takes it, and its counters and `where`
+    bitmaps equal the interpreter's and the oracle's."""
+    from deequ_amd.runner import ScanPlan, scan_states
+
+    t, host = _table(dq, n, seed=29 + n, null_frac=0.1)
+    f = host["c_f32"].values
+    f[: n // 10] = np.float32(16777216.0)
+    from deequ_amd.table import column_from_numpy
+
+    t.columns["c_f32"] = column_from_numpy("c_f32", "f32", f, host["c_f32"].valid)
+    an = [dq.Compliance(f"q{k}", p) for k, p in enumerate(NARROW_PREDICATES)]
+    an += [dq.Sum("c_i16", where="c_f32 > 0")]
+    plan = ScanPlan(an, t.schema, pred_pass="compiled")
+    ok, note = plan.pred_compiled()
+    plan.close()
+    assert ok, note
+    comp = scan_states(t, an, "compiled")
+    _check(comp, an, host, n)
+    interp = scan_states(t, an, "interpreter")
+    for a in an:
+        assert comp[a] == interp[a], a
