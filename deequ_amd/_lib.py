@@ -8,7 +8,7 @@ from __future__ import annotations
 import ctypes
 import os
 
-ABI_VERSION = 5  # include/dqscan.h DQ_ABI_VERSION
+ABI_VERSION = 6  # include/dqscan.h DQ_ABI_VERSION
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DQ_LIB_PATH") or os.path.join(_HERE, "libdqscan.so")  # override: diagnostic A/B builds
@@ -24,6 +24,15 @@ DQ_E_STATE = -6
 TYPE_F64, TYPE_I64, TYPE_I32, TYPE_UTF8, TYPE_LARGE_UTF8 = 1, 2, 3, 4, 5
 # round 6: FloatType, ShortType, ByteType, BooleanType (bit-packed), DateType (int32 days), TimestampType (int64 us)
 TYPE_F32, TYPE_I16, TYPE_I8, TYPE_BOOL, TYPE_DATE32, TYPE_TIMESTAMP = 6, 7, 8, 9, 10, 11
+# DecimalType(p, s): 16-byte two's-complement unscaled values; its type code carries p and s (DQ_DECIMAL128)
+TYPE_DECIMAL128 = 12
+
+
+def decimal_type(precision: int, scale: int) -> int:
+    """DQ_DECIMAL128(p, s): the type code of a DecimalType(p, s) column (1 <= p <= 38, 0 <= s <= p)."""
+    if not (1 <= precision <= 38 and 0 <= scale <= precision):
+        raise ValueError(f"DecimalType({precision},{scale}) is not a GPU column type (precision 1..38, scale 0..p)")
+    return TYPE_DECIMAL128 | precision << 8 | scale << 16
 
 # column-pass kernel variants (deequ_amd/csrc/dq_device.h ColVariant)
 VARIANT_NAMES = {0: "validity", 1: "f64_stats", 2: "f64_stats_hll", 3: "f64_hll", 4: "i64_stats",
@@ -31,7 +40,8 @@ VARIANT_NAMES = {0: "validity", 1: "f64_stats", 2: "f64_stats_hll", 3: "f64_hll"
                  10: "utf8_hll", 11: "large_utf8_hll", 12: "utf8_dtype", 13: "utf8_hll_dtype",
                  14: "large_utf8_dtype", 15: "large_utf8_hll_dtype", 16: "f64_dtype",
                  17: "f32_stats", 18: "f32_stats_hll", 19: "f32_hll", 20: "i16_stats", 21: "i16_stats_hll",
-                 22: "i16_hll", 23: "i8_stats", 24: "i8_stats_hll", 25: "i8_hll", 26: "f32_dtype", 27: "bool"}
+                 22: "i16_hll", 23: "i8_stats", 24: "i8_stats_hll", 25: "i8_hll", 26: "f32_dtype", 27: "bool",
+                 28: "d128_stats", 29: "d128_stats_hll", 30: "d128_hll", 31: "d128_dtype"}
 
 OP_SIZE = 1
 OP_COMPLETENESS = 2
@@ -104,11 +114,14 @@ class _Ratio(ctypes.Structure):
 
 
 class _Sum(ctypes.Structure):
-    _fields_ = [("sum", ctypes.c_double), ("partial", ctypes.c_int64)]
+    _fields_ = [("sum", ctypes.c_double), ("partial", ctypes.c_int64), ("partial_hi", ctypes.c_int64),
+                ("guard", ctypes.c_double), ("dec_scale", ctypes.c_int32), ("dec_digits", ctypes.c_int32)]
 
 
 class _Mean(ctypes.Structure):
-    _fields_ = [("sum", ctypes.c_double), ("count", ctypes.c_int64), ("partial", ctypes.c_int64)]
+    _fields_ = [("sum", ctypes.c_double), ("count", ctypes.c_int64), ("partial", ctypes.c_int64),
+                ("partial_hi", ctypes.c_int64), ("guard", ctypes.c_double), ("dec_scale", ctypes.c_int32),
+                ("dec_digits", ctypes.c_int32)]
 
 
 class _StdDev(ctypes.Structure):

@@ -22,13 +22,18 @@ from .metrics import (DoubleMetric, EmptyStateException, Entity, Failure, NoSuch
                       WrongColumnTypeException, wrap_if_necessary)
 from .predicates import PredicatePool
 from .states import State, state_from_c
-from .table import NUMERIC
+from .table import decimal_ps, is_numeric
 
 Schema = Sequence  # list of (name, dtype, nullable)
 # the Spark SQL type each column dtype carries (WrongColumnTypeException text, Analyzer.scala:330-332)
 SPARK_TYPE = {"f64": "DoubleType", "f32": "FloatType", "i64": "LongType", "i32": "IntegerType", "i16": "ShortType",
               "i8": "ByteType", "bool": "BooleanType", "date32": "DateType", "timestamp": "TimestampType",
               "utf8": "StringType", "large_utf8": "StringType"}
+
+
+def spark_type(dtype: str) -> str:
+    ps = decimal_ps(dtype)
+    return f"DecimalType({ps[0]},{ps[1]})" if ps else SPARK_TYPE.get(dtype, dtype)
 
 
 def _opt(x: Optional[str]) -> str:
@@ -47,10 +52,10 @@ class Preconditions:
     def isNumeric(column: str) -> Callable:
         def check(schema):
             t = dict((c[0], c[1]) for c in schema)[column]
-            if t not in NUMERIC:
+            if not is_numeric(t):
                 raise WrongColumnTypeException(
                     f"Expected type of column {column} to be one of (ByteType,ShortType,IntegerType,LongType,"
-                    f"FloatType,DoubleType,DecimalType), but found {SPARK_TYPE.get(t, t)} instead!")
+                    f"FloatType,DoubleType,DecimalType), but found {spark_type(t)} instead!")
         return check
 
     @staticmethod
@@ -85,11 +90,11 @@ class PlanBuilder:
 
     def schema_ctypes(self):
         arr = (L.ColumnDesc * max(1, len(self.columns)))()
-        from .table import DTYPES
+        from .table import type_code
 
         for i, name in enumerate(self.columns):
             _, dt, nullable = self.by_name[name]
-            arr[i].type = DTYPES[dt]
+            arr[i].type = type_code(dt)
             arr[i].nullable = 1 if nullable else 0
         return arr
 
@@ -342,10 +347,10 @@ class PatternMatch(_ColumnAnalyzer):  # PatternMatch.scala:37-56
 
     def _lower(self, b):
         from .predicates import UnsupportedPredicate
-        from .table import DTYPES
+        from .table import type_code
 
         col = b.col(self.column)
-        if DTYPES[b.by_name[self.column][1]] not in (L.TYPE_UTF8, L.TYPE_LARGE_UTF8):
+        if type_code(b.by_name[self.column][1]) not in (L.TYPE_UTF8, L.TYPE_LARGE_UTF8):
             raise UnsupportedPredicate(f"PatternMatch on non-string column {self.column} (Spark casts it to string)")
         root = b.pool.add_regex(col, self.pattern, L.REGEX_EXTRACT_NONEMPTY)
         return (L.OP_PATTERN_MATCH, col, -1, root, b.pred(self.where))

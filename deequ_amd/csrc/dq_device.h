@@ -37,10 +37,15 @@ constexpr int kMaxRegexWords = 32768;       // compiled regex DFAs of one plan (
 enum ColKind : int32_t {
   CK_F64 = 1, CK_I64 = 2, CK_I32 = 3, CK_UTF8 = 4, CK_LUTF8 = 5,
   CK_F32 = 6, CK_I16 = 7, CK_I8 = 8, CK_BOOL = 9,  // (BOOL: LSB-first value bitmap)
+  CK_D128 = 10,  // DecimalType: 16-byte two's-complement unscaled values (the column pass)
+  // a decimal column's 64-bit halves as predicate atom operands (stride 16; the planner splits a 128-bit
+  // comparison into atoms on them): the low word as a signed long (precision <= 18: the whole value), the high
+  // word, and the low word with its sign bit flipped (unsigned order as signed order)
+  CK_D128_LO = 11, CK_D128_HI = 12, CK_D128_LOU = 13,
 };
 constexpr bool ck_float(int k) { return k == CK_F64 || k == CK_F32; }
 constexpr int ck_bytes(int k) {
-  return k == CK_F64 || k == CK_I64 ? 8 : k == CK_I32 || k == CK_F32 ? 4 : k == CK_I16 ? 2 : 1;
+  return k >= CK_D128 ? 16 : k == CK_F64 || k == CK_I64 ? 8 : k == CK_I32 || k == CK_F32 ? 4 : k == CK_I16 ? 2 : 1;
 }
 
 // column-pass variants (kind x what is accumulated); VALIDITY = count of selected rows only
@@ -59,8 +64,11 @@ enum ColVariant : int32_t {
   CV_I16_S = 20, CV_I16_SH = 21, CV_I16_H = 22,
   CV_I8_S = 23, CV_I8_SH = 24, CV_I8_H = 25,
   CV_F32_D = 26, CV_BOOL = 27,
+  // DecimalType (ColTask::arg = precision | scale << 8): values cast to double as Decimal.toDouble (correctly
+  // rounded), the exact 128-bit sum, Spark 2.2's decimal hash, and the DataType count of BigDecimal.toString
+  CV_D128_S = 28, CV_D128_SH = 29, CV_D128_H = 30, CV_D128_D = 31,
 };
-constexpr int kNumVariants = 28;
+constexpr int kNumVariants = 32;
 
 // per-variant row-range counts of one scan (dq_finalize merges nr[i] partials for tasks [first, end))
 // column-task ranges whose range count differs from the scan's default (string passes, the validity pass, a
@@ -76,6 +84,8 @@ struct ColTask {
   int32_t col;       // column index
   int32_t where;     // where-bitmap index or -1
   int32_t hll_slot;  // index into HLL partial / accumulator arrays, -1 if none
+  int32_t arg;       // CV_D128_*: precision | scale << 8
+  int32_t pad[3];
 };
 
 struct PairTask {
@@ -134,7 +144,7 @@ struct alignas(16) ColPartial {
   double fmin, fmax;    // min / max over selected non-NaN values (F64)
   int64_t pinf_count;   // selected +inf values (F64; kept out of the moments, added back in dq_finish)
   int64_t ninf_count;   // selected -inf values (F64)
-  int64_t pad;
+  int64_t isum_hi;      // D128: high word of the exact 128-bit sum (isum its low word; `sum` the fp64 guard)
 };
 static_assert(sizeof(ColPartial) == 96, "ColPartial layout");
 

@@ -561,9 +561,12 @@ static dq_status freq_build_impl(const int32_t* types, int32_t n_cols, const dq_
     return set_error(DQ_E_INVALID, "dq_freq_build: 1..%d grouping columns", kMaxGroupCols);
   if (n_chunks < 0 || n_chunks > kMaxGroupChunks || (n_chunks > 0 && (!cols || !chunk_rows)))
     return set_error(DQ_E_INVALID, "dq_freq_build: bad chunks (at most %d)", kMaxGroupChunks);
-  for (int c = 0; c < n_cols; ++c)
-    if (types[c] < DQ_TYPE_F64 || types[c] > DQ_TYPE_MAX)
+  for (int c = 0; c < n_cols; ++c) {
+    if (!type_valid(types[c]))
       return set_error(DQ_E_TYPE, "dq_freq_build: column %d has unknown type %d", c, types[c]);
+    if (is_decimal(types[c]))
+      return set_error(DQ_E_UNSUPPORTED, "dq_freq_build: grouping by a DecimalType column runs on the fallback");
+  }
   int64_t total = 0;
   for (int k = 0; k < n_chunks; ++k) {
     if (chunk_rows[k] < 0 || chunk_rows[k] >= (1ll << kRowBits)) return set_error(DQ_E_INVALID, "chunk rows");

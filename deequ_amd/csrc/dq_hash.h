@@ -5,7 +5,7 @@
 
 #include <cstdint>
 
-#if defined(__HIPCC__) || defined(__HIP__)
+#if defined(__HIP__)
 #define DQ_HD __host__ __device__ __forceinline__
 #else
 #define DQ_HD inline

@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 #include <thread>
 #include <vector>
@@ -46,6 +47,20 @@ int32_t type_of_format(const char* f) {
   // timestamp[us, tz]: Spark's TimestampType is UTC microseconds whatever the session zone (other units are not
   // TimestampType values: a producer converts them)
   if (std::strncmp(f, "tsu:", 4) == 0) return DQ_TYPE_TIMESTAMP;
+  // decimal128 "d:precision,scale[,128]" (Spark's DecimalType(p, s); no negative scales, no 256-bit width)
+  if (f[0] == 'd' && f[1] == ':') {
+    int p = -1, sc = -1, w = 128, n = 0;
+    const int k = std::sscanf(f + 2, "%d,%d%n", &p, &sc, &n);
+    if (k != 2) return 0;
+    const char* rest = f + 2 + n;
+    if (*rest == ',') {
+      if (std::sscanf(rest + 1, "%d", &w) != 1) return 0;
+    } else if (*rest != '\0') {
+      return 0;
+    }
+    if (w != 128 || p < 1 || p > dq::kDecMaxPrecision || sc < 0 || sc > p) return 0;
+    return DQ_DECIMAL128(p, sc);
+  }
   return 0;
 }
 
@@ -56,7 +71,7 @@ int64_t value_width(int32_t type) {
     case DQ_TYPE_I32: case DQ_TYPE_F32: case DQ_TYPE_DATE32: return 4;
     case DQ_TYPE_I16: return 2;
     case DQ_TYPE_I8: return 1;
-    default: return 0;
+    default: return dq::is_decimal(type) ? 16 : 0;
   }
 }
 
@@ -157,7 +172,7 @@ dq_status dq_arrow_import(const struct ArrowSchema* schema, const struct ArrowAr
   if (!schema->release || !array->release) return set_error(DQ_E_INVALID, "dq_arrow_import: released Arrow structure");
   const int32_t type = type_of_format(schema->format);
   if (!type)
-    return set_error(DQ_E_UNSUPPORTED, "Arrow format '%s' is not a GPU column type (g, f, l, i, s, c, b, tdD, tsu:, u, U)",
+    return set_error(DQ_E_UNSUPPORTED, "Arrow format '%s' is not a GPU column type (g, f, l, i, s, c, b, tdD, tsu:, d:p,s, u, U)",
                      schema->format ? schema->format : "(null)");
   if (schema->n_children != 0 || array->n_children != 0 || schema->dictionary || array->dictionary)
     return set_error(DQ_E_UNSUPPORTED, "nested / dictionary-encoded Arrow arrays are not GPU columns");

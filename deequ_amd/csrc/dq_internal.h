@@ -4,9 +4,28 @@
 #include <cstdarg>
 #include <cstdint>
 
+#include <hip/hip_runtime.h>  // (dq_decimal.h's host + device functions: every TU here is compiled as HIP)
+
 #include "../../include/dqscan.h"
+#include "dq_decimal.h"
 
 namespace dq {
+
+// Column type codes: a DECIMAL128 code carries (precision, scale) above its enum value (DQ_DECIMAL128); every other
+// code is its enum value alone.
+inline bool is_decimal(int32_t t) { return DQ_TYPE_BASE(t) == DQ_TYPE_DECIMAL128; }
+inline bool type_valid(int32_t t) {
+  if (t >= DQ_TYPE_F64 && t <= DQ_TYPE_TIMESTAMP) return true;
+  if ((t & ~0xFFFFFF) != 0 || !is_decimal(t)) return false;
+  const int p = DQ_DECIMAL_PRECISION(t), s = DQ_DECIMAL_SCALE(t);
+  return p >= 1 && p <= kDecMaxPrecision && s <= p;
+}
+// dq_decimal.h's constants for host code (dq_state.cpp)
+const DecTab& dec_host_tab();
+// Sum of a DECIMAL128 column as Spark 2.2 finishes it: the exact sum (128-bit, wrapped) at scale s cast to double;
+// false when the sum is Spark's NULL (unscaled magnitude >= 10^digits, or the fp64 guard says the wrapped image is
+// not the sum)
+bool dec_sum_value(int64_t lo, int64_t hi, double guard, int s, int digits, double& out);
 
 // HLL++ geometry (StatefulHyperloglogPlus.scala:154-161, HLLConstants.scala:27-35)
 constexpr int kHllP = 9;

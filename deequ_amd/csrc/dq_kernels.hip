@@ -20,9 +20,16 @@
 
 #include "dq_device.h"
 #include "dq_hash.h"
+#include "dq_decimal.h"
 #include "dq_lane.h"
 
 namespace dq {
+
+// DecimalType conversion constants (tools/gen_dec_tables.py) in constant memory
+#define DQ_DEC_TABLE static __constant__ const
+#include "dq_dec_tables.inc"
+#undef DQ_DEC_TABLE
+__device__ __forceinline__ DecTab dec_dev_tab() { return DecTab{kDecP10Lo, kDecP10Hi, kDecRcpHi, kDecRcpLo}; }
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -139,6 +146,7 @@ struct ColStats {
   int64_t isum, count, nan_count;
   double fmin, fmax;
   int64_t pinf, ninf;  // selected +-inf values of an F64 column (outside n / mean / m2 / sum)
+  int64_t isum_hi;     // D128: (isum, isum_hi) = the exact 128-bit sum (wrapping)
 };
 
 __device__ __forceinline__ void stats_init(ColStats& s) {
@@ -147,6 +155,7 @@ __device__ __forceinline__ void stats_init(ColStats& s) {
   s.fmin = __longlong_as_double(0x7FF0000000000000ll);   // +inf
   s.fmax = __longlong_as_double((long long)0xFFF0000000000000ull);  // -inf
   s.pinf = 0; s.ninf = 0;
+  s.isum_hi = 0;
 }
 
 // a <- a (+) b ; exact Chan/Welford combination (same algebra as StandardDeviationState.sum)
@@ -164,7 +173,11 @@ __device__ __forceinline__ void stats_merge(ColStats& a, const ColStats& b) {
   }
   a.n = n;
   a.sum += b.sum;
-  a.isum = (int64_t)((uint64_t)a.isum + (uint64_t)b.isum);
+  {  // 128-bit add (the high word only matters for decimal columns)
+    const uint64_t lo = (uint64_t)a.isum + (uint64_t)b.isum;
+    a.isum_hi = (int64_t)((uint64_t)a.isum_hi + (uint64_t)b.isum_hi + (lo < (uint64_t)a.isum ? 1u : 0u));
+    a.isum = (int64_t)lo;
+  }
   a.count += b.count;
   a.nan_count += b.nan_count;
   a.fmin = hw_min(a.fmin, b.fmin);
@@ -180,18 +193,20 @@ __device__ __forceinline__ ColStats stats_shfl_xor(const ColStats& s, int m) {
   o.isum = __shfl_xor(s.isum, m); o.count = __shfl_xor(s.count, m); o.nan_count = __shfl_xor(s.nan_count, m);
   o.fmin = __shfl_xor(s.fmin, m); o.fmax = __shfl_xor(s.fmax, m);
   o.pinf = __shfl_xor(s.pinf, m); o.ninf = __shfl_xor(s.ninf, m);
+  o.isum_hi = __shfl_xor(s.isum_hi, m);
   return o;
 }
 
 __device__ __forceinline__ void stats_store(ColPartial* p, const ColStats& s) {
   p->n = s.n; p->mean = s.mean; p->m2 = s.m2; p->sum = s.sum; p->isum = s.isum; p->count = s.count;
   p->nan_count = s.nan_count; p->fmin = s.fmin; p->fmax = s.fmax; p->pinf_count = s.pinf; p->ninf_count = s.ninf;
-  p->pad = 0;
+  p->isum_hi = s.isum_hi;
 }
 __device__ __forceinline__ ColStats stats_load(const ColPartial* p) {
   ColStats s;
   s.n = p->n; s.mean = p->mean; s.m2 = p->m2; s.sum = p->sum; s.isum = p->isum; s.count = p->count;
   s.nan_count = p->nan_count; s.fmin = p->fmin; s.fmax = p->fmax; s.pinf = p->pinf_count; s.ninf = p->ninf_count;
+  s.isum_hi = p->isum_hi;
   return s;
 }
 
@@ -1210,6 +1225,111 @@ __device__ void bool_range(const uint32_t* values, const uint32_t* validity, con
   if (c > t) flags[1] = 1;
 }
 
+// DecimalType column (ColTask::arg = precision | scale << 8; 16-byte two's-complement unscaled values):
+// lane-per-row 512-row blocks with the selection as scalar lane masks, as numeric_range.  STATS: every selected value
+// cast to double as Spark's Decimal.toDouble (correctly rounded, dq_decimal.h) into the shifted moments and min / max
+// (the cast is monotone: min of the casts = the cast of Spark's decimal min), the exact 128-bit sum into (isum,
+// isum_hi) and the fp64 sum of the casts into `sum` (dq_finish's overflow guard); HLL: Spark 2.2's decimal hash
+// (hashLong of the unscaled long, or of BigInteger.toByteArray's bytes above precision 18); DT: the count of values
+// whose BigDecimal.toString is plain decimal (isum) -- dq_finish makes them FRACTIONAL (scale > 0; the rest STRING)
+// or all INTEGRAL (scale 0).  Rows past row1 are not read (exec-masked loads); values are 16-byte aligned.
+template <bool STATS, bool HLL, bool DT>
+__device__ void decimal_range(const void* values, const uint32_t* validity, const uint32_t* mask, int64_t row0,
+                              int64_t row1, ColStats& s, int32_t* regs, int32_t arg) {
+  const int prec = arg & 0xFF, sc = (arg >> 8) & 0xFF;
+  const DecTab tab = dec_dev_tab();
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t* v = reinterpret_cast<const uint64_t*>(values);
+  auto load = [&](int64_t r, uint64_t& lo, uint64_t& hi) {
+    lo = hi = 0;
+    if (r < row1) {
+      lo = __builtin_nontemporal_load(v + 2 * r);
+      hi = __builtin_nontemporal_load(v + 2 * r + 1);
+    }
+  };
+  // the range's shift: mean of the casts of its first 64-row group with a selected value
+  double shift = 0.0;
+  if (STATS) {
+    for (int64_t r = row0; r < row1; r += 64) {
+      uint64_t sel = ~0ull;
+      const int64_t w = r >> 5;
+      const bool two = r + 32 < row1;
+      if (validity) sel = ((uint64_t)(two ? ((const_u32s)validity)[w + 1] : 0u) << 32) | ((const_u32s)validity)[w];
+      if (mask) sel &= ((uint64_t)(two ? ((const_u32s)mask)[w + 1] : 0u) << 32) | ((const_u32s)mask)[w];
+      if (r + 64 > row1) sel &= (1ull << (row1 - r)) - 1ull;
+      if (sel == 0) continue;
+      uint64_t lo, hi;
+      load(r + lane, lo, hi);
+      const double x = lane_bit(sel) ? dec_to_double(lo, hi, sc, tab) : 0.0;
+      shift = wave_uniform(wave_sum_f64(x) / (double)__builtin_popcountll(sel));
+      break;
+    }
+  }
+  LaneMoments a{0.0, 0.0, 0};
+  uint64_t slo = 0, shi = 0;  // the lane's exact sum (128-bit, wrapping)
+  double guard = 0.0;
+  int64_t cnt_w = 0, frac = 0;
+  const int32_t nr = (int32_t)(row1 - row0);
+  for (int32_t rb = 0; rb < nr; rb += kRowsPerIter) {
+    const int64_t base = row0 + rb + wave * 512;
+    const int32_t rem = nr - rb - wave * 512;
+    uint64_t m[8];
+    block_masks(validity, mask, base, rem, rb + kRowsPerIter <= nr, m);
+    uint64_t lo[8], hi[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) load(base + 64 * j + lane, lo[j], hi[j]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      cnt_w += __builtin_popcountll(m[j]);
+      const bool sel = lane_bit(m[j]);
+      if constexpr (STATS) {
+        const double x = dec_to_double(lo[j], hi[j], sc, tab);
+        masked_moments<false, false>(a, s.fmin, s.fmax, x, 0, shift, m[j], m[j]);
+        if (sel) {
+          const uint64_t l2 = slo + lo[j];
+          shi += hi[j] + (l2 < slo ? 1u : 0u);
+          slo = l2;
+          guard += x;
+        }
+      }
+      if constexpr (HLL) {
+        const uint64_t b = dec_hash_head(lo[j], hi[j], prec);
+        const HllKey key = hll_key_from_fmix(b);
+        if (sel) {
+          if (key.q >= 0) atomicMax(reinterpret_cast<int32_t*>(reinterpret_cast<char*>(regs) + key.addr), key.q);
+          else hll_update(regs, fmix_tail(b));
+        }
+      }
+      if constexpr (DT) frac += __builtin_popcountll(__builtin_amdgcn_ballot_w64(dec_dt_class(lo[j], hi[j], sc, tab) == 1) & m[j]);
+    }
+  }
+  if constexpr (STATS) {
+    const double S1 = wave_sum_f64(a.sd), S2 = wave_sum_f64(a.sdd), G = wave_sum_f64(guard);
+#pragma unroll
+    for (int k = 32; k >= 1; k >>= 1) {
+      const uint64_t olo = __shfl_xor(slo, k), ohi = __shfl_xor(shi, k);
+      const uint64_t l2 = slo + olo;
+      shi = shi + ohi + (l2 < slo ? 1u : 0u);
+      slo = l2;
+    }
+    if (lane == 0 && cnt_w > 0) {
+      const double n = (double)cnt_w, q = S1 / n;
+      s.n = n;
+      s.mean = shift + q;
+      const double m2 = __builtin_fma(-S1, q, S2);
+      s.m2 = m2 < 0.0 ? 0.0 : m2;
+      s.sum = G;
+      s.isum = (int64_t)slo;
+      s.isum_hi = (int64_t)shi;
+    }
+  }
+  if (lane == 0) {
+    s.count += cnt_w;
+    if (DT) s.isum += frac;
+  }
+}
+
 // Only the count of selected rows (Completeness): popcount of validity (& where) words.
 __device__ void validity_range(const uint32_t* validity, const uint32_t* mask, int64_t row0, int64_t row1, ColStats& s) {
   // row0 is a multiple of 2048 -> word aligned; each thread handles whole 32-row words
@@ -1265,6 +1385,10 @@ __device__ __forceinline__ void run_variant(const ColTask& t, const ScanCols& co
   else if constexpr (V == CV_F64_D) float_dtype_range(reinterpret_cast<const double*>(v), val, mask, row0, row1, s);
   else if constexpr (V == CV_F32_D) float_dtype_range(reinterpret_cast<const float*>(v), val, mask, row0, row1, s);
   else if constexpr (V == CV_BOOL) bool_range(reinterpret_cast<const uint32_t*>(v), val, mask, row0, row1, s, regs);
+  else if constexpr (V == CV_D128_S) decimal_range<true, false, false>(v, val, mask, row0, row1, s, regs, t.arg);
+  else if constexpr (V == CV_D128_SH) decimal_range<true, true, false>(v, val, mask, row0, row1, s, regs, t.arg);
+  else if constexpr (V == CV_D128_H) decimal_range<false, true, false>(v, val, mask, row0, row1, s, regs, t.arg);
+  else if constexpr (V == CV_D128_D) decimal_range<false, false, true>(v, val, mask, row0, row1, s, regs, t.arg);
   else if constexpr (V == CV_UTF8_H || V == CV_UTF8_D || V == CV_UTF8_HD)
     utf8_range<int32_t, V != CV_UTF8_D, V != CV_UTF8_H, LONG>(
         reinterpret_cast<const uint8_t*>(v), reinterpret_cast<const int32_t*>(cols.offsets[t.col]), val, mask, row0,
@@ -1301,7 +1425,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kMinWave
                                                          uint32_t* __restrict__ hll_acc) {
   constexpr bool kHll = !(V == CV_VALIDITY || V == CV_F64_S || V == CV_I64_S || V == CV_I32_S || V == CV_F64_D ||
                          V == CV_UTF8_D || V == CV_LUTF8_D || V == CV_F32_S || V == CV_I16_S || V == CV_I8_S ||
-                         V == CV_F32_D || V == CV_BOOL);
+                         V == CV_F32_D || V == CV_BOOL || V == CV_D128_S || V == CV_D128_D);
   constexpr bool kBool = V == CV_BOOL;  // (its two HLL hashes are constants: flags instead of registers)
   constexpr bool kStr = V == CV_UTF8_H || V == CV_LUTF8_H || V == CV_UTF8_HD || V == CV_LUTF8_HD;
   __shared__ int32_t regs[kHll ? 512 : 2];  // q = pw - 1, -1 = empty (see hll_q_exact); CV_BOOL: any TRUE / FALSE
@@ -1470,6 +1594,16 @@ __device__ __forceinline__ void pred_load(const void* p, int kind, int64_t row0,
 #pragma unroll
     for (int j = 0; j < 8; ++j)
       v[j] = (uint64_t)(int64_t)(int8_t)__builtin_amdgcn_raw_buffer_load_b8(r, (int)(base - row0 + 64 * j + lane), 0, 2);
+  } else if (kind >= CK_D128_LO) {
+    // a decimal's 64-bit half (16-byte rows): the low word (CK_D128_LOU: sign bit flipped, so that a signed
+    // compare orders it unsigned) or the high word
+    const int off = kind == CK_D128_HI ? 8 : 0;
+    const uint64_t flip = kind == CK_D128_LOU ? (1ull << 63) : 0ull;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const auto w2 = __builtin_amdgcn_raw_buffer_load_b64(r, lane * 16 + off, (int)((base - row0 + 64 * j) * 16), 2);
+      v[j] = (((uint64_t)w2[1] << 32) | w2[0]) ^ flip;
+    }
   } else {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -1498,6 +1632,7 @@ struct AtomBuf {
   // what the buffer holds (wave-uniform): block base, columns of a / b (-1: none), values loaded (CMP)
   int64_t t_base = -1;
   int32_t t_col_a = -1, t_col_b = -1;
+  int32_t t_kind_a = 0, t_kind_b = 0;  // the loaded views (a decimal column is read as different halves)
   bool t_vals = false;
 };
 
@@ -1852,13 +1987,13 @@ __global__ __launch_bounds__(kBlock) void dq_pred_scan(const PredProgram* __rest
     const int kind_a = (int)((lw >> 20) & 15u), kind_b = (int)((lw >> 24) & 15u);
     const bool same_blk = C.t_base == base;
     auto fetch = [&](int col, int kind, bool vals, uint64_t (&dst)[8], uint32_t& vdst) __attribute__((always_inline)) {
-      if (same_blk && col == C.t_col_a && (C.t_vals || !vals)) {
+      if (same_blk && col == C.t_col_a && (!vals || (C.t_vals && kind == C.t_kind_a))) {
         if (vals) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) dst[j] = C.a[j];
         }
         vdst = C.va;
-      } else if (same_blk && col == C.t_col_b && C.t_vals) {
+      } else if (same_blk && col == C.t_col_b && C.t_vals && (!vals || kind == C.t_kind_b)) {
         if (vals) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) dst[j] = C.b[j];
@@ -1875,6 +2010,8 @@ __global__ __launch_bounds__(kBlock) void dq_pred_scan(const PredProgram* __rest
     L.t_base = base;
     L.t_col_a = col_a;
     L.t_col_b = cmp ? col_b : -1;
+    L.t_kind_a = kind_a;
+    L.t_kind_b = kind_b;
     L.t_vals = cmp;
   };
   if (n_loads > 0) issue(0, row0 + (int64_t)wave * 512, B0, B1);
@@ -2071,6 +2208,7 @@ hipError_t launch_column_scan(int32_t variant, const ColTask* tasks, int32_t nta
     DQ_V(CV_UTF8_D) DQ_V(CV_UTF8_HD) DQ_V(CV_LUTF8_D) DQ_V(CV_LUTF8_HD) DQ_V(CV_F64_D)
     DQ_V(CV_F32_S) DQ_V(CV_F32_SH) DQ_V(CV_F32_H) DQ_V(CV_I16_S) DQ_V(CV_I16_SH) DQ_V(CV_I16_H)
     DQ_V(CV_I8_S) DQ_V(CV_I8_SH) DQ_V(CV_I8_H) DQ_V(CV_F32_D) DQ_V(CV_BOOL)
+    DQ_V(CV_D128_S) DQ_V(CV_D128_SH) DQ_V(CV_D128_H) DQ_V(CV_D128_D)
     default: return hipErrorInvalidValue;
   }
 #undef DQ_V

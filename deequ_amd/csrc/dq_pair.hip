@@ -776,7 +776,7 @@ __device__ __forceinline__ bool pair_range(const PairWaveTask& T, const ScanCols
       r.fmax = fmax;
       r.pinf_count = pinf;
       r.ninf_count = ninf;
-      r.pad = 0;
+      r.isum_hi = 0;
       col_part[(size_t)T.mom_out[k] * kMaxWG + range] = r;
     }
   }

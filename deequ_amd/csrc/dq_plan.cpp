@@ -104,10 +104,10 @@ static dq_status cap_error(const char* fmt, ...) {
                        #expr, hipGetErrorString(e_), __FILE__, __LINE__);                          \
   } while (0)
 
-// Preconditions.isNumeric (Analyzer.scala:322-334): ByteType .. DoubleType (DecimalType: not a GPU column type)
+// Preconditions.isNumeric (Analyzer.scala:322-334): ByteType .. DoubleType and DecimalType
 static bool is_numeric(int32_t t) {
   return t == DQ_TYPE_F64 || t == DQ_TYPE_I64 || t == DQ_TYPE_I32 || t == DQ_TYPE_F32 || t == DQ_TYPE_I16 ||
-         t == DQ_TYPE_I8;
+         t == DQ_TYPE_I8 || is_decimal(t);
 }
 static bool is_integral(int32_t t) { return t == DQ_TYPE_I64 || t == DQ_TYPE_I32 || t == DQ_TYPE_I16 || t == DQ_TYPE_I8; }
 static bool is_floating(int32_t t) { return t == DQ_TYPE_F64 || t == DQ_TYPE_F32; }
@@ -122,7 +122,8 @@ static int32_t kind_of(int32_t t) {
     case DQ_TYPE_I8: return CK_I8;
     case DQ_TYPE_BOOL: return CK_BOOL;
     case DQ_TYPE_UTF8: return CK_UTF8;
-    default: return CK_LUTF8;
+    case DQ_TYPE_LARGE_UTF8: return CK_LUTF8;
+    default: return CK_D128;  // (type_valid: a DECIMAL128 code)
   }
 }
 // algorithmic bytes per row (x1000) of a column's value (or UTF8 offset) buffer
@@ -132,7 +133,7 @@ static int64_t value_bytes_x1000(int32_t t) {
     case DQ_TYPE_I16: return 2000;
     case DQ_TYPE_I8: return 1000;
     case DQ_TYPE_BOOL: return 125;
-    default: return 8000;
+    default: return is_decimal(t) ? 16000 : 8000;
   }
 }
 // (double)(float)v as Java's long -> float conversion rounds it (to nearest, ties to even)
@@ -300,9 +301,101 @@ struct Lowering {
     return set_error(DQ_E_UNSUPPORTED, "unsupported comparison operand (node kind %d)", n.kind);
   }
 
+  // DecimalType(p, s) column CMP an integer / decimal literal.  Spark 2.2 (DecimalPrecision) casts an integer
+  // literal to DecimalType(10, 0) (an int) or (20, 0) (a long) and both sides to the wider decimal type
+  // (max of the integer digits + max of the scales); while that fits 38 digits every cast is exact, so the
+  // comparison is the exact rational one, rewritten here into a bound B on the unscaled value u: u CMP B.  Wider
+  // types (Spark bounds them to 38 digits and can turn values NULL), double literals (the decimal is cast to
+  // double) and boolean literals stay on the fallback.  Precision <= 18: one atom on the low word (the whole value,
+  // |u| < 10^18); wider: the 128-bit comparison as atoms on the high word H and the low word L (compared unsigned),
+  // e.g. u < B  <=>  H < Bh OR (H = Bh AND L <u Bl).
+  dq_status emit_dec_lit(const Operand& o, int cmp, const Lit& lit, int32_t type) {
+    const int prec = DQ_DECIMAL_PRECISION(type), sc = DQ_DECIMAL_SCALE(type);
+    auto fits = [&](const Lit& l) {  // the wider decimal type of the column and the literal fits 38 digits
+      if (l.k == Lit::NUL) return true;
+      if (l.k != Lit::INT && l.k != Lit::DEC) return false;
+      const int ls = l.k == Lit::DEC ? l.scale : 0;
+      int lp;
+      if (l.k == Lit::INT) lp = (l.i >= INT32_MIN && l.i <= INT32_MAX) ? 10 : 20;
+      else {
+        const uint64_t a = l.i < 0 ? (uint64_t)0 - (uint64_t)l.i : (uint64_t)l.i;
+        lp = std::max((int)std::to_string(a).size(), ls);
+      }
+      return std::max(prec - sc, lp - ls) + std::max(sc, ls) <= kDecMaxPrecision;
+    };
+    if (!fits(lit) || (o.has_fallback && !fits(o.fallback)))
+      return set_error(DQ_E_UNSUPPORTED, "decimal column %d compared with a %s literal", o.col,
+                       lit.k == Lit::DBL || o.fallback.k == Lit::DBL ? "double" : "wider or boolean");
+    const int nr = o.has_fallback ? lit_cmp_result(cmp, o.fallback, lit) : NR_NULL;
+    if (lit.k == Lit::NUL) { push_const(NR_NULL); return DQ_OK; }
+    // u / 10^sc CMP L / 10^t  ->  u CMP' B
+    const int t = lit.k == Lit::DEC ? lit.scale : 0;
+    int c2;
+    i128 B;
+    if (t <= sc) {
+      i128 m = 1;
+      for (int k = 0; k < sc - t; ++k) m *= 10;
+      B = (i128)lit.i * m;  // (fits: the wider type has at most 38 digits)
+      c2 = to_cmpop(cmp);
+    } else {
+      int64_t p10;
+      pow10_i64(t - sc, p10);
+      const int64_t u = lit.i;
+      const int64_t fl = u >= 0 ? u / p10 : -((-u + p10 - 1) / p10);
+      const bool exact = (u % p10) == 0;
+      const int64_t ce = exact ? fl : fl + 1;
+      switch (cmp) {
+        case DQ_CMP_LT: c2 = C_LT; B = ce; break;
+        case DQ_CMP_LE: c2 = C_LE; B = fl; break;
+        case DQ_CMP_GT: c2 = C_GT; B = fl; break;
+        case DQ_CMP_GE: c2 = C_GE; B = ce; break;
+        case DQ_CMP_EQ: c2 = exact ? C_EQ : C_FALSE; B = fl; break;
+        default: c2 = exact ? C_NE : C_TRUE; B = fl; break;
+      }
+    }
+    auto atom = [&](int kind, int c, int64_t v) {
+      PredInstr p{};
+      p.op = PO_ATOM_CMP; p.col_a = o.col; p.col_b = -1; p.kind_a = kind; p.kind_b = 0;
+      p.ctype = CT_INT; p.cmp = c; p.lit_i = v; p.null_res = nr;
+      out.push_back(p);
+    };
+    auto logic = [&](int op) {
+      PredInstr p{};
+      p.op = op; p.col_a = p.col_b = -1;
+      out.push_back(p);
+    };
+    if (c2 == C_TRUE || c2 == C_FALSE) { atom(CK_D128_LO, c2, 0); return DQ_OK; }
+    if (prec <= 18) {
+      if (B > (i128)INT64_MAX || B < (i128)INT64_MIN) {  // every |u| < 10^18 lies on one side of B
+        const bool below = B > 0;  // u < B for every u
+        const bool holds = c2 == C_LT || c2 == C_LE || c2 == C_NE ? below : (c2 == C_EQ ? false : !below);
+        atom(CK_D128_LO, holds ? C_TRUE : C_FALSE, 0);
+      } else {
+        atom(CK_D128_LO, c2, (int64_t)B);
+      }
+      return DQ_OK;
+    }
+    const int64_t bh = (int64_t)(B >> 64);
+    const int64_t bl = (int64_t)((uint64_t)B ^ (1ull << 63));  // (CK_D128_LOU flips the loaded low word the same way)
+    if (c2 == C_EQ || c2 == C_NE) {
+      atom(CK_D128_HI, c2, bh);
+      atom(CK_D128_LOU, c2, bl);
+      logic(c2 == C_EQ ? PO_AND : PO_OR);
+      return DQ_OK;
+    }
+    const bool lt = c2 == C_LT || c2 == C_LE;
+    atom(CK_D128_HI, lt ? C_LT : C_GT, bh);
+    atom(CK_D128_HI, C_EQ, bh);
+    atom(CK_D128_LOU, c2, bl);
+    logic(PO_AND);
+    logic(PO_OR);
+    return DQ_OK;
+  }
+
   // column CMP literal, with Spark 2.2 coercions (integral vs decimal exact, anything vs double in double)
   dq_status emit_col_lit(const Operand& o, int cmp, Lit lit) {
     const dq_column_desc& cd = (*schema)[o.col];
+    if (is_decimal(cd.type)) return emit_dec_lit(o, cmp, lit, cd.type);
     const bool boolean = cd.type == DQ_TYPE_BOOL;
     if (!is_numeric(cd.type) && !boolean)
       return set_error(DQ_E_UNSUPPORTED, "comparison on a non-numeric column (%d)", o.col);
@@ -476,6 +569,8 @@ struct Lowering {
         const bool bools = ta == DQ_TYPE_BOOL && tb == DQ_TYPE_BOOL;
         if (!bools && (!is_numeric(ta) || !is_numeric(tb)))
           return set_error(DQ_E_UNSUPPORTED, "comparison of non-numeric columns");
+        if (is_decimal(ta) || is_decimal(tb))
+          return set_error(DQ_E_UNSUPPORTED, "comparison of a decimal column with a column");
         // FloatType vs Int / LongType compares in FloatType (the integer rounded to float), which a double
         // compare does not restate for integers beyond 2^24: the fallback (ShortType / ByteType are exact)
         auto wide_int = [](int32_t t) { return t == DQ_TYPE_I32 || t == DQ_TYPE_I64; };
@@ -818,8 +913,8 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
     return DQ_OK;
   };
   auto col_task = [&](int32_t col, int32_t bm, bool stats, bool hll, int32_t& t, bool dtype = false) -> dq_status {
-    // a double / float column's DataType count is a variant of its own (CV_F64_D / CV_F32_D)
-    auto key = std::make_tuple(col, bm, dtype && is_floating(p->schema[col].type) ? 1 : 0);
+    // a double / float / decimal column's DataType count is a variant of its own (CV_F64_D / CV_F32_D / CV_D128_D)
+    auto key = std::make_tuple(col, bm, dtype && (is_floating(p->schema[col].type) || is_decimal(p->schema[col].type)) ? 1 : 0);
     auto it = col_task_of.find(key);
     if (it == col_task_of.end()) {
       if ((int32_t)p->col_tasks.size() >= kMaxColTasks) return cap_error("more than %d column tasks", kMaxColTasks);
@@ -907,10 +1002,10 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
         o.col_type = p->schema[s.col_a].type;
         int32_t bm;
         if (dq_status st = bitmap(where_slot, bm)) return st;
-        // only floating-point and string values need classifying: an integral value's string always matches
+        // only floating-point, decimal and string values need classifying: an integral value's string always matches
         // INTEGRAL, a boolean's ("true" / "false") BOOLEAN, a date's / timestamp's ("2020-01-31 ...") STRING -- the
         // selected-row count suffices (dq_finish puts it in the type's class)
-        const bool classify = is_floating(o.col_type) || is_string(o.col_type);
+        const bool classify = is_floating(o.col_type) || is_string(o.col_type) || is_decimal(o.col_type);
         if (dq_status st = col_task(s.col_a, bm, false, false, o.col_task, classify)) return st;
         break;
       }
@@ -919,6 +1014,8 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
         if (dq_status st = need_col(s.col_b)) return st;
         if (!is_numeric(p->schema[s.col_a].type) || !is_numeric(p->schema[s.col_b].type))
           return set_error(DQ_E_TYPE, "spec %zu: Correlation needs numeric columns", i);
+        if (is_decimal(p->schema[s.col_a].type) || is_decimal(p->schema[s.col_b].type))
+          return set_error(DQ_E_UNSUPPORTED, "spec %zu: Correlation of a DecimalType column runs on the fallback", i);
         int32_t bm;
         if (dq_status st = bitmap(where_slot, bm)) return st;
         auto key = std::make_tuple(s.col_a, s.col_b, bm);
@@ -947,9 +1044,12 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
     const bool stats = col_task_needs[t].stats, hll = col_task_needs[t].hll, dtype = col_task_needs[t].dtype;
     int32_t type = p->schema[ct.col].type;
     if (hll) ct.hll_slot = p->n_hll++;
+    if (is_decimal(type)) ct.arg = DQ_DECIMAL_PRECISION(type) | DQ_DECIMAL_SCALE(type) << 8;
     if (dtype && type == DQ_TYPE_F64) ct.variant = CV_F64_D;
     else if (dtype && type == DQ_TYPE_F32) ct.variant = CV_F32_D;
+    else if (dtype && is_decimal(type)) ct.variant = CV_D128_D;
     else if (!stats && !hll && !dtype) ct.variant = CV_VALIDITY;
+    else if (is_decimal(type)) ct.variant = stats && hll ? CV_D128_SH : (stats ? CV_D128_S : CV_D128_H);
     else if (type == DQ_TYPE_UTF8) ct.variant = hll && dtype ? CV_UTF8_HD : (dtype ? CV_UTF8_D : CV_UTF8_H);
     else if (type == DQ_TYPE_LARGE_UTF8) ct.variant = hll && dtype ? CV_LUTF8_HD : (dtype ? CV_LUTF8_D : CV_LUTF8_H);
     else if (type == DQ_TYPE_BOOL) ct.variant = CV_BOOL;  // (HLL only: a boolean is not numeric)
@@ -1529,7 +1629,7 @@ dq_status dq_plan_create_opts(const dq_analyzer_spec* specs, int32_t n_specs, co
     return set_error(DQ_E_INVALID, "dq_plan_create: bad schema (at most %d columns)", kMaxSchemaCols);
   if (n_pred < 0 || (n_pred > 0 && !pred_pool)) return set_error(DQ_E_INVALID, "dq_plan_create: bad predicate pool");
   for (int32_t c = 0; c < n_cols; ++c)
-    if (schema[c].type < DQ_TYPE_F64 || schema[c].type > DQ_TYPE_MAX)
+    if (!type_valid(schema[c].type))
       return set_error(DQ_E_TYPE, "dq_plan_create: column %d has unknown type %d", c, schema[c].type);
   int ndev = 0;
   HIP_TRY(hipGetDeviceCount(&ndev));
@@ -1991,15 +2091,37 @@ dq_status dq_finish(dq_plan* p, dq_state* out) {
         else { s.u.ratio.count = rows; s.has_value[1] = 1; }
         break;
       case DQ_OP_SUM:  // Spark's Sum: LongType for integral children, DoubleType (each value cast) otherwise
-        s.u.sum.sum = is_floating(o.col_type) ? f64_sum(*c) : (double)c->isum;
-        s.integral = !is_floating(o.col_type);
-        s.u.sum.partial = s.integral ? c->isum : 0;
+        if (is_decimal(o.col_type)) {  // DecimalType: the exact decimal sum, cast at the end (state.integral 2)
+          s.integral = 2;
+          s.u.sum.dec_scale = DQ_DECIMAL_SCALE(o.col_type);
+          s.u.sum.dec_digits = std::min(38, DQ_DECIMAL_PRECISION(o.col_type) + 10);  // Sum's result precision
+          s.u.sum.partial = c->isum;
+          s.u.sum.partial_hi = c->isum_hi;
+          s.u.sum.guard = c->sum;
+          if (!dec_sum_value(c->isum, c->isum_hi, c->sum, s.u.sum.dec_scale, s.u.sum.dec_digits, s.u.sum.sum))
+            s.u.sum.sum = nan;
+        } else {
+          s.u.sum.sum = is_floating(o.col_type) ? f64_sum(*c) : (double)c->isum;
+          s.integral = !is_floating(o.col_type);
+          s.u.sum.partial = s.integral ? c->isum : 0;
+        }
         set1(c->count > 0);
         break;
       case DQ_OP_MEAN:
-        s.u.mean.sum = is_floating(o.col_type) ? f64_sum(*c) : (double)c->isum;
-        s.integral = !is_floating(o.col_type);
-        s.u.mean.partial = s.integral ? c->isum : 0;
+        if (is_decimal(o.col_type)) {
+          s.integral = 2;
+          s.u.mean.dec_scale = DQ_DECIMAL_SCALE(o.col_type);
+          s.u.mean.dec_digits = std::min(38, DQ_DECIMAL_PRECISION(o.col_type) + 10);  // Sum's result precision
+          s.u.mean.partial = c->isum;
+          s.u.mean.partial_hi = c->isum_hi;
+          s.u.mean.guard = c->sum;
+          if (!dec_sum_value(c->isum, c->isum_hi, c->sum, s.u.mean.dec_scale, s.u.mean.dec_digits, s.u.mean.sum))
+            s.u.mean.sum = nan;
+        } else {
+          s.u.mean.sum = is_floating(o.col_type) ? f64_sum(*c) : (double)c->isum;
+          s.integral = !is_floating(o.col_type);
+          s.u.mean.partial = s.integral ? c->isum : 0;
+        }
         s.u.mean.count = c->count;
         s.has_value[0] = c->count > 0;
         s.has_value[1] = 1;  // count(...) is never NULL
@@ -2042,6 +2164,9 @@ dq_status dq_finish(dq_plan* p, dq_state* out) {
           d.num_boolean = (int64_t)c->sum;
         } else if (is_floating(o.col_type)) {
           d.num_fractional = c->isum;
+        } else if (is_decimal(o.col_type)) {  // BigDecimal.toString: plain (isum) or scientific; scale 0: integers
+          if (DQ_DECIMAL_SCALE(o.col_type) == 0) d.num_integral = c->count;
+          else d.num_fractional = c->isum;
         } else if (is_integral(o.col_type)) {
           d.num_integral = c->count;
         } else if (o.col_type == DQ_TYPE_BOOL) {
@@ -2173,7 +2298,7 @@ int64_t dq_plan_explain(const dq_analyzer_spec* specs, int32_t n_specs, const dq
   for (int32_t k = 0; k < n_patterns; ++k)
     if (!patterns[k]) return set_error(DQ_E_INVALID, "dq_plan_explain: pattern %d is NULL", k);
   for (int32_t c = 0; c < n_cols; ++c)
-    if (schema[c].type < DQ_TYPE_F64 || schema[c].type > DQ_TYPE_MAX)
+    if (!type_valid(schema[c].type))
       return set_error(DQ_E_TYPE, "dq_plan_explain: column %d has unknown type %d", c, schema[c].type);
   if (cap < 0 || (cap > 0 && !out)) return set_error(DQ_E_INVALID, "dq_plan_explain: bad output buffer");
   std::unique_ptr<dq_plan> holder(new dq_plan());

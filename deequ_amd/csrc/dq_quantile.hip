@@ -645,9 +645,20 @@ __global__ void dq_digest_gather(const unsigned long long* __restrict__ sorted, 
 // statistic of the widened values is the widened order statistic -- then the F64 / I32 select and digest run
 // unchanged.  One extra streaming pass (read 1-4 B, write 4-8 B per row) ahead of passes that read the column
 // several times.
+// DecimalType columns the same way: each value cast to double as Spark's Decimal.toDouble (correctly rounded,
+// dq_decimal.h -- StatefulApproxQuantile's input is Cast(child, DoubleType)), so the F64 passes see what Spark's
+// digest sees.
+#define DQ_DEC_TABLE static __constant__ const
+#include "dq_dec_tables.inc"
+#undef DQ_DEC_TABLE
 __global__ void widen_column(const void* __restrict__ src, int32_t type, void* __restrict__ dst, int64_t n) {
+  const DecTab tab{kDecP10Lo, kDecP10Hi, kDecRcpHi, kDecRcpLo};
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
-    if (type == DQ_TYPE_F32) reinterpret_cast<double*>(dst)[r] = (double)__builtin_nontemporal_load(reinterpret_cast<const float*>(src) + r);
+    if (DQ_TYPE_BASE(type) == DQ_TYPE_DECIMAL128) {
+      const uint64_t* v = reinterpret_cast<const uint64_t*>(src) + 2 * r;
+      reinterpret_cast<double*>(dst)[r] =
+          dec_to_double(__builtin_nontemporal_load(v), __builtin_nontemporal_load(v + 1), DQ_DECIMAL_SCALE(type), tab);
+    } else if (type == DQ_TYPE_F32) reinterpret_cast<double*>(dst)[r] = (double)__builtin_nontemporal_load(reinterpret_cast<const float*>(src) + r);
     else if (type == DQ_TYPE_I16) reinterpret_cast<int32_t*>(dst)[r] = __builtin_nontemporal_load(reinterpret_cast<const int16_t*>(src) + r);
     else reinterpret_cast<int32_t*>(dst)[r] = __builtin_nontemporal_load(reinterpret_cast<const int8_t*>(src) + r);
   }
@@ -664,14 +675,17 @@ struct Widened {
   }
 };
 
-bool is_narrow(int32_t type) { return type == DQ_TYPE_F32 || type == DQ_TYPE_I16 || type == DQ_TYPE_I8; }
+bool is_narrow(int32_t type) {
+  return type == DQ_TYPE_F32 || type == DQ_TYPE_I16 || type == DQ_TYPE_I8 || (type_valid(type) && is_decimal(type));
+}
 
 dq_status widen(int32_t type, const dq_column_view* cols, const int64_t* chunk_rows, int32_t n_chunks, int32_t device,
                 hipStream_t stream, Widened& w) {
   QHIP(hipSetDevice(device));
-  w.type = type == DQ_TYPE_F32 ? DQ_TYPE_F64 : DQ_TYPE_I32;
+  const bool to_f64 = type == DQ_TYPE_F32 || is_decimal(type);
+  w.type = to_f64 ? DQ_TYPE_F64 : DQ_TYPE_I32;
   w.stream = stream;
-  const int64_t bytes = type == DQ_TYPE_F32 ? 8 : 4;
+  const int64_t bytes = to_f64 ? 8 : 4;
   w.views.assign(cols, cols + n_chunks);
   for (int c = 0; c < n_chunks; ++c) {
     const int64_t n = chunk_rows[c];

@@ -16,6 +16,9 @@
 #include "dq_internal.h"
 
 #include "hll_p9_tables.inc"
+#define DQ_DEC_TABLE static const
+#include "dq_dec_tables.inc"
+#undef DQ_DEC_TABLE
 
 namespace dq {
 
@@ -152,8 +155,43 @@ double hll_count(const int64_t* words52) {
 
 static inline int64_t wrap_add(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); }
 
+const DecTab& dec_host_tab() {
+  static const DecTab t{kDecP10Lo, kDecP10Hi, kDecRcpHi, kDecRcpLo};
+  return t;
+}
+
+bool dec_sum_value(int64_t lo, int64_t hi, double guard, int s, int digits, double& out) {
+  const DecTab& t = dec_host_tab();
+  if (s < 0 || s > kDecMaxPrecision || digits < 1 || digits > kDecMaxPrecision) return false;
+  // the wrapped 128-bit image is the sum while |sum| < 2^127 (~1.7e38 unscaled): the fp64 guard rules out the rest
+  if (!(std::fabs(guard) * std::pow(10.0, s) < 1.6e38)) return false;
+  if (dec_mag((uint64_t)lo, (uint64_t)hi) >= dec_p10(t, digits)) return false;
+  out = dec_to_double((uint64_t)lo, (uint64_t)hi, s, t);
+  return true;
+}
+
+// a Sum / Mean state of a DECIMAL128 column holding Spark's NULL (an overflowing decimal sum)
+static bool dec_overflow(const dq_state& s) {
+  if (s.integral != 2) return false;
+  double v;
+  if (s.op == DQ_OP_SUM) return !dec_sum_value(s.u.sum.partial, s.u.sum.partial_hi, s.u.sum.guard, s.u.sum.dec_scale,
+                                               s.u.sum.dec_digits, v);
+  if (s.op == DQ_OP_MEAN)
+    return !dec_sum_value(s.u.mean.partial, s.u.mean.partial_hi, s.u.mean.guard, s.u.mean.dec_scale,
+                          s.u.mean.dec_digits, v);
+  return false;
+}
+
+// 128-bit wrapping add of decimal partials
+static void dec_add(int64_t alo, int64_t ahi, int64_t blo, int64_t bhi, int64_t& lo, int64_t& hi) {
+  const uint64_t l = (uint64_t)alo + (uint64_t)blo;
+  hi = (int64_t)((uint64_t)ahi + (uint64_t)bhi + (l < (uint64_t)alo ? 1u : 0u));
+  lo = (int64_t)l;
+}
+
 int32_t state_is_defined(const dq_state& s) {
   if (!s.has_value[0] || !s.has_value[1]) return 0;
+  if (dec_overflow(s)) return 0;  // sum(decimal) overflowed: Spark's NULL
   if (s.op == DQ_OP_STDDEV) return s.u.stddev.n > 0.0;   // StandardDeviation.scala:40-51
   if (s.op == DQ_OP_CORRELATION) return s.u.corr.n > 0.0; // Correlation.scala:66-82
   return 1;
@@ -260,7 +298,15 @@ dq_status state_combine(const dq_state& a, const dq_state& b, dq_state& o) {
     // hold doubles, Sum.scala:27-29, Mean.scala:27-31) combines by double addition.
     case DQ_OP_SUM:
       pick(0, [] {}, [&] { o.u.sum = b.u.sum; o.integral = b.integral; }, [&] {
-        if (a.integral && b.integral) {
+        if (a.integral == 2 && b.integral == 2 && a.u.sum.dec_scale == b.u.sum.dec_scale &&
+            a.u.sum.dec_digits == b.u.sum.dec_digits) {  // decimal partials: exact sum, cast at the end
+          dec_add(a.u.sum.partial, a.u.sum.partial_hi, b.u.sum.partial, b.u.sum.partial_hi, o.u.sum.partial,
+                  o.u.sum.partial_hi);
+          o.u.sum.guard = a.u.sum.guard + b.u.sum.guard;
+          if (!dec_sum_value(o.u.sum.partial, o.u.sum.partial_hi, o.u.sum.guard, o.u.sum.dec_scale,
+                             o.u.sum.dec_digits, o.u.sum.sum))
+            o.u.sum.sum = std::numeric_limits<double>::quiet_NaN();
+        } else if (a.integral == 1 && b.integral == 1) {
           o.u.sum.partial = wrap_add(a.u.sum.partial, b.u.sum.partial);
           o.u.sum.sum = (double)o.u.sum.partial;
         } else {
@@ -271,9 +317,22 @@ dq_status state_combine(const dq_state& a, const dq_state& b, dq_state& o) {
       });
       break;
     case DQ_OP_MEAN:
-      pick(0, [] {}, [&] { o.u.mean.sum = b.u.mean.sum; o.u.mean.partial = b.u.mean.partial; o.integral = b.integral; },
+      pick(0, [] {}, [&] {
+             const int64_t cnt = o.u.mean.count;  // (slot 1, picked below)
+             o.u.mean = b.u.mean;
+             o.u.mean.count = cnt;
+             o.integral = b.integral;
+           },
            [&] {
-             if (a.integral && b.integral) {
+             if (a.integral == 2 && b.integral == 2 && a.u.mean.dec_scale == b.u.mean.dec_scale &&
+                 a.u.mean.dec_digits == b.u.mean.dec_digits) {
+               dec_add(a.u.mean.partial, a.u.mean.partial_hi, b.u.mean.partial, b.u.mean.partial_hi, o.u.mean.partial,
+                       o.u.mean.partial_hi);
+               o.u.mean.guard = a.u.mean.guard + b.u.mean.guard;
+               if (!dec_sum_value(o.u.mean.partial, o.u.mean.partial_hi, o.u.mean.guard, o.u.mean.dec_scale,
+                                  o.u.mean.dec_digits, o.u.mean.sum))
+                 o.u.mean.sum = std::numeric_limits<double>::quiet_NaN();
+             } else if (a.integral == 1 && b.integral == 1) {
                o.u.mean.partial = wrap_add(a.u.mean.partial, b.u.mean.partial);
                o.u.mean.sum = (double)o.u.mean.partial;
              } else {

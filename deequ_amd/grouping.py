@@ -23,7 +23,12 @@ _TYPES = {"f64": L.TYPE_F64, "i64": L.TYPE_I64, "i32": L.TYPE_I32, "utf8": L.TYP
 
 
 def _gpu_type(dtype: str) -> int:
-    """The grouping / quantile kernels' column type code."""
+    """The grouping / quantile kernels' column type code (a DecimalType's carries its precision / scale)."""
+    from .table import decimal_ps
+
+    ps = decimal_ps(dtype)
+    if ps:
+        return L.decimal_type(*ps)
     t = _TYPES.get(dtype)
     if t is None:
         from .metrics import UnsupportedOnGpuPathException
@@ -114,6 +119,12 @@ def build_frequencies(data, columns: Sequence[str]) -> "FrequenciesAndNumRows":
 
     chunks = _chunks(data)
     schema = {name: dt for name, dt, _ in chunks[0].schema}
+    from .table import decimal_ps
+
+    if any(decimal_ps(schema[c]) for c in columns):
+        from .metrics import UnsupportedOnGpuPathException
+
+        raise UnsupportedOnGpuPathException("grouping by a DecimalType column is not on the GPU path")
     types = (ctypes.c_int32 * len(columns))(*[_gpu_type(schema[c]) for c in columns])
     views = (L.ColumnView * max(1, len(chunks) * len(columns)))()
     rows = (ctypes.c_int64 * max(1, len(chunks)))()

@@ -15,7 +15,7 @@ from typing import Dict, List, Sequence
 from . import _lib as L
 
 _FORMAT_DTYPE = {"g": "f64", "l": "i64", "i": "i32", "u": "utf8", "U": "large_utf8", "f": "f32", "s": "i16",
-                 "c": "i8", "b": "bool", "tdD": "date32"}  # + "tsu:<tz>" -> timestamp
+                 "c": "i8", "b": "bool", "tdD": "date32"}  # + "tsu:<tz>" -> timestamp, "d:p,s" -> decimal(p,s)
 
 
 class ArrowSchemaC(ctypes.Structure):
@@ -103,6 +103,8 @@ def arrow_schema(batch) -> List[tuple]:
               pa.bool_(): "bool", pa.date32(): "date32"}.get(f.type)
         if dt is None and pa.types.is_timestamp(f.type) and f.type.unit == "us":
             dt = "timestamp"
+        if dt is None and pa.types.is_decimal128(f.type) and 1 <= f.type.precision <= 38 and 0 <= f.type.scale:
+            dt = f"decimal({f.type.precision},{f.type.scale})"
         if dt is None:
             raise TypeError(f"column {f.name}: Arrow type {f.type} is not a GPU column type")
         out.append((f.name, dt, f.nullable))

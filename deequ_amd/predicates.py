@@ -44,13 +44,13 @@ class PredicatePool:
     registers for it (columns enter a plan on first reference)."""
 
     def __init__(self, builder):
-        from .table import DTYPES
+        from .table import type_code
 
         self.b = builder
         names = [c[0] for c in builder.table_schema]
         self._names = names
         arr_n = (ctypes.c_char_p * max(1, len(names)))(*[n.encode("utf-8") for n in names])
-        arr_t = (ctypes.c_int32 * max(1, len(names)))(*[DTYPES[c[1]] for c in builder.table_schema])
+        arr_t = (ctypes.c_int32 * max(1, len(names)))(*[type_code(c[1]) for c in builder.table_schema])
         h = ctypes.c_void_p()
         L.check(L.lib.dq_pred_pool_create(arr_n, arr_t, len(names), ctypes.byref(h)))
         self._h = h

@@ -9,7 +9,7 @@ import ctypes
 import os
 from typing import List, Sequence
 
-from .table import NUMERIC, Column, Table
+from .table import Column, Table, is_numeric
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _lib = None
@@ -194,7 +194,7 @@ def profile_analyzers(table: Table):
     out = [Size()]
     for name, dtype, _ in table.schema:
         out += [Completeness(name), ApproxCountDistinct(name)]
-        if dtype in NUMERIC:
+        if is_numeric(dtype):
             out += [Minimum(name), Maximum(name), Mean(name), StandardDeviation(name), Sum(name)]
     return out
 

@@ -1,7 +1,8 @@
 """HBM-resident columnar tables (Arrow physical layout) handed to the scan.
 
 A Column owns device buffers (torch CUDA/HIP tensors are used purely as device allocations):
-values (f64 / f32 / i64 / i32 / i16 / i8 / date32 / timestamp, bit-packed bool, or UTF-8 bytes), an optional LSB-first validity bitmap, and int32
+values (f64 / f32 / i64 / i32 / i16 / i8 / date32 / timestamp, decimal(p,s) as 16-byte two's-complement unscaled
+integers, bit-packed bool, or UTF-8 bytes), an optional LSB-first validity bitmap, and int32
 (utf8) / int64 (large_utf8) offsets.  Buffers are allocated with the padding dqscan.h requires:
 values 16-byte aligned, bitmaps readable in whole 32-bit words, UTF-8 data readable up to the
 next 4-byte boundary past the last string.
@@ -18,8 +19,35 @@ from . import _lib as L
 DTYPES = {"f64": L.TYPE_F64, "i64": L.TYPE_I64, "i32": L.TYPE_I32, "utf8": L.TYPE_UTF8,
           "large_utf8": L.TYPE_LARGE_UTF8, "f32": L.TYPE_F32, "i16": L.TYPE_I16, "i8": L.TYPE_I8,
           "bool": L.TYPE_BOOL, "date32": L.TYPE_DATE32, "timestamp": L.TYPE_TIMESTAMP}
-# Preconditions.isNumeric (Analyzer.scala:322-334): ByteType .. DoubleType
+# Preconditions.isNumeric (Analyzer.scala:322-334): ByteType .. DoubleType, and DecimalType ("decimal(p,s)")
 NUMERIC = ("f64", "i64", "i32", "f32", "i16", "i8")
+
+
+def decimal_ps(dtype: str) -> Optional[Tuple[int, int]]:
+    """(precision, scale) of a "decimal(p,s)" dtype (DecimalType(p, s)), else None."""
+    if not dtype.startswith("decimal(") or not dtype.endswith(")"):
+        return None
+    p, s = dtype[8:-1].split(",")
+    return int(p), int(s)
+
+
+def is_numeric(dtype: str) -> bool:
+    return dtype in NUMERIC or decimal_ps(dtype) is not None
+
+
+def type_code(dtype: str) -> int:
+    ps = decimal_ps(dtype)
+    return L.decimal_type(*ps) if ps else DTYPES[dtype]
+
+
+def decimal_unscaled(v, scale: int) -> int:
+    """A value as the unscaled integer of DecimalType(_, scale): an int is taken as the value itself, a
+    decimal.Decimal / str / float through its exact decimal value, rounded HALF_UP to the scale (Spark's
+    Decimal.changePrecision)."""
+    import decimal
+
+    d = v if isinstance(v, decimal.Decimal) else decimal.Decimal(str(v) if isinstance(v, float) else v)
+    return int((d.scaleb(scale)).quantize(decimal.Decimal(1), rounding=decimal.ROUND_HALF_UP))
 # fixed-width physical layouts (bool: bit-packed values; date32: int32 days since 1970-01-01; timestamp: int64 us)
 _NP = {"f64": np.float64, "i64": np.int64, "i32": np.int32, "f32": np.float32, "i16": np.int16, "i8": np.int8,
        "date32": np.int32, "timestamp": np.int64}
@@ -67,7 +95,7 @@ class Column:
 
     @property
     def type_code(self) -> int:
-        return DTYPES[self.dtype]
+        return type_code(self.dtype)
 
 
 class Table:
@@ -106,6 +134,10 @@ class Table:
             elif dtype in FIXED:
                 arr = np.array([0 if v is None else v for v in vals], dtype=_NP[dtype])
                 cols.append(column_from_numpy(name, dtype, arr, valid, device=device, nullable=nl))
+            elif decimal_ps(dtype):
+                sc = decimal_ps(dtype)[1]
+                u = [0 if v is None else decimal_unscaled(v, sc) for v in vals]
+                cols.append(column_from_numpy(name, dtype, u, valid, device=device, nullable=nl))
             else:
                 b = [None if v is None else (v.encode("utf-8") if isinstance(v, str) else bytes(v)) for v in vals]
                 cols.append(utf8_column(name, b, device=device, large=(dtype == "large_utf8"), nullable=nl))
@@ -119,6 +151,19 @@ def column_from_numpy(name: str, dtype: str, values: np.ndarray, valid: Optional
         n = len(values)
         raw = pack_validity(np.asarray(values, dtype=bool))
         raw = _pad_u8(raw, 16, 16)
+    elif decimal_ps(dtype):  # Arrow decimal128: the unscaled values (Python ints) as 16-byte little-endian
+        p, _ = decimal_ps(dtype)
+        L.decimal_type(p, 0)  # (validates the precision)
+        n = len(values)
+        mask = (1 << 64) - 1
+        w = np.zeros((n, 2), dtype=np.uint64)
+        if n:
+            u = [int(v) for v in values]
+            if any(abs(v) >= 10 ** p for v in u):
+                raise ValueError(f"a value exceeds the precision of {dtype}")
+            w[:, 0] = [v & mask for v in u]
+            w[:, 1] = [(v >> 64) & mask for v in u]
+        raw = _pad_u8(w.view(np.uint8).reshape(-1), 16, 16)
     else:
         values = np.ascontiguousarray(values, dtype=_NP[dtype])
         n = len(values)

@@ -31,12 +31,13 @@
 extern "C" {
 #endif
 
-#define DQ_ABI_VERSION 5  /* 2: dq_state.reserved[0] = integral flag + Sum / Mean int64 partials; ingestion, pool and state-array entry points;
+#define DQ_ABI_VERSION 6  /* 2: dq_state.reserved[0] = integral flag + Sum / Mean int64 partials; ingestion, pool and state-array entry points;
                              3: dq_plan_create_opts (predicate-pass mode), dq_plan_create_time, dq_plan_explain, dq_quantile_digest;
                              4: any number of analyzers / columns per plan (split into fused plans over the
                                 per-plan capacities), AUTO compiles the predicate kernel in the background,
                                 dq_plan_pred_wait;
-                             5: column types F32 / I16 / I8 / BOOL / DATE32 / TIMESTAMP (scan, predicates, Arrow import) */
+                             5: column types F32 / I16 / I8 / BOOL / DATE32 / TIMESTAMP (scan, predicates, Arrow import);
+                             6: DECIMAL128 (type codes carry precision / scale, dq_state Sum / Mean decimal partials) */
 
 typedef int32_t dq_status;
 #define DQ_OK 0
@@ -48,13 +49,16 @@ typedef int32_t dq_status;
 #define DQ_E_STATE (-6)       /* state algebra misuse (op mismatch, bad byte image) */
 
 /* Column physical types (Arrow layouts) and the Spark SQL types they carry.  The numeric types are the ones
- * Preconditions.isNumeric accepts (analyzers/Analyzer.scala:322-334; DecimalType stays on the fallback):
- * F64 / F32 / I64 / I32 / I16 / I8.  Values are converted to double exactly as Spark casts them (Sum of an
- * integral type is Spark's wrapping LongType sum); ApproxCountDistinct hashes each type as Spark 2.2's
- * XxHash64Function does: hashLong for LongType / TimestampType / DoubleType (doubleToLongBits), hashInt for
- * IntegerType / ShortType / ByteType / DateType (the value widened to int), FloatType (floatToIntBits) and
- * BooleanType (1 / 0).  BOOL / DATE32 / TIMESTAMP are not numeric: Completeness, Size, ApproxCountDistinct,
- * DataType and IS [NOT] NULL atoms (BOOL also = / != against TRUE / FALSE). */
+ * Preconditions.isNumeric accepts (analyzers/Analyzer.scala:322-334): F64 / F32 / I64 / I32 / I16 / I8 /
+ * DECIMAL128.  Values are converted to double as Spark casts them (exactly, or for a decimal correctly rounded:
+ * Decimal.toDouble; Sum of an integral type is Spark's wrapping LongType sum, of a decimal the exact decimal sum
+ * cast at the end); ApproxCountDistinct hashes each type as Spark 2.2's XxHash64Function does: hashLong for
+ * LongType / TimestampType / DoubleType (doubleToLongBits) / DecimalType of precision <= 18 (the unscaled long),
+ * hashInt for IntegerType / ShortType / ByteType / DateType (the value widened to int), FloatType
+ * (floatToIntBits) and BooleanType (1 / 0), hashUnsafeBytes of BigInteger.toByteArray for a wider DecimalType.
+ * BOOL / DATE32 / TIMESTAMP are not numeric: Completeness, Size, ApproxCountDistinct, DataType and IS [NOT] NULL
+ * atoms (BOOL also = / != against TRUE / FALSE).  A DECIMAL128 type code carries its precision (1..38) and scale
+ * (0..precision): DQ_DECIMAL128(p, s); every other code is its enum value alone. */
 enum dq_type {
   DQ_TYPE_F64 = 1,        /* DoubleType: 8-byte values */
   DQ_TYPE_I64 = 2,        /* LongType: 8-byte values */
@@ -66,9 +70,15 @@ enum dq_type {
   DQ_TYPE_I8 = 8,         /* ByteType: 1-byte values */
   DQ_TYPE_BOOL = 9,       /* BooleanType: LSB-first bit-packed values (Arrow `b`), bit 0 = row 0 of the chunk */
   DQ_TYPE_DATE32 = 10,    /* DateType: int32 days since 1970-01-01 (Arrow `tdD`) */
-  DQ_TYPE_TIMESTAMP = 11  /* TimestampType: int64 microseconds since the epoch (Arrow `tsu:<timezone>`) */
+  DQ_TYPE_TIMESTAMP = 11, /* TimestampType: int64 microseconds since the epoch (Arrow `tsu:<timezone>`) */
+  DQ_TYPE_DECIMAL128 = 12 /* DecimalType(p, s): 16-byte little-endian two's-complement unscaled values (Arrow
+                             `d:p,s` / `d:p,s,128`); use the code DQ_DECIMAL128(p, s) */
 };
-#define DQ_TYPE_MAX 11
+#define DQ_TYPE_MAX 12
+#define DQ_DECIMAL128(p, s) (DQ_TYPE_DECIMAL128 | ((p) << 8) | ((s) << 16))
+#define DQ_TYPE_BASE(t) ((t) & 0xFF)
+#define DQ_DECIMAL_PRECISION(t) (((t) >> 8) & 0xFF)
+#define DQ_DECIMAL_SCALE(t) (((t) >> 16) & 0xFF)
 
 /* Analyzer ops: the GPU-eligible ScanShareableAnalyzers. */
 enum dq_op {
@@ -202,7 +212,8 @@ typedef struct dq_host_column {
   int32_t reserved;
 } dq_host_column;
 /* Map an exported Arrow array (formats g = float64, f = float32, l = int64, i = int32, s = int16, c = int8,
- * b = boolean, tdD = date32, tsu:<tz> = timestamp[us], u = utf8, U = large_utf8) to host column buffers; slices
+ * b = boolean, tdD = date32, tsu:<tz> = timestamp[us], d:p,s[,128] = decimal128 (precision <= 38, scale 0..p),
+ * u = utf8, U = large_utf8) to host column buffers; slices
  * at any row offset are rebased by dq_upload (a boolean slice's value bits are shifted like its validity:
  * validity_bit holds the slice's bit offset of both bitmaps).  DQ_E_UNSUPPORTED: other
  * types, nested / dictionary arrays.  DQ_E_INVALID: a required buffer is NULL (an empty array may
@@ -230,15 +241,22 @@ void dq_uploader_destroy(dq_uploader* u);
 typedef struct dq_state {
   int32_t op;           /* enum dq_op */
   uint8_t has_value[2];
-  uint8_t integral;     /* SUM / MEAN of an integral column: `partial` holds Spark's int64 partial-aggregate
+  uint8_t integral;     /* SUM / MEAN of an integral column (1): `partial` holds Spark's int64 partial-aggregate
                            sum (wraps like Spark's LongType sum); dq_state_combine adds the partials and
-                           casts, so row shards combine exactly as Spark's partial -> final merge */
+                           casts, so row shards combine exactly as Spark's partial -> final merge.  Of a
+                           DECIMAL128 column (2): `partial` / `partial_hi` hold the exact decimal sum (128-bit,
+                           unscaled at scale `dec_scale`), `guard` the fp64 sum of the values (it tells a sum
+                           past 2^127 from its wrapped image); an unscaled sum of 10^dec_digits or more (Spark
+                           2.2's sum type DecimalType(min(38, p + 10), s) overflows: a NULL sum) makes the state
+                           undefined */
   uint8_t reserved;
   union {
     struct { int64_t num_matches; } size;                     /* NumMatches */
     struct { int64_t num_matches; int64_t count; } ratio;     /* NumMatchesAndCount (Completeness, Compliance, PatternMatch) */
-    struct { double sum; int64_t partial; } sum;              /* SumState (+ integral partial) */
-    struct { double sum; int64_t count; int64_t partial; } mean;  /* MeanState (+ integral partial) */
+    struct { double sum; int64_t partial; int64_t partial_hi; double guard; int32_t dec_scale, dec_digits; } sum;
+    /* SumState (+ integral / decimal partial) */
+    struct { double sum; int64_t count; int64_t partial; int64_t partial_hi; double guard; int32_t dec_scale, dec_digits; } mean;
+    /* MeanState (+ partial) */
     struct { double n, avg, m2; } stddev;                     /* StandardDeviationState */
     struct { double value; } minmax;                          /* MinState / MaxState */
     struct { double n, x_avg, y_avg, ck, x_mk, y_mk; } corr;  /* CorrelationState */

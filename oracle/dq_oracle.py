@@ -47,6 +47,7 @@ import math
 import re
 import struct
 from dataclasses import dataclass
+from fractions import Fraction
 from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -641,10 +642,59 @@ def float_to_int_bits(f: float) -> int:
     return struct.unpack("<i", struct.pack("<f", f))[0]
 
 
+# DecimalType(p, s) (dtype "decimal(p,s)"; values: the unscaled Python ints).  Spark 2.2 reads a decimal through
+# java.math.BigDecimal: Decimal.toDouble = BigDecimal.doubleValue (correctly rounded), Decimal.toString =
+# BigDecimal.toString, and XxHash64 hashes hashLong(unscaled) for p <= 18, else BigInteger.toByteArray's bytes
+# (InterpretedHashFunction.hash).  Sum is the exact decimal sum (sum(col) has type DecimalType(min(38, p + 10), s))
+# cast to double at the end (Sum.scala:40).
+def decimal_ps(dtype: str) -> Optional[Tuple[int, int]]:
+    """(precision, scale) of a "decimal(p,s)" dtype, else None."""
+    if not dtype.startswith("decimal("):
+        return None
+    p, s = dtype[8:-1].split(",")
+    return int(p), int(s)
+
+
+def decimal_to_double(u: int, s: int) -> float:
+    """BigDecimal.doubleValue of unscaled u at scale s: Fraction -> float rounds to nearest, ties to even."""
+    return float(Fraction(int(u), 10 ** s))
+
+
+def decimal_to_string(u: int, s: int) -> str:
+    """java.math.BigDecimal.toString (scale >= 0): plain unless the adjusted exponent is below -6."""
+    u = int(u)
+    sign = "-" if u < 0 else ""
+    coeff = str(abs(u))
+    adjusted = len(coeff) - 1 - s
+    if s == 0:
+        return sign + coeff
+    if adjusted >= -6:
+        if len(coeff) > s:
+            return f"{sign}{coeff[:-s]}.{coeff[-s:]}"
+        return f"{sign}0.{'0' * (s - len(coeff))}{coeff}"
+    mant = coeff[0] + ("." + coeff[1:] if len(coeff) > 1 else "")
+    return f"{sign}{mant}E{adjusted}"
+
+
+def decimal_hash_input(u: int, p: int):
+    """What XxHash64 hashes for a decimal: ("long", unscaled) for p <= 18, else ("bytes", toByteArray)."""
+    u = int(u)
+    if p <= 18:
+        return "long", u
+    bl = (u if u >= 0 else ~u).bit_length()  # BigInteger.bitLength
+    return "bytes", u.to_bytes(bl // 8 + 1, "big", signed=True)
+
+
+def decimal_hash(u: int, p: int) -> int:
+    kind, v = decimal_hash_input(u, p)
+    return xxh64_long(v) if kind == "long" else xxh64_bytes(v)
+
+
 @dataclass
 class OColumn:
-    """A column for the oracle: dtype in {f64, f32, i64, i32, i16, i8, bool, date32, timestamp, utf8}; values +
-    boolean validity (bool: a bool array; date32: int32 days; timestamp: int64 microseconds, UTC)."""
+    """A column for the oracle: dtype in {f64, f32, i64, i32, i16, i8, bool, date32, timestamp, utf8,
+    decimal(p,s)}; values + boolean validity (bool: a bool array; date32: int32 days; timestamp: int64
+    microseconds, UTC; decimal: the unscaled values as Python ints)."""
 
     dtype: str
     values: object  # np.ndarray for numerics, list[bytes|None] for utf8
@@ -848,6 +898,9 @@ class OracleExpr:
                 return list(c.values), "str", c.valid.copy()
             if c.dtype in ("date32", "timestamp"):  # only their NULLs are read (IS [NOT] NULL)
                 return [int(x) for x in c.values], c.dtype, c.valid.copy()
+            if decimal_ps(c.dtype):  # DecimalType: exact values (vs int / decimal: exact; vs double: the cast)
+                sc = decimal_ps(c.dtype)[1]
+                return [Fraction(int(x), 10 ** sc) for x in c.values], "dec", c.valid.copy()
             raise NotImplementedError(c.dtype)
         if kind == "coalesce":
             parts = [self._ev(a, cols, n) for a in e[1]]
@@ -1158,6 +1211,9 @@ def _as_double_list(c: OColumn):
     """Cast(child, DoubleType) of every value (exact for float and every integral type)."""
     if c.dtype in FLOATING:
         return [float(x) for x in c.values]
+    ps = decimal_ps(c.dtype)
+    if ps:  # Decimal.toDouble: correctly rounded
+        return [decimal_to_double(int(x), ps[1]) for x in c.values]
     return [float(int(x)) for x in c.values]
 
 
@@ -1223,9 +1279,17 @@ def spark_corr_buffer(x: List[float], y: List[float], sel: np.ndarray, n_partiti
 
 
 def spark_sum(c: OColumn, sel: np.ndarray, n_partitions: int = 1):
-    """sum(col): integral -> wrapping long sum; double -> sequential double sum; None if empty."""
+    """sum(col): integral -> wrapping long sum; double -> sequential double sum; decimal(p, s) -> the exact sum in
+    DecimalType(min(38, p + 10), s), NULL past that precision (Spark 2.2 overflow; an intermediate overflow depends
+    on Spark's row order and is not restated), cast to double; None if empty."""
     if not sel.any():
         return None
+    ps = decimal_ps(c.dtype)
+    if ps:
+        tot = sum(int(c.values[i]) for i in np.nonzero(sel)[0])
+        if abs(tot) >= 10 ** min(38, ps[0] + 10):
+            return None
+        return decimal_to_double(tot, ps[1])
     parts = []
     for lo, hi in _partitions(len(sel), n_partitions):
         if not sel[lo:hi].any():
@@ -1258,6 +1322,10 @@ def spark_min(c: OColumn, sel: np.ndarray, is_max: bool = False):
     """min/max(col) with Spark's NaN-as-largest ordering; integral compared as integers."""
     if not sel.any():
         return None
+    ps = decimal_ps(c.dtype)
+    if ps:  # min / max of the exact decimals, cast to double
+        vals = [int(c.values[i]) for i in np.nonzero(sel)[0]]
+        return decimal_to_double(max(vals) if is_max else min(vals), ps[1])
     best = None
     for i in np.nonzero(sel)[0]:
         v = int(c.values[i]) if c.dtype in INTEGRAL else float(c.values[i])
@@ -1289,6 +1357,9 @@ def hll_words_for(c: OColumn, sel: np.ndarray) -> Tuple[int, ...]:
                                   dtype=np.int64))
     elif c.dtype == "utf8":
         h = np.array([xxh64_bytes(c.values[i]) & MASK64 for i in idx], dtype=np.uint64)
+    elif decimal_ps(c.dtype):  # hashLong(unscaled) for p <= 18, else hashUnsafeBytes(BigInteger.toByteArray)
+        p = decimal_ps(c.dtype)[0]
+        h = np.array([decimal_hash(int(c.values[i]), p) & MASK64 for i in idx], dtype=np.uint64)
     else:
         raise ValueError(c.dtype)
     regs = np_hll_registers(h)
@@ -1365,6 +1436,8 @@ def _value_string(c: "OColumn", i: int) -> bytes:
         return b"true" if c.values[i] else b"false"
     if c.dtype == "date32":
         return (datetime.date(1970, 1, 1) + datetime.timedelta(days=int(c.values[i]))).isoformat().encode()
+    if decimal_ps(c.dtype):  # Decimal.toString = BigDecimal.toString
+        return decimal_to_string(int(c.values[i]), decimal_ps(c.dtype)[1]).encode()
     if c.dtype == "timestamp":  # DateTimeUtils.timestampToString: yyyy-MM-dd HH:mm:ss[.fraction, zeros trimmed]
         t = datetime.datetime(1970, 1, 1) + datetime.timedelta(microseconds=int(c.values[i]))
         frac = f"{t.microsecond:06d}".rstrip("0")

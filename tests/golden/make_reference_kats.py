@@ -147,6 +147,8 @@ datasets = {
     },
     # profiles/ColumnProfilerTest.scala:177-190: a BooleanType column (true x3, false x2, null)
     "dfBooleanColumn": {"columns": {"attribute": ["bool", [True, True, True, False, False, N]]}},
+    # AnalyzerTests.scala:489-505: a DecimalType.SYSTEM_DEFAULT = DecimalType(38, 18) column (values as decimal text)
+    "dfDecimalSystemDefault": {"columns": {"num": ["decimal(38,18)", ["123.45", "99", "678"]]}},
 }
 
 S = "analyzers/AnalyzerTests.scala"
@@ -277,6 +279,7 @@ cases = [
      "profiles/ColumnProfilerTest.scala:177-190 fixture; StatefulDataType.scala:62-67 on \"true\" / \"false\" (by hand)", []),
     ("dfBooleanColumn", ["ApproxCountDistinct", "attribute", N], 2.0,
      "profiles/ColumnProfilerTest.scala:177-190 fixture (two distinct values); expected value computed by hand", []),
+    ("dfDecimalSystemDefault", ["Minimum", "num", N], 99.0, S + ":489-505 (Minimum on decimal columns)", []),
     # partition merge (analyzers/StateAggregationIntegrationTest.scala:56-104)
     ("stateAggregation", ["Completeness", "origin", N], 0.625, "analyzers/StateAggregationIntegrationTest.scala:77", []),
 ]

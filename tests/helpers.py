@@ -24,6 +24,10 @@ def oracle_columns(ds: dict):
             v = np.array([0.0 if x is None else x for x in vals], dtype=np.float64 if t == "f64" else np.float32)
         elif t == "bool":
             v = np.array([False if x is None else bool(x) for x in vals], dtype=bool)
+        elif O.decimal_ps(t):  # decimal text -> unscaled ints at the column's scale
+            from deequ_amd.table import decimal_unscaled
+
+            v = [0 if x is None else decimal_unscaled(x, O.decimal_ps(t)[1]) for x in vals]
         else:
             v = np.array([0 if x is None else x for x in vals], dtype=_INT_NP[t])
         cols[name] = O.OColumn(t, v, valid)
@@ -51,6 +55,10 @@ def host_column(col, n):
         return raw[: n * w].view(fixed[col.dtype]).copy(), valid, bm
     if col.dtype == "bool":
         return np.unpackbits(raw, bitorder="little")[:n].astype(bool), valid, bm
+    if O.decimal_ps(col.dtype):  # 16-byte two's-complement unscaled values -> Python ints
+        w = raw[: n * 16].view(np.uint64).reshape(-1, 2)
+        return [int(lo) | int(hi) << 64 if hi < (1 << 63) else (int(lo) | int(hi) << 64) - (1 << 128)
+                for lo, hi in w], valid, bm
     offs_raw = col.offsets.cpu().numpy()
     offs = offs_raw[: (n + 1) * (4 if col.dtype == "utf8" else 8)].view(np.int32 if col.dtype == "utf8" else np.int64)
     data = raw.tobytes()

@@ -31,7 +31,7 @@ def test_header_symbols_exported(dq):
     for name in declared:
         assert hasattr(L.lib, name), name
     assert declared == set(L.EXPORTED)
-    assert L.lib.dq_abi_version() == L.ABI_VERSION == 5
+    assert L.lib.dq_abi_version() == L.ABI_VERSION == 6
 
 
 def test_struct_layouts(dq):

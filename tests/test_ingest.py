@@ -220,3 +220,73 @@ def test_arrow_ingest_round6_types_vs_device_scan():
         assert st[a].words == O.compute_state(("ApproxCountDistinct", a.column, None), ocols, n).words, a
     assert (st[an[9]].numMatches, st[an[9]].count) == (int(masks[3].sum()), n)
     assert st[an[10]].numMatches == int((b & masks[3]).sum())
+
+
+def _decimal_batch(n, seed):
+    """DecimalType(38, 18) and (9, 2) columns as Arrow decimal128 (Spark's export of DecimalType)."""
+    import decimal
+
+    rng = np.random.default_rng(seed)
+    u38 = [int(rng.integers(-(10 ** 18), 10 ** 18)) * 10 ** int(rng.integers(0, 15)) for _ in range(n)]
+    u9 = [int(rng.integers(-(10 ** 9) + 1, 10 ** 9)) for _ in range(n)]
+    m38, m9 = rng.random(n) > 0.1, rng.random(n) > 0.2
+    a38 = pa.array([decimal.Decimal(u).scaleb(-18) if ok else None for u, ok in zip(u38, m38)], type=pa.decimal128(38, 18))
+    a9 = pa.array([decimal.Decimal(u).scaleb(-2) if ok else None for u, ok in zip(u9, m9)], type=pa.decimal128(9, 2))
+    return pa.record_batch([a38, a9], names=["d38", "d9"]), (u38, u9), (m38, m9)
+
+
+def test_arrow_import_decimal128():
+    """dq_arrow_import maps decimal128(p, s) arrays (format "d:p,s") to DECIMAL128 columns of 16-byte values; a
+    decimal256 or a negative scale stays on the fallback."""
+    from deequ_amd import _lib as L
+    from deequ_amd.ingest import ImportedArray, arrow_schema
+
+    bt, _, _ = _decimal_batch(1000, 5)
+    assert [d for _, d, _ in arrow_schema(bt)] == ["decimal(38,18)", "decimal(9,2)"]
+    for k, (p, s) in enumerate(((38, 18), (9, 2))):
+        arr = bt.column(k)
+        im = ImportedArray(arr)
+        assert im.host.type == L.decimal_type(p, s) and im.host.values == arr.buffers()[1].address
+        assert im.host.value_bytes == 16 * 1000
+        im.close()
+        im = ImportedArray(arr.slice(7, 100))
+        assert im.host.values == arr.buffers()[1].address + 16 * 7 and im.host.validity_bit == 7
+        im.close()
+    with pytest.raises(L.DQError):
+        ImportedArray(pa.array([1, 2], type=pa.decimal256(40, 2)))
+
+
+@pytest.mark.gpu
+def test_arrow_ingest_decimal_vs_device_scan():
+    """Arrow decimal128 batches sliced at odd row offsets through the pinned upload: the same states as the device
+    tables, and the oracle's (exact sums cast to double, Decimal.toDouble min / max, Spark's decimal hash)."""
+    import torch
+
+    import deequ_amd as dq
+    from deequ_amd.ingest import scan_arrow
+    from deequ_amd.runner import scan_results
+    from deequ_amd.states import state_from_c
+    from deequ_amd.table import column_from_numpy
+    from oracle import dq_oracle as O
+
+    assert torch.cuda.is_available()
+    n, parts = 50_000, [0, 17_001, 33_333, 50_000]
+    bt, (u38, u9), (m38, m9) = _decimal_batch(n, 11)
+    an = [dq.Sum("d38"), dq.Minimum("d38"), dq.Maximum("d9"), dq.Mean("d9"), dq.StandardDeviation("d38"),
+          dq.ApproxCountDistinct("d38"), dq.ApproxCountDistinct("d9"), dq.DataType("d38"), dq.Completeness("d9"),
+          dq.Compliance("pos", "d38 > 0 AND d9 <= 100.5")]
+    batches = [bt.slice(parts[k], parts[k + 1] - parts[k]) for k in range(3)]
+    got = scan_arrow(batches, an)
+    tables = []
+    for k in range(3):
+        sl = slice(parts[k], parts[k + 1])
+        tables.append(dq.Table([column_from_numpy("d38", "decimal(38,18)", u38[sl], m38[sl]),
+                                column_from_numpy("d9", "decimal(9,2)", u9[sl], m9[sl])]))
+    want = scan_results(tables, an)
+    for a, g, w in zip(an, got, want):
+        assert bytes(g) == bytes(w), a
+    ocols = {"d38": O.OColumn("decimal(38,18)", u38, m38), "d9": O.OColumn("decimal(9,2)", u9, m9)}
+    st = {a: state_from_c(g) for a, g in zip(an, got)}
+    for a in an[:4] + an[5:7]:
+        ref = O.compute_state((type(a).__name__, a.column, None), ocols, n)
+        assert ref is not None and st[a].metricValue() == ref.metricValue(), a
