@@ -368,7 +368,8 @@ def config_setup(cfg, n, chunk):
                 "columns and 93 analyzers, string payload of non-NULL rows only")
     elif cfg == "types":
         analyzers = synth.profile_analyzers(tables[0]) + [dq.DataType(c) for c in names]
-        desc = ("round-6 column types (f32, i16, i8, bool, date32, timestamp; 10% nulls): Size + Completeness + "
+        desc = ("round-6 column types (f32, i16, i8, bool, date32, timestamp, decimal(18,2), decimal(38,18); 10% nulls): "
+                "Size + Completeness + "
                 "ApproxCountDistinct + DataType per column, Min/Max/Mean/StdDev/Sum of the numeric ones")
     else:
         analyzers = [dq.Correlation(names[i], names[j]) for i in range(8) for j in range(i + 1, 8)]

@@ -160,8 +160,8 @@ def c5_table(n, row0=0, seed=42, null_frac=0.10, null_empty=False) -> Table:
 
 def types_table(n, row0=0, seed=42, null_frac=0.10) -> Table:
     """The round-6 column types, one column each: FloatType ~ N(100, 30), ShortType / ByteType uniform, BooleanType
-    (30 % true), DateType (days in [-50000, 50000)), TimestampType (micros in +-2^52); 10 % nulls (torch-generated
-    on the device, seeded by row0 so chunks differ)."""
+    (30 % true), DateType (days in [-50000, 50000)), TimestampType (micros in +-2^52), DecimalType(18, 2) and
+    (38, 18); 10 % nulls (torch-generated on the device, seeded by row0 so chunks differ)."""
     import torch
 
     g = torch.Generator(device="cuda")
@@ -183,6 +183,13 @@ def types_table(n, row0=0, seed=42, null_frac=0.10) -> Table:
     col("d", "date32", torch.randint(-50000, 50000, (n,), device="cuda", generator=g, dtype=torch.int32), 4 * n, 5)
     col("t", "timestamp", torch.randint(-(1 << 52), 1 << 52, (n,), device="cuda", generator=g, dtype=torch.int64),
         8 * n, 6)
+    # DecimalType: (18, 2) money amounts (|unscaled| < 10^12, high word the sign extension) and (38, 18) values of
+    # up to 2^79 unscaled (~ +-6e5): 16-byte two's-complement (low word uniform, high word in [-2^15, 2^15))
+    lo = torch.randint(-(10 ** 12), 10 ** 12, (n,), device="cuda", generator=g, dtype=torch.int64)
+    col("m", "decimal(18,2)", torch.stack([lo, lo >> 63], 1), 16 * n, 7)
+    lo = torch.randint(-(1 << 63), (1 << 63) - 1, (n,), device="cuda", generator=g, dtype=torch.int64)
+    hi = torch.randint(-(1 << 15), 1 << 15, (n,), device="cuda", generator=g, dtype=torch.int64)
+    col("q", "decimal(38,18)", torch.stack([lo, hi], 1), 16 * n, 8)
     return Table(cols)
 
 
