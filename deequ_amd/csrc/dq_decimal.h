@@ -7,7 +7,7 @@
 //     else hashUnsafeBytes of BigInteger.toByteArray (minimal big-endian two's complement);
 //   * the DataType class of its string (Decimal.toString = BigDecimal.toString: plain notation -- FRACTIONAL,
 //     or INTEGRAL at scale 0 -- unless the adjusted exponent is below -6, then "1.5E-7": a STRING).
-// The conversion: the magnitude a as a double-double (RN(a) + RN(a - RN(a))) times 10^-s as a double-double
+// The conversion: the value as a double-double (its 32-bit limbs added by TwoSums) times 10^-s as a double-double
 // (tables from tools/gen_dec_tables.py) -- within 2^-101 of the quotient -- rounded once; a result whose
 // residual lies within 2^-95 of a rounding midpoint (rare: exact ties exist, e.g. 9007199254740992.5) is settled
 // by an exact integer comparison of a * 2^k with the midpoint times 10^s (320-bit limbs).
@@ -106,28 +106,50 @@ DQ_HD_COLD double dec_settle(u128 a, u128 p10, double y, bool up) {  // (rare: o
   return c < 0 || (c == 0 && !even) ? dec_from_bits(yb - 1) : y;
 }
 
-// Decimal.toDouble of unscaled (lo, hi) at scale s (0 <= s <= 38)
-DQ_HD double dec_to_double(uint64_t lo, uint64_t hi, int s, const DecTab& t) {
+// Knuth's TwoSum: s + e == a + b exactly
+DQ_HD void dec_two_sum(double a, double b, double& s, double& e) {
+#if defined(__clang__)
+#pragma clang fp contract(off)
+#endif
+  s = a + b;
+  const double bb = s - a;
+  e = (a - (s - bb)) + (b - bb);
+}
+
+// Decimal.toDouble of unscaled (lo, hi) at scale s (0 <= s <= 38).  narrow: the value fits a signed long (precision
+// <= 18: hi is lo's sign extension).  The signed value's 32-bit limbs (two's complement: the top limb signed) are
+// exact doubles; TwoSums add them into h + l (within 2^-104), which times 10^-s (rh + rl) is rounded once.
+DQ_HD double dec_to_double(uint64_t lo, uint64_t hi, int s, const DecTab& t, bool narrow = false) {
 #if defined(__clang__)
 #pragma clang fp contract(off)  // the error-free products and sums below must not be fused (device default: fast)
 #endif
-  const u128 a = dec_mag(lo, hi);
-  const bool neg = (int64_t)hi < 0;
-  if (a == 0) return 0.0;
-  const double ah = (double)a;  // RN
-  if (s == 0) return neg ? -ah : ah;
-  const double al = (double)(i128)(a - (u128)ah);  // RN of the exact residual
+  double h, l;
+  if (narrow) {
+    dec_two_sum((double)(int32_t)(uint32_t)(lo >> 32) * 0x1p32, (double)(uint32_t)lo, h, l);
+  } else {
+    double e1, e2;
+    dec_two_sum((double)(int32_t)(uint32_t)(hi >> 32) * 0x1p96, (double)(uint32_t)hi * 0x1p64, h, l);
+    dec_two_sum(h, (double)(uint32_t)(lo >> 32) * 0x1p32, h, e1);
+    dec_two_sum(h, (double)(uint32_t)lo, h, e2);
+    l = l + e1 + e2;
+  }
+  if (h == 0.0) return 0.0;  // (the value 0: every limb term vanished)
+  const bool neg = h < 0.0;
+  if (neg) {
+    h = -h;
+    l = -l;
+  }
   const double rh = t.rh[s], rl = t.rl[s];
-  const double p = ah * rh;
-  const double e = __builtin_fma(ah, rh, -p);
-  const double tt = __builtin_fma(ah, rl, __builtin_fma(al, rh, e));
+  const double p = h * rh;
+  const double e = __builtin_fma(h, rh, -p);
+  const double tt = __builtin_fma(h, rl, __builtin_fma(l, rh, e));
   double y = p + tt;
   const double r = (p - y) + tt;  // ~ a / 10^s - y, within 2^-101 y
-  const uint64_t yb = dec_bits(y);
-  const double hu = 0.5 * (dec_from_bits(yb + 1) - y), hd = 0.5 * (y - dec_from_bits(yb - 1));
-  const double tol = y * 0x1p-95;
-  const bool nu = __builtin_fabs(r - hu) <= tol, nd = __builtin_fabs(r + hd) <= tol;
-  if (nu || nd) y = dec_settle(a, dec_p10(t, s), y, nu);
+  // a rounding midpoint near y + r: half an ulp of y from its exponent (a quarter below a power of two)
+  const double hu = dec_from_bits(((dec_bits(y) >> 52) - 53) << 52);
+  const double tol = y * 0x1p-95, ar = __builtin_fabs(r);
+  if (__builtin_fabs(ar - hu) <= tol || __builtin_fabs(ar - 0.5 * hu) <= tol)
+    y = dec_settle(dec_mag(lo, hi), dec_p10(t, s), y, r > 0.0);
   return neg ? -y : y;
 }
 

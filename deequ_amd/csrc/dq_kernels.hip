@@ -1261,7 +1261,7 @@ __device__ void decimal_range(const void* values, const uint32_t* validity, cons
       if (sel == 0) continue;
       uint64_t lo, hi;
       load(r + lane, lo, hi);
-      const double x = lane_bit(sel) ? dec_to_double(lo, hi, sc, tab) : 0.0;
+      const double x = lane_bit(sel) ? dec_to_double(lo, hi, sc, tab, prec <= 18) : 0.0;
       shift = wave_uniform(wave_sum_f64(x) / (double)__builtin_popcountll(sel));
       break;
     }
@@ -1284,7 +1284,7 @@ __device__ void decimal_range(const void* values, const uint32_t* validity, cons
       cnt_w += __builtin_popcountll(m[j]);
       const bool sel = lane_bit(m[j]);
       if constexpr (STATS) {
-        const double x = dec_to_double(lo[j], hi[j], sc, tab);
+        const double x = dec_to_double(lo[j], hi[j], sc, tab, prec <= 18);
         masked_moments<false, false>(a, s.fmin, s.fmax, x, 0, shift, m[j], m[j]);
         if (sel) {
           const uint64_t l2 = slo + lo[j];

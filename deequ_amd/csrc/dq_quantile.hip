@@ -657,7 +657,8 @@ __global__ void widen_column(const void* __restrict__ src, int32_t type, void* _
     if (DQ_TYPE_BASE(type) == DQ_TYPE_DECIMAL128) {
       const uint64_t* v = reinterpret_cast<const uint64_t*>(src) + 2 * r;
       reinterpret_cast<double*>(dst)[r] =
-          dec_to_double(__builtin_nontemporal_load(v), __builtin_nontemporal_load(v + 1), DQ_DECIMAL_SCALE(type), tab);
+          dec_to_double(__builtin_nontemporal_load(v), __builtin_nontemporal_load(v + 1), DQ_DECIMAL_SCALE(type), tab,
+                        DQ_DECIMAL_PRECISION(type) <= 18);
     } else if (type == DQ_TYPE_F32) reinterpret_cast<double*>(dst)[r] = (double)__builtin_nontemporal_load(reinterpret_cast<const float*>(src) + r);
     else if (type == DQ_TYPE_I16) reinterpret_cast<int32_t*>(dst)[r] = __builtin_nontemporal_load(reinterpret_cast<const int16_t*>(src) + r);
     else reinterpret_cast<int32_t*>(dst)[r] = __builtin_nontemporal_load(reinterpret_cast<const int8_t*>(src) + r);

@@ -14,7 +14,7 @@ int main() {
   unsigned long long lo, hi;
   int s, p;
   while (std::scanf("%llu %llu %d %d", &lo, &hi, &s, &p) == 4) {
-    const double d = dq::dec_to_double(lo, hi, s, t);
+    const double d = dq::dec_to_double(lo, hi, s, t, p <= 18);  // (the kernels pass narrow for precision <= 18)
     std::printf("%016" PRIx64 " %016" PRIx64 " %d\n", dq::dec_bits(d), dq::dec_hash(lo, hi, p),
                 dq::dec_dt_class(lo, hi, s, t));
   }
