@@ -77,6 +77,12 @@ __device__ __forceinline__ uint64_t value_bits(const GroupCols& g, int c, int64_
   }
 }
 
+// a DecimalType column: grouped (like strings) by a hash of its 16-byte unscaled value, checked word by word
+__device__ __forceinline__ bool is_dec(int32_t t) { return DQ_TYPE_BASE(t) == DQ_TYPE_DECIMAL128; }
+__device__ __forceinline__ const uint64_t* dec_at(const GroupCols& g, int c, int64_t r) {
+  return reinterpret_cast<const uint64_t*>(g.values[c]) + 2 * r;
+}
+
 __device__ __forceinline__ void str_of(const GroupCols& g, int c, int64_t r, const uint8_t*& p, int64_t& len) {
   int64_t o0, o1;
   if (g.type[c] == DQ_TYPE_LARGE_UTF8) {
@@ -115,6 +121,9 @@ __device__ uint64_t tuple_hash(const GroupCols& g, int64_t r, uint64_t seed = kS
       }
       for (; i + b < len; ++b) k |= (uint64_t)p[i + b] << (8 * b);
       h = mix8(h, k ^ ((uint64_t)len << 56) ^ 0xA5);
+    } else if (is_dec(g.type[c])) {
+      const uint64_t* v = dec_at(g, c, r);
+      h = mix8(mix8(h, v[0]), v[1]);
     } else {
       h = mix8(h, value_bits(g, c, r));
     }
@@ -144,6 +153,9 @@ __device__ __forceinline__ bool tuple_equal_rows(const GroupCols& ga, const Grou
       }
       for (; i < la; ++i)
         if (pa[i] != pb[i]) return false;
+    } else if (is_dec(ga.type[c])) {
+      const uint64_t *va = dec_at(ga, c, a), *vb = dec_at(gb, c, b);
+      if (va[0] != vb[0] || va[1] != vb[1]) return false;
     } else if (value_bits(ga, c, a) != value_bits(gb, c, b)) {
       return false;
     }
@@ -318,7 +330,7 @@ __global__ void summary_final(const SumPart* __restrict__ part, int32_t nparts, 
 
 // key of one column of a row (exact value for numeric columns, 64-bit hash of the bytes for strings)
 __device__ uint64_t col_key(const GroupCols& g, int c, int64_t r) {
-  if (g.type[c] != DQ_TYPE_UTF8 && g.type[c] != DQ_TYPE_LARGE_UTF8) return value_bits(g, c, r);
+  if (g.type[c] != DQ_TYPE_UTF8 && g.type[c] != DQ_TYPE_LARGE_UTF8 && !is_dec(g.type[c])) return value_bits(g, c, r);
   GroupCols one = g;
   one.n_cols = 1;
   one.values[0] = g.values[c];
@@ -331,6 +343,10 @@ __device__ bool col_equal(const GroupCols* chunks, int c, uint64_t ra, uint64_t 
   const GroupCols& ga = chunks[ra >> kRowBits];
   const GroupCols& gb = chunks[rb >> kRowBits];
   const int64_t a = (int64_t)(ra & ((1ull << kRowBits) - 1)), b = (int64_t)(rb & ((1ull << kRowBits) - 1));
+  if (is_dec(ga.type[c])) {
+    const uint64_t *va = dec_at(ga, c, a), *vb = dec_at(gb, c, b);
+    return va[0] == vb[0] && va[1] == vb[1];
+  }
   if (ga.type[c] != DQ_TYPE_UTF8 && ga.type[c] != DQ_TYPE_LARGE_UTF8) return value_bits(ga, c, a) == value_bits(gb, c, b);
   const uint8_t *pa, *pb;
   int64_t la, lb;
@@ -564,8 +580,6 @@ static dq_status freq_build_impl(const int32_t* types, int32_t n_cols, const dq_
   for (int c = 0; c < n_cols; ++c) {
     if (!type_valid(types[c]))
       return set_error(DQ_E_TYPE, "dq_freq_build: column %d has unknown type %d", c, types[c]);
-    if (is_decimal(types[c]))
-      return set_error(DQ_E_UNSUPPORTED, "dq_freq_build: grouping by a DecimalType column runs on the fallback");
   }
   int64_t total = 0;
   for (int k = 0; k < n_chunks; ++k) {
@@ -580,7 +594,7 @@ static dq_status freq_build_impl(const int32_t* types, int32_t n_cols, const dq_
   t->stream = reinterpret_cast<hipStream_t>(hip_stream);
   t->types.assign(types, types + n_cols);
   // one fixed-width column: grouped by its exact value bits (strings and tuples: by hash, checked exactly)
-  const bool numeric1 = n_cols == 1 && types[0] != DQ_TYPE_UTF8 && types[0] != DQ_TYPE_LARGE_UTF8;
+  const bool numeric1 = n_cols == 1 && types[0] != DQ_TYPE_UTF8 && types[0] != DQ_TYPE_LARGE_UTF8 && !is_decimal(types[0]);
   t->hashed = numeric1 && !mi ? 0 : 1;
 
   // test hook: keep only some bits of the primary tuple hash, to force collisions between distinct tuples

@@ -37,6 +37,21 @@ def _gpu_type(dtype: str) -> int:
     return t
 
 
+def _java_decimal_to_string(u: int, scale: int) -> str:
+    """java.math.BigDecimal.toString of unscaled u at scale >= 0 (Spark's CAST(decimal AS STRING)): plain notation
+    unless the adjusted exponent digits - 1 - scale is below -6, then "1.5E-7" / "0E-18"."""
+    sign = "-" if u < 0 else ""
+    coeff = str(abs(u))
+    adjusted = len(coeff) - 1 - scale
+    if scale == 0:
+        return sign + coeff
+    if adjusted >= -6:
+        if len(coeff) > scale:
+            return f"{sign}{coeff[:-scale]}.{coeff[-scale:]}"
+        return f"{sign}0.{'0' * (scale - len(coeff))}{coeff}"
+    return f"{sign}{coeff[0]}{'.' + coeff[1:] if len(coeff) > 1 else ''}E{adjusted}"
+
+
 def _java_float_to_string(f: float) -> str:
     """java.lang.Float.toString (CAST(float AS STRING)): Double.toString's forms with float's shortest digits."""
     import math
@@ -119,12 +134,6 @@ def build_frequencies(data, columns: Sequence[str]) -> "FrequenciesAndNumRows":
 
     chunks = _chunks(data)
     schema = {name: dt for name, dt, _ in chunks[0].schema}
-    from .table import decimal_ps
-
-    if any(decimal_ps(schema[c]) for c in columns):
-        from .metrics import UnsupportedOnGpuPathException
-
-        raise UnsupportedOnGpuPathException("grouping by a DecimalType column is not on the GPU path")
     types = (ctypes.c_int32 * len(columns))(*[_gpu_type(schema[c]) for c in columns])
     views = (L.ColumnView * max(1, len(chunks) * len(columns)))()
     rows = (ctypes.c_int64 * max(1, len(chunks)))()
@@ -401,14 +410,20 @@ class Histogram(Analyzer):  # Histogram.scala:33-99
     def _render(self, data, dtype: str, key: int, rep: int) -> str:
         import numpy as np
 
-        if dtype not in ("utf8", "large_utf8"):
+        from .table import decimal_ps
+
+        ps = decimal_ps(dtype)
+        if dtype not in ("utf8", "large_utf8") and not ps:
             return _render_fixed(dtype, key)
         if rep == (1 << 64) - 1:
-            raise NotImplementedError("Histogram of a merged string frequency table (no representative rows)")
+            raise NotImplementedError("Histogram of a merged string / decimal frequency table (no representative rows)")
         from .runner import _chunks
 
         col = _chunks(data)[rep >> 40].columns[self.column]
         r = rep & ((1 << 40) - 1)
+        if ps:  # the representative row's 16-byte unscaled value, as Decimal.toString
+            u = int.from_bytes(bytes(col.values[16 * r:16 * r + 16].cpu().numpy()), "little", signed=True)
+            return _java_decimal_to_string(u, ps[1])
         width = 8 if col.dtype == "large_utf8" else 4
         o = col.offsets[r * width:(r + 2) * width].cpu().numpy().view(np.int64 if width == 8 else np.int32)
         return bytes(col.values[int(o[0]):int(o[1])].cpu().numpy()).decode("utf-8", "replace")
@@ -422,7 +437,9 @@ class Histogram(Analyzer):  # Histogram.scala:33-99
         reps = (ctypes.c_uint64 * max(1, n))()
         got = ctypes.c_int32()
         L.check(L.lib.dq_freq_top(state.frequencies.handle, n, keys, counts, reps, ctypes.byref(got)))
-        dtype = {v: k for k, v in _TYPES.items()}[state.frequencies.types[0]]
+        t0 = state.frequencies.types[0]
+        dtype = ({v: k for k, v in _TYPES.items()}.get(t0) or
+                 f"decimal({(t0 >> 8) & 0xFF},{(t0 >> 16) & 0xFF})")  # (a DQ_DECIMAL128 code carries p, s)
         bins = [(self._render(data, dtype, keys[i], reps[i]), int(counts[i])) for i in range(got.value)]
         summary = state.frequencies.summary(state.numRows)
         nulls = state.numRows - summary.num_values

@@ -188,21 +188,56 @@ def test_decimal_compliance_vs_oracle(dq, n):
 
 def test_decimal_unsupported_routes(dq):
     """What stays on the fallback: a decimal compared with a double literal or a column, a literal whose wider
-    decimal type exceeds 38 digits (DecimalType(38, 30) vs an int: 10 + 30 digits), Correlation and grouping over a
-    decimal column."""
+    decimal type exceeds 38 digits (DecimalType(38, 30) vs an int: 10 + 30 digits), Correlation over a decimal
+    column."""
     from deequ_amd.metrics import UnsupportedOnGpuPathException
 
     t, _ = _table(dq, 1000, seed=2, null_frac=0.1, decimals=[(38, 18), (5, 2), (38, 30)])
     an = [dq.Compliance("dbl", "d38_18 > 1e0"), dq.Compliance("cols", "d5_2 < d38_18"),
-          dq.Compliance("wide", "d38_30 > 1"), dq.Correlation("d38_18", "i"),
-          dq.Uniqueness("d5_2"), dq.Compliance("ok", "d38_18 > 1")]
+          dq.Compliance("wide", "d38_30 > 1"), dq.Correlation("d38_18", "i"), dq.Compliance("ok", "d38_18 > 1")]
     ctx = dq.AnalysisRunner.onData(t).addAnalyzers(an).run()
     for a in an[:-1]:
         m = ctx.metric(a)
-        assert m.value.isFailure, (a, m)
-        if type(a).__name__ != "Uniqueness":
-            assert isinstance(m.value.failed, UnsupportedOnGpuPathException), (a, m)
+        assert m.value.isFailure and isinstance(m.value.failed, UnsupportedOnGpuPathException), (a, m)
     assert ctx.metric(an[-1]).value.isSuccess
+
+
+@pytest.mark.parametrize("n", [1, 4099, 70_001])
+def test_decimal_grouping_and_histogram_vs_oracle(dq, n):
+    """Uniqueness / Distinctness / CountDistinct / Entropy / MutualInformation / Histogram over decimal columns:
+    grouped by their exact unscaled value (hashed, checked word by word), Histogram bins rendered as
+    BigDecimal.toString ("0E-18", "-1.5E-7", "123.450000000000000000")."""
+    from deequ_amd.table import column_from_numpy
+    from tests.helpers import close
+
+    rng = np.random.default_rng(n + 3)
+    pools = {"a": ("decimal(38,18)", [0, 123450000000000000000, -15 * 10 ** 10, 1, -(10 ** 38 - 1), 99 * 10 ** 18,
+                                      2 ** 70, -(2 ** 64)]),
+             "b": ("decimal(5,2)", [0, 150, -150, 99999, 5, -1]),
+             "c": ("decimal(20,0)", [0, 10 ** 19, -(10 ** 19) + 7, 2 ** 63, -(2 ** 63) - 1, 42])}
+    data = {k: (t, [int(x) for x in rng.choice(np.array(pool, dtype=object), n)], rng.random(n) >= 0.1)
+            for k, (t, pool) in pools.items()}
+    t = dq.Table([column_from_numpy(k, ty, v, m) for k, (ty, v, m) in data.items()])
+    ocols = {k: O.OColumn(ty, v, m) for k, (ty, v, m) in data.items()}
+    an = [dq.Uniqueness("a"), dq.Distinctness("b"), dq.CountDistinct("c"), dq.Entropy("a"),
+          dq.Uniqueness(["a", "b"]), dq.CountDistinct(["b", "c"]), dq.MutualInformation("a", "c")]
+    ctx = dq.AnalysisRunner.onData(t).addAnalyzers(an).run()
+    for a in an:
+        spec = (type(a).__name__, a.columns[0] if type(a).__name__ == "Entropy" else a.columns)
+        ref = O.compute_state(spec, ocols, n)
+        m = ctx.metric(a)
+        if ref is None:
+            assert m.value.isFailure, (a, m)
+            continue
+        want, got = ref.metricValue(), m.value.get()
+        ok = close(got, want, 1e-12, 1e-15) if type(a).__name__ in ("Entropy", "MutualInformation") else got == want
+        assert ok, (a, got, want)
+    for col in data:
+        want = O.histogram(ocols, col, n)
+        h = dq.Histogram(col).calculate(t).value.get()
+        assert h.numberOfBins == len(want), (col, h.numberOfBins, len(want))
+        for k, v in h.values.items():
+            assert want[k] == v.absolute, (col, k, v.absolute, want.get(k))
 
 
 @pytest.mark.parametrize("n", [1, 1000, 100_003])
