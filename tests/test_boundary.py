@@ -301,3 +301,55 @@ def test_combine_integral_with_double_partials(dq):
         nul.has_value[0] = 0
         L.check(L.lib.dq_state_combine(ctypes.byref(nul), ctypes.byref(a), ctypes.byref(out)))
         assert out.integral == 1 and (out.u.sum if op == L.OP_SUM else out.u.mean).partial == 4
+
+
+def test_combine_decimal_partials(dq):
+    """Sum / Mean states of a DecimalType column (integral = 2): row shards' exact 128-bit partials add before the
+    cast (Spark's DecimalType partial buffers), the result is Decimal.toDouble of the exact sum, and a sum reaching
+    10^dec_digits (Spark's sum-type overflow: NULL) leaves the state undefined -- host-only state algebra."""
+    import ctypes
+    from fractions import Fraction
+
+    from deequ_amd import _lib as L
+
+    mask = (1 << 64) - 1
+
+    def mk(op, u, scale, digits, count=1):
+        s = L.State()
+        s.op = op
+        s.has_value[0] = s.has_value[1] = 1
+        s.integral = 2
+        x = s.u.sum if op == L.OP_SUM else s.u.mean
+        x.partial = ctypes.c_int64(u & mask).value
+        x.partial_hi = ctypes.c_int64((u >> 64) & mask).value
+        x.guard = float(Fraction(u, 10 ** scale))
+        x.dec_scale, x.dec_digits = scale, digits
+        x.sum = float(Fraction(u, 10 ** scale))
+        if op == L.OP_MEAN:
+            x.count = count
+        return s
+
+    rng = __import__("random").Random(6)
+    for op in (L.OP_SUM, L.OP_MEAN):
+        for _ in range(200):
+            scale = rng.randint(0, 38)
+            a, b = rng.randint(-(10 ** 37), 10 ** 37), rng.randint(-(10 ** 37), 10 ** 37)
+            out = L.State()
+            L.check(L.lib.dq_state_combine(ctypes.byref(mk(op, a, scale, 38)), ctypes.byref(mk(op, b, scale, 38)),
+                                           ctypes.byref(out)))
+            x = out.u.sum if op == L.OP_SUM else out.u.mean
+            assert out.integral == 2 and ((x.partial_hi & mask) << 64 | (x.partial & mask)) == (a + b) & ((1 << 128) - 1)
+            assert L.lib.dq_state_is_defined(ctypes.byref(out)) == 1
+            assert x.sum == float(Fraction(a + b, 10 ** scale)), (a, b, scale)  # exact sum, one rounding
+        # past the sum type's precision: Spark's NULL -> undefined; DecimalType(5, 2)'s sum type holds 15 digits
+        out = L.State()
+        L.check(L.lib.dq_state_combine(ctypes.byref(mk(op, 6 * 10 ** 37, 0, 38)), ctypes.byref(mk(op, 5 * 10 ** 37, 0, 38)),
+                                       ctypes.byref(out)))
+        assert L.lib.dq_state_is_defined(ctypes.byref(out)) == 0
+        L.check(L.lib.dq_state_combine(ctypes.byref(mk(op, 6 * 10 ** 14, 2, 15)), ctypes.byref(mk(op, 4 * 10 ** 14, 2, 15)),
+                                       ctypes.byref(out)))
+        assert L.lib.dq_state_is_defined(ctypes.byref(out)) == 0
+        L.check(L.lib.dq_state_combine(ctypes.byref(mk(op, 6 * 10 ** 14, 2, 15)), ctypes.byref(mk(op, -4 * 10 ** 14, 2, 15)),
+                                       ctypes.byref(out)))
+        assert L.lib.dq_state_is_defined(ctypes.byref(out)) == 1
+        assert (out.u.sum if op == L.OP_SUM else out.u.mean).sum == 2e12
