@@ -39,6 +39,7 @@
 #include <cstdint>
 #include <type_traits>
 
+#include "dq_decimal.h"
 #include "dq_device.h"
 #include "dq_lane.h"
 
@@ -99,22 +100,35 @@ __device__ __forceinline__ uint64_t vbits64_tail(const uint32_t* bm, int64_t bas
   return x;
 }
 
+// DecimalType conversion constants (tools/gen_dec_tables.py)
+#define DQ_DEC_TABLE static __constant__ const
+#include "dq_dec_tables.inc"
+#undef DQ_DEC_TABLE
+
 // raw 64-bit value of element `idx` of a column (fp64 bits; f32: the bits of the exactly widened double, Spark's
-// Cast(child, DoubleType); integers sign-extended) and its double
+// Cast(child, DoubleType); a decimal (kind CK_D128 | scale << 8 | narrow << 16): the bits of Decimal.toDouble, the
+// correctly rounded cast Corr's input gets; integers sign-extended) and its double
 __device__ __forceinline__ int64_t load_raw(const char* col, int kind, int64_t idx) {
-  switch (kind) {
+  switch (kind & 0xFF) {
     case CK_I32: return reinterpret_cast<const int32_t*>(col)[idx];
     case CK_I16: return reinterpret_cast<const int16_t*>(col)[idx];
     case CK_I8: return reinterpret_cast<const int8_t*>(col)[idx];
     case CK_F32: return __builtin_bit_cast(int64_t, (double)reinterpret_cast<const float*>(col)[idx]);
+    case CK_D128: {
+      const uint64_t* v = reinterpret_cast<const uint64_t*>(col) + 2 * idx;
+      const DecTab tab{kDecP10Lo, kDecP10Hi, kDecRcpHi, kDecRcpLo};
+      return __builtin_bit_cast(int64_t, dec_to_double(v[0], v[1], (kind >> 8) & 0xFF, tab, (kind >> 16) & 1));
+    }
     default: return reinterpret_cast<const int64_t*>(col)[idx];
   }
 }
+// the kind's raw value is the bits of its double (fp64, f32 widened, a decimal's cast), not an integer
+__device__ __forceinline__ bool raw_is_double(int kind) { return ck_float(kind) || (kind & 0xFF) == CK_D128; }
 __device__ __forceinline__ double raw_to_double(int64_t raw, int kind) {
-  if (ck_float(kind)) return __builtin_bit_cast(double, raw);
+  if (raw_is_double(kind)) return __builtin_bit_cast(double, raw);
   return __builtin_fma((double)(int32_t)(raw >> 32), 4294967296.0, (double)(uint32_t)raw);  // exact int64 -> double
 }
-__device__ __forceinline__ int elem_bytes(int kind) { return ck_bytes(kind); }
+__device__ __forceinline__ int elem_bytes(int kind) { return ck_bytes(kind & 0xFF); }
 
 // the shift of a column in a range (pointers at the range's first row, nr rows): the mean of its first 64-row group holding finite selected values
 __device__ double range_shift(const char* col, int kind, const uint32_t* vb, const uint32_t* where, int64_t nr,
@@ -224,7 +238,7 @@ __device__ __forceinline__ void fold(PairAcc& A, const int64_t (&raw)[kPairPos],
           A.lo[k] = hw_min(A.lo[k], x[c]);
           A.hi[k] = hw_max(A.hi[k], x[c]);
         }
-        if constexpr (!F64) A.is[k] = (int64_t)((uint64_t)A.is[k] + (uint64_t)(!ck_float(kind[c]) ? raw[c] : 0));
+        if constexpr (!F64) A.is[k] = (int64_t)((uint64_t)A.is[k] + (uint64_t)(!raw_is_double(kind[c]) ? raw[c] : 0));
       }
     }
   }
@@ -342,7 +356,7 @@ __device__ __forceinline__ void fold_fast(PairAcc& A, const int64_t (&raw)[kPair
   if constexpr (!F64) {
 #pragma unroll
     for (int k = 0; k < kPairMoments; ++k)
-      if (!ck_float(kind[2 * k]) && lane_bit(m[2 * k])) A.is[k] = (int64_t)((uint64_t)A.is[k] + (uint64_t)raw[2 * k]);
+      if (!raw_is_double(kind[2 * k]) && lane_bit(m[2 * k])) A.is[k] = (int64_t)((uint64_t)A.is[k] + (uint64_t)raw[2 * k]);
   }
 }
 

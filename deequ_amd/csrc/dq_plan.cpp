@@ -126,6 +126,12 @@ static int32_t kind_of(int32_t t) {
     default: return CK_D128;  // (type_valid: a DECIMAL128 code)
   }
 }
+// the Correlation pass's kind of a column: its ColKind, for a decimal CK_D128 | scale << 8 | (precision <= 18) << 16
+// (dq_pair.hip casts it to double as it loads it)
+static int32_t pair_kind(int32_t t) {
+  if (!is_decimal(t)) return kind_of(t);
+  return CK_D128 | DQ_DECIMAL_SCALE(t) << 8 | (DQ_DECIMAL_PRECISION(t) <= 18 ? 1 : 0) << 16;
+}
 // algorithmic bytes per row (x1000) of a column's value (or UTF8 offset) buffer
 static int64_t value_bytes_x1000(int32_t t) {
   switch (t) {
@@ -1014,8 +1020,6 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
         if (dq_status st = need_col(s.col_b)) return st;
         if (!is_numeric(p->schema[s.col_a].type) || !is_numeric(p->schema[s.col_b].type))
           return set_error(DQ_E_TYPE, "spec %zu: Correlation needs numeric columns", i);
-        if (is_decimal(p->schema[s.col_a].type) || is_decimal(p->schema[s.col_b].type))
-          return set_error(DQ_E_UNSUPPORTED, "spec %zu: Correlation of a DecimalType column runs on the fallback", i);
         int32_t bm;
         if (dq_status st = bitmap(where_slot, bm)) return st;
         auto key = std::make_tuple(s.col_a, s.col_b, bm);
@@ -1025,7 +1029,7 @@ static dq_status build_plan(dq_plan* p, const dq_pred_node* pool, int32_t n_pred
           pair_of[key] = o.pair_task;
           PairTask pt{};
           pt.col_x = s.col_a; pt.col_y = s.col_b;
-          pt.kind_x = kind_of(p->schema[s.col_a].type); pt.kind_y = kind_of(p->schema[s.col_b].type);
+          pt.kind_x = pair_kind(p->schema[s.col_a].type); pt.kind_y = pair_kind(p->schema[s.col_b].type);
           pt.where = bm;
           p->pair_tasks.push_back(pt);
         } else {

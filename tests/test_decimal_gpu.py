@@ -188,18 +188,37 @@ def test_decimal_compliance_vs_oracle(dq, n):
 
 def test_decimal_unsupported_routes(dq):
     """What stays on the fallback: a decimal compared with a double literal or a column, a literal whose wider
-    decimal type exceeds 38 digits (DecimalType(38, 30) vs an int: 10 + 30 digits), Correlation over a decimal
-    column."""
+    decimal type exceeds 38 digits (DecimalType(38, 30) vs an int: 10 + 30 digits)."""
     from deequ_amd.metrics import UnsupportedOnGpuPathException
 
     t, _ = _table(dq, 1000, seed=2, null_frac=0.1, decimals=[(38, 18), (5, 2), (38, 30)])
     an = [dq.Compliance("dbl", "d38_18 > 1e0"), dq.Compliance("cols", "d5_2 < d38_18"),
-          dq.Compliance("wide", "d38_30 > 1"), dq.Correlation("d38_18", "i"), dq.Compliance("ok", "d38_18 > 1")]
+          dq.Compliance("wide", "d38_30 > 1"), dq.Compliance("ok", "d38_18 > 1")]
     ctx = dq.AnalysisRunner.onData(t).addAnalyzers(an).run()
     for a in an[:-1]:
         m = ctx.metric(a)
         assert m.value.isFailure and isinstance(m.value.failed, UnsupportedOnGpuPathException), (a, m)
     assert ctx.metric(an[-1]).value.isSuccess
+
+
+@pytest.mark.parametrize("n", [2, 4099, 100_003])
+def test_decimal_correlation_vs_oracle(dq, n):
+    """Correlation over decimal columns (Corr's inputs are the casts: each value converted as it is loaded by the
+    pair pass), beside int64 columns, with a `where`; the same columns' Mean / Sum stay exact in the column pass."""
+    from deequ_amd.runner import scan_states
+
+    t, host = _table(dq, n, seed=17 + n, null_frac=0.1, decimals=[(38, 18), (18, 6), (5, 2), (28, 10)])
+    cols = ["d38_18", "d18_6", "d5_2", "d28_10", "i"]
+    an = [dq.Correlation(a, b) for k, a in enumerate(cols) for b in cols[k + 1:]]
+    an += [dq.Correlation("d5_2", "d18_6", where="i > 0"), dq.Mean("d5_2"), dq.Sum("d38_18"), dq.StandardDeviation("d18_6")]
+    states = scan_states(t, an)
+    from tests.test_gpu_parity import assert_state_close
+
+    for a in an:
+        if type(a).__name__ == "Correlation":
+            ref = O.compute_state(("Correlation", a.firstColumn, a.secondColumn, a.where), host, n)
+            assert_state_close(states[a], ref), a
+    _check(states, an[-3:], host, n)
 
 
 @pytest.mark.parametrize("n", [1, 4099, 70_001])
