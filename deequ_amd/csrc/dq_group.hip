@@ -13,12 +13,11 @@
 // is a 64-bit hash of the tuple, the rows ride along the sort, and every pair of neighbours with equal
 // keys is compared exactly: a collision between distinct tuples is reported (DQ_E_UNSUPPORTED), never
 // merged silently.  Keys are radix-sorted (hipCUB) and run-length encoded into (key, count) groups;
-// the summary is a fixed-order two-level reduction, so results are deterministic.  A hashed table also
+// (the sort, the runs and the scans are dq_prim.hip's hand-written kernels); the summary is a fixed-order two-level reduction, so results are deterministic.  A hashed table also
 // keeps a second, independently seeded 64-bit hash per group (its representative row's tuple), so that
 // dq_freq_merge -- which no longer has the rows -- detects two distinct tuples whose first hashes collide
 // (equal first hash, different second hash: DQ_E_UNSUPPORTED) instead of adding their counts.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include <cstdlib>
 #include <cstring>
@@ -30,6 +29,7 @@
 #include "dq_device.h"
 #include "dq_hash.h"
 #include "dq_internal.h"
+#include "dq_prim.h"
 
 namespace dq {
 namespace {
@@ -511,9 +511,6 @@ __global__ void merge_gather_check(const uint64_t* __restrict__ k1s, const uint6
     if (i > 0 && k1s[i] == k1s[i - 1] && k2[p] != k2[pos[i - 1]]) atomicOr(collision, 1);
   }
 }
-struct TakeFirst {
-  __host__ __device__ uint64_t operator()(const uint64_t& a, const uint64_t&) const { return a; }
-};
 __global__ void iota_u32(uint32_t* __restrict__ out, int64_t n) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     out[i] = (uint32_t)i;
@@ -533,26 +530,17 @@ __global__ void gather_top(const uint32_t* __restrict__ idx, int32_t n, const ui
 }  // namespace dq
 
 static dq_status rle_into(dq_freq_table* t, const uint64_t* sorted, int64_t n, const uint64_t* sorted_rows = nullptr) {
-  DevBuf nruns(t->device, 20), tmp(t->device, 21);
+  DevBuf nruns(t->device, 20), tmp(t->device, 21), starts(t->device, 22);
   if (dq_status s = nruns.alloc(sizeof(int64_t))) return s;
   GHIP(hipMalloc(&t->d_keys, std::max<int64_t>(1, n) * sizeof(uint64_t)));
   GHIP(hipMalloc(&t->d_counts, std::max<int64_t>(1, n) * sizeof(int64_t)));
   if (n == 0) { t->n_groups = 0; return DQ_OK; }
-  size_t tb = 0;
-  GHIP(hipcub::DeviceRunLengthEncode::Encode(nullptr, tb, sorted, t->d_keys, t->d_counts, nruns.as<int64_t>(),
-                                             (int)n, t->stream));
-  if (dq_status s = tmp.alloc(tb)) return s;
-  GHIP(hipcub::DeviceRunLengthEncode::Encode(tmp.p, tb, sorted, t->d_keys, t->d_counts, nruns.as<int64_t>(),
-                                             (int)n, t->stream));
+  if (dq_status s = tmp.alloc(prim::runs_temp_bytes(n))) return s;
+  if (dq_status s = starts.alloc((size_t)n * 8)) return s;
+  GHIP(prim::runs(sorted, n, t->d_keys, starts.as<int64_t>(), t->d_counts, nruns.as<int64_t>(), tmp.p, t->stream));
   GHIP(hipMemcpyAsync(&t->n_groups, nruns.p, sizeof(int64_t), hipMemcpyDeviceToHost, t->stream));
   GHIP(hipStreamSynchronize(t->stream));
   if (sorted_rows && t->n_groups > 0) {  // representative row of every group (Histogram renders its value)
-    DevBuf starts(t->device, 22);
-    if (dq_status s = starts.alloc(t->n_groups * 8)) return s;
-    size_t tb2 = 0;
-    GHIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, t->d_counts, starts.as<int64_t>(), (int)t->n_groups, t->stream));
-    if (dq_status s = tmp.alloc(tb2)) return s;
-    GHIP(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb2, t->d_counts, starts.as<int64_t>(), (int)t->n_groups, t->stream));
     GHIP(hipMalloc(&t->d_rep, t->n_groups * 8));
     hipLaunchKernelGGL(gather_rep, dim3(grid_for(t->n_groups)), dim3(256), 0, t->stream, sorted_rows,
                        starts.as<int64_t>(), t->n_groups, t->d_rep);
@@ -648,16 +636,12 @@ static dq_status freq_build_impl(const int32_t* types, int32_t n_cols, const dq_
   t->n_values = nv;
   if (dq_status s = sorted_keys.alloc(std::max<int64_t>(1, nv) * 8)) return s;
   if (nv > 0) {
-    size_t tb = 0;
     if (t->hashed) {
       if (dq_status s = sorted_rows.alloc(nv * 8)) return s;
-      GHIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, sel_keys.as<uint64_t>(), sorted_keys.as<uint64_t>(),
-                                              sel_rows.as<uint64_t>(), sorted_rows.as<uint64_t>(), (int)nv, 0, end_bit,
-                                              t->stream));
+      const size_t tb = prim::sort_temp_bytes(nv, 8);
       if (dq_status s = tmp.alloc(tb)) return s;
-      GHIP(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, sel_keys.as<uint64_t>(), sorted_keys.as<uint64_t>(),
-                                              sel_rows.as<uint64_t>(), sorted_rows.as<uint64_t>(), (int)nv, 0, end_bit,
-                                              t->stream));
+      GHIP(prim::sort_pairs(sel_keys.as<uint64_t>(), sorted_keys.as<uint64_t>(), sel_rows.as<uint64_t>(),
+                            sorted_rows.as<uint64_t>(), 8, nv, 0, end_bit, false, tmp.p, tb, t->stream));
       // exact check of equal-hash neighbours
       if (dq_status s = d_chunks.alloc(gcs.size() * sizeof(GroupCols))) return s;
       GHIP(hipMemcpyAsync(d_chunks.p, gcs.data(), gcs.size() * sizeof(GroupCols), hipMemcpyHostToDevice, t->stream));
@@ -674,11 +658,10 @@ static dq_status freq_build_impl(const int32_t* types, int32_t n_cols, const dq_
       GHIP(hipStreamSynchronize(t->stream));
       if (coll) return set_error(DQ_E_UNSUPPORTED, "dq_freq_build: 64-bit tuple-hash collision between distinct values");
     } else {
-      GHIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, sel_keys.as<uint64_t>(), sorted_keys.as<uint64_t>(),
-                                             (int)nv, 0, end_bit, t->stream));
+      const size_t tb = prim::sort_temp_bytes(nv, 0);
       if (dq_status s = tmp.alloc(tb)) return s;
-      GHIP(hipcub::DeviceRadixSort::SortKeys(tmp.p, tb, sel_keys.as<uint64_t>(), sorted_keys.as<uint64_t>(), (int)nv,
-                                             0, end_bit, t->stream));
+      GHIP(prim::sort_pairs(sel_keys.as<uint64_t>(), sorted_keys.as<uint64_t>(), nullptr, nullptr, 0, nv, 0, end_bit,
+                            false, tmp.p, tb, t->stream));
     }
   }
   if (mi) return mi_from_joint(t, sorted_keys.as<uint64_t>(), sorted_rows.as<uint64_t>(), nv, d_chunks.as<GroupCols>(), *mi);
@@ -714,39 +697,24 @@ static dq_status mi_from_joint(dq_freq_table* t, const uint64_t* sorted_keys, co
   for (DevBuf* b : {&nruns, &res, &coll})
     if (dq_status s = b->alloc(8)) return s;
   if (dq_status s = part.alloc(kSumBlocks * sizeof(double))) return s;
-  size_t tb = 0, need = 0;
-  GHIP(hipcub::DeviceRunLengthEncode::Encode(nullptr, tb, sorted_keys, gk.as<uint64_t>(), gc.as<int64_t>(),
-                                             nruns.as<int64_t>(), (int)nv, S));
-  need = std::max(need, tb);
-  GHIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, gc.as<int64_t>(), starts.as<int64_t>(), (int)nv, S));
-  need = std::max(need, tb);
-  GHIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, xk.as<uint64_t>(), sk.as<uint64_t>(), idx.as<uint64_t>(),
-                                          sidx.as<uint64_t>(), (int)nv, 0, 64, S));
-  need = std::max(need, tb);
-  GHIP(hipcub::DeviceScan::InclusiveSum(nullptr, tb, head.as<uint32_t>(), seg.as<uint32_t>(), (int)nv, S));
-  need = std::max(need, tb);
-  if (dq_status s = tmp.alloc(need)) return s;
-  tb = need;
-  GHIP(hipcub::DeviceRunLengthEncode::Encode(tmp.p, tb, sorted_keys, gk.as<uint64_t>(), gc.as<int64_t>(),
-                                             nruns.as<int64_t>(), (int)nv, S));
+  const size_t tb = std::max({prim::runs_temp_bytes(nv), prim::sort_temp_bytes(nv, 8), prim::scan_temp_bytes(nv)});
+  if (dq_status s = tmp.alloc(tb)) return s;
+  // joint groups: keys, counts and first positions of the runs of the sorted joint keys
+  GHIP(prim::runs(sorted_keys, nv, gk.as<uint64_t>(), starts.as<int64_t>(), gc.as<int64_t>(), nruns.as<int64_t>(), tmp.p, S));
   int64_t G = 0;
   GHIP(hipMemcpyAsync(&G, nruns.p, 8, hipMemcpyDeviceToHost, S));
   GHIP(hipStreamSynchronize(S));
-  tb = need;
-  GHIP(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, gc.as<int64_t>(), starts.as<int64_t>(), (int)G, S));
   hipLaunchKernelGGL(mi_group_keys, dim3(grid_for(G)), dim3(256), 0, S, sorted_rows, starts.as<int64_t>(), G, d_chunks,
                      rep.as<uint64_t>(), xk.as<uint64_t>(), yk.as<uint64_t>(), idx.as<uint64_t>());
   GHIP(hipGetLastError());
   GHIP(hipMemsetAsync(coll.p, 0, 8, S));
   for (int c = 0; c < 2; ++c) {
-    tb = need;
-    GHIP(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, (c == 0 ? xk : yk).as<uint64_t>(), sk.as<uint64_t>(),
-                                            idx.as<uint64_t>(), sidx.as<uint64_t>(), (int)G, 0, 64, S));
+    GHIP(prim::sort_pairs((c == 0 ? xk : yk).as<uint64_t>(), sk.as<uint64_t>(), idx.as<uint64_t>(),
+                          sidx.as<uint64_t>(), 8, G, 0, 64, false, tmp.p, tb, S));
     hipLaunchKernelGGL(mi_heads, dim3(grid_for(G)), dim3(256), 0, S, sk.as<uint64_t>(), sidx.as<uint64_t>(),
                        rep.as<uint64_t>(), G, d_chunks, c, head.as<uint32_t>(), coll.as<int32_t>());
     GHIP(hipGetLastError());
-    tb = need;
-    GHIP(hipcub::DeviceScan::InclusiveSum(tmp.p, tb, head.as<uint32_t>(), seg.as<uint32_t>(), (int)G, S));
+    GHIP(prim::inclusive_sum_u32(head.as<uint32_t>(), seg.as<uint32_t>(), G, tmp.p, S));
     GHIP(hipMemsetAsync(segsum.p, 0, G * 8, S));
     hipLaunchKernelGGL(mi_segsum, dim3(grid_for(G)), dim3(256), 0, S, sidx.as<uint64_t>(), seg.as<uint32_t>(),
                        gc.as<int64_t>(), G, segsum.as<unsigned long long>());
@@ -792,7 +760,7 @@ dq_status dq_freq_merge(const dq_freq_table* a, const dq_freq_table* b, dq_freq_
   if (a->types != b->types || a->hashed != b->hashed)
     return set_error(DQ_E_STATE, "dq_freq_merge: frequency tables over different column types");
   const int64_t n = a->n_groups + b->n_groups;
-  if (n >= (int64_t(1) << 31))  // hipCUB sorts take an int item count
+  if (n >= (int64_t(1) << 31))  // dq_prim's sort positions are 32-bit
     return set_error(DQ_E_UNSUPPORTED, "dq_freq_merge: %lld groups in the two tables (at most 2^31 - 1)", (long long)n);
   if (a->hashed && ((a->n_groups > 0 && !a->d_keys2) || (b->n_groups > 0 && !b->d_keys2)))
     return set_error(DQ_E_STATE, "dq_freq_merge: hashed table without its verification hashes");
@@ -833,18 +801,14 @@ dq_status dq_freq_merge(const dq_freq_table* a, const dq_freq_table* b, dq_freq_
     GHIP(hipStreamSynchronize(t->stream));
     const uint64_t lo = std::min(ends[0], ends[2]), hi = std::max(ends[1], ends[3]);
     const int end_bit = (lo ^ hi) ? 64 - __builtin_clzll(lo ^ hi) : 1;
-    size_t tb = 0;
-    GHIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k_in.as<uint64_t>(), k_s.as<uint64_t>(), c_in.as<int64_t>(),
-                                            c_s.as<int64_t>(), (int)n, 0, end_bit, t->stream));
+    const size_t tb = std::max({prim::sort_temp_bytes(n, 8), prim::runs_temp_bytes(n), prim::run_sums_temp_bytes(n)});
     if (dq_status s = tmp.alloc(tb)) return s;
-    GHIP(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, k_in.as<uint64_t>(), k_s.as<uint64_t>(), c_in.as<int64_t>(),
-                                            c_s.as<int64_t>(), (int)n, 0, end_bit, t->stream));
-    tb = 0;
-    GHIP(hipcub::DeviceReduce::ReduceByKey(nullptr, tb, k_s.as<uint64_t>(), t->d_keys, c_s.as<int64_t>(), t->d_counts,
-                                           nruns.as<int64_t>(), hipcub::Sum(), (int)n, t->stream));
-    if (dq_status s = tmp.alloc(tb)) return s;
-    GHIP(hipcub::DeviceReduce::ReduceByKey(tmp.p, tb, k_s.as<uint64_t>(), t->d_keys, c_s.as<int64_t>(), t->d_counts,
-                                           nruns.as<int64_t>(), hipcub::Sum(), (int)n, t->stream));
+    if (dq_status s = pos.alloc(n * 8)) return s;  // the runs' starts
+    GHIP(prim::sort_pairs(k_in.as<uint64_t>(), k_s.as<uint64_t>(), c_in.as<int64_t>(), c_s.as<int64_t>(), 8, n, 0,
+                          end_bit, false, tmp.p, tb, t->stream));
+    // equal keys of the two tables are now neighbours: one group each, counts added
+    GHIP(prim::runs(k_s.as<uint64_t>(), n, t->d_keys, pos.as<int64_t>(), nullptr, nruns.as<int64_t>(), tmp.p, t->stream));
+    GHIP(prim::run_sums_i64(c_s.as<int64_t>(), n, pos.as<int64_t>(), nruns.as<int64_t>(), t->d_counts, tmp.p, t->stream));
     GHIP(hipMemcpyAsync(&t->n_groups, nruns.p, 8, hipMemcpyDeviceToHost, t->stream));
   } else if (n > 0) {
     // hashed keys: sort by the first hash carrying positions, gather (second hash, count), refuse equal first
@@ -857,31 +821,19 @@ dq_status dq_freq_merge(const dq_freq_table* a, const dq_freq_table* b, dq_freq_
                         t->stream));
     hipLaunchKernelGGL(iota_u64, dim3(grid_for(n)), dim3(256), 0, t->stream, pos.as<uint64_t>(), n);
     GHIP(hipGetLastError());
-    size_t tb = 0, need = 0;
-    GHIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k_in.as<uint64_t>(), k_s.as<uint64_t>(), pos.as<uint64_t>(),
-                                            pos_s.as<uint64_t>(), (int)n, 0, 64, t->stream));
-    need = tb;
-    GHIP(hipcub::DeviceReduce::ReduceByKey(nullptr, tb, k_s.as<uint64_t>(), t->d_keys, c_s.as<int64_t>(), t->d_counts,
-                                           nruns.as<int64_t>(), hipcub::Sum(), (int)n, t->stream));
-    need = std::max(need, tb);
-    GHIP(hipcub::DeviceReduce::ReduceByKey(nullptr, tb, k_s.as<uint64_t>(), kdrop.as<uint64_t>(), k2_s.as<uint64_t>(),
-                                           t->d_keys2, nruns.as<int64_t>(), TakeFirst(), (int)n, t->stream));
-    need = std::max(need, tb);
-    if (dq_status s = tmp.alloc(need)) return s;
-    tb = need;
-    GHIP(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb, k_in.as<uint64_t>(), k_s.as<uint64_t>(), pos.as<uint64_t>(),
-                                            pos_s.as<uint64_t>(), (int)n, 0, 64, t->stream));
+    const size_t tb = std::max({prim::sort_temp_bytes(n, 8), prim::runs_temp_bytes(n), prim::run_sums_temp_bytes(n)});
+    if (dq_status s = tmp.alloc(tb)) return s;
+    GHIP(prim::sort_pairs(k_in.as<uint64_t>(), k_s.as<uint64_t>(), pos.as<uint64_t>(), pos_s.as<uint64_t>(), 8, n, 0, 64,
+                          false, tmp.p, tb, t->stream));
     GHIP(hipMemsetAsync(coll.p, 0, 8, t->stream));
     hipLaunchKernelGGL(merge_gather_check, dim3(grid_for(n)), dim3(256), 0, t->stream, k_s.as<uint64_t>(),
                        pos_s.as<uint64_t>(), k2_in.as<uint64_t>(), c_in.as<int64_t>(), n, k2_s.as<uint64_t>(),
                        c_s.as<int64_t>(), coll.as<int32_t>());
     GHIP(hipGetLastError());
-    tb = need;
-    GHIP(hipcub::DeviceReduce::ReduceByKey(tmp.p, tb, k_s.as<uint64_t>(), t->d_keys, c_s.as<int64_t>(), t->d_counts,
-                                           nruns.as<int64_t>(), hipcub::Sum(), (int)n, t->stream));
-    tb = need;
-    GHIP(hipcub::DeviceReduce::ReduceByKey(tmp.p, tb, k_s.as<uint64_t>(), kdrop.as<uint64_t>(), k2_s.as<uint64_t>(),
-                                           t->d_keys2, nruns.as<int64_t>(), TakeFirst(), (int)n, t->stream));
+    // runs of equal first hashes (kdrop: their starts): counts added, the first second hash kept
+    GHIP(prim::runs(k_s.as<uint64_t>(), n, t->d_keys, kdrop.as<int64_t>(), nullptr, nruns.as<int64_t>(), tmp.p, t->stream));
+    GHIP(prim::run_sums_i64(c_s.as<int64_t>(), n, kdrop.as<int64_t>(), nruns.as<int64_t>(), t->d_counts, tmp.p, t->stream));
+    GHIP(prim::run_firsts_u64(k2_s.as<uint64_t>(), n, kdrop.as<int64_t>(), nruns.as<int64_t>(), t->d_keys2, t->stream));
     int32_t collided = 0;
     GHIP(hipMemcpyAsync(&collided, coll.p, 4, hipMemcpyDeviceToHost, t->stream));
     GHIP(hipMemcpyAsync(&t->n_groups, nruns.p, 8, hipMemcpyDeviceToHost, t->stream));
@@ -954,13 +906,13 @@ dq_status dq_freq_top(const dq_freq_table* t, int32_t n, uint64_t* keys, int64_t
     if (dq_status s = b->alloc((size_t)m * 8)) return s;
   hipLaunchKernelGGL(iota_u32, dim3(grid_for(G)), dim3(256), 0, t->stream, idx.as<uint32_t>(), G);
   GHIP(hipGetLastError());
-  // counts descending, ties in key order (stable radix sort over groups already in key order)
-  size_t tb = 0;
-  GHIP(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tb, t->d_counts, sc.as<int64_t>(), idx.as<uint32_t>(),
-                                                    sidx.as<uint32_t>(), (int)G, 0, 64, t->stream));
+  // counts descending, ties in key order (stable radix sort over groups already in key order); every count is in
+  // [1, n_values], so the bits above n_values' highest set bit are zero in all of them
+  const int end_bit = t->n_values > 0 ? 64 - __builtin_clzll((unsigned long long)t->n_values) : 1;
+  const size_t tb = prim::sort_temp_bytes(G, 4);
   if (dq_status s = tmp.alloc(tb)) return s;
-  GHIP(hipcub::DeviceRadixSort::SortPairsDescending(tmp.p, tb, t->d_counts, sc.as<int64_t>(), idx.as<uint32_t>(),
-                                                    sidx.as<uint32_t>(), (int)G, 0, 64, t->stream));
+  GHIP(prim::sort_pairs(reinterpret_cast<const uint64_t*>(t->d_counts), sc.as<uint64_t>(), idx.as<uint32_t>(),
+                        sidx.as<uint32_t>(), 4, G, 0, end_bit, true, tmp.p, tb, t->stream));
   hipLaunchKernelGGL(gather_top, dim3((m + 255) / 256), dim3(256), 0, t->stream, sidx.as<uint32_t>(), m, t->d_keys,
                      t->d_counts, t->d_rep, ok.as<uint64_t>(), oc.as<int64_t>(), orp.as<uint64_t>());
   GHIP(hipGetLastError());

@@ -20,7 +20,6 @@
 // bound, no sort, no scratch the size of the column.  Chunks and row shards add their histograms, so
 // the same select runs over any number of chunks (and across ranks with one all-reduce per pass).
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cmath>
@@ -32,6 +31,7 @@
 #include <vector>
 
 #include "dq_internal.h"
+#include "dq_prim.h"
 
 namespace dq {
 namespace {
@@ -1090,9 +1090,7 @@ dq_status dq_quantile_digest(int32_t type, const dq_column_view* cols, const int
     }
   }
   // second scratch block: candidates | sorted candidates | sample indices | gathered keys | radix-sort temp
-  size_t tb = 0;
-  QHIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
-                                         (int)std::max<int64_t>(1, batch_max), 0, 64, stream));
+  const size_t tb = prim::sort_temp_bytes(std::max<int64_t>(1, batch_max), 0);
   StreamTmp big;
   const size_t o_sorted = (size_t)batch_max * 8, o_idx = o_sorted + (size_t)batch_max * 8,
                o_got = o_idx + (size_t)m * 8, o_tmp = (o_got + (size_t)m * 8 + 255) & ~(size_t)255;
@@ -1147,7 +1145,9 @@ dq_status dq_quantile_digest(int32_t type, const dq_column_view* cols, const int
       c_or |= cur[2 + 2 * i];
     }
     const int end_bit = (c_and ^ c_or) ? 64 - __builtin_clzll(c_and ^ c_or) : 1;
-    if (nc > 0) QHIP(hipcub::DeviceRadixSort::SortKeys(bb + o_tmp, tb, cand, sorted, (int)nc, 0, end_bit, stream));
+    if (nc > 0)
+      QHIP(prim::sort_pairs(reinterpret_cast<const uint64_t*>(cand), reinterpret_cast<uint64_t*>(sorted), nullptr, nullptr,
+                            0, nc, 0, end_bit, false, bb + o_tmp, tb, stream));
     // 4. sample i = the sorted candidate at (its rank within its bucket, past the bucket's eq keys) + (the batch's
     // candidates of the buckets before)
     idx.clear();
