@@ -279,17 +279,30 @@ __global__ __launch_bounds__(256) void group_compact(GroupCols g, int64_t n, int
   }
 }
 
-// neighbours with equal hash keys must hold equal tuples.  ONE: a single chunk, whose column descriptor comes in the
-// kernel arguments (scalar loads) instead of from a per-row lookup in global memory -- one dependent load fewer
-// per compared pair
+// neighbours with equal hash keys must hold equal tuples.  A wave takes 64 consecutive sorted positions; a position
+// that continues a run is compared with the run's first position within the wave (found from the ballot of run
+// heads), or -- the wave's first position -- with the one before it: by transitivity every run is checked exactly,
+// and the compared-against tuple is shared by the wave's lanes of a run, so its scattered loads hit the cache (a
+// column of few distinct values used to load two random strings per pair).  ONE: a single chunk, whose column
+// descriptor comes in the kernel arguments (scalar loads) instead of from a per-row lookup in global memory
 template <bool ONE>
 __global__ void verify_runs(const uint64_t* __restrict__ keys, const uint64_t* __restrict__ rows, int64_t n,
                             const GroupCols* __restrict__ chunks, GroupCols g0, int32_t* __restrict__ collision) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x + 1; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    if (keys[i] != keys[i - 1]) continue;
-    const bool eq = ONE ? tuple_equal_rows(g0, g0, (int64_t)(rows[i] & ((1ull << kRowBits) - 1)),
-                                           (int64_t)(rows[i - 1] & ((1ull << kRowBits) - 1)))
-                        : tuple_equal(chunks, rows[i], rows[i - 1]);
+  const uint64_t rmask = (1ull << kRowBits) - 1ull;
+  const int lane = threadIdx.x & 63;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;  // a multiple of 64: waves stay 64-aligned
+  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x - lane; i0 < n; i0 += stride) {
+    const int64_t i = i0 + lane;
+    const bool in = i < n;
+    const uint64_t k = in ? keys[i] : 0ull;
+    const bool head = !in || i == 0 || keys[i - 1] != k;
+    const uint64_t heads = __builtin_amdgcn_ballot_w64(head);
+    if (head) continue;
+    const uint64_t upto = heads & (lane == 63 ? ~0ull : ((1ull << (lane + 1)) - 1ull));
+    const int first = upto ? 63 - __builtin_clzll(upto) : 0;  // the run's first lane in this wave (< lane), or 0
+    const int64_t partner = lane == 0 ? i - 1 : i0 + first;
+    const uint64_t ra = rows[partner], rb = rows[i];
+    const bool eq = ONE ? tuple_equal_rows(g0, g0, (int64_t)(ra & rmask), (int64_t)(rb & rmask)) : tuple_equal(chunks, ra, rb);
     if (!eq) atomicOr(collision, 1);
   }
 }
@@ -646,11 +659,12 @@ static dq_status freq_build_impl(const int32_t* types, int32_t n_cols, const dq_
       if (dq_status s = d_chunks.alloc(gcs.size() * sizeof(GroupCols))) return s;
       GHIP(hipMemcpyAsync(d_chunks.p, gcs.data(), gcs.size() * sizeof(GroupCols), hipMemcpyHostToDevice, t->stream));
       GHIP(hipMemsetAsync(nsel.p, 0, 8, t->stream));
+      const int vgrid = grid_for(nv);
       if (gcs.size() == 1)
-        hipLaunchKernelGGL(verify_runs<true>, dim3(grid_for(nv)), dim3(256), 0, t->stream, sorted_keys.as<uint64_t>(),
+        hipLaunchKernelGGL(verify_runs<true>, dim3(vgrid), dim3(256), 0, t->stream, sorted_keys.as<uint64_t>(),
                            sorted_rows.as<uint64_t>(), nv, d_chunks.as<GroupCols>(), gcs[0], nsel.as<int32_t>());
       else
-        hipLaunchKernelGGL(verify_runs<false>, dim3(grid_for(nv)), dim3(256), 0, t->stream, sorted_keys.as<uint64_t>(),
+        hipLaunchKernelGGL(verify_runs<false>, dim3(vgrid), dim3(256), 0, t->stream, sorted_keys.as<uint64_t>(),
                            sorted_rows.as<uint64_t>(), nv, d_chunks.as<GroupCols>(), gcs[0], nsel.as<int32_t>());
       GHIP(hipGetLastError());
       int32_t coll = 0;
