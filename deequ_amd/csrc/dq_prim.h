@@ -15,7 +15,9 @@ namespace prim {
 // Radix sort: by key bits [begin_bit, end_bit) (the bits at and above end_bit are taken to be equal in every key:
 // callers pass the highest bit in which their keys differ); ascending, or descending over that bit range; equal keys
 // keep their input order either way.  keys_in / vals_in are read only; keys_out / vals_out get the sorted sequence
-// (they must not overlap the inputs).  val_bytes: 0 (keys only; vals_* ignored), 4 or 8.
+// (they must not overlap the inputs).  val_bytes: 0 (keys only; vals_* ignored), 4 or 8.  Below 2^30 keys the call
+// ends with a synchronisation of `stream` (it reads back the look-back's give-up flag: hipErrorLaunchTimeOut if a
+// tile's wait for its predecessors ever exceeded its bound, so a wrong order is never returned).
 size_t sort_temp_bytes(int64_t n, int val_bytes);
 hipError_t sort_pairs(const uint64_t* keys_in, uint64_t* keys_out, const void* vals_in, void* vals_out, int val_bytes,
                       int64_t n, int begin_bit, int end_bit, bool descending, void* temp, size_t temp_bytes,
