@@ -307,7 +307,35 @@ __global__ void verify_runs(const uint64_t* __restrict__ keys, const uint64_t* _
   }
 }
 
+// The compaction-order form of the exact check, for tables of few groups (most rows share their group with many
+// others: the sorted-order check then loads one scattered string per row).  It walks the keys and row ids as the
+// compaction kernel appended them (each workgroup tile's rows in row order, so a row's own tuple is read nearly
+// sequentially), finds the row's group by binary search of its key in the table's sorted group keys, and compares
+// the row with the group's representative row, whose tuple the group's rows share (cache hits).
+template <bool ONE>
+__global__ void verify_compacted(const uint64_t* __restrict__ keys, const uint64_t* __restrict__ rows, int64_t nv,
+                                 const uint64_t* __restrict__ gkeys, int64_t G, const uint64_t* __restrict__ rep,
+                                 const GroupCols* __restrict__ chunks, GroupCols g0, int32_t* __restrict__ collision) {
+  const uint64_t rmask = (1ull << kRowBits) - 1ull;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = keys[i], self = rows[i];
+    int64_t lo = 0, hi = G - 1;  // the group holding k (present: the table was built from these keys)
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (gkeys[mid] < k) lo = mid + 1;
+      else hi = mid;
+    }
+    const uint64_t rp = rep[lo];
+    if (rp == self) continue;
+    const bool eq = ONE ? tuple_equal_rows(g0, g0, (int64_t)(rp & rmask), (int64_t)(self & rmask))
+                        : tuple_equal(chunks, rp, self);
+    if (!eq) atomicOr(collision, 1);
+  }
+}
+
 constexpr int kSumBlocks = 1024;
+constexpr int64_t kRowOrderVerify = 8;  // compaction-order check when the table has <= 1 group per 8 grouped rows
+constexpr int64_t kCompactedMaxGroups = 1 << 16;  // ... and its group keys (the binary search) stay cache-resident
 struct SumPart { int64_t unique; double ent; };
 
 // fixed-order partials: block b sums groups b, b + kSumBlocks, ... in a fixed tree
@@ -563,6 +591,24 @@ static dq_status rle_into(dq_freq_table* t, const uint64_t* sorted, int64_t n, c
   return DQ_OK;
 }
 
+// the exact check of equal-hash neighbours in sorted order (verify_runs); nsel's first word is the collision flag
+static dq_status verify_sorted(dq_freq_table* t, const uint64_t* sorted_keys, const uint64_t* sorted_rows, int64_t nv,
+                               const std::vector<GroupCols>& gcs, DevBuf& d_chunks, DevBuf& nsel) {
+  GHIP(hipMemsetAsync(nsel.p, 0, 8, t->stream));
+  if (gcs.size() == 1)
+    hipLaunchKernelGGL(verify_runs<true>, dim3(grid_for(nv)), dim3(256), 0, t->stream, sorted_keys, sorted_rows, nv,
+                       d_chunks.as<GroupCols>(), gcs[0], nsel.as<int32_t>());
+  else
+    hipLaunchKernelGGL(verify_runs<false>, dim3(grid_for(nv)), dim3(256), 0, t->stream, sorted_keys, sorted_rows, nv,
+                       d_chunks.as<GroupCols>(), gcs[0], nsel.as<int32_t>());
+  GHIP(hipGetLastError());
+  int32_t coll = 0;
+  GHIP(hipMemcpyAsync(&coll, nsel.p, 4, hipMemcpyDeviceToHost, t->stream));
+  GHIP(hipStreamSynchronize(t->stream));
+  if (coll) return set_error(DQ_E_UNSUPPORTED, "dq_freq_build: 64-bit tuple-hash collision between distinct values");
+  return DQ_OK;
+}
+
 extern "C" {
 
 struct MiRequest { double total; double* value; int32_t* defined; };
@@ -655,22 +701,13 @@ static dq_status freq_build_impl(const int32_t* types, int32_t n_cols, const dq_
       if (dq_status s = tmp.alloc(tb)) return s;
       GHIP(prim::sort_pairs(sel_keys.as<uint64_t>(), sorted_keys.as<uint64_t>(), sel_rows.as<uint64_t>(),
                             sorted_rows.as<uint64_t>(), 8, nv, 0, end_bit, false, tmp.p, tb, t->stream));
-      // exact check of equal-hash neighbours
       if (dq_status s = d_chunks.alloc(gcs.size() * sizeof(GroupCols))) return s;
       GHIP(hipMemcpyAsync(d_chunks.p, gcs.data(), gcs.size() * sizeof(GroupCols), hipMemcpyHostToDevice, t->stream));
-      GHIP(hipMemsetAsync(nsel.p, 0, 8, t->stream));
-      const int vgrid = grid_for(nv);
-      if (gcs.size() == 1)
-        hipLaunchKernelGGL(verify_runs<true>, dim3(vgrid), dim3(256), 0, t->stream, sorted_keys.as<uint64_t>(),
-                           sorted_rows.as<uint64_t>(), nv, d_chunks.as<GroupCols>(), gcs[0], nsel.as<int32_t>());
-      else
-        hipLaunchKernelGGL(verify_runs<false>, dim3(vgrid), dim3(256), 0, t->stream, sorted_keys.as<uint64_t>(),
-                           sorted_rows.as<uint64_t>(), nv, d_chunks.as<GroupCols>(), gcs[0], nsel.as<int32_t>());
-      GHIP(hipGetLastError());
-      int32_t coll = 0;
-      GHIP(hipMemcpyAsync(&coll, nsel.p, 4, hipMemcpyDeviceToHost, t->stream));
-      GHIP(hipStreamSynchronize(t->stream));
-      if (coll) return set_error(DQ_E_UNSUPPORTED, "dq_freq_build: 64-bit tuple-hash collision between distinct values");
+      // exact check of equal-hash neighbours in sorted order here for MutualInformation; the frequency table's runs
+      // choose between the two forms below
+      if (mi)
+        if (dq_status s = verify_sorted(t, sorted_keys.as<uint64_t>(), sorted_rows.as<uint64_t>(), nv, gcs, d_chunks, nsel))
+          return s;
     } else {
       const size_t tb = prim::sort_temp_bytes(nv, 0);
       if (dq_status s = tmp.alloc(tb)) return s;
@@ -681,6 +718,32 @@ static dq_status freq_build_impl(const int32_t* types, int32_t n_cols, const dq_
   if (mi) return mi_from_joint(t, sorted_keys.as<uint64_t>(), sorted_rows.as<uint64_t>(), nv, d_chunks.as<GroupCols>(), *mi);
   if (dq_status s = rle_into(t, sorted_keys.as<uint64_t>(), nv, t->hashed ? sorted_rows.as<uint64_t>() : nullptr))
     return s;
+  if (t->hashed && nv > 0) {
+    // few groups (rows repeat their group's tuple many times): each row checked against its group's representative
+    // in compaction order; otherwise equal-hash neighbours in sorted order
+    static const char* force = std::getenv("DQ_GROUP_VERIFY");  // A/B knob: "sorted" / "compacted"
+    const bool compacted = force ? force[0] == 'c'
+                                 : t->n_groups <= kCompactedMaxGroups && t->n_groups * kRowOrderVerify <= nv;
+    if (compacted) {
+      GHIP(hipMemsetAsync(nsel.p, 0, 8, t->stream));
+      if (gcs.size() == 1)
+        hipLaunchKernelGGL(verify_compacted<true>, dim3(grid_for(nv)), dim3(256), 0, t->stream, sel_keys.as<uint64_t>(),
+                           sel_rows.as<uint64_t>(), nv, t->d_keys, t->n_groups, t->d_rep, d_chunks.as<GroupCols>(),
+                           gcs[0], nsel.as<int32_t>());
+      else
+        hipLaunchKernelGGL(verify_compacted<false>, dim3(grid_for(nv)), dim3(256), 0, t->stream,
+                           sel_keys.as<uint64_t>(), sel_rows.as<uint64_t>(), nv, t->d_keys, t->n_groups, t->d_rep,
+                           d_chunks.as<GroupCols>(), gcs[0], nsel.as<int32_t>());
+      GHIP(hipGetLastError());
+      int32_t coll = 0;
+      GHIP(hipMemcpyAsync(&coll, nsel.p, 4, hipMemcpyDeviceToHost, t->stream));
+      GHIP(hipStreamSynchronize(t->stream));
+      if (coll) return set_error(DQ_E_UNSUPPORTED, "dq_freq_build: 64-bit tuple-hash collision between distinct values");
+    } else if (dq_status s = verify_sorted(t, sorted_keys.as<uint64_t>(), sorted_rows.as<uint64_t>(), nv, gcs, d_chunks,
+                                          nsel)) {
+      return s;
+    }
+  }
   if (t->hashed) {
     GHIP(hipMalloc(&t->d_keys2, std::max<int64_t>(1, t->n_groups) * 8));
     if (t->n_groups > 0) {

@@ -30,11 +30,12 @@ hipError_t exclusive_sum_i64(const int64_t* in, int64_t* out, int64_t n, void* t
 hipError_t inclusive_sum_u32(const uint32_t* in, uint32_t* out, int64_t n, void* temp, hipStream_t stream);
 
 // Runs of equal keys of keys[0 .. n) (sorted, or any order: a run is a maximal stretch of equal neighbours):
-// unique[r] = run r's key, starts[r] = its first index, lengths[r] = its length (any of the three may be null),
-// *num_runs (device memory) = the number of runs.  Each output array holds up to n entries.
+// unique[r] = run r's key, starts[r] = its first index, lengths[r] = its length, run_of[i] = the run holding position
+// i (any of the four may be null), *num_runs (device memory) = the number of runs.  Each output array holds up to n
+// entries (n < 2^31).
 size_t runs_temp_bytes(int64_t n);
 hipError_t runs(const uint64_t* keys, int64_t n, uint64_t* unique, int64_t* starts, int64_t* lengths,
-                int64_t* num_runs, void* temp, hipStream_t stream);
+                int64_t* num_runs, void* temp, hipStream_t stream, int32_t* run_of = nullptr);
 
 // Per-run reductions over the runs() of the same n keys (starts / num_runs from runs(), on the device):
 // sums[r] = the wrapping sum of vals over run r; firsts[r] = vals[starts[r]].

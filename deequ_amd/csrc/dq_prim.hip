@@ -178,7 +178,8 @@ __global__ __launch_bounds__(kT) void runs_count(const uint64_t* __restrict__ ke
 
 __global__ __launch_bounds__(kT) void runs_write(const uint64_t* __restrict__ keys, int64_t n, int64_t tpw,
                                                   const uint64_t* __restrict__ part, int nwg, uint64_t* __restrict__ unique,
-                                                  int64_t* __restrict__ starts, int64_t* __restrict__ num_runs) {
+                                                  int64_t* __restrict__ starts, int64_t* __restrict__ num_runs,
+                                                  int32_t* __restrict__ run_of) {
   __shared__ uint64_t lds[4];
   uint64_t carry = part[blockIdx.x];
   const int64_t lo = (int64_t)blockIdx.x * tpw * kScanTile, hi = std::min<int64_t>(n, lo + tpw * kScanTile);
@@ -200,6 +201,7 @@ __global__ __launch_bounds__(kT) void runs_write(const uint64_t* __restrict__ ke
         starts[r] = i0 + q;
         ++r;
       }
+      if (run_of && i0 + q < hi) run_of[i0 + q] = (int32_t)(r - 1);  // the run holding position i0 + q
     }
     carry += tot;
   }
@@ -483,7 +485,7 @@ hipError_t inclusive_sum_u32(const uint32_t* in, uint32_t* out, int64_t n, void*
 size_t runs_temp_bytes(int64_t n) { return align256((size_t)kMaxWg * 8) + align256((size_t)std::max<int64_t>(1, n) * 8); }
 
 hipError_t runs(const uint64_t* keys, int64_t n, uint64_t* unique, int64_t* starts, int64_t* lengths,
-                int64_t* num_runs, void* temp, hipStream_t stream) {
+                int64_t* num_runs, void* temp, hipStream_t stream, int32_t* run_of) {
   if (n <= 0) return hipMemsetAsync(num_runs, 0, sizeof(int64_t), stream);
   char* t = static_cast<char*>(temp);
   uint64_t* part = reinterpret_cast<uint64_t*>(t);
@@ -491,7 +493,8 @@ hipError_t runs(const uint64_t* keys, int64_t n, uint64_t* unique, int64_t* star
   const Geom g = geom(n, kScanTile);
   hipLaunchKernelGGL(runs_count, dim3(g.nwg), dim3(kT), 0, stream, keys, n, g.tpw, part);
   hipLaunchKernelGGL(scan_parts<uint64_t>, dim3(1), dim3(kT), 0, stream, part, g.nwg);
-  hipLaunchKernelGGL(runs_write, dim3(g.nwg), dim3(kT), 0, stream, keys, n, g.tpw, part, g.nwg, unique, st, num_runs);
+  hipLaunchKernelGGL(runs_write, dim3(g.nwg), dim3(kT), 0, stream, keys, n, g.tpw, part, g.nwg, unique, st, num_runs,
+                     run_of);
   if (lengths) hipLaunchKernelGGL(runs_lengths, dim3(grid_for(n)), dim3(kT), 0, stream, st, num_runs, n, lengths);
   return hipGetLastError();
 }

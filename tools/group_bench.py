@@ -1,7 +1,7 @@
 """Grouping analyzers on the device: dq_freq_build (sort-based GROUP BY) + Uniqueness / Entropy at 1e8 rows (diagnostic).
 
     python tools/group_bench.py [--rows 1e8] [--reps 3]
-One i64 column at several cardinalities (device-generated, 10 % nulls) and the C5 utf8 column; ms per
+One i64 column at several cardinalities (device-generated, 10 % nulls) and the four C5 utf8 columns; ms per
 build_frequencies and per Uniqueness + Distinctness + Entropy calculation (one shared build).
 """
 from __future__ import annotations
@@ -54,8 +54,12 @@ def main():
         del vals, t, st
         torch.cuda.empty_cache()
     t5 = synth.c5_table(n, row0=0, seed=42)
-    sname = [c for c, col in t5.columns.items() if col.dtype == "utf8"][0]
-    timed(f"freq_build utf8 ({sname}, C5 strings)", lambda: build_frequencies(t5, [sname]))
+    for k, sname in enumerate(c for c, col in t5.columns.items() if col.dtype == "utf8"):
+        d = synth.STR_DISTINCT[k]
+        st = timed(f"freq_build utf8 ({sname}, C5 strings, drawn from {d:.3g} values)" if d else
+                   f"freq_build utf8 ({sname}, C5 strings, unique)", lambda: build_frequencies(t5, [sname]))
+        print(f"   groups={L.lib.dq_freq_num_groups(st.frequencies.handle)}", flush=True)
+        del st
 
 
 if __name__ == "__main__":
