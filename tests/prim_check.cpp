@@ -48,13 +48,13 @@ int prim_inclusive_sum_u32(const uint32_t* in, uint32_t* out, int64_t n) {
 // runs + per-run sums / firsts of vals (either may be null); *num_runs_host gets the run count
 int prim_runs(const uint64_t* keys, int64_t n, uint64_t* unique, int64_t* starts, int64_t* lengths,
               const int64_t* sum_vals, int64_t* sums, const uint64_t* first_vals, uint64_t* firsts,
-              int64_t* num_runs_host) {
+              int64_t* num_runs_host, int32_t* run_of) {
   Scratch s, r, nr;
   if (hipError_t e = s.alloc(dq::prim::runs_temp_bytes(n))) return (int)e;
   if (hipError_t e = r.alloc(dq::prim::run_sums_temp_bytes(n))) return (int)e;
   if (hipError_t e = nr.alloc(8)) return (int)e;
   int64_t* d_num = static_cast<int64_t*>(nr.p);
-  if (hipError_t e = dq::prim::runs(keys, n, unique, starts, lengths, d_num, s.p, nullptr)) return (int)e;
+  if (hipError_t e = dq::prim::runs(keys, n, unique, starts, lengths, d_num, s.p, nullptr, run_of)) return (int)e;
   if (sum_vals && sums && starts)
     if (hipError_t e = dq::prim::run_sums_i64(sum_vals, n, starts, d_num, sums, r.p, nullptr)) return (int)e;
   if (first_vals && firsts && starts)

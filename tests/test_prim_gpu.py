@@ -2,7 +2,7 @@
 
 GPU (`-m gpu`): the stable LSD radix sort (keys only, 4- and 8-byte values, bit ranges, descending, ragged sizes,
 all-equal and few-distinct keys), the prefix sums (wrapping) and the runs of equal keys (unique keys, starts,
-lengths, per-run sums and firsts), each compared element for element with numpy's stable sort / cumsum / unique,
+lengths, per-position run ids, per-run sums and firsts), each compared element for element with numpy's stable sort / cumsum / unique,
 through the test harness tests/prim_check.cpp (deequ_amd/build/libdqprimcheck.so).  CPU: the harness exports load.
 """
 from __future__ import annotations
@@ -27,7 +27,7 @@ def _lib():
     lib.prim_sort_pairs.argtypes = [p, p, p, p, i32, i64, i32, i32, i32]
     lib.prim_exclusive_sum_i64.argtypes = [p, p, i64]
     lib.prim_inclusive_sum_u32.argtypes = [p, p, i64]
-    lib.prim_runs.argtypes = [p, i64, p, p, p, p, p, p, p, ctypes.POINTER(ctypes.c_int64)]
+    lib.prim_runs.argtypes = [p, i64, p, p, p, p, p, p, p, ctypes.POINTER(ctypes.c_int64), p]
     for f in (lib.prim_sort_pairs, lib.prim_exclusive_sum_i64, lib.prim_inclusive_sum_u32, lib.prim_runs):
         f.restype = ctypes.c_int
     return lib
@@ -194,9 +194,10 @@ def test_runs(n, distinct):
     fv = rng.integers(0, 2**64 - 1, size=n, dtype=np.uint64, endpoint=True)
     k, sv, f = _dev(keys.view(np.int64)), _dev(vals), _dev(fv.view(np.int64))
     uq, st, ln, sm, fs = (_empty(n, 8) for _ in range(5))
+    ro = _empty(n, 4)
     nr = ctypes.c_int64(-1)
     rc = lib.prim_runs(k.data_ptr(), n, uq.data_ptr(), st.data_ptr(), ln.data_ptr(), sv.data_ptr(), sm.data_ptr(),
-                       f.data_ptr(), fs.data_ptr(), ctypes.byref(nr))
+                       f.data_ptr(), fs.data_ptr(), ctypes.byref(nr), ro.data_ptr())
     assert rc == 0
     wu, ws, wl = np.unique(keys, return_index=True, return_counts=True)
     R = len(wu)
@@ -206,6 +207,7 @@ def test_runs(n, distinct):
     assert np.array_equal(_host(ln, np.int64)[:R], wl)
     assert np.array_equal(_host(sm, np.int64)[:R], np.add.reduceat(vals, ws))
     assert np.array_equal(_host(fs, np.uint64)[:R], fv[ws])
+    assert np.array_equal(_host(ro, np.int32)[:n], np.repeat(np.arange(R, dtype=np.int32), wl))  # run of each position
 
 
 @pytest.mark.gpu
@@ -218,7 +220,7 @@ def test_runs_unsorted_neighbours():
     uq, st, ln = (_empty(n, 8) for _ in range(3))
     nr = ctypes.c_int64(-1)
     assert lib.prim_runs(k.data_ptr(), n, uq.data_ptr(), st.data_ptr(), ln.data_ptr(), None, None, None, None,
-                         ctypes.byref(nr)) == 0
+                         ctypes.byref(nr), None) == 0
     assert nr.value == 5
     assert _host(uq, np.uint64)[:5].tolist() == [5, 1, 5, 9, 5]
     assert _host(st, np.int64)[:5].tolist() == [0, 2, 5, 6, 8]
