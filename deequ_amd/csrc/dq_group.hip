@@ -310,22 +310,36 @@ __global__ void verify_runs(const uint64_t* __restrict__ keys, const uint64_t* _
 // The compaction-order form of the exact check, for tables of few groups (most rows share their group with many
 // others: the sorted-order check then loads one scattered string per row).  It walks the keys and row ids as the
 // compaction kernel appended them (each workgroup tile's rows in row order, so a row's own tuple is read nearly
-// sequentially), finds the row's group by binary search of its key in the table's sorted group keys, and compares
+// sequentially), finds the row's group by binary search of its key in the table's sorted group keys (LDS-sampled),
+// and compares
 // the row with the group's representative row, whose tuple the group's rows share (cache hits).
+constexpr int kVSample = 2048;  // group keys sampled into LDS: the search's first steps
 template <bool ONE>
-__global__ void verify_compacted(const uint64_t* __restrict__ keys, const uint64_t* __restrict__ rows, int64_t nv,
-                                 const uint64_t* __restrict__ gkeys, int64_t G, const uint64_t* __restrict__ rep,
-                                 const GroupCols* __restrict__ chunks, GroupCols g0, int32_t* __restrict__ collision) {
+__global__ __launch_bounds__(256) void verify_compacted(const uint64_t* __restrict__ keys, const uint64_t* __restrict__ rows,
+                                                        int64_t nv, const uint64_t* __restrict__ gkeys, int64_t G,
+                                                        const uint64_t* __restrict__ rep, const GroupCols* __restrict__ chunks,
+                                                        GroupCols g0, int32_t* __restrict__ collision) {
+  __shared__ uint64_t smp[kVSample];  // every stride-th group key (all of them for G <= 2048)
   const uint64_t rmask = (1ull << kRowBits) - 1ull;
+  const int64_t stride = (G + kVSample - 1) / kVSample;
+  const int ns = (int)((G + stride - 1) / stride);
+  for (int s = threadIdx.x; s < ns; s += blockDim.x) smp[s] = gkeys[(int64_t)s * stride];
+  __syncthreads();
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += (int64_t)gridDim.x * blockDim.x) {
     const uint64_t k = keys[i], self = rows[i];
-    int64_t lo = 0, hi = G - 1;  // the group holding k (present: the table was built from these keys)
+    int lo = 0, hi = ns - 1;  // the last sample <= k (k is one of the group keys, so smp[0] <= k)
     while (lo < hi) {
-      const int64_t mid = (lo + hi) >> 1;
-      if (gkeys[mid] < k) lo = mid + 1;
-      else hi = mid;
+      const int mid = (lo + hi + 1) >> 1;
+      if (smp[mid] <= k) lo = mid;
+      else hi = mid - 1;
     }
-    const uint64_t rp = rep[lo];
+    int64_t a = (int64_t)lo * stride, b = (a + stride < G ? a + stride : G) - 1;  // then within its stride
+    while (a < b) {
+      const int64_t mid = (a + b) >> 1;
+      if (gkeys[mid] < k) a = mid + 1;
+      else b = mid;
+    }
+    const uint64_t rp = rep[a];
     if (rp == self) continue;
     const bool eq = ONE ? tuple_equal_rows(g0, g0, (int64_t)(rp & rmask), (int64_t)(self & rmask))
                         : tuple_equal(chunks, rp, self);
