@@ -149,6 +149,9 @@ datasets = {
     "dfBooleanColumn": {"columns": {"attribute": ["bool", [True, True, True, False, False, N]]}},
     # AnalyzerTests.scala:489-505: a DecimalType.SYSTEM_DEFAULT = DecimalType(38, 18) column (values as decimal text)
     "dfDecimalSystemDefault": {"columns": {"num": ["decimal(38,18)", ["123.45", "99", "678"]]}},
+    # constraints/ConstraintsTest.scala:126-146: dataFrameWithColumn(column, DoubleType / StringType, Row(..), Row(..))
+    "dfDoubleColumn": {"columns": {"column": ["f64", [1.0, 2.0]]}},
+    "dfStringNumericColumn": {"columns": {"column": ["utf8", ["1", "2.0"]]}},
 }
 
 S = "analyzers/AnalyzerTests.scala"
@@ -280,6 +283,12 @@ cases = [
     ("dfBooleanColumn", ["ApproxCountDistinct", "attribute", N], 2.0,
      "profiles/ColumnProfilerTest.scala:177-190 fixture (two distinct values); expected value computed by hand", []),
     ("dfDecimalSystemDefault", ["Minimum", "num", N], 99.0, S + ":489-505 (Minimum on decimal columns)", []),
+    # DataType constraints (constraints/ConstraintsTest.scala:126-146): Fractional ratio 1.0 of a DoubleType column;
+    # Fractional 0.5 and Numeric (fractional + integral) 1.0 of a StringType column of "1" and "2.0"
+    ("dfDoubleColumn", ["DataType", "column", N], {"DataTypeHistogram": [0, 2, 0, 0, 0]},
+     "constraints/ConstraintsTest.scala:126-130", []),
+    ("dfStringNumericColumn", ["DataType", "column", N], {"DataTypeHistogram": [0, 1, 1, 0, 0]},
+     "constraints/ConstraintsTest.scala:132-136,143-146", []),
     # partition merge (analyzers/StateAggregationIntegrationTest.scala:56-104)
     ("stateAggregation", ["Completeness", "origin", N], 0.625, "analyzers/StateAggregationIntegrationTest.scala:77", []),
 ]

@@ -153,6 +153,17 @@ def test_gpu_quantiles_skip_equal_digits(dq, case):
 
 
 @pytest.mark.gpu
+def test_gpu_quantile_constraint_kat(dq):
+    """constraints/ConstraintsTest.scala:73-77: approxQuantileConstraint("att1", 0.5, _ == 3.0) succeeds on
+    getDfWithNumericValues (att1 = Int 1..6, utils/FixtureSupport.scala:137-148)."""
+    from deequ_amd.table import column_from_numpy
+
+    t = dq.Table([column_from_numpy("att1", "i32", np.arange(1, 7, dtype=np.int32), None)])
+    assert dq.ApproxQuantile("att1", 0.5).calculate(t).value.get() == 3.0
+    assert O.approx_quantiles_exact(np.arange(1, 7), np.ones(6, bool), [0.5], 0.01) == [3.0]
+
+
+@pytest.mark.gpu
 def test_gpu_quantiles_chunks_nulls_and_reference_bands(dq):
     from deequ_amd.table import column_from_numpy
 
