@@ -12,8 +12,8 @@
 // does; -0.0 and 0.0 stay distinct groups in Spark 2.2).  Otherwise (strings, several columns) the key
 // is a 64-bit hash of the tuple, the rows ride along the sort, and every pair of neighbours with equal
 // keys is compared exactly: a collision between distinct tuples is reported (DQ_E_UNSUPPORTED), never
-// merged silently.  Keys are radix-sorted (hipCUB) and run-length encoded into (key, count) groups;
-// (the sort, the runs and the scans are dq_prim.hip's hand-written kernels); the summary is a fixed-order two-level reduction, so results are deterministic.  A hashed table also
+// merged silently.  Keys are radix-sorted and run-length encoded into (key, count) groups by dq_prim.hip's
+// hand-written kernels; the summary is a fixed-order two-level reduction, so results are deterministic.  A hashed table also
 // keeps a second, independently seeded 64-bit hash per group (its representative row's tuple), so that
 // dq_freq_merge -- which no longer has the rows -- detects two distinct tuples whose first hashes collide
 // (equal first hash, different second hash: DQ_E_UNSUPPORTED) instead of adding their counts.
