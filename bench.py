@@ -33,7 +33,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md (HBM3E peak 8.0 TB/s)
 # FETCH_SIZE summary of this round's kernels (tools/profile_round.sh -> tools/summarize_prof.py):
 # per-dispatch HBM read bytes of each kernel at the default 125 M-row chunk, gfx950-corrected
-PMC_FILE = os.path.join(ROOT, "profiles", "r6t2_pmc.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r6u2_pmc.json")
 # tools/clock_probe.sh: held clock per kernel, one file per probe box (boxes hold 1.87-1.98 GHz under the same
 # kernels); the floor at the held clock takes the highest clock any probe saw (the conservative floor)
 CLOCK_FILES = [os.path.join(ROOT, "profiles", f) for f in ("r3_clock.json", "r3z_clock.json", "r4z_clock.json",
@@ -42,7 +42,7 @@ CLOCK_FILES = [os.path.join(ROOT, "profiles", f) for f in ("r3_clock.json", "r3z
                                                          "r5fin3_clock.json", "r5fin5_clock.json",
                                                          "r6p_clock.json", "r6f_clock.json", "r6y_clock.json",
                                                          "r6q2_clock.json", "r6s2_clock.json",
-                                                         "r6t2_clock.json")]
+                                                         "r6t2_clock.json", "r6u2_clock.json")]
 DEFAULT_CHUNK = 125_000_000  # 8 chunks per 1e9 rows; a UTF8 chunk's bytes (~2.0e9) stay < 2 GiB
 
 
