@@ -27,7 +27,7 @@ def dq():
 
 
 def _data(dq, n, distinct, seed, chunks=1, rare=0):
-    """s: strings, l: wide i64 keys (all 64 bits differ), f: f64 with NaN / -0.0 / 0.0, i: i32; NULLs in s and f.
+    """s: strings (t: the same, reversed per chunk, LARGE_UTF8), l: wide i64 keys (all 64 bits differ), f: f64 with NaN / -0.0 / 0.0, i: i32; NULLs in s and f.
     `rare` extra string and i64 values occur once each (groups an evenly spaced sample likely misses)."""
     from deequ_amd.table import Table, column_from_numpy, utf8_column
 
@@ -49,7 +49,7 @@ def _data(dq, n, distinct, seed, chunks=1, rare=0):
     out = []
     for lo in range(0, n, step):
         hi = min(n, lo + step)
-        out.append(Table([utf8_column("s", s[lo:hi]),
+        out.append(Table([utf8_column("s", s[lo:hi]), utf8_column("t", s[lo:hi][::-1], large=True),
                           column_from_numpy("l", "i64", lv[lo:hi], np.ones(hi - lo, bool)),
                           column_from_numpy("f", "f64", fv[lo:hi], fok[lo:hi]),
                           column_from_numpy("i", "i32", iv[lo:hi], np.ones(hi - lo, bool))]))
@@ -72,7 +72,7 @@ def _both(monkeypatch, data, cols, mode="1"):
     return ref, got
 
 
-COLS = [["s"], ["l"], ["f"], ["s", "i"], ["l", "f", "s"]]
+COLS = [["s"], ["t"], ["l"], ["f"], ["s", "i"], ["l", "f", "s"]]
 
 
 @pytest.mark.parametrize("n,distinct,chunks", [(1, 1, 1), (3000, 7, 1), (20_000, 300, 3), (50_000, 2000, 2)])
@@ -104,7 +104,8 @@ def test_dictionary_sample_misses_groups(dq, monkeypatch):
 
 
 @pytest.mark.parametrize("chunks", [1, 3])
-def test_dictionary_refuses_collisions(dq, monkeypatch, chunks):
+@pytest.mark.parametrize("col", ["s", "t"])
+def test_dictionary_refuses_collisions(dq, monkeypatch, chunks, col):
     from deequ_amd import _lib as L
     from deequ_amd.grouping import build_frequencies
 
@@ -112,8 +113,32 @@ def test_dictionary_refuses_collisions(dq, monkeypatch, chunks):
     monkeypatch.setenv("DQ_GROUP_DICT", "1")
     monkeypatch.setenv("DQ_TEST_GROUP_HASH_MASK", "f")  # 16 possible keys for 100 distinct strings
     with pytest.raises(L.DQError) as e:
-        build_frequencies(data, ["s"])
+        build_frequencies(data, [col])
     assert "collision" in str(e.value)
+
+
+def test_string_check_same_length_strings(dq, monkeypatch):
+    """Equal-length strings that differ in one byte at every position (first 8 bytes, the 8-byte steps, the
+    4-byte step, the last bytes), colliding under the mask: refused; without the mask, exact counts."""
+    from deequ_amd import _lib as L
+    from deequ_amd.grouping import build_frequencies
+    from deequ_amd.table import Table, utf8_column
+
+    base = "abcdefghijklmnopqrstuvwxyz0123456789!"
+    rng = np.random.default_rng(2)
+    for cut in (3, 7, 9, 17, 29, 33, 37):
+        b = base[:cut]
+        pool = [b] + [b[:i] + "#" + b[i + 1:] for i in range(cut)]
+        vals = [pool[i].encode() for i in rng.integers(0, len(pool), size=8000)]
+        data = Table([utf8_column("s", vals)])
+        monkeypatch.setenv("DQ_GROUP_DICT", "1")
+        _, _, c = _table_of(data, ["s"])
+        assert sorted(c.tolist()) == sorted(collections.Counter(vals).values()), cut
+        monkeypatch.setenv("DQ_TEST_GROUP_HASH_MASK", "0")  # every string in one hash group
+        with pytest.raises(L.DQError) as e:
+            build_frequencies(data, ["s"])
+        assert "collision" in str(e.value), cut
+        monkeypatch.delenv("DQ_TEST_GROUP_HASH_MASK")
 
 
 def test_dictionary_default_thresholds(dq, monkeypatch):
